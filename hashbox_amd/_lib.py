@@ -1,0 +1,81 @@
+"""ctypes binding of libhbxgpu.so (the C-ABI declared in include/hbxgpu.h).
+
+There is no fallback: if the library is missing or cannot load, importing the
+engine raises.  Build it with ``python -m hashbox_amd.build``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libhbxgpu.so")
+
+HBX_OK = 0
+ERRORS = {-1: "HBX_ERR_ARG", -2: "HBX_ERR_HIP", -3: "HBX_ERR_CAPACITY", -4: "HBX_ERR_IO",
+          -5: "HBX_ERR_NODEV", -6: "HBX_ERR_STATE"}
+
+# Every symbol include/hbxgpu.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "hbx_version", "hbx_device_count", "hbx_max_chunks", "hbx_ctx_create", "hbx_ctx_destroy",
+    "hbx_last_error", "hbx_chunk_hash", "hbx_chunk_hash_batch", "hbx_chunk_hash_device",
+    "hbx_submit_device", "hbx_wait", "hbx_block_id", "hbx_arena_alloc", "hbx_arena_free",
+    "hbx_memcpy_h2d", "hbx_alloc_pinned", "hbx_free_pinned", "hbx_stage_times",
+    "hbx_set_tile_iters",
+]
+
+
+class FileSummary(ctypes.Structure):
+    _fields_ = [("content_id", ctypes.c_uint8 * 16), ("content_type", ctypes.c_int32),
+                ("n_chunks", ctypes.c_uint32)]
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64
+    # (same soname libamdhip64.so.7).  Loading torch first makes our NEEDED
+    # entry bind to that copy; loading ours first would put a second HIP/HSA
+    # runtime in the process and torch would then see no GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -m hashbox_amd.build` "
+                           "(the engine has no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    P = ctypes.c_void_p
+    U64 = ctypes.c_uint64
+    I = ctypes.c_int
+    L.hbx_version.restype = I
+    L.hbx_device_count.argtypes = [ctypes.POINTER(I)]
+    L.hbx_max_chunks.argtypes = [U64]
+    L.hbx_max_chunks.restype = U64
+    L.hbx_ctx_create.argtypes = [I, ctypes.POINTER(P)]
+    L.hbx_ctx_destroy.argtypes = [P]
+    L.hbx_ctx_destroy.restype = None
+    L.hbx_last_error.argtypes = [P]
+    L.hbx_last_error.restype = ctypes.c_char_p
+    L.hbx_chunk_hash.argtypes = [P, P, U64, P, P, U64, ctypes.POINTER(U64)]
+    L.hbx_chunk_hash_batch.argtypes = [P, U64, P, P, P, P, P, P, P]
+    L.hbx_chunk_hash_device.argtypes = [P, P, U64, P, P, P, P, P, P, P]
+    L.hbx_submit_device.argtypes = [P, P, U64, P, P, P, P, P, P, P]
+    L.hbx_wait.argtypes = [P]
+    L.hbx_block_id.argtypes = [P, P, ctypes.c_uint32, P, U64, P]
+    L.hbx_arena_alloc.argtypes = [P, U64, ctypes.POINTER(P)]
+    L.hbx_arena_free.argtypes = [P, P]
+    L.hbx_memcpy_h2d.argtypes = [P, P, P, U64]
+    L.hbx_alloc_pinned.argtypes = [U64, ctypes.POINTER(P)]
+    L.hbx_free_pinned.argtypes = [P]
+    L.hbx_stage_times.argtypes = [P, ctypes.POINTER(ctypes.c_float)]
+    L.hbx_set_tile_iters.argtypes = [P, ctypes.c_uint32]
+    for name in EXPORTS:
+        if name not in ("hbx_ctx_destroy", "hbx_last_error", "hbx_max_chunks"):
+            getattr(L, name).restype = I
+    _lib = L
+    return L

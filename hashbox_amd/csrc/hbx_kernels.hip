@@ -1,0 +1,627 @@
+// hbx_kernels.hip — gfx950 kernels for the rollsum-split + block-ID path.
+//
+//   K1 hbx_k1_digest_scan  window digest D(q) at every file position, reduced
+//                          to one max per 4096-position slice (+ the digest
+//                          just before the slice, which IS the rollsum state)
+//                          replaces the Rollin/Rollout/Digest loop of
+//                          hashback/store.go:141-165 (smtc/rollsum, A1).
+//   K2 hbx_k2_cut_chain    the sequential split rule store.go:111-130,166-173:
+//                          cut = LAST argmax D over [s+MIN, s+L], L = min(MAX,
+//                          N-s), only if L > 2*MIN.  One wave per file.
+//   K3 hbx_k3_block_md5    BlockID = MD5(BE32(0) || BE32(len) || chunk)
+//                          (pkg/core/block.go:96-111, utils.go:81-84); one lane
+//                          per chunk.
+//   K4 hbx_k4_content_id   file content id (store.go:187-196): single chunk ->
+//                          its id (type 2); else MD5 of the FileChainBlock
+//                          (hashback/hashback.go:162-170) with links = ids
+//                          (type 3).
+// No MFMA anywhere: this is a byte scan plus an integer hash.
+#include "hbx_device.h"
+
+using namespace hbx;
+
+namespace {
+
+// ------------------------------------------------------------------ K1 --
+constexpr int kK1Threads = 1024;  // 16 waves; 16 x 4096 B = one MIN window per iteration
+
+// Per-lane in-aggregates of a 64-byte run: half (positions 0..31) and full.
+struct RunAgg {
+  uint32_t ah, jh, af, jf;
+};
+__device__ __forceinline__ RunAgg run_aggregates(const uint32_t (&v)[16]) {
+  RunAgg r;
+  uint32_t a = 0, j = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    a = dot4(v[k], 0x01010101u, a);
+    j = dot4(v[k], jw(k), j);
+  }
+  r.ah = a;
+  r.jh = j;
+#pragma unroll
+  for (int k = 8; k < 16; k++) {
+    a = dot4(v[k], 0x01010101u, a);
+    j = dot4(v[k], jw(k), j);
+  }
+  r.af = a;
+  r.jf = j;
+  return r;
+}
+
+// Per-position digest pass over one lane's 64 positions, as two packed u16
+// streams: low half = positions 0..31, high half = positions 32..63.
+//   S1 += in - out; s2 += S1; D = s2<<16 | S1; M = max(M, D)
+// TAIL masks positions >= lim (iteration-relative) out of the max.
+template <bool TAIL>
+__device__ __forceinline__ uint32_t digest_pass(const uint32_t (&in)[16], const uint32_t (&out)[16],
+                                                uint32_t S1p, uint32_t S2p, uint32_t e_l,
+                                                uint32_t lim) {
+  u16x2 s1 = as_u16x2(S1p), s2 = as_u16x2(S2p);
+  uint32_t M = 0;
+#pragma unroll
+  for (int j = 0; j < 32; j++) {
+    const int k = j >> 2, b = j & 3;
+    const uint32_t sel = (uint32_t)(4 + b) | (0x0cu << 8) | ((uint32_t)b << 16) | (0x0cu << 24);
+    const u16x2 pin = as_u16x2(__builtin_amdgcn_perm(in[k], in[8 + k], sel));
+    const u16x2 pout = as_u16x2(__builtin_amdgcn_perm(out[k], out[8 + k], sel));
+    s1 = s1 + pin;
+    s1 = s1 - pout;
+    s2 = s2 + s1;
+    uint32_t DA = __builtin_amdgcn_perm(as_u32(s2), as_u32(s1), 0x05040100u);
+    uint32_t DB = __builtin_amdgcn_perm(as_u32(s2), as_u32(s1), 0x07060302u);
+    if (TAIL) {
+      DA = (e_l + (uint32_t)j < lim) ? DA : 0u;
+      DB = (e_l + 32u + (uint32_t)j < lim) ? DB : 0u;
+    }
+    M = max(M, max(DA, DB));
+  }
+  return M;
+}
+
+}  // namespace
+
+// tiles[t] = {file index, tile index within file}; a tile is tile_iters
+// consecutive 64 KiB iterations of one file.
+extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan(
+    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
+    const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ slice_base,
+    const uint2* __restrict__ tiles, uint32_t tile_iters, uint32_t* __restrict__ slice_max,
+    uint32_t* __restrict__ slice_prev) {
+  __shared__ uint2 wtot[2][16];
+  const uint2 td = tiles[blockIdx.x];
+  const uint32_t f = td.x;
+  const uint64_t N = file_len[f];
+  const uint64_t q0 = (uint64_t)td.y * tile_iters * kMinBlock;
+  const uint8_t* fb = arena + file_off[f];
+  const uint64_t sb = slice_base[f];
+
+  const uint32_t tid = threadIdx.x;
+  const uint32_t l = tid & 63u;
+  const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+  const uint32_t e_l = w * kSlice + l * 64u;  // iteration-relative first position of this lane
+
+  const uint64_t rem = N - q0;
+  const uint32_t n_it = (uint32_t)min((uint64_t)tile_iters, (rem + kMinBlock - 1) / kMinBlock);
+  // rounded up to 16 B: every dwordx4 is entirely in or out of range (the
+  // arena guarantees HBX_ARENA_SLACK readable bytes after each file)
+  const uint32_t nbytes = (uint32_t)((min(rem, (uint64_t)n_it * kMinBlock) + 15ull) & ~15ull);
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(fb + q0, nbytes);
+
+  // ---- priming: "out" bytes of iteration 0 = the MIN bytes before q0, and
+  //      the rollsum state at q0-1 = digest state of exactly that window.
+  uint32_t out[16];
+  RunAgg pa;
+  uint32_t S1c, s2c;
+  if (q0 == 0) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) out[k] = 0u;
+    pa = RunAgg{0u, 0u, 0u, 0u};
+    S1c = 0u;
+    s2c = 0x8000u;
+  } else {
+    const __amdgpu_buffer_rsrc_t rh = make_rsrc(fb + q0 - kMinBlock, kMinBlock);
+    load_run64(rh, e_l, 0u, out);
+    pa = run_aggregates(out);
+    const uint32_t iA = wave_incl_sum(pa.af);
+    const uint32_t iC = wave_incl_sum(e_l * pa.af + pa.jf);
+    if (l == 63u) wtot[1][w] = make_uint2(iA, iC);
+    __syncthreads();
+    const uint2 t = (l < 16u) ? wtot[1][l] : make_uint2(0u, 0u);
+    const uint32_t sA = row_incl_sum(t.x), sC = row_incl_sum(t.y);
+    S1c = readlane(sA, 15);
+    s2c = 0x8000u - readlane(sC, 15);  // virtual-zero start: s2 = 2^15 - sum k*x_k
+  }
+
+  uint32_t cur[16], nxt[16];
+  load_run64(rs, e_l, 0u, cur);
+  for (uint32_t it = 0; it < n_it; it++) {
+    if (it + 1 < n_it) load_run64(rs, e_l, (it + 1) * kMinBlock, nxt);
+
+    const RunAgg ca = run_aggregates(cur);
+    const uint32_t A_hA = ca.ah - pa.ah, J_hA = ca.jh - pa.jh;
+    const uint32_t A_l = ca.af - pa.af, J_l = ca.jf - pa.jf;
+    const uint32_t C_l = e_l * A_l + J_l;
+    const uint32_t iA = wave_incl_sum(A_l);
+    const uint32_t iC = wave_incl_sum(C_l);
+    if (l == 63u) wtot[it & 1u][w] = make_uint2(iA, iC);
+    __syncthreads();
+    const uint2 t = (l < 16u) ? wtot[it & 1u][l] : make_uint2(0u, 0u);
+    const uint32_t sA = row_incl_sum(t.x), sC = row_incl_sum(t.y);
+    const uint32_t WA = w ? readlane(sA, (int)w - 1) : 0u;
+    const uint32_t WC = w ? readlane(sC, (int)w - 1) : 0u;
+    const uint32_t totA = readlane(sA, 15), totC = readlane(sC, 15);
+
+    // state before the lane's first position (*), then before position 32
+    const uint32_t A_pre = WA + (iA - A_l), C_pre = WC + (iC - C_l);
+    const uint32_t S1_t = S1c + A_pre;
+    const uint32_t s2_t = s2c + e_l * S1_t - C_pre;
+    const uint32_t A_pre2 = A_pre + A_hA, C_pre2 = C_pre + e_l * A_hA + J_hA;
+    const uint32_t S1_b = S1c + A_pre2;
+    const uint32_t s2_b = s2c + (e_l + 32u) * S1_b - C_pre2;
+    const uint32_t S1p = (S1_t & 0xffffu) | (S1_b << 16);
+    const uint32_t S2p = (s2_t & 0xffffu) | (s2_b << 16);
+
+    const uint64_t qs = q0 + (uint64_t)it * kMinBlock;  // iteration start position
+    const bool slice_ok = qs + (uint64_t)w * kSlice < N;
+    const uint64_t sidx = sb + ((qs >> kSliceShift) + w);
+    if (l == 0u && slice_ok) slice_prev[sidx] = (s2_t << 16) | (S1_t & 0xffffu);
+
+    uint32_t M;
+    if (qs + kMinBlock <= N) {
+      M = digest_pass<false>(cur, out, S1p, S2p, e_l, 0u);
+    } else {
+      M = digest_pass<true>(cur, out, S1p, S2p, e_l, (uint32_t)(N - qs));
+    }
+    M = wave_max_to_lane63(M);
+    if (l == 63u && slice_ok) slice_max[sidx] = M;
+
+    S1c += totA;
+    s2c -= totC;  // 65536*(...) vanishes mod 2^16
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      out[k] = cur[k];
+      cur[k] = nxt[k];
+    }
+    pa = ca;
+  }
+}
+
+// ------------------------------------------------------------------ K2 --
+namespace {
+
+// Exact (max D, last slice-relative position) over [lo, hi] of slice j.
+__device__ void slice_argmax(const uint8_t* fb, uint64_t N, uint64_t j, uint32_t prevD, int lo,
+                             int hi, uint32_t& Dm, int& Pm) {
+  const uint32_t l = threadIdx.x & 63u;
+  const uint64_t sq = j << kSliceShift;
+  const uint64_t avail = N - sq;
+  const __amdgpu_buffer_rsrc_t ri =
+      make_rsrc(fb + sq, (uint32_t)((min(avail, (uint64_t)kSlice) + 15ull) & ~15ull));
+  uint32_t in[16], out[16];
+  load_run64(ri, l * 64u, 0u, in);
+  if (sq >= kMinBlock) {
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(fb + sq - kMinBlock, kSlice);
+    load_run64(ro, l * 64u, 0u, out);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; k++) out[k] = 0u;
+  }
+  uint32_t A = 0, J = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    A = dot4(in[k], 0x01010101u, A) - dot4(out[k], 0x01010101u, 0u);
+    J = dot4(in[k], jw(k), J) - dot4(out[k], jw(k), 0u);
+  }
+  const uint32_t e = l * 64u;
+  const uint32_t C = e * A + J;
+  const uint32_t xA = wave_incl_sum(A) - A;
+  const uint32_t xC = wave_incl_sum(C) - C;
+  const uint32_t S1 = (prevD & 0xffffu) + xA;
+  const uint32_t s2 = (prevD >> 16) + e * S1 - xC;
+  uint32_t bD = 0u;
+  int bP = -1;
+  run_argmax_exact(in, out, S1, s2, (int)e, lo, hi, bD, bP);
+  Dm = wave_max_all(bP >= 0 ? bD : 0u);
+  Pm = wave_max_all_i((bP >= 0 && bD == Dm) ? bP : -1);
+}
+
+}  // namespace
+
+extern "C" __global__ __launch_bounds__(64) void hbx_k2_cut_chain(
+    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
+    const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ slice_base,
+    const uint32_t* __restrict__ slice_max, const uint32_t* __restrict__ slice_prev,
+    const uint64_t* __restrict__ cut_base, uint64_t* __restrict__ cut_ends,
+    uint32_t* __restrict__ cut_count) {
+  const uint32_t f = blockIdx.x;
+  const uint32_t l = threadIdx.x;
+  const uint64_t N = file_len[f];
+  const uint8_t* fb = arena + file_off[f];
+  const uint64_t sb = slice_base[f];
+  const uint64_t cb = cut_base[f];
+  uint64_t s = 0;
+  uint32_t k = 0;
+  while (s < N) {
+    const uint64_t L = min((uint64_t)kMaxBlock, N - s);  // store.go:116-120
+    uint64_t cut;
+    if (L <= 2ull * kMinBlock) {  // store.go:129-130: no split candidate
+      cut = s + L;
+    } else {
+      // candidates p in [s+MIN, s+L]  <=>  q = p-1 in [qa, qb]
+      const uint64_t qa = s + kMinBlock - 1, qb = s + L - 1;
+      const uint64_t ja = qa >> kSliceShift, jb = qb >> kSliceShift;  // jb - ja >= 16
+      // interior slices (ja, jb): max + last slice holding it
+      uint32_t bv = 0u;
+      int64_t bj = -1;
+      for (uint64_t j = ja + 1 + l; j < jb; j += 64) {
+        const uint32_t v = slice_max[sb + j];
+        if (v >= bv) {
+          bv = v;
+          bj = (int64_t)j;
+        }
+      }
+      const uint32_t MI = wave_max_all(bj >= 0 ? bv : 0u);
+      const uint32_t jrel = wave_max_all((bj >= 0 && bv == MI) ? (uint32_t)(bj - (int64_t)ja) : 0u);
+      const uint64_t jI = ja + jrel;
+
+      uint32_t Mbest = MI;
+      uint64_t qwin = 0;
+      int src = 1;  // 0 = first edge slice, 1 = interior, 2 = last edge slice
+      // last (partial) slice: wins ties
+      if (slice_max[sb + jb] >= Mbest) {
+        uint32_t D;
+        int P;
+        slice_argmax(fb, N, jb, slice_prev[sb + jb], 0, (int)(qb - (jb << kSliceShift)), D, P);
+        if (P >= 0 && D >= Mbest) {
+          Mbest = D;
+          qwin = (jb << kSliceShift) + (uint64_t)P;
+          src = 2;
+        }
+      }
+      // first (partial) slice: must be strictly greater
+      if (slice_max[sb + ja] > Mbest) {
+        uint32_t D;
+        int P;
+        slice_argmax(fb, N, ja, slice_prev[sb + ja], (int)(qa - (ja << kSliceShift)),
+                     (int)kSlice - 1, D, P);
+        if (P >= 0 && D > Mbest) {
+          Mbest = D;
+          qwin = (ja << kSliceShift) + (uint64_t)P;
+          src = 0;
+        }
+      }
+      if (src == 1) {
+        uint32_t D;
+        int P;
+        slice_argmax(fb, N, jI, slice_prev[sb + jI], 0, (int)kSlice - 1, D, P);
+        qwin = (jI << kSliceShift) + (uint64_t)P;
+      }
+      cut = qwin + 1;
+      // defensive: the chain must always advance within [s+MIN, s+L]; a
+      // violation can only come from a bug, never stall the wave on it
+      if (cut < s + kMinBlock || cut > s + L) cut = s + L;
+    }
+    if (l == 0) cut_ends[cb + k] = cut;
+    k++;
+    s = cut;
+  }
+  if (l == 0) cut_count[f] = k;
+}
+
+// -------------------------------------------------------------- MD5 -----
+namespace {
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int s) {
+  return __builtin_rotateleft32(x, (uint32_t)s);
+}
+#define HBX_F(b, c, d) ((((c) ^ (d)) & (b)) ^ (d))
+#define HBX_G(b, c, d) ((((b) ^ (c)) & (d)) ^ (c))
+#define HBX_H(b, c, d) ((b) ^ (c) ^ (d))
+#define HBX_I(b, c, d) ((c) ^ ((b) | ~(d)))
+#define HBX_STEP(FN, a, b, c, d, x, t, s) a = (b) + rotl((a) + (FN(b, c, d)) + (x) + (t), s)
+
+__device__ __forceinline__ void md5_compress(uint32_t (&h)[4], const uint32_t (&m)[16]) {
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
+  HBX_STEP(HBX_F, a, b, c, d, m[0], 0xd76aa478u, 7);
+  HBX_STEP(HBX_F, d, a, b, c, m[1], 0xe8c7b756u, 12);
+  HBX_STEP(HBX_F, c, d, a, b, m[2], 0x242070dbu, 17);
+  HBX_STEP(HBX_F, b, c, d, a, m[3], 0xc1bdceeeu, 22);
+  HBX_STEP(HBX_F, a, b, c, d, m[4], 0xf57c0fafu, 7);
+  HBX_STEP(HBX_F, d, a, b, c, m[5], 0x4787c62au, 12);
+  HBX_STEP(HBX_F, c, d, a, b, m[6], 0xa8304613u, 17);
+  HBX_STEP(HBX_F, b, c, d, a, m[7], 0xfd469501u, 22);
+  HBX_STEP(HBX_F, a, b, c, d, m[8], 0x698098d8u, 7);
+  HBX_STEP(HBX_F, d, a, b, c, m[9], 0x8b44f7afu, 12);
+  HBX_STEP(HBX_F, c, d, a, b, m[10], 0xffff5bb1u, 17);
+  HBX_STEP(HBX_F, b, c, d, a, m[11], 0x895cd7beu, 22);
+  HBX_STEP(HBX_F, a, b, c, d, m[12], 0x6b901122u, 7);
+  HBX_STEP(HBX_F, d, a, b, c, m[13], 0xfd987193u, 12);
+  HBX_STEP(HBX_F, c, d, a, b, m[14], 0xa679438eu, 17);
+  HBX_STEP(HBX_F, b, c, d, a, m[15], 0x49b40821u, 22);
+  HBX_STEP(HBX_G, a, b, c, d, m[1], 0xf61e2562u, 5);
+  HBX_STEP(HBX_G, d, a, b, c, m[6], 0xc040b340u, 9);
+  HBX_STEP(HBX_G, c, d, a, b, m[11], 0x265e5a51u, 14);
+  HBX_STEP(HBX_G, b, c, d, a, m[0], 0xe9b6c7aau, 20);
+  HBX_STEP(HBX_G, a, b, c, d, m[5], 0xd62f105du, 5);
+  HBX_STEP(HBX_G, d, a, b, c, m[10], 0x02441453u, 9);
+  HBX_STEP(HBX_G, c, d, a, b, m[15], 0xd8a1e681u, 14);
+  HBX_STEP(HBX_G, b, c, d, a, m[4], 0xe7d3fbc8u, 20);
+  HBX_STEP(HBX_G, a, b, c, d, m[9], 0x21e1cde6u, 5);
+  HBX_STEP(HBX_G, d, a, b, c, m[14], 0xc33707d6u, 9);
+  HBX_STEP(HBX_G, c, d, a, b, m[3], 0xf4d50d87u, 14);
+  HBX_STEP(HBX_G, b, c, d, a, m[8], 0x455a14edu, 20);
+  HBX_STEP(HBX_G, a, b, c, d, m[13], 0xa9e3e905u, 5);
+  HBX_STEP(HBX_G, d, a, b, c, m[2], 0xfcefa3f8u, 9);
+  HBX_STEP(HBX_G, c, d, a, b, m[7], 0x676f02d9u, 14);
+  HBX_STEP(HBX_G, b, c, d, a, m[12], 0x8d2a4c8au, 20);
+  HBX_STEP(HBX_H, a, b, c, d, m[5], 0xfffa3942u, 4);
+  HBX_STEP(HBX_H, d, a, b, c, m[8], 0x8771f681u, 11);
+  HBX_STEP(HBX_H, c, d, a, b, m[11], 0x6d9d6122u, 16);
+  HBX_STEP(HBX_H, b, c, d, a, m[14], 0xfde5380cu, 23);
+  HBX_STEP(HBX_H, a, b, c, d, m[1], 0xa4beea44u, 4);
+  HBX_STEP(HBX_H, d, a, b, c, m[4], 0x4bdecfa9u, 11);
+  HBX_STEP(HBX_H, c, d, a, b, m[7], 0xf6bb4b60u, 16);
+  HBX_STEP(HBX_H, b, c, d, a, m[10], 0xbebfbc70u, 23);
+  HBX_STEP(HBX_H, a, b, c, d, m[13], 0x289b7ec6u, 4);
+  HBX_STEP(HBX_H, d, a, b, c, m[0], 0xeaa127fau, 11);
+  HBX_STEP(HBX_H, c, d, a, b, m[3], 0xd4ef3085u, 16);
+  HBX_STEP(HBX_H, b, c, d, a, m[6], 0x04881d05u, 23);
+  HBX_STEP(HBX_H, a, b, c, d, m[9], 0xd9d4d039u, 4);
+  HBX_STEP(HBX_H, d, a, b, c, m[12], 0xe6db99e5u, 11);
+  HBX_STEP(HBX_H, c, d, a, b, m[15], 0x1fa27cf8u, 16);
+  HBX_STEP(HBX_H, b, c, d, a, m[2], 0xc4ac5665u, 23);
+  HBX_STEP(HBX_I, a, b, c, d, m[0], 0xf4292244u, 6);
+  HBX_STEP(HBX_I, d, a, b, c, m[7], 0x432aff97u, 10);
+  HBX_STEP(HBX_I, c, d, a, b, m[14], 0xab9423a7u, 15);
+  HBX_STEP(HBX_I, b, c, d, a, m[5], 0xfc93a039u, 21);
+  HBX_STEP(HBX_I, a, b, c, d, m[12], 0x655b59c3u, 6);
+  HBX_STEP(HBX_I, d, a, b, c, m[3], 0x8f0ccc92u, 10);
+  HBX_STEP(HBX_I, c, d, a, b, m[10], 0xffeff47du, 15);
+  HBX_STEP(HBX_I, b, c, d, a, m[1], 0x85845dd1u, 21);
+  HBX_STEP(HBX_I, a, b, c, d, m[8], 0x6fa87e4fu, 6);
+  HBX_STEP(HBX_I, d, a, b, c, m[15], 0xfe2ce6e0u, 10);
+  HBX_STEP(HBX_I, c, d, a, b, m[6], 0xa3014314u, 15);
+  HBX_STEP(HBX_I, b, c, d, a, m[13], 0x4e0811a1u, 21);
+  HBX_STEP(HBX_I, a, b, c, d, m[4], 0xf7537e82u, 6);
+  HBX_STEP(HBX_I, d, a, b, c, m[11], 0xbd3af235u, 10);
+  HBX_STEP(HBX_I, c, d, a, b, m[2], 0x2ad7d2bbu, 15);
+  HBX_STEP(HBX_I, b, c, d, a, m[9], 0xeb86d391u, 21);
+  h[0] += a;
+  h[1] += b;
+  h[2] += c;
+  h[3] += d;
+}
+
+__device__ __forceinline__ void md5_init(uint32_t (&h)[4]) {
+  h[0] = 0x67452301u;
+  h[1] = 0xefcdab89u;
+  h[2] = 0x98badcfeu;
+  h[3] = 0x10325476u;
+}
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+__device__ __forceinline__ uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t sh) {
+  return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+
+// MD5( BE32(0) || BE32(len) || data[0..len) ) for one lane.  `rs` is a
+// wave-uniform descriptor; `voff` the byte offset of the data start in it.
+// Reads outside the descriptor return 0 (never fault).
+__device__ void md5_block_id(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t len,
+                             uint32_t (&h)[4]) {
+  md5_init(h);
+  const uint32_t sh = voff & 3u;
+  const uint32_t va = voff - sh;  // dword-aligned raw base: raw R[r] at va + 4r
+  const uint32_t T = len + 8u;    // message bytes (prefix + data)
+  const uint32_t nfull = T >> 6;
+  uint32_t c0 = 0u, c1 = 0u;  // R[16b-2], R[16b-1] carried from the previous block
+  for (uint32_t b = 0; b < nfull; b++) {
+    uint32_t R[16];  // R[16b .. 16b+15]; never below the chunk start
+    const uint32_t base = va + 64u * b;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      u32x4 t = bload16(rs, base + 16u * i, 0u);
+      R[4 * i + 0] = t.x;
+      R[4 * i + 1] = t.y;
+      R[4 * i + 2] = t.z;
+      R[4 * i + 3] = t.w;
+    }
+    // message word i = data word 16b+i-2 = bytes of R[16b+i-2], R[16b+i-1]
+    uint32_t m[16];
+    m[0] = alignbyte(c1, c0, sh);
+    m[1] = alignbyte(R[0], c1, sh);
+#pragma unroll
+    for (int i = 2; i < 16; i++) m[i] = alignbyte(R[i - 1], R[i - 2], sh);
+    if (b == 0) {
+      m[0] = 0u;
+      m[1] = bswap32(len);
+    }
+    c0 = R[14];
+    c1 = R[15];
+    md5_compress(h, m);
+  }
+  // tail: remaining message bytes + 0x80 + zeros + 64-bit bit length
+  const uint32_t rem = T - 64u * nfull;  // 0..63
+  const uint32_t ntail = (rem + 9u > 64u) ? 2u : 1u;
+  for (uint32_t tb = 0; tb < ntail; tb++) {
+    const uint32_t b = nfull + tb;
+    uint32_t m[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const uint32_t widx = 16u * b + (uint32_t)i;  // message word index
+      uint32_t wv;
+      if (widx == 0u) {
+        wv = 0u;
+      } else if (widx == 1u) {
+        wv = bswap32(len);
+      } else {
+        const uint32_t dpos = 4u * (widx - 2u);  // data byte index of this word
+        if (dpos >= len + 4u) {
+          wv = 0u;
+        } else {
+          uint32_t raw = 0u;
+          if (dpos < len) {
+            const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rs, va + dpos, 0u, 0);
+            const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rs, va + dpos + 4u, 0u, 0);
+            raw = alignbyte(hi, lo, sh);
+          }
+          if (dpos + 4u <= len) {
+            wv = raw;
+          } else {
+            const uint32_t nv = (dpos < len) ? (len - dpos) : 0u;  // valid bytes 0..3
+            if (dpos > len) {
+              wv = 0u;
+            } else {
+              const uint32_t mask = nv ? ((1u << (8u * nv)) - 1u) : 0u;
+              wv = (raw & mask) | (0x80u << (8u * nv));
+            }
+          }
+        }
+      }
+      m[i] = wv;
+    }
+    if (tb + 1 == ntail) {
+      const uint64_t bits = (uint64_t)T * 8ull;
+      m[14] = (uint32_t)bits;
+      m[15] = (uint32_t)(bits >> 32);
+    }
+    md5_compress(h, m);
+  }
+}
+
+}  // namespace
+
+// Lane per chunk.  grid = (ceil(max_cap/64), n_files); block = 64.
+extern "C" __global__ __launch_bounds__(64) void hbx_k3_block_md5(
+    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
+    const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ cut_base,
+    const uint64_t* __restrict__ cut_ends, const uint32_t* __restrict__ cut_count,
+    uint32_t* __restrict__ ids) {
+  const uint32_t f = blockIdx.y;
+  const uint32_t cnt = cut_count[f];
+  const uint32_t k0 = blockIdx.x * 64u;
+  if (k0 >= cnt) return;
+  const uint64_t cb = cut_base[f];
+  const uint64_t N = file_len[f];
+  const uint32_t k = k0 + threadIdx.x;
+  // wave-uniform descriptor over [start of chunk k0, file end), <= 64 x 8 MiB
+  const uint64_t base_off = k0 ? cut_ends[cb + k0 - 1] : 0ull;
+  const uint64_t base_al = base_off & ~3ull;
+  // file end + slack, 16-B granular (see HBX_ARENA_SLACK)
+  const uint64_t span = min((N - base_al + 64ull + 15ull) & ~15ull, (uint64_t)0xFFFFFF00ull);
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(arena + file_off[f] + base_al, (uint32_t)span);
+  if (k >= cnt) return;
+  const uint64_t start = k ? cut_ends[cb + k - 1] : 0ull;
+  const uint64_t end = cut_ends[cb + k];
+  uint32_t h[4];
+  md5_block_id(rs, (uint32_t)(start - base_al), (uint32_t)(end - start), h);
+  uint4* o = reinterpret_cast<uint4*>(ids) + (cb + k);
+  *o = make_uint4(h[0], h[1], h[2], h[3]);
+}
+
+// Lane per file: ContentBlockID (store.go:187-196).
+extern "C" __global__ __launch_bounds__(64) void hbx_k4_content_id(
+    uint32_t n_files, const uint64_t* __restrict__ cut_base, const uint32_t* __restrict__ cut_count,
+    const uint32_t* __restrict__ ids, uint32_t* __restrict__ content_ids,
+    int32_t* __restrict__ content_type) {
+  const uint32_t f = blockIdx.x * 64u + threadIdx.x;
+  if (f >= n_files) return;
+  const uint32_t k = cut_count[f];
+  const uint4* id = reinterpret_cast<const uint4*>(ids) + cut_base[f];
+  uint4* co = reinterpret_cast<uint4*>(content_ids) + f;
+  if (k == 0u) {
+    *co = make_uint4(0u, 0u, 0u, 0u);
+    content_type[f] = 0;
+    return;
+  }
+  if (k == 1u) {
+    *co = id[0];
+    content_type[f] = 2;  // ContentTypeFileData
+    return;
+  }
+  // Message words (little-endian u32 view of the hashed byte stream):
+  //   BE32(k) | id_1..id_k | BE32(8+32k) | "fchn" | BE32(k) | (id_i | 0^16)*k
+  const uint32_t nw = 12u * k + 4u;
+  const uint32_t T = 4u * nw;
+  const uint32_t nblk = (T + 9u + 63u) / 64u;
+  uint32_t h[4];
+  md5_init(h);
+  for (uint32_t b = 0; b < nblk; b++) {
+    uint32_t m[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const uint32_t j = 16u * b + (uint32_t)i;
+      uint32_t v;
+      if (j == 0u) {
+        v = bswap32(k);
+      } else if (j <= 4u * k) {
+        const uint4 q = id[(j - 1u) >> 2];
+        const uint32_t r = (j - 1u) & 3u;
+        v = r == 0 ? q.x : r == 1 ? q.y : r == 2 ? q.z : q.w;
+      } else if (j == 4u * k + 1u) {
+        v = bswap32(8u + 32u * k);
+      } else if (j == 4u * k + 2u) {
+        v = bswap32(0x6663686Eu);
+      } else if (j == 4u * k + 3u) {
+        v = bswap32(k);
+      } else if (j < nw) {
+        const uint32_t t = j - (4u * k + 4u);
+        const uint32_t r = t & 7u;
+        if (r < 4u) {
+          const uint4 q = id[t >> 3];
+          v = r == 0 ? q.x : r == 1 ? q.y : r == 2 ? q.z : q.w;
+        } else {
+          v = 0u;
+        }
+      } else if (j == nw) {
+        v = 0x80u;
+      } else {
+        v = 0u;
+      }
+      m[i] = v;
+    }
+    if (b + 1 == nblk) {
+      const uint64_t bits = (uint64_t)T * 8ull;
+      m[14] = (uint32_t)bits;
+      m[15] = (uint32_t)(bits >> 32);
+    }
+    md5_compress(h, m);
+  }
+  *co = make_uint4(h[0], h[1], h[2], h[3]);
+  content_type[f] = 3;  // ContentTypeFileChain
+}
+
+// Plain MD5 over a device buffer (used by hbx_block_id for arbitrary blocks
+// with links: the host lays out BE32(n)|links|BE32(len) in front).
+extern "C" __global__ __launch_bounds__(64) void hbx_k5_md5_raw(const uint8_t* __restrict__ msg,
+                                                                 uint32_t n, uint32_t* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  uint32_t h[4];
+  md5_init(h);
+  const uint32_t nblk = (n + 9u + 63u) / 64u;
+  for (uint32_t b = 0; b < nblk; b++) {
+    uint32_t m[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      uint32_t v = 0u;
+#pragma unroll
+      for (int y = 0; y < 4; y++) {
+        const uint32_t p = 64u * b + 4u * (uint32_t)i + (uint32_t)y;
+        const uint32_t by = p < n ? msg[p] : (p == n ? 0x80u : 0u);
+        v |= by << (8 * y);
+      }
+      m[i] = v;
+    }
+    if (b + 1 == nblk) {
+      const uint64_t bits = (uint64_t)n * 8ull;
+      m[14] = (uint32_t)bits;
+      m[15] = (uint32_t)(bits >> 32);
+    }
+    md5_compress(h, m);
+  }
+  out[0] = h[0];
+  out[1] = h[1];
+  out[2] = h[2];
+  out[3] = h[3];
+}

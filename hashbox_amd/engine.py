@@ -1,0 +1,215 @@
+"""Host-side mirror of Hashback's chunking + block-ID interface on libhbxgpu.
+
+Reference interface (fredli74/hashbox):
+  * ``BackupSession.storeFile(path, entry)`` — hashback/store.go:84-199: splits
+    a file by the rollsum rule and stores each chunk with
+    ``Client.StoreData`` (pkg/core/client.go:556-560), whose
+    ``NewHashboxBlock -> HashData`` (pkg/core/block.go:39-43, 96-111) yields
+    the 16-byte BlockID; then sets ``entry.ContentType`` /
+    ``entry.ContentBlockID`` (store.go:187-196).
+  * ``HashboxBlock.HashData`` for blocks with links (chain/directory blocks).
+
+:class:`Engine` exposes the same results — chunk end offsets, BlockIDs,
+content type and content BlockID — computed on an MI355X.  Every call goes
+through the C-ABI (include/hbxgpu.h); there is no CPU fallback, and errors
+raise :class:`HbxError` (the reference panics via core.Abort,
+pkg/core/utils.go:22-37).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Union
+
+import numpy as np
+
+from . import _lib
+
+MIN_BLOCK_SIZE = 64 * 1024  # hashback/hashback.go:38
+MAX_BLOCK_SIZE = 8 * 1024 * 1024  # hashback/hashback.go:37
+CONTENT_TYPE_FILE_DATA = 2  # store.go:193
+CONTENT_TYPE_FILE_CHAIN = 3  # store.go:189
+ARENA_ALIGN = 16
+ARENA_SLACK = 64
+
+BytesLike = Union[bytes, bytearray, memoryview, np.ndarray]
+
+
+class HbxError(RuntimeError):
+    """A non-zero status from libhbxgpu."""
+
+
+def max_chunks(n: int) -> int:
+    return n // MIN_BLOCK_SIZE + 1
+
+
+@dataclass
+class FileChunks:
+    """What storeFile records for one file."""
+    cut_ends: np.ndarray  # uint64 [k]: chunk i = [cut_ends[i-1], cut_ends[i])
+    ids: np.ndarray  # uint8 [k, 16]: BlockID per chunk (core.Byte128)
+    content_type: int  # 2 FileData, 3 FileChain (0 for an empty file)
+    content_id: bytes  # entry.ContentBlockID
+
+    @property
+    def n_chunks(self) -> int:
+        return int(self.cut_ends.shape[0])
+
+    def chunk_bounds(self):
+        starts = np.concatenate([[0], self.cut_ends[:-1]]).astype(np.uint64)
+        return starts, self.cut_ends
+
+
+def _u8(data: BytesLike) -> np.ndarray:
+    if isinstance(data, np.ndarray):
+        return np.ascontiguousarray(data.reshape(-1).view(np.uint8))
+    return np.frombuffer(memoryview(data).cast("B"), dtype=np.uint8)
+
+
+def _p(a: np.ndarray) -> int:
+    return a.ctypes.data if a.size else 0
+
+
+class Engine:
+    """One MI355X (one HIP stream) running the chunk + block-ID path."""
+
+    def __init__(self, device: int = 0, tile_iters: Optional[int] = None):
+        self._L = _lib.load()
+        self._ctx = ctypes.c_void_p()
+        rc = self._L.hbx_ctx_create(int(device), ctypes.byref(self._ctx))
+        if rc != 0:
+            raise HbxError(f"hbx_ctx_create(device={device}) failed: {_lib.ERRORS.get(rc, rc)}")
+        self.device = device
+        self._pending = None
+        if tile_iters is not None:
+            self._check(self._L.hbx_set_tile_iters(self._ctx, int(tile_iters)), "set_tile_iters")
+
+    # ----------------------------------------------------------- plumbing --
+    def close(self):
+        if self._ctx:
+            self._L.hbx_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            msg = self._L.hbx_last_error(self._ctx)
+            raise HbxError(f"{what}: {_lib.ERRORS.get(rc, rc)}: "
+                           f"{msg.decode() if msg else ''}")
+
+    @staticmethod
+    def _alloc_out(lens: Sequence[int]):
+        caps = np.array([max_chunks(int(n)) for n in lens], np.uint64)
+        base = np.zeros(len(lens), np.uint64)
+        if len(lens):
+            base[1:] = np.cumsum(caps)[:-1]
+        tot = int(caps.sum()) if len(lens) else 0
+        cuts = np.zeros(max(tot, 1), np.uint64)
+        ids = np.zeros((max(tot, 1), 16), np.uint8)
+        sums = (_lib.FileSummary * max(len(lens), 1))()
+        return caps, base, cuts, ids, sums
+
+    @staticmethod
+    def _unpack(lens, caps, base, cuts, ids, sums) -> List[FileChunks]:
+        out = []
+        for f in range(len(lens)):
+            s = sums[f]
+            k = int(s.n_chunks)
+            b = int(base[f])
+            out.append(FileChunks(cuts[b:b + k].copy(), ids[b:b + k].copy(), int(s.content_type),
+                                  bytes(s.content_id) if k else b""))
+        return out
+
+    # -------------------------------------------------------------- API ----
+    def chunk_hash(self, data: BytesLike) -> FileChunks:
+        """storeFile over one in-memory file (store.go:111-196)."""
+        return self.chunk_hash_batch([data])[0]
+
+    def chunk_hash_batch(self, files: Sequence[BytesLike]) -> List[FileChunks]:
+        arrs = [_u8(f) for f in files]
+        lens = np.array([a.size for a in arrs], np.uint64)
+        ptrs = np.array([_p(a) for a in arrs], np.uint64)
+        caps, base, cuts, ids, sums = self._alloc_out(lens)
+        self._check(self._L.hbx_chunk_hash_batch(self._ctx, len(arrs), _p(ptrs), _p(lens),
+                                                 _p(cuts), _p(ids), _p(base), _p(caps), sums),
+                    "hbx_chunk_hash_batch")
+        return self._unpack(lens, caps, base, cuts, ids, sums)
+
+    def chunk_hash_device(self, d_arena: int, offs: Sequence[int], lens: Sequence[int]
+                          ) -> List[FileChunks]:
+        """Files resident in device memory (pointer ``d_arena``, e.g. a torch
+        uint8 tensor's ``data_ptr()``).  Offsets 16-B aligned; each file must be
+        followed by >= 64 readable bytes."""
+        self.submit_device(d_arena, offs, lens)
+        return self.wait()
+
+    def submit_device(self, d_arena: int, offs: Sequence[int], lens: Sequence[int]):
+        if self._pending is not None:
+            raise HbxError("a batch is already pending on this engine")
+        offs = np.ascontiguousarray(offs, np.uint64)
+        lens = np.ascontiguousarray(lens, np.uint64)
+        caps, base, cuts, ids, sums = self._alloc_out(lens)
+        self._check(self._L.hbx_submit_device(self._ctx, ctypes.c_void_p(int(d_arena)), len(lens),
+                                              _p(offs), _p(lens), _p(cuts), _p(ids), _p(base),
+                                              _p(caps), sums), "hbx_submit_device")
+        self._pending = (offs, lens, caps, base, cuts, ids, sums)
+
+    def wait(self) -> List[FileChunks]:
+        if self._pending is None:
+            return []
+        offs, lens, caps, base, cuts, ids, sums = self._pending
+        self._pending = None
+        self._check(self._L.hbx_wait(self._ctx), "hbx_wait")
+        return self._unpack(lens, caps, base, cuts, ids, sums)
+
+    def block_id(self, data: BytesLike, links: Sequence[bytes] = ()) -> bytes:
+        """HashboxBlock.HashData (pkg/core/block.go:96-111) on the device."""
+        a = _u8(data)
+        ln = np.frombuffer(b"".join(bytes(x) for x in links), np.uint8) if links else \
+            np.zeros(0, np.uint8)
+        out = np.zeros(16, np.uint8)
+        self._check(self._L.hbx_block_id(self._ctx, _p(ln), len(links), _p(a), a.size, _p(out)),
+                    "hbx_block_id")
+        return out.tobytes()
+
+    def store_file(self, path: Union[str, os.PathLike]) -> FileChunks:
+        """storeFile(path) for a regular file on disk (store.go:84-199)."""
+        with open(path, "rb") as fh:
+            data = np.fromfile(fh, dtype=np.uint8)
+        return self.chunk_hash(data)
+
+    def stage_times(self) -> np.ndarray:
+        """Device ms of the last batch: K1, K2, K3, K4, total."""
+        ms = (ctypes.c_float * 5)()
+        self._check(self._L.hbx_stage_times(self._ctx, ms), "hbx_stage_times")
+        return np.array(list(ms), np.float64)
+
+
+def device_count() -> int:
+    L = _lib.load()
+    n = ctypes.c_int(0)
+    L.hbx_device_count(ctypes.byref(n))
+    return int(n.value)
+
+
+def pack_arena_layout(lens: Sequence[int], align: int = 256):
+    """Offsets for packing files into one device arena (16-B aligned, with
+    slack after the last file).  Returns (offsets, total_bytes_to_allocate)."""
+    offs = np.zeros(len(lens), np.uint64)
+    pos = 0
+    for i, n in enumerate(lens):
+        offs[i] = pos
+        pos += (int(n) + align - 1) // align * align
+    return offs, pos + max(ARENA_SLACK, align)

@@ -1,0 +1,136 @@
+/*
+ * hbxgpu.h — C-ABI of the MI355X rollsum-split + block-ID engine
+ * (libhbxgpu.so).  Drop-in for Hashback's per-file chunker and block hashing.
+ *
+ * Reference interfaces replaced (fredli74/hashbox; the reference has no FFI
+ * seam for this path, so the seam is cut at storeFile — SURVEY.md §8b):
+ *
+ *   hbx_chunk_hash        hashback/store.go:111-185  storeFile's split loop
+ *                         (store.go:129-166) + the per-chunk
+ *                         Client.StoreData -> NewHashboxBlock -> HashData
+ *                         (pkg/core/client.go:556-560, block.go:39-43, 96-111)
+ *   hbx_chunk_hash_batch  the same, for many files at once (tree walk order
+ *                         store.go:201-397 is the caller's business)
+ *   hbx_chunk_hash_device the same, files already resident in device memory
+ *   hbx_submit_device /   asynchronous form (one batch in flight per context)
+ *   hbx_wait
+ *   hbx_block_id          HashboxBlock.HashData for an arbitrary block with
+ *                         links (pkg/core/block.go:96-111), e.g. the
+ *                         FileChainBlock of store.go:187-188
+ *   hbx_file_summary      entry.ContentType / entry.ContentBlockID written by
+ *                         store.go:187-196
+ *
+ * Conventions
+ *   - Every function returns an int status: 0 = OK, negative = error
+ *     (HBX_ERR_*).  hbx_last_error(ctx) describes the last failure.  The
+ *     library never aborts or exits (the Go wrapper turns a non-zero status
+ *     into core.Abort, pkg/core/utils.go:22-37).
+ *   - The caller owns every buffer passed in.  The library never frees caller
+ *     memory and never keeps a caller pointer after the call returns, except
+ *     between hbx_submit_device and hbx_wait, where the output arrays must
+ *     stay valid (use hbx_alloc_pinned memory from cgo: cgo forbids C from
+ *     retaining Go pointers).
+ *   - One context = one GPU + one HIP stream.  Calls on one context are
+ *     serialised by an internal lock; use one context per GPU (or per
+ *     goroutine) to run in parallel.
+ *   - Block IDs are 16 raw MD5 bytes, exactly Go's core.Byte128 (core.go:26).
+ *   - cut_ends[i] is the file offset where chunk i ends (exclusive); chunk i
+ *     starts at cut_ends[i-1] (0 for i = 0).
+ *   - Capacity: every chunk except the last is >= 64 KiB, so a file of len
+ *     bytes has at most hbx_max_chunks(len) = len/65536 + 1 chunks.
+ */
+#ifndef HBXGPU_H
+#define HBXGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HBX_OK 0
+#define HBX_ERR_ARG (-1)
+#define HBX_ERR_HIP (-2)
+#define HBX_ERR_CAPACITY (-3)
+#define HBX_ERR_IO (-4)
+#define HBX_ERR_NODEV (-5)
+#define HBX_ERR_STATE (-6)
+
+#define HBX_MIN_BLOCK_SIZE 65536u   /* hashback/hashback.go:38 */
+#define HBX_MAX_BLOCK_SIZE 8388608u /* hashback/hashback.go:37 */
+#define HBX_CONTENT_FILE_DATA 2     /* ContentTypeFileData,  store.go:193 */
+#define HBX_CONTENT_FILE_CHAIN 3    /* ContentTypeFileChain, store.go:189 */
+/* Device arenas must be readable this many bytes past the end of every file
+ * (loads are 16-byte granular and bounds-checked, never fault, but the last
+ * granule of a file may straddle its end). */
+#define HBX_ARENA_SLACK 64u
+#define HBX_ARENA_ALIGN 16u
+
+typedef struct hbx_ctx hbx_ctx;
+
+/* Per-file result beside the chunk list (store.go:187-196). */
+typedef struct {
+  uint8_t content_id[16]; /* entry.ContentBlockID */
+  int32_t content_type;   /* 2 = FileData (1 chunk), 3 = FileChain, 0 = empty */
+  uint32_t n_chunks;
+} hbx_file_summary;
+
+int hbx_version(void);
+int hbx_device_count(int *n);
+uint64_t hbx_max_chunks(uint64_t len);
+
+int hbx_ctx_create(int device, hbx_ctx **out);
+void hbx_ctx_destroy(hbx_ctx *ctx);
+const char *hbx_last_error(const hbx_ctx *ctx);
+
+/* One file in host memory (the storeFile drop-in).  ids must hold 16*cap
+ * bytes; *n_chunks receives the chunk count. */
+int hbx_chunk_hash(hbx_ctx *ctx, const uint8_t *data, uint64_t len, uint64_t *cut_ends,
+                   uint8_t *ids, uint64_t cap, uint64_t *n_chunks);
+
+/* Many files in host memory.  File f's chunks go to cut_ends[out_base[f] ..]
+ * and ids[16*out_base[f] ..], at most caps[f] of them; summaries[f] gets the
+ * count and the file content id. */
+int hbx_chunk_hash_batch(hbx_ctx *ctx, uint64_t n_files, const uint8_t *const *datas,
+                         const uint64_t *lens, uint64_t *cut_ends, uint8_t *ids,
+                         const uint64_t *out_base, const uint64_t *caps,
+                         hbx_file_summary *summaries);
+
+/* Files already in device memory: file f is d_arena[file_offs[f] ..
+ * +file_lens[f]).  file_offs must be multiples of HBX_ARENA_ALIGN and each
+ * file must be followed by HBX_ARENA_SLACK readable bytes. */
+int hbx_chunk_hash_device(hbx_ctx *ctx, const void *d_arena, uint64_t n_files,
+                          const uint64_t *file_offs, const uint64_t *file_lens,
+                          uint64_t *cut_ends, uint8_t *ids, const uint64_t *out_base,
+                          const uint64_t *caps, hbx_file_summary *summaries);
+
+/* Asynchronous device form: enqueue on the context's stream, return at once;
+ * hbx_wait completes the batch and fills the output arrays given here. */
+int hbx_submit_device(hbx_ctx *ctx, const void *d_arena, uint64_t n_files,
+                      const uint64_t *file_offs, const uint64_t *file_lens, uint64_t *cut_ends,
+                      uint8_t *ids, const uint64_t *out_base, const uint64_t *caps,
+                      hbx_file_summary *summaries);
+int hbx_wait(hbx_ctx *ctx);
+
+/* MD5(BE32(n_links) || links || BE32(len) || data) on the device. */
+int hbx_block_id(hbx_ctx *ctx, const uint8_t *links, uint32_t n_links, const uint8_t *data,
+                 uint64_t len, uint8_t out[16]);
+
+/* Device arena helpers (allocations include HBX_ARENA_SLACK). */
+int hbx_arena_alloc(hbx_ctx *ctx, uint64_t bytes, void **d_ptr);
+int hbx_arena_free(hbx_ctx *ctx, void *d_ptr);
+int hbx_memcpy_h2d(hbx_ctx *ctx, void *d_dst, const void *h_src, uint64_t bytes);
+int hbx_alloc_pinned(uint64_t bytes, void **out);
+int hbx_free_pinned(void *p);
+
+/* Device time (ms) of the last completed batch per stage:
+ * [0] K1 window-digest scan, [1] K2 cut chain, [2] K3 block MD5,
+ * [3] K4 content id, [4] whole batch on the stream. */
+int hbx_stage_times(hbx_ctx *ctx, float ms[5]);
+/* Tile length of K1 in 64 KiB iterations (default 32 = 2 MiB tiles). */
+int hbx_set_tile_iters(hbx_ctx *ctx, uint32_t iters);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HBXGPU_H */

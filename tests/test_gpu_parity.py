@@ -1,0 +1,110 @@
+"""GPU parity: libhbxgpu (HIP, gfx950) vs the CPU oracle, bit-exact.
+
+Chunk boundaries, block IDs, content type and content ID must equal the
+oracle's restatement of hashback/store.go:111-196 + pkg/core/block.go:96-111.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+MIN = 65536
+MAXB = 8 * 1024 * 1024
+
+
+def _check(got, ref):
+    assert np.array_equal(got.cut_ends, ref.cut_ends), (got.cut_ends[:8], ref.cut_ends[:8])
+    assert np.array_equal(got.ids, ref.ids), "block ids differ"
+    assert got.content_type == ref.content_type
+    assert got.content_id == ref.content_id
+
+
+EDGE_SIZES = [0, 1, 5, 55, 56, 57, 63, 64, 65, 119, 120, 121, 4095, 4096, MIN - 1, MIN, MIN + 1,
+              2 * MIN - 1, 2 * MIN, 2 * MIN + 1, 2 * MIN + 2, 3 * MIN + 17, MAXB - 1, MAXB,
+              MAXB + 1, MAXB + 2 * MIN + 1, 2 * MAXB + 12345]
+
+
+@pytest.mark.parametrize("n", EDGE_SIZES)
+def test_edge_sizes_random(engine, oracle, n):
+    x = oracle.random_bytes(n, 100 + n % 997)
+    _check(engine.chunk_hash(x), oracle.store_file(x, fast=True))
+
+
+def test_hello_known_answer(engine):
+    r = engine.chunk_hash(b"hello")
+    assert r.n_chunks == 1 and r.cut_ends[0] == 5
+    assert r.ids[0].tobytes().hex() == "9e06002f060f42397d3862c8777fb39b"
+    assert r.content_type == 2
+
+
+def test_literal_oracle_small(engine, oracle):
+    # the literal re-rolled loop (store.go:141-165) on a few sizes
+    for n, seed in [(131073, 1), (200000, 2), (300001, 3), (1 << 20, 4)]:
+        x = oracle.random_bytes(n, seed)
+        _check(engine.chunk_hash(x), oracle.store_file(x, fast=False))
+
+
+@pytest.mark.parametrize("val", [0, 0x5A, 255])
+def test_constant_bytes_tie_rule(engine, oracle, val):
+    # all digests equal -> ">=" keeps the LAST position -> 8 MiB chunks
+    x = np.full(3 * MAXB + 777, val, np.uint8)
+    r = engine.chunk_hash(x)
+    assert list(r.cut_ends[:3]) == [MAXB, 2 * MAXB, 3 * MAXB]
+    _check(r, oracle.store_file(x, fast=True))
+
+
+def test_periodic_ties(engine, oracle):
+    x = np.tile(oracle.random_bytes(70001, 5), 300)
+    _check(engine.chunk_hash(x), oracle.store_file(x, fast=True))
+    x = np.tile(oracle.random_bytes(4096, 6), 3000)  # period < window
+    _check(engine.chunk_hash(x), oracle.store_file(x, fast=True))
+
+
+def test_zipf_duplicates(engine, oracle):
+    x = oracle.zipf_corpus(48 * 1024 * 1024, 7)
+    _check(engine.chunk_hash(x), oracle.store_file(x, fast=True))
+
+
+def test_batch_mixed(engine, oracle):
+    g = np.random.default_rng(9)
+    sizes = [int(s) for s in np.exp(g.uniform(np.log(1), np.log(20e6), 60))] + [0, 1, 2 * MIN + 1]
+    files = [oracle.random_bytes(n, 1000 + i) for i, n in enumerate(sizes)]
+    got = engine.chunk_hash_batch(files)
+    for f, r in zip(files, got):
+        _check(r, oracle.store_file(f, fast=True))
+
+
+@pytest.mark.parametrize("tile_iters", [1, 3, 32])
+def test_tile_sizes(oracle, tile_iters):
+    from hashbox_amd import Engine
+    with Engine(0, tile_iters=tile_iters) as e:
+        x = oracle.random_bytes(37 * MIN + 999, 77)
+        _check(e.chunk_hash(x), oracle.store_file(x, fast=True))
+
+
+def test_device_resident(engine, oracle):
+    import torch
+    from hashbox_amd import pack_arena_layout
+    sizes = [5 * MAXB + 3, 129 * 1024, 7, 3 * MAXB]
+    files = [oracle.random_bytes(n, 50 + i) for i, n in enumerate(sizes)]
+    offs, total = pack_arena_layout(sizes)
+    host = np.zeros(total, np.uint8)
+    for o, f in zip(offs, files):
+        host[int(o):int(o) + f.size] = f
+    dev = torch.from_numpy(host).to("cuda:0")
+    torch.cuda.synchronize()
+    got = engine.chunk_hash_device(dev.data_ptr(), offs, sizes)
+    for f, r in zip(files, got):
+        _check(r, oracle.store_file(f, fast=True))
+    # async submit/wait gives the same
+    engine.submit_device(dev.data_ptr(), offs, sizes)
+    got2 = engine.wait()
+    for a, b in zip(got, got2):
+        _check(a, b)
+
+
+def test_block_id_with_links(engine, oracle):
+    links = [bytes(range(i, i + 16)) for i in range(5)]
+    data = b"fchn" + bytes(100)
+    assert engine.block_id(data, links) == oracle.py_block_id(data, links)
+    assert engine.block_id(b"") == oracle.py_block_id(b"")
