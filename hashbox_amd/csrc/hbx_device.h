@@ -29,6 +29,10 @@ constexpr uint32_t kMaxBlock = 8388608u;  // hashback/hashback.go:37
 constexpr uint32_t kSlice = 4096u;        // positions per slice summary
 constexpr uint32_t kSliceShift = 12u;
 
+// 64-bit integer min (HIP's min() has no unsigned long overload and would
+// silently go through double).
+__device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+
 // ---------------------------------------------------------------- DPP ----
 // gfx9 DPP controls.
 constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0x118;
@@ -97,6 +101,18 @@ __device__ __forceinline__ uint32_t as_u32(u16x2 x) { return __builtin_bit_cast(
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t nbytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)nbytes,
                                            0x00020000);
+}
+// Same, with the inputs forced wave-uniform (readfirstlane): the compiler
+// cannot always prove a pointer loaded from memory is uniform and would wrap
+// every buffer op in a waterfall loop (guide T20).  Callers guarantee the
+// values really are uniform.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc_u(const void* base, uint32_t nbytes) {
+  const uint64_t p = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)p);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(p >> 32));
+  const uint32_t n = (uint32_t)__builtin_amdgcn_readfirstlane((int)nbytes);
+  const void* pu = reinterpret_cast<const void*>(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(pu), (short)0, (int)n, 0x00020000);
 }
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ u32x4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {

@@ -102,11 +102,11 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan(
   const uint32_t e_l = w * kSlice + l * 64u;  // iteration-relative first position of this lane
 
   const uint64_t rem = N - q0;
-  const uint32_t n_it = (uint32_t)min((uint64_t)tile_iters, (rem + kMinBlock - 1) / kMinBlock);
+  const uint32_t n_it = (uint32_t)umin64(tile_iters, (rem + kMinBlock - 1) / kMinBlock);
   // rounded up to 16 B: every dwordx4 is entirely in or out of range (the
   // arena guarantees HBX_ARENA_SLACK readable bytes after each file)
-  const uint32_t nbytes = (uint32_t)((min(rem, (uint64_t)n_it * kMinBlock) + 15ull) & ~15ull);
-  const __amdgpu_buffer_rsrc_t rs = make_rsrc(fb + q0, nbytes);
+  const uint32_t nbytes = (uint32_t)((umin64(rem, (uint64_t)n_it * kMinBlock) + 15ull) & ~15ull);
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc_u(fb + q0, nbytes);
 
   // ---- priming: "out" bytes of iteration 0 = the MIN bytes before q0, and
   //      the rollsum state at q0-1 = digest state of exactly that window.
@@ -120,7 +120,7 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan(
     S1c = 0u;
     s2c = 0x8000u;
   } else {
-    const __amdgpu_buffer_rsrc_t rh = make_rsrc(fb + q0 - kMinBlock, kMinBlock);
+    const __amdgpu_buffer_rsrc_t rh = make_rsrc_u(fb + q0 - kMinBlock, kMinBlock);
     load_run64(rh, e_l, 0u, out);
     pa = run_aggregates(out);
     const uint32_t iA = wave_incl_sum(pa.af);
@@ -197,11 +197,11 @@ __device__ void slice_argmax(const uint8_t* fb, uint64_t N, uint64_t j, uint32_t
   const uint64_t sq = j << kSliceShift;
   const uint64_t avail = N - sq;
   const __amdgpu_buffer_rsrc_t ri =
-      make_rsrc(fb + sq, (uint32_t)((min(avail, (uint64_t)kSlice) + 15ull) & ~15ull));
+      make_rsrc_u(fb + sq, (uint32_t)((umin64(avail, kSlice) + 15ull) & ~15ull));
   uint32_t in[16], out[16];
   load_run64(ri, l * 64u, 0u, in);
   if (sq >= kMinBlock) {
-    const __amdgpu_buffer_rsrc_t ro = make_rsrc(fb + sq - kMinBlock, kSlice);
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc_u(fb + sq - kMinBlock, kSlice);
     load_run64(ro, l * 64u, 0u, out);
   } else {
 #pragma unroll
@@ -243,7 +243,7 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k2_cut_chain(
   uint64_t s = 0;
   uint32_t k = 0;
   while (s < N) {
-    const uint64_t L = min((uint64_t)kMaxBlock, N - s);  // store.go:116-120
+    const uint64_t L = umin64(kMaxBlock, N - s);  // store.go:116-120
     uint64_t cut;
     if (L <= 2ull * kMinBlock) {  // store.go:129-130: no split candidate
       cut = s + L;
@@ -415,17 +415,28 @@ __device__ void md5_block_id(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t 
   const uint32_t va = voff - sh;  // dword-aligned raw base: raw R[r] at va + 4r
   const uint32_t T = len + 8u;    // message bytes (prefix + data)
   const uint32_t nfull = T >> 6;
-  uint32_t c0 = 0u, c1 = 0u;  // R[16b-2], R[16b-1] carried from the previous block
-  for (uint32_t b = 0; b < nfull; b++) {
-    uint32_t R[16];  // R[16b .. 16b+15]; never below the chunk start
-    const uint32_t base = va + 64u * b;
+  // Full blocks.  Block b needs raw dwords R[16b-2 .. 16b+15]: 16 loaded with
+  // it (4 x dwordx4 at va+64b, never below the chunk start) plus 2 carried.
+  // Loads run 4 blocks ahead through a 4-deep register ring.  The loop is
+  // wave-uniform (bound = the wave's longest chunk, lanes past their own end
+  // compute and discard) so the compiler keeps exact vmcnt counting and never
+  // drains the ring at a divergent join.
+  const uint32_t nmax = wave_max_all(nfull);
+  uint32_t c0 = 0u, c1 = 0u;  // R[16b-2], R[16b-1]
+  u32x4 ring[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) ring[r][i] = bload16(rs, va + 64u * r + 16u * i, 0u);
+  }
+  auto block = [&](int r, uint32_t b, bool refill) {
+    uint32_t R[16];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      u32x4 t = bload16(rs, base + 16u * i, 0u);
-      R[4 * i + 0] = t.x;
-      R[4 * i + 1] = t.y;
-      R[4 * i + 2] = t.z;
-      R[4 * i + 3] = t.w;
+      R[4 * i + 0] = ring[r][i].x;
+      R[4 * i + 1] = ring[r][i].y;
+      R[4 * i + 2] = ring[r][i].z;
+      R[4 * i + 3] = ring[r][i].w;
     }
     // message word i = data word 16b+i-2 = bytes of R[16b+i-2], R[16b+i-1]
     uint32_t m[16];
@@ -433,13 +444,33 @@ __device__ void md5_block_id(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t 
     m[1] = alignbyte(R[0], c1, sh);
 #pragma unroll
     for (int i = 2; i < 16; i++) m[i] = alignbyte(R[i - 1], R[i - 2], sh);
-    if (b == 0) {
+    if (b == 0) {  // wave-uniform
       m[0] = 0u;
       m[1] = bswap32(len);
     }
     c0 = R[14];
     c1 = R[15];
-    md5_compress(h, m);
+    // refill only after the slot's registers are consumed: the load then
+    // reuses them and the ring needs no copies at the loop back-edge
+    if (refill) {
+#pragma unroll
+      for (int i = 0; i < 4; i++) ring[r][i] = bload16(rs, va + 64u * (b + 4u) + 16u * i, 0u);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the refill ahead of this block's compression
+    uint32_t t[4] = {h[0], h[1], h[2], h[3]};
+    md5_compress(t, m);
+    const bool live = b < nfull;
+#pragma unroll
+    for (int i = 0; i < 4; i++) h[i] = live ? t[i] : h[i];
+  };
+  uint32_t b = 0;
+  for (; b + 4u <= nmax; b += 4u) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) block(r, b + (uint32_t)r, true);
+  }
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    if (b + (uint32_t)r < nmax) block(r, b + (uint32_t)r, false);
   }
   // tail: remaining message bytes + 0x80 + zeros + 64-bit bit length
   const uint32_t rem = T - 64u * nfull;  // 0..63
@@ -509,15 +540,19 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k3_block_md5(
   const uint64_t base_off = k0 ? cut_ends[cb + k0 - 1] : 0ull;
   const uint64_t base_al = base_off & ~3ull;
   // file end + slack, 16-B granular (see HBX_ARENA_SLACK)
-  const uint64_t span = min((N - base_al + 64ull + 15ull) & ~15ull, (uint64_t)0xFFFFFF00ull);
-  const __amdgpu_buffer_rsrc_t rs = make_rsrc(arena + file_off[f] + base_al, (uint32_t)span);
-  if (k >= cnt) return;
-  const uint64_t start = k ? cut_ends[cb + k - 1] : 0ull;
-  const uint64_t end = cut_ends[cb + k];
+  const uint64_t span = umin64((N - base_al + 64ull + 15ull) & ~15ull, 0xFFFFFF00ull);
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc_u(arena + file_off[f] + base_al, (uint32_t)span);
+  // every lane stays alive (md5_block_id uses wave-wide reductions); lanes
+  // past the last chunk hash an empty message and store nothing
+  const bool active = k < cnt;
+  const uint64_t start = active ? (k ? cut_ends[cb + k - 1] : 0ull) : base_al;
+  const uint64_t end = active ? cut_ends[cb + k] : base_al;
   uint32_t h[4];
   md5_block_id(rs, (uint32_t)(start - base_al), (uint32_t)(end - start), h);
-  uint4* o = reinterpret_cast<uint4*>(ids) + (cb + k);
-  *o = make_uint4(h[0], h[1], h[2], h[3]);
+  if (active) {
+    uint4* o = reinterpret_cast<uint4*>(ids) + (cb + k);
+    *o = make_uint4(h[0], h[1], h[2], h[3]);
+  }
 }
 
 // Lane per file: ContentBlockID (store.go:187-196).
