@@ -108,3 +108,30 @@ def test_block_id_with_links(engine, oracle):
     data = b"fchn" + bytes(100)
     assert engine.block_id(data, links) == oracle.py_block_id(data, links)
     assert engine.block_id(b"") == oracle.py_block_id(b"")
+
+
+def test_golden_fixtures_on_device(engine):
+    """The committed fixtures (tests/golden/chunking.json) through the HIP path."""
+    import json
+    import os
+    from tests.golden.make_golden import make_input
+    with open(os.path.join(os.path.dirname(__file__), "golden", "chunking.json")) as f:
+        cases = json.load(f)["cases"]
+    xs = [make_input(c) for c in cases]
+    got = engine.chunk_hash_batch(xs)
+    for c, g in zip(cases, got):
+        assert [int(v) for v in g.cut_ends] == c["cut_ends"], (c["kind"], c["n"])
+        assert [bytes(i).hex() for i in g.ids] == c["ids"]
+        assert g.content_type == c["content_type"] and g.content_id.hex() == c["content_id"]
+
+
+def test_kat_block_ids_on_device(engine):
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "kat.json")) as f:
+        kat = json.load(f)
+    datas = [bytes.fromhex(r["data_hex"]) for r in kat["block_id"]]
+    got = engine.chunk_hash_batch(datas)  # each <= 2*MIN: one chunk = the block id
+    for r, g in zip(kat["block_id"], got):
+        assert g.ids[0].tobytes().hex() == r["id"] if g.n_chunks else r["data_hex"] == ""
+        assert engine.block_id(bytes.fromhex(r["data_hex"])).hex() == r["id"]
