@@ -1,11 +1,12 @@
 // hbx_engine.hip — host engine + C-ABI (include/hbxgpu.h) for libhbxgpu.so.
 //
 // One context = one GPU + one HIP stream + a grown-on-demand workspace.  A
-// batch of files runs as four launches on the stream:
-//   K1 window-digest scan   grid = tiles (2 MiB of one file each), 1024 thr
-//   K2 cut chain            grid = files, 1 wave each (sequential store.go loop)
-//   K3 block MD5            grid = (chunk groups of 64, files), lane per chunk
-//   K4 content id           grid = files/64, lane per file
+// batch of files runs as five launches on the stream:
+//   K1  window-digest scan  grid = tiles (2 MiB of one file each), 1024 thr
+//   K2  cut chain           grid = files, 1 wave each (sequential store.go loop)
+//   K2c plan                1 workgroup: chunks bucketed by length, longest first
+//   K3  block MD5           fixed grid of 1-wave workgroups, lane per chunk
+//   K4  content id          grid = files/64, lane per file
 // then one D2H of counts/cuts/ids/content ids into pinned memory.
 // Reference seams: hashback/store.go:111-199 (storeFile), pkg/core/client.go:
 // 556-560 + block.go:96-111 (StoreData -> HashData).
@@ -13,6 +14,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -99,6 +101,7 @@ struct hbx_ctx {
   std::mutex mu;
   std::string err;
   uint32_t tile_iters = 32;
+  uint32_t md5_waves = 2048;  // persistent K3 grid: 2 waves per SIMD
   float stage_ms[5] = {0, 0, 0, 0, 0};
 
   // host-side plan of the current batch
@@ -106,7 +109,7 @@ struct hbx_ctx {
   std::vector<uint2> h_tiles;
 
   DevBuf d_meta;  // file_off | file_len | slice_base | cut_base | tiles
-  DevBuf d_smax, d_sprev, d_cuts, d_count, d_ids, d_cid, d_ctype;
+  DevBuf d_smax, d_sprev, d_cuts, d_count, d_ids, d_cid, d_ctype, d_work, d_ctl;
   DevBuf d_stage;  // host-input arena
   DevBuf d_msg;    // hbx_block_id message
   PinBuf h_meta, h_res;
@@ -166,7 +169,7 @@ int enqueue_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* o
   c->h_slice_base.resize(n);
   c->h_cut_base.resize(n);
   c->h_tiles.clear();
-  uint64_t slices = 0, caps = 0, max_cap = 0;
+  uint64_t slices = 0, caps = 0;
   const uint64_t tile_bytes = (uint64_t)c->tile_iters * HBX_MIN_BLOCK_SIZE;
   for (uint64_t f = 0; f < n; f++) {
     if (offs[f] % HBX_ARENA_ALIGN) return c->fail(HBX_ERR_ARG, "file offset not 16-byte aligned");
@@ -175,7 +178,6 @@ int enqueue_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* o
     c->h_cut_base[f] = caps;
     const uint64_t cap = max_chunks(N);
     caps += cap;
-    max_cap = std::max(max_cap, cap);
     if (N > 2ull * HBX_MIN_BLOCK_SIZE) {  // only files with split candidates scan
       slices += (N + kSlice - 1) / kSlice;
       const uint64_t nt = (N + tile_bytes - 1) / tile_bytes;
@@ -200,6 +202,8 @@ int enqueue_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* o
   HBX_TRY(c, c->d_cuts.ensure(caps * 8));
   HBX_TRY(c, c->d_count.ensure(n * 4));
   HBX_TRY(c, c->d_ids.ensure(caps * 16));
+  HBX_TRY(c, c->d_work.ensure(caps * 8));
+  HBX_TRY(c, c->d_ctl.ensure(64));
   HBX_TRY(c, c->d_cid.ensure(n * 16));
   HBX_TRY(c, c->d_ctype.ensure(n * 4));
   const ResLayout rl = res_layout(n, caps);
@@ -227,17 +231,14 @@ int enqueue_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* o
                      c->d_cuts.as<uint64_t>(), c->d_count.as<uint32_t>());
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(c->ev[2], s));
-  const uint64_t gx = (max_cap + 63) / 64;
-  if (gx > 0x7FFFFFFFull || n > 65535) {
-    // grid.y is limited; split over files in chunks of 65535
-  }
-  for (uint64_t f0 = 0; f0 < n; f0 += 65535) {
-    const uint32_t nf = (uint32_t)std::min<uint64_t>(65535, n - f0);
-    hipLaunchKernelGGL(hbx_k3_block_md5, dim3((uint32_t)gx, nf), dim3(64), 0, s, arena,
-                       d_off + f0, d_len + f0, d_cb + f0, c->d_cuts.as<uint64_t>(),
-                       c->d_count.as<uint32_t>() + f0, c->d_ids.as<uint32_t>());
-    HBX_TRY(c, hipGetLastError());
-  }
+  hipLaunchKernelGGL(hbx_k2c_plan, dim3(1), dim3(kPlanThreads), 0, s, (uint32_t)n, d_cb,
+                     c->d_cuts.as<uint64_t>(), c->d_count.as<uint32_t>(), c->d_work.as<uint2>(),
+                     c->d_ctl.as<uint32_t>());
+  HBX_TRY(c, hipGetLastError());
+  hipLaunchKernelGGL(hbx_k3_block_md5, dim3(c->md5_waves), dim3(64), 0, s, arena, d_off, d_cb,
+                     c->d_cuts.as<uint64_t>(), c->d_work.as<uint2>(), c->d_ctl.as<uint32_t>(),
+                     c->d_ids.as<uint32_t>());
+  HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(c->ev[3], s));
   hipLaunchKernelGGL(hbx_k4_content_id, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, s,
                      (uint32_t)n, d_cb, c->d_count.as<uint32_t>(), c->d_ids.as<uint32_t>(),
@@ -325,6 +326,8 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (device < 0 || device >= nd) return HBX_ERR_ARG;
   hbx_ctx* c = new hbx_ctx();
   c->device = device;
+  if (const char* v = std::getenv("HBX_MD5_WAVES")) c->md5_waves = (uint32_t)std::max(1, std::atoi(v));
+  if (const char* v = std::getenv("HBX_TILE_ITERS")) c->tile_iters = (uint32_t)std::min(1024, std::max(1, std::atoi(v)));
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
@@ -345,7 +348,7 @@ void hbx_ctx_destroy(hbx_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->d_meta, &c->d_smax, &c->d_sprev, &c->d_cuts, &c->d_count, &c->d_ids,
-                    &c->d_cid, &c->d_ctype, &c->d_stage, &c->d_msg})
+                    &c->d_cid, &c->d_ctype, &c->d_work, &c->d_ctl, &c->d_stage, &c->d_msg})
     b->release();
   c->h_meta.release();
   c->h_res.release();

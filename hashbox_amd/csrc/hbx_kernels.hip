@@ -405,16 +405,32 @@ __device__ __forceinline__ uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t
   return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
 
-// MD5( BE32(0) || BE32(len) || data[0..len) ) for one lane.  `rs` is a
-// wave-uniform descriptor; `voff` the byte offset of the data start in it.
-// Reads outside the descriptor return 0 (never fault).
-__device__ void md5_block_id(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t len,
-                             uint32_t (&h)[4]) {
+// One message word of MD5(BE32(0) || BE32(len) || data) given the two raw
+// dwords around its data bytes (lo at data byte dpos-sh, hi after it).
+__device__ __forceinline__ uint32_t msg_word(uint32_t widx, uint32_t lo, uint32_t hi, uint32_t sh,
+                                             uint32_t len) {
+  if (widx == 0u) return 0u;
+  if (widx == 1u) return bswap32(len);
+  const uint32_t dpos = 4u * (widx - 2u);  // data byte index of this word
+  const uint32_t raw = alignbyte(hi, lo, sh);
+  if (dpos + 4u <= len) return raw;
+  if (dpos > len) return 0u;
+  const uint32_t nv = len - dpos;  // 0..3 valid bytes, then the 0x80 pad byte
+  const uint32_t mask = nv ? ((1u << (8u * nv)) - 1u) : 0u;
+  return (raw & mask) | (0x80u << (8u * nv));
+}
+
+// MD5( BE32(0) || BE32(len) || data[0..len) ) for one lane ("lane mode":
+// 64 chunks per wave, one per lane).  `c` is the lane's chunk start.  Reads
+// stay within the chunk + 64 bytes (HBX_ARENA_SLACK): every dword that holds
+// chunk bytes, and never more than 63 bytes past the chunk end.
+__device__ void md5_block_id(const uint8_t* c, uint32_t len, uint32_t (&h)[4]) {
   md5_init(h);
-  const uint32_t sh = voff & 3u;
-  const uint32_t va = voff - sh;  // dword-aligned raw base: raw R[r] at va + 4r
-  const uint32_t T = len + 8u;    // message bytes (prefix + data)
+  const uint32_t sh = (uint32_t)reinterpret_cast<uintptr_t>(c) & 3u;
+  const uint32_t* va = reinterpret_cast<const uint32_t*>(c - sh);  // raw R[r] = va[r]
+  const uint32_t T = len + 8u;  // message bytes (prefix + data)
   const uint32_t nfull = T >> 6;
+  const uint32_t nlast = nfull ? nfull - 1u : 0u;  // clamp prefetches to this block
   // Full blocks.  Block b needs raw dwords R[16b-2 .. 16b+15]: 16 loaded with
   // it (4 x dwordx4 at va+64b, never below the chunk start) plus 2 carried.
   // Loads run 4 blocks ahead through a 4-deep register ring.  The loop is
@@ -426,8 +442,9 @@ __device__ void md5_block_id(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t 
   u32x4 ring[4][4];
 #pragma unroll
   for (int r = 0; r < 4; r++) {
+    const u32x4* src = reinterpret_cast<const u32x4*>(va + 16u * min((uint32_t)r, nlast));
 #pragma unroll
-    for (int i = 0; i < 4; i++) ring[r][i] = bload16(rs, va + 64u * r + 16u * i, 0u);
+    for (int i = 0; i < 4; i++) ring[r][i] = __builtin_nontemporal_load(src + i);
   }
   auto block = [&](int r, uint32_t b, bool refill) {
     uint32_t R[16];
@@ -453,8 +470,9 @@ __device__ void md5_block_id(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t 
     // refill only after the slot's registers are consumed: the load then
     // reuses them and the ring needs no copies at the loop back-edge
     if (refill) {
+      const u32x4* src = reinterpret_cast<const u32x4*>(va + 16u * min(b + 4u, nlast));
 #pragma unroll
-      for (int i = 0; i < 4; i++) ring[r][i] = bload16(rs, va + 64u * (b + 4u) + 16u * i, 0u);
+      for (int i = 0; i < 4; i++) ring[r][i] = __builtin_nontemporal_load(src + i);
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the refill ahead of this block's compression
     uint32_t t[4] = {h[0], h[1], h[2], h[3]};
@@ -476,41 +494,18 @@ __device__ void md5_block_id(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t 
   const uint32_t rem = T - 64u * nfull;  // 0..63
   const uint32_t ntail = (rem + 9u > 64u) ? 2u : 1u;
   for (uint32_t tb = 0; tb < ntail; tb++) {
-    const uint32_t b = nfull + tb;
+    const uint32_t bb = nfull + tb;
     uint32_t m[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) {
-      const uint32_t widx = 16u * b + (uint32_t)i;  // message word index
-      uint32_t wv;
-      if (widx == 0u) {
-        wv = 0u;
-      } else if (widx == 1u) {
-        wv = bswap32(len);
-      } else {
-        const uint32_t dpos = 4u * (widx - 2u);  // data byte index of this word
-        if (dpos >= len + 4u) {
-          wv = 0u;
-        } else {
-          uint32_t raw = 0u;
-          if (dpos < len) {
-            const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rs, va + dpos, 0u, 0);
-            const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rs, va + dpos + 4u, 0u, 0);
-            raw = alignbyte(hi, lo, sh);
-          }
-          if (dpos + 4u <= len) {
-            wv = raw;
-          } else {
-            const uint32_t nv = (dpos < len) ? (len - dpos) : 0u;  // valid bytes 0..3
-            if (dpos > len) {
-              wv = 0u;
-            } else {
-              const uint32_t mask = nv ? ((1u << (8u * nv)) - 1u) : 0u;
-              wv = (raw & mask) | (0x80u << (8u * nv));
-            }
-          }
-        }
+      const uint32_t widx = 16u * bb + (uint32_t)i;
+      uint32_t lo = 0u, hi = 0u;
+      const uint32_t dpos = 4u * (widx - 2u);
+      if (widx >= 2u && dpos < len) {
+        lo = va[dpos >> 2];
+        hi = va[(dpos >> 2) + 1u];
       }
-      m[i] = wv;
+      m[i] = msg_word(widx, lo, hi, sh, len);
     }
     if (tb + 1 == ntail) {
       const uint64_t bits = (uint64_t)T * 8ull;
@@ -523,35 +518,88 @@ __device__ void md5_block_id(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t 
 
 }  // namespace
 
-// Lane per chunk.  grid = (ceil(max_cap/64), n_files); block = 64.
+// ----------------------------------------------------------- K2c plan --
+// Orders all chunks of the batch by length bucket (floor(log2 len)),
+// longest first, so each K3 wave gets 64 chunks of similar length (a wave
+// runs as long as its longest lane) and the longest chunks — the serial MD5
+// critical path — start first.
+constexpr int kPlanThreads = 1024;
+
+extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
+    uint32_t n_files, const uint64_t* __restrict__ cut_base, const uint64_t* __restrict__ cut_ends,
+    const uint32_t* __restrict__ cut_count, uint2* __restrict__ work, uint32_t* __restrict__ ctl) {
+  __shared__ uint32_t hist[32], cur[32];
+  const uint32_t tid = threadIdx.x;
+  if (tid < 32) hist[tid] = 0u;
+  __syncthreads();
+  for (uint32_t f = tid; f < n_files; f += kPlanThreads) {
+    const uint64_t cb = cut_base[f];
+    const uint32_t k = cut_count[f];
+    uint64_t prev = 0;
+    for (uint32_t i = 0; i < k; i++) {
+      const uint64_t e = cut_ends[cb + i];
+      atomicAdd(&hist[31 - __builtin_clz((uint32_t)(e - prev))], 1u);
+      prev = e;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t pos = 0;
+    for (int bk = 31; bk >= 0; bk--) {
+      cur[bk] = pos;
+      pos += hist[bk];
+    }
+    ctl[0] = 0u;
+    ctl[1] = pos;  // all chunks
+  }
+  __syncthreads();
+  for (uint32_t f = tid; f < n_files; f += kPlanThreads) {
+    const uint64_t cb = cut_base[f];
+    const uint32_t k = cut_count[f];
+    uint64_t prev = 0;
+    for (uint32_t i = 0; i < k; i++) {
+      const uint64_t e = cut_ends[cb + i];
+      const uint32_t p = atomicAdd(&cur[31 - __builtin_clz((uint32_t)(e - prev))], 1u);
+      work[p] = make_uint2(f, i);
+      prev = e;
+    }
+  }
+}
+
+// ---------------------------------------------------------- K3 block MD5 --
+namespace {
+
+}  // namespace
+
+// Block-ID kernel (lane mode: lane = chunk, 64 similar-length chunks per
+// wave in the planner's longest-first order).  grid = a fixed number of
+// one-wave workgroups; only every (grid / groups)-th workgroup works, so the
+// few busy waves of a batch with few chunks land on different CUs (adjacent
+// workgroups share a CU, and two serial MD5 chains on one SIMD slow both).
 extern "C" __global__ __launch_bounds__(64) void hbx_k3_block_md5(
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
-    const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ cut_base,
-    const uint64_t* __restrict__ cut_ends, const uint32_t* __restrict__ cut_count,
-    uint32_t* __restrict__ ids) {
-  const uint32_t f = blockIdx.y;
-  const uint32_t cnt = cut_count[f];
-  const uint32_t k0 = blockIdx.x * 64u;
-  if (k0 >= cnt) return;
-  const uint64_t cb = cut_base[f];
-  const uint64_t N = file_len[f];
-  const uint32_t k = k0 + threadIdx.x;
-  // wave-uniform descriptor over [start of chunk k0, file end), <= 64 x 8 MiB
-  const uint64_t base_off = k0 ? cut_ends[cb + k0 - 1] : 0ull;
-  const uint64_t base_al = base_off & ~3ull;
-  // file end + slack, 16-B granular (see HBX_ARENA_SLACK)
-  const uint64_t span = umin64((N - base_al + 64ull + 15ull) & ~15ull, 0xFFFFFF00ull);
-  const __amdgpu_buffer_rsrc_t rs = make_rsrc_u(arena + file_off[f] + base_al, (uint32_t)span);
-  // every lane stays alive (md5_block_id uses wave-wide reductions); lanes
-  // past the last chunk hash an empty message and store nothing
-  const bool active = k < cnt;
-  const uint64_t start = active ? (k ? cut_ends[cb + k - 1] : 0ull) : base_al;
-  const uint64_t end = active ? cut_ends[cb + k] : base_al;
-  uint32_t h[4];
-  md5_block_id(rs, (uint32_t)(start - base_al), (uint32_t)(end - start), h);
-  if (active) {
-    uint4* o = reinterpret_cast<uint4*>(ids) + (cb + k);
-    *o = make_uint4(h[0], h[1], h[2], h[3]);
+    const uint64_t* __restrict__ cut_base, const uint64_t* __restrict__ cut_ends,
+    const uint2* __restrict__ work, const uint32_t* __restrict__ ctl, uint32_t* __restrict__ ids) {
+  const uint32_t lane = threadIdx.x;
+  const uint32_t n_total = ctl[1];
+  const uint32_t groups = (n_total + 63u) / 64u;
+  if (groups == 0u) return;
+  const uint32_t stride = max(1u, gridDim.x / groups);
+  if (blockIdx.x % stride != 0u) return;
+  const uint32_t nworkers = gridDim.x / stride;
+  for (uint32_t g = blockIdx.x / stride; g < groups; g += nworkers) {
+    const uint32_t k = 64u * g + lane;
+    const bool active = k < n_total;
+    const uint2 wk = work[active ? k : 64u * g];
+    const uint64_t cb = cut_base[wk.x];
+    const uint64_t start = wk.y ? cut_ends[cb + wk.y - 1] : 0ull;
+    const uint64_t end = cut_ends[cb + wk.y];
+    // every lane stays alive for the wave-wide loop bound; idle lanes hash
+    // an empty message and store nothing
+    const uint32_t len = active ? (uint32_t)(end - start) : 0u;
+    uint32_t h[4];
+    md5_block_id(arena + file_off[wk.x] + start, len, h);
+    if (active) reinterpret_cast<uint4*>(ids)[cb + wk.y] = make_uint4(h[0], h[1], h[2], h[3]);
   }
 }
 
