@@ -127,6 +127,8 @@ def main():
         el = float(t.item())
     stage /= max(a.steps, 1)
     n_chunks = sum(r.n_chunks for r in res)
+    longest = max(int(np.max(np.diff(np.concatenate([[0], r.cut_ends]).astype(np.int64))))
+                  for r in res if r.n_chunks)
 
     check = None
     if a.check and rank == 0:
@@ -167,6 +169,7 @@ def main():
         "config": {"workload": f"{nf} x {a.file_mib} MiB random buffers per GPU, rollsum split + "
                                "MD5 block IDs + file content ids, device-resident (configs[1])",
                    "files_per_gpu": nf, "file_bytes": fbytes, "chunks_per_gpu": n_chunks,
+                   "longest_chunk_bytes": longest,
                    "parallelism": f"file-sharded x{world} (independent HIP streams, no data-path "
                                   "collective)"},
         "roofline": {"kernel": names[dom], "bound": "hbm", "achieved": round(achieved, 2),

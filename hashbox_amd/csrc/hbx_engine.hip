@@ -5,7 +5,7 @@
 //   K1  window-digest scan  grid = tiles (2 MiB of one file each), 1024 thr
 //   K2  cut chain           grid = files, 1 wave each (sequential store.go loop)
 //   K2c plan                1 workgroup: chunks bucketed by length, longest first
-//   K3  block MD5           fixed grid of 1-wave workgroups, lane per chunk
+//   K3  block MD5           one 512-thread workgroup per CU, lane per chunk
 //   K4  content id          grid = files/64, lane per file
 // then one D2H of counts/cuts/ids/content ids into pinned memory.
 // Reference seams: hashback/store.go:111-199 (storeFile), pkg/core/client.go:
@@ -101,7 +101,7 @@ struct hbx_ctx {
   std::mutex mu;
   std::string err;
   uint32_t tile_iters = 32;
-  uint32_t md5_waves = 2048;  // persistent K3 grid: 2 waves per SIMD
+  uint32_t md5_wgs = 256;  // K3 grid: one 512-thread workgroup per CU (set from the device)
   float stage_ms[5] = {0, 0, 0, 0, 0};
 
   // host-side plan of the current batch
@@ -235,7 +235,7 @@ int enqueue_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* o
                      c->d_cuts.as<uint64_t>(), c->d_count.as<uint32_t>(), c->d_work.as<uint2>(),
                      c->d_ctl.as<uint32_t>());
   HBX_TRY(c, hipGetLastError());
-  hipLaunchKernelGGL(hbx_k3_block_md5, dim3(c->md5_waves), dim3(64), 0, s, arena, d_off, d_cb,
+  hipLaunchKernelGGL(hbx_k3_block_md5, dim3(c->md5_wgs), dim3(kK3Threads), 0, s, arena, d_off, d_cb,
                      c->d_cuts.as<uint64_t>(), c->d_work.as<uint2>(), c->d_ctl.as<uint32_t>(),
                      c->d_ids.as<uint32_t>());
   HBX_TRY(c, hipGetLastError());
@@ -326,7 +326,10 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (device < 0 || device >= nd) return HBX_ERR_ARG;
   hbx_ctx* c = new hbx_ctx();
   c->device = device;
-  if (const char* v = std::getenv("HBX_MD5_WAVES")) c->md5_waves = (uint32_t)std::max(1, std::atoi(v));
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    c->md5_wgs = (uint32_t)prop.multiProcessorCount;
+  if (const char* v = std::getenv("HBX_MD5_WGS")) c->md5_wgs = (uint32_t)std::max(1, std::atoi(v));
   if (const char* v = std::getenv("HBX_TILE_ITERS")) c->tile_iters = (uint32_t)std::min(1024, std::max(1, std::atoi(v)));
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {

@@ -572,22 +572,23 @@ namespace {
 }  // namespace
 
 // Block-ID kernel (lane mode: lane = chunk, 64 similar-length chunks per
-// wave in the planner's longest-first order).  grid = a fixed number of
-// one-wave workgroups; only every (grid / groups)-th workgroup works, so the
-// few busy waves of a batch with few chunks land on different CUs (adjacent
-// workgroups share a CU, and two serial MD5 chains on one SIMD slow both).
-extern "C" __global__ __launch_bounds__(64) void hbx_k3_block_md5(
+// wave in the planner's longest-first order).  grid = one 512-thread
+// workgroup per CU; group g runs on wave (g / grid) % 8 of workgroup
+// g % grid, so the first 4 x grid groups (the longest chunks) each get a SIMD
+// of their own: the MD5 chain is serial and a second chain on the same SIMD
+// would slow both.
+constexpr int kK3Threads = 512;
+
+extern "C" __global__ __launch_bounds__(kK3Threads) void hbx_k3_block_md5(
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
     const uint64_t* __restrict__ cut_base, const uint64_t* __restrict__ cut_ends,
     const uint2* __restrict__ work, const uint32_t* __restrict__ ctl, uint32_t* __restrict__ ids) {
-  const uint32_t lane = threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t n_total = ctl[1];
   const uint32_t groups = (n_total + 63u) / 64u;
-  if (groups == 0u) return;
-  const uint32_t stride = max(1u, gridDim.x / groups);
-  if (blockIdx.x % stride != 0u) return;
-  const uint32_t nworkers = gridDim.x / stride;
-  for (uint32_t g = blockIdx.x / stride; g < groups; g += nworkers) {
+  const uint32_t nwaves = gridDim.x * (kK3Threads / 64);
+  for (uint32_t g = wave * gridDim.x + blockIdx.x; g < groups; g += nwaves) {
     const uint32_t k = 64u * g + lane;
     const bool active = k < n_total;
     const uint2 wk = work[active ? k : 64u * g];
