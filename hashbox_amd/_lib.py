@@ -20,7 +20,7 @@ EXPORTS = [
     "hbx_version", "hbx_device_count", "hbx_max_chunks", "hbx_ctx_create", "hbx_ctx_destroy",
     "hbx_last_error", "hbx_chunk_hash", "hbx_chunk_hash_batch", "hbx_chunk_hash_device",
     "hbx_submit_device", "hbx_wait", "hbx_block_id", "hbx_arena_alloc", "hbx_arena_free",
-    "hbx_memcpy_h2d", "hbx_alloc_pinned", "hbx_free_pinned", "hbx_stage_times",
+    "hbx_memcpy_h2d", "hbx_memcpy_h2d_async", "hbx_alloc_pinned", "hbx_free_pinned", "hbx_stage_times",
     "hbx_set_tile_iters",
 ]
 
@@ -70,6 +70,7 @@ def load() -> ctypes.CDLL:
     L.hbx_arena_alloc.argtypes = [P, U64, ctypes.POINTER(P)]
     L.hbx_arena_free.argtypes = [P, P]
     L.hbx_memcpy_h2d.argtypes = [P, P, P, U64]
+    L.hbx_memcpy_h2d_async.argtypes = [P, P, P, U64]
     L.hbx_alloc_pinned.argtypes = [U64, ctypes.POINTER(P)]
     L.hbx_free_pinned.argtypes = [P]
     L.hbx_stage_times.argtypes = [P, ctypes.POINTER(ctypes.c_float)]

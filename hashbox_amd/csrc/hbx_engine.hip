@@ -515,6 +515,14 @@ int hbx_memcpy_h2d(hbx_ctx* c, void* d, const void* h, uint64_t n) {
   return HBX_OK;
 }
 
+int hbx_memcpy_h2d_async(hbx_ctx* c, void* d, const void* h, uint64_t n) {
+  if (!c || (n && (!d || !h))) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  HBX_TRY(c, hipSetDevice(c->device));
+  HBX_TRY(c, hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, c->stream));
+  return HBX_OK;
+}
+
 int hbx_alloc_pinned(uint64_t bytes, void** out) {
   if (!out) return HBX_ERR_ARG;
   return hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) == hipSuccess ? HBX_OK

@@ -184,6 +184,12 @@ class Engine:
                     "hbx_block_id")
         return out.tobytes()
 
+    def memcpy_h2d_async(self, d_dst: int, h_src: int, nbytes: int):
+        """Enqueue an H2D copy on this engine's stream (pinned source)."""
+        self._check(self._L.hbx_memcpy_h2d_async(self._ctx, ctypes.c_void_p(int(d_dst)),
+                                                 ctypes.c_void_p(int(h_src)), int(nbytes)),
+                    "hbx_memcpy_h2d_async")
+
     def store_file(self, path: Union[str, os.PathLike]) -> FileChunks:
         """storeFile(path) for a regular file on disk (store.go:84-199)."""
         with open(path, "rb") as fh:

@@ -120,6 +120,12 @@ int hbx_block_id(hbx_ctx *ctx, const uint8_t *links, uint32_t n_links, const uin
 int hbx_arena_alloc(hbx_ctx *ctx, uint64_t bytes, void **d_ptr);
 int hbx_arena_free(hbx_ctx *ctx, void *d_ptr);
 int hbx_memcpy_h2d(hbx_ctx *ctx, void *d_dst, const void *h_src, uint64_t bytes);
+/* Enqueue an H2D copy on the context's stream and return at once: a
+ * following hbx_submit_device on the same context runs after it.  h_src
+ * should be hbx_alloc_pinned memory (pageable memory makes the copy
+ * synchronous).  Use two contexts to overlap the next batch's copy with the
+ * current batch's kernels. */
+int hbx_memcpy_h2d_async(hbx_ctx *ctx, void *d_dst, const void *h_src, uint64_t bytes);
 int hbx_alloc_pinned(uint64_t bytes, void **out);
 int hbx_free_pinned(void *p);
 
