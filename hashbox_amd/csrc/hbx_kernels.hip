@@ -575,8 +575,9 @@ namespace {
 // wave in the planner's longest-first order).  grid = one 512-thread
 // workgroup per CU; group g runs on wave (g / grid) % 8 of workgroup
 // g % grid, so the first 4 x grid groups (the longest chunks) each get a SIMD
-// of their own: the MD5 chain is serial and a second chain on the same SIMD
-// would slow both.
+// of their own.  The MD5 chain is bound by its 4 dependent VALU per step;
+// lane mode runs 64 such chains in one instruction stream at that bound
+// (DESIGN.md "K3"; tools/experiments/md5_wave_mode.hip for what did not pay).
 constexpr int kK3Threads = 512;
 
 extern "C" __global__ __launch_bounds__(kK3Threads) void hbx_k3_block_md5(

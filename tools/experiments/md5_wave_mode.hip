@@ -1,92 +1,23 @@
-// EXPERIMENT (not built): "wave mode" block MD5 — one chunk per wave, the 64
-// lanes precompute W_i = M[g(i)] + T_i for the next block into LDS so the
-// serial chain needs 4 VALU per step instead of 5.  Measured on MI355X
-// (round 1): 85 ms for a ~8 MiB chunk vs 73 ms in lane mode, and 1.7x slower
-// than lane mode on the 64 x 128 MiB batch (many single-chain waves share
-// SIMDs).  Kept for reference; see DESIGN.md "K3".
-// Depends on hbx_kernels.hip helpers (HBX_F.., rotl, msg_word, md5_init).
-// The step words are wave-uniform (LDS broadcast), so the compiler would move
-// the whole chain onto the scalar unit (3 SALU per F + readfirstlane
-// round-trips).  An empty asm with "v" operands makes them opaque VGPR values
-// and keeps the chain on the VALU at 4 instructions per step.
+// EXPERIMENT (not built): "wave mode" block MD5 — one chunk per wave.
+// v1 (W from LDS each group) and v2 (below: W for the next block read one
+// block early into a second register set, chain = 4 VALU/step, ~315 instrs
+// per 64-B block against ~373 in lane mode) both measured 633-637 ns per
+// block on exact 8 MiB chains — the same as lane mode — and v2 ran the
+// 64 x 128 MiB batch in 136 ms against 88 ms in lane mode.  Conclusion: the
+// MD5 chain is bound by its 4 dependent VALU per step (~6 cycles each at
+// 2.4 GHz), not by issue; lane mode already packs 64 chains into one
+// instruction stream at that bound.  See DESIGN.md "K3".
+// Depends on hbx_kernels.hip helpers (HBX_F.., rotl, msg_word, md5_init,
+// make_rsrc_u, u32x4).
+// ------------------------------------------------------ K3 wave mode ----
+// One chunk per wave.  The 64 lanes build the step words of a future block in
+// parallel (lane i: W_i = M[g(i)] + T_i) into an LDS slot; the next block's
+// 64 words are read into a second register set one block ahead; the serial
+// chain then costs 4 VALU per step (bitop3, add3, alignbit, add) with no
+// memory wait, against ~5.8 in lane mode.  Used for the longest chunks (the
+// batch's critical path), at most 2 such waves per SIMD.
 #define HBX_VREG4(w) asm("" : "+v"(w))
 #define HBX_STEPW(FN, a, b, c, d, w, s) a = (b) + rotl((a) + (FN(b, c, d)) + (w), s)
-
-// MD5 compression with the per-step words already added to the step
-// constants (W_i = M[g(i)] + T_i): 4 VALU per step on the serial chain.
-__device__ __forceinline__ void md5_compress_w(uint32_t (&h)[4], const uint32_t* __restrict__ Wl) {
-  const u32x4* W4 = reinterpret_cast<const u32x4*>(Wl);
-  uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
-  u32x4 w;
-  w = W4[0];
-  HBX_VREG4(w);
-  HBX_STEPW(HBX_F, a, b, c, d, w.x, 7); HBX_STEPW(HBX_F, d, a, b, c, w.y, 12);
-  HBX_STEPW(HBX_F, c, d, a, b, w.z, 17); HBX_STEPW(HBX_F, b, c, d, a, w.w, 22);
-  w = W4[1];
-  HBX_VREG4(w);
-  HBX_STEPW(HBX_F, a, b, c, d, w.x, 7); HBX_STEPW(HBX_F, d, a, b, c, w.y, 12);
-  HBX_STEPW(HBX_F, c, d, a, b, w.z, 17); HBX_STEPW(HBX_F, b, c, d, a, w.w, 22);
-  w = W4[2];
-  HBX_VREG4(w);
-  HBX_STEPW(HBX_F, a, b, c, d, w.x, 7); HBX_STEPW(HBX_F, d, a, b, c, w.y, 12);
-  HBX_STEPW(HBX_F, c, d, a, b, w.z, 17); HBX_STEPW(HBX_F, b, c, d, a, w.w, 22);
-  w = W4[3];
-  HBX_VREG4(w);
-  HBX_STEPW(HBX_F, a, b, c, d, w.x, 7); HBX_STEPW(HBX_F, d, a, b, c, w.y, 12);
-  HBX_STEPW(HBX_F, c, d, a, b, w.z, 17); HBX_STEPW(HBX_F, b, c, d, a, w.w, 22);
-  w = W4[4];
-  HBX_VREG4(w);
-  HBX_STEPW(HBX_G, a, b, c, d, w.x, 5); HBX_STEPW(HBX_G, d, a, b, c, w.y, 9);
-  HBX_STEPW(HBX_G, c, d, a, b, w.z, 14); HBX_STEPW(HBX_G, b, c, d, a, w.w, 20);
-  w = W4[5];
-  HBX_VREG4(w);
-  HBX_STEPW(HBX_G, a, b, c, d, w.x, 5); HBX_STEPW(HBX_G, d, a, b, c, w.y, 9);
-  HBX_STEPW(HBX_G, c, d, a, b, w.z, 14); HBX_STEPW(HBX_G, b, c, d, a, w.w, 20);
-  w = W4[6];
-  HBX_VREG4(w);
-  HBX_STEPW(HBX_G, a, b, c, d, w.x, 5); HBX_STEPW(HBX_G, d, a, b, c, w.y, 9);
-  HBX_STEPW(HBX_G, c, d, a, b, w.z, 14); HBX_STEPW(HBX_G, b, c, d, a, w.w, 20);
-  w = W4[7];
-  HBX_VREG4(w);
-  HBX_STEPW(HBX_G, a, b, c, d, w.x, 5); HBX_STEPW(HBX_G, d, a, b, c, w.y, 9);
-  HBX_STEPW(HBX_G, c, d, a, b, w.z, 14); HBX_STEPW(HBX_G, b, c, d, a, w.w, 20);
-  w = W4[8];
-  HBX_VREG4(w);
-  HBX_STEPW(HBX_H, a, b, c, d, w.x, 4); HBX_STEPW(HBX_H, d, a, b, c, w.y, 11);
-  HBX_STEPW(HBX_H, c, d, a, b, w.z, 16); HBX_STEPW(HBX_H, b, c, d, a, w.w, 23);
-  w = W4[9];
-  HBX_VREG4(w);
-  HBX_STEPW(HBX_H, a, b, c, d, w.x, 4); HBX_STEPW(HBX_H, d, a, b, c, w.y, 11);
-  HBX_STEPW(HBX_H, c, d, a, b, w.z, 16); HBX_STEPW(HBX_H, b, c, d, a, w.w, 23);
-  w = W4[10];
-  HBX_VREG4(w);
-  HBX_STEPW(HBX_H, a, b, c, d, w.x, 4); HBX_STEPW(HBX_H, d, a, b, c, w.y, 11);
-  HBX_STEPW(HBX_H, c, d, a, b, w.z, 16); HBX_STEPW(HBX_H, b, c, d, a, w.w, 23);
-  w = W4[11];
-  HBX_VREG4(w);
-  HBX_STEPW(HBX_H, a, b, c, d, w.x, 4); HBX_STEPW(HBX_H, d, a, b, c, w.y, 11);
-  HBX_STEPW(HBX_H, c, d, a, b, w.z, 16); HBX_STEPW(HBX_H, b, c, d, a, w.w, 23);
-  w = W4[12];
-  HBX_VREG4(w);
-  HBX_STEPW(HBX_I, a, b, c, d, w.x, 6); HBX_STEPW(HBX_I, d, a, b, c, w.y, 10);
-  HBX_STEPW(HBX_I, c, d, a, b, w.z, 15); HBX_STEPW(HBX_I, b, c, d, a, w.w, 21);
-  w = W4[13];
-  HBX_VREG4(w);
-  HBX_STEPW(HBX_I, a, b, c, d, w.x, 6); HBX_STEPW(HBX_I, d, a, b, c, w.y, 10);
-  HBX_STEPW(HBX_I, c, d, a, b, w.z, 15); HBX_STEPW(HBX_I, b, c, d, a, w.w, 21);
-  w = W4[14];
-  HBX_VREG4(w);
-  HBX_STEPW(HBX_I, a, b, c, d, w.x, 6); HBX_STEPW(HBX_I, d, a, b, c, w.y, 10);
-  HBX_STEPW(HBX_I, c, d, a, b, w.z, 15); HBX_STEPW(HBX_I, b, c, d, a, w.w, 21);
-  w = W4[15];
-  HBX_VREG4(w);
-  HBX_STEPW(HBX_I, a, b, c, d, w.x, 6); HBX_STEPW(HBX_I, d, a, b, c, w.y, 10);
-  HBX_STEPW(HBX_I, c, d, a, b, w.z, 15); HBX_STEPW(HBX_I, b, c, d, a, w.w, 21);
-  h[0] += a;
-  h[1] += b;
-  h[2] += c;
-  h[3] += d;
-}
 
 __constant__ uint32_t kMd5T[64] = {
     0xd76aa478u, 0xe8c7b756u, 0x242070dbu, 0xc1bdceeeu, 0xf57c0fafu, 0x4787c62au, 0xa8304613u,
@@ -100,10 +31,49 @@ __constant__ uint32_t kMd5T[64] = {
     0x6fa87e4fu, 0xfe2ce6e0u, 0xa3014314u, 0x4e0811a1u, 0xf7537e82u, 0xbd3af235u, 0x2ad7d2bbu,
     0xeb86d391u};
 
-// "Wave mode": one chunk per wave.  The 64 lanes prepare the next block's
-// step words in parallel (lane i: W_i = M[g(i)] + T_i, one word each) into an
-// LDS double buffer while every lane runs the same serial chain on the
-// current block with 4 VALU per step.  Raw data is loaded 4 blocks ahead.
+// 16 x u32x4 = the 64 step words of one block, replicated in every lane.
+struct WBlock {
+  u32x4 w[16];
+};
+
+__device__ __forceinline__ void wblock_read(WBlock& W, const uint32_t* slot) {
+  const u32x4* p = reinterpret_cast<const u32x4*>(slot);
+#pragma unroll
+  for (int i = 0; i < 16; i++) W.w[i] = p[i];
+}
+
+// Make a block's words opaque VGPR values (keeps the chain on the VALU) and
+// force their LDS reads complete — call it BEFORE issuing the next block's
+// reads: the in-order lgkm counter saturates at 15 outstanding reads.
+__device__ __forceinline__ void wblock_pin(WBlock& W) {
+#pragma unroll
+  for (int i = 0; i < 16; i++) HBX_VREG4(W.w[i]);
+}
+
+__device__ __forceinline__ void md5_compress_wb(uint32_t (&h)[4], const WBlock& W) {
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
+#define HBX_R4(FN, q, s0, s1, s2, s3)                 \
+  HBX_STEPW(FN, a, b, c, d, W.w[q].x, s0);            \
+  HBX_STEPW(FN, d, a, b, c, W.w[q].y, s1);            \
+  HBX_STEPW(FN, c, d, a, b, W.w[q].z, s2);            \
+  HBX_STEPW(FN, b, c, d, a, W.w[q].w, s3);
+  HBX_R4(HBX_F, 0, 7, 12, 17, 22) HBX_R4(HBX_F, 1, 7, 12, 17, 22)
+  HBX_R4(HBX_F, 2, 7, 12, 17, 22) HBX_R4(HBX_F, 3, 7, 12, 17, 22)
+  HBX_R4(HBX_G, 4, 5, 9, 14, 20) HBX_R4(HBX_G, 5, 5, 9, 14, 20)
+  HBX_R4(HBX_G, 6, 5, 9, 14, 20) HBX_R4(HBX_G, 7, 5, 9, 14, 20)
+  HBX_R4(HBX_H, 8, 4, 11, 16, 23) HBX_R4(HBX_H, 9, 4, 11, 16, 23)
+  HBX_R4(HBX_H, 10, 4, 11, 16, 23) HBX_R4(HBX_H, 11, 4, 11, 16, 23)
+  HBX_R4(HBX_I, 12, 6, 10, 15, 21) HBX_R4(HBX_I, 13, 6, 10, 15, 21)
+  HBX_R4(HBX_I, 14, 6, 10, 15, 21) HBX_R4(HBX_I, 15, 6, 10, 15, 21)
+#undef HBX_R4
+  h[0] += a;
+  h[1] += b;
+  h[2] += c;
+  h[3] += d;
+}
+
+// MD5(BE32(0) || BE32(len) || chunk) by one whole wave; result in every lane.
+// wring: this wave's 2 x 64 u32 LDS slots.
 __device__ void md5_chunk_wave(const uint8_t* c, uint32_t len, uint32_t* __restrict__ wring,
                                uint32_t (&h)[4]) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -114,21 +84,18 @@ __device__ void md5_chunk_wave(const uint8_t* c, uint32_t len, uint32_t* __restr
   const uint32_t Ti = kMd5T[lane];
   const uint64_t cp = reinterpret_cast<uint64_t>(c);
   const uint32_t sh = (uint32_t)cp & 3u;
-  // wave-uniform descriptor from the 4-aligned chunk start; reads past the
-  // chunk + slack return 0
   const __amdgpu_buffer_rsrc_t rs =
       make_rsrc_u(reinterpret_cast<const void*>(cp - sh), (sh + len + 64u + 15u) & ~15u);
   const uint32_t T = len + 8u;
   const uint32_t nb = (T + 9u + 63u) >> 6;  // blocks incl. padding
   const uint64_t bits = (uint64_t)T * 8ull;
-  // raw dword pair for (block bb, this lane): R[16bb+gi-2], R[16bb+gi-1]
+  // raw dword pair around message word g(i) of block bb: R[16bb+gi-2..-1]
   auto raw_load = [&](uint32_t bb) -> uint2 {
     const uint32_t off = 4u * (16u * bb + gi) - 8u;  // wraps below 0 -> out of range -> 0
     return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0u, 0));
   };
   auto produce = [&](uint32_t bb, uint2 raw, uint32_t slot) {
-    const uint32_t widx = 16u * bb + gi;
-    uint32_t m = msg_word(widx, raw.x, raw.y, sh, len);
+    uint32_t m = msg_word(16u * bb + gi, raw.x, raw.y, sh, len);
     if (bb + 1u == nb) {
       if (gi == 14u) m = (uint32_t)bits;
       if (gi == 15u) m = (uint32_t)(bits >> 32);
@@ -141,18 +108,41 @@ __device__ void md5_chunk_wave(const uint8_t* c, uint32_t len, uint32_t* __restr
   for (int r = 0; r < 4; r++) ring[r] = raw_load((uint32_t)r);
   produce(0u, ring[0], 0u);
   ring[0] = raw_load(4u);
-  for (uint32_t b0 = 0; b0 < nb; b0 += 4u) {
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const uint32_t b = b0 + (uint32_t)r;
-      if (b < nb) {  // wave-uniform
-        const int rn = (r + 1) & 3;
-        if (b + 1u < nb) produce(b + 1u, ring[rn], (b + 1u) & 1u);
-        ring[rn] = raw_load(b + 5u);
-        __builtin_amdgcn_sched_barrier(0);
-        md5_compress_w(h, wring + (b & 1u) * 64u);
-      }
+  if (nb > 1u) {
+    produce(1u, ring[1], 1u);
+    ring[1] = raw_load(5u);
+  }
+  WBlock Wa, Wb;
+  wblock_read(Wa, wring);
+  // invariant at the top: Wa = W(b); LDS slot (b+1)&1 holds W(b+1);
+  // ring[k&3] holds the raw words of block k for k in b+2 .. b+5
+  for (uint32_t b = 0; b < nb; b += 2u) {  // wave-uniform
+    wblock_pin(Wa);
+    __builtin_amdgcn_sched_barrier(0);
+    if (b + 1u < nb) wblock_read(Wb, wring + 64u);
+    if (b + 2u < nb) {
+      produce(b + 2u, ring[2], 0u);
+      ring[2] = raw_load(b + 6u);
     }
+    __builtin_amdgcn_sched_barrier(0);
+    md5_compress_wb(h, Wa);
+    if (b + 1u < nb) {
+      wblock_pin(Wb);
+      __builtin_amdgcn_sched_barrier(0);
+      if (b + 2u < nb) wblock_read(Wa, wring);
+      if (b + 3u < nb) {
+        produce(b + 3u, ring[3], 1u);
+        ring[3] = raw_load(b + 7u);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      md5_compress_wb(h, Wb);
+    }
+    // rotate the raw ring by two blocks
+    const uint2 t0 = ring[0], t1 = ring[1];
+    ring[0] = ring[2];
+    ring[1] = ring[3];
+    ring[2] = t0;
+    ring[3] = t1;
   }
 }
 

@@ -31,6 +31,18 @@ __global__ void chain(uint32_t* out, uint64_t* cyc, uint32_t seed) {
   if (threadIdx.x == 0) cyc[0] = t1 - t0;
 }
 
+// waves-per-SIMD scaling of the md5-like chain: blockDim 64/256/512/1024
+void scaling(uint32_t* d, uint64_t* c) {
+  for (int bd : {64, 256, 512, 1024}) {
+    for (int rep = 0; rep < 2; rep++) {
+      hipLaunchKernelGGL(chain<7>, 1, bd, 0, 0, d, c, 7);
+      uint64_t cy = 0; (void)hipMemcpy(&cy, c, 8, hipMemcpyDeviceToHost);
+      if (rep) printf("md5 chain, %4d threads (%d waves/SIMD): %6.2f ticks/op per wave\n", bd,
+                      bd / 256 ? bd / 256 : 1, (double)cy / (256.0 * 16 * 4));
+    }
+  }
+}
+
 int main() {
   uint32_t* d; uint64_t* c; hipMalloc(&d, 4096); hipMalloc(&c, 64);
   const char* names[] = {"v_add_u32", "v_add3_u32", "v_alignbit_b32", "v_bitop3_b32", "v_xor_b32",
@@ -52,5 +64,6 @@ int main() {
     double per = (double)cy / (256.0 * 16 * ((op >= 7) ? 4 : 1));
     if (rep) printf("%-26s %6.2f cycles/op (s_memtime ticks)\n", names[op], per);
   }
+  scaling(d, c);
   return 0;
 }
