@@ -100,7 +100,8 @@ struct hbx_ctx {
   hipEvent_t ev[5] = {};
   std::mutex mu;
   std::string err;
-  uint32_t tile_iters = 32;
+  uint32_t tile_iters = 64;  // K1 tile = 64 x 64 KiB (measured best: fewer halo primes)
+  uint32_t k1_dma = 1;     // K1 lands tiles in LDS by DMA (HBX_K1_DMA=0: register prefetch)
   uint32_t md5_wgs = 256;  // K3 grid: one 512-thread workgroup per CU (set from the device)
   float stage_ms[5] = {0, 0, 0, 0, 0};
 
@@ -109,7 +110,7 @@ struct hbx_ctx {
   std::vector<uint2> h_tiles;
 
   DevBuf d_meta;  // file_off | file_len | slice_base | cut_base | tiles
-  DevBuf d_smax, d_sprev, d_cuts, d_count, d_ids, d_cid, d_ctype, d_work, d_ctl;
+  DevBuf d_ssum, d_cuts, d_count, d_ids, d_cid, d_ctype, d_work, d_ctl;
   DevBuf d_stage;  // host-input arena
   DevBuf d_msg;    // hbx_block_id message
   PinBuf h_meta, h_res;
@@ -197,8 +198,7 @@ int enqueue_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* o
   std::memcpy(hm + 3 * n, c->h_cut_base.data(), n * 8);
   if (nt) std::memcpy(hm + 4 * n, c->h_tiles.data(), nt * sizeof(uint2));
 
-  HBX_TRY(c, c->d_smax.ensure(std::max<uint64_t>(slices, 1) * 4));
-  HBX_TRY(c, c->d_sprev.ensure(std::max<uint64_t>(slices, 1) * 4));
+  HBX_TRY(c, c->d_ssum.ensure((slices + 1) * sizeof(uint2)));  // +1: dummy slot
   HBX_TRY(c, c->d_cuts.ensure(caps * 8));
   HBX_TRY(c, c->d_count.ensure(n * 4));
   HBX_TRY(c, c->d_ids.ensure(caps * 16));
@@ -220,14 +220,19 @@ int enqueue_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* o
 
   HBX_TRY(c, hipEventRecord(c->ev[0], s));
   if (nt) {
-    hipLaunchKernelGGL(hbx_k1_digest_scan, dim3((uint32_t)nt), dim3(kK1Threads), 0, s, arena,
-                       d_off, d_len, d_sb, d_tiles, c->tile_iters, c->d_smax.as<uint32_t>(),
-                       c->d_sprev.as<uint32_t>());
+    if (c->k1_dma)
+      hipLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3((uint32_t)nt), dim3(kK1Threads), 0, s,
+                         arena, d_off, d_len, d_sb, d_tiles, c->tile_iters, c->d_ssum.as<uint2>(),
+                         slices);
+    else
+      hipLaunchKernelGGL(hbx_k1_digest_scan, dim3((uint32_t)nt), dim3(kK1Threads), 0, s, arena,
+                         d_off, d_len, d_sb, d_tiles, c->tile_iters, c->d_ssum.as<uint2>(),
+                         slices);
     HBX_TRY(c, hipGetLastError());
   }
   HBX_TRY(c, hipEventRecord(c->ev[1], s));
   hipLaunchKernelGGL(hbx_k2_cut_chain, dim3((uint32_t)n), dim3(64), 0, s, arena, d_off, d_len,
-                     d_sb, c->d_smax.as<uint32_t>(), c->d_sprev.as<uint32_t>(), d_cb,
+                     d_sb, c->d_ssum.as<uint2>(), d_cb,
                      c->d_cuts.as<uint64_t>(), c->d_count.as<uint32_t>());
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(c->ev[2], s));
@@ -329,6 +334,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->md5_wgs = (uint32_t)prop.multiProcessorCount;
+  if (const char* v = std::getenv("HBX_K1_DMA")) c->k1_dma = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("HBX_MD5_WGS")) c->md5_wgs = (uint32_t)std::max(1, std::atoi(v));
   if (const char* v = std::getenv("HBX_TILE_ITERS")) c->tile_iters = (uint32_t)std::min(1024, std::max(1, std::atoi(v)));
   if (hipSetDevice(device) != hipSuccess ||
@@ -350,7 +356,7 @@ void hbx_ctx_destroy(hbx_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (DevBuf* b : {&c->d_meta, &c->d_smax, &c->d_sprev, &c->d_cuts, &c->d_count, &c->d_ids,
+  for (DevBuf* b : {&c->d_meta, &c->d_ssum, &c->d_cuts, &c->d_count, &c->d_ids,
                     &c->d_cid, &c->d_ctype, &c->d_work, &c->d_ctl, &c->d_stage, &c->d_msg})
     b->release();
   c->h_meta.release();

@@ -23,7 +23,13 @@ using namespace hbx;
 namespace {
 
 // ------------------------------------------------------------------ K1 --
-constexpr int kK1Threads = 1024;  // 16 waves; 16 x 4096 B = one MIN window per iteration
+constexpr int kK1Threads = 1024;
+#ifndef HBX_K1_SDWA
+#define HBX_K1_SDWA 1
+#endif
+#ifndef HBX_K1_COALESCED
+#define HBX_K1_COALESCED 1
+#endif  // 16 waves; 16 x 4096 B = one MIN window per iteration
 
 // Per-lane in-aggregates of a 64-byte run: half (positions 0..31) and full.
 struct RunAgg {
@@ -79,15 +85,150 @@ __device__ __forceinline__ uint32_t digest_pass(const uint32_t (&in)[16], const 
   return M;
 }
 
+// Same pass with the digest kept as ONE register per stream, X = s2<<16 | s1:
+//   X.lo += in_byte; X.lo -= out_byte   (SDWA: 16-bit result, high half kept)
+//   X += X << 16                        (s2 += s1, mod 2^16, low half kept)
+// so X IS the digest — 3 VALU per position instead of ~4.25 + hazard nops.
+// Two independent streams per lane (positions 0..31 and 32..63).
+#define HBX_SDWA_STEP(X, IN, OUT, B)                                                          \
+  asm("v_add_u16_sdwa %0, %0, %1 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 " \
+      "src1_sel:BYTE_" #B "\n\t"                                                              \
+      "v_sub_u16_sdwa %0, %0, %2 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 " \
+      "src1_sel:BYTE_" #B "\n\t"                                                              \
+      "v_lshl_add_u32 %0, %0, 16, %0"                                                        \
+      : "+v"(X)                                                                               \
+      : "v"(IN), "v"(OUT))
+
+template <bool TAIL>
+__device__ __forceinline__ uint32_t digest_pass_sdwa(const uint32_t (&in)[16],
+                                                     const uint32_t (&out)[16], uint32_t XA,
+                                                     uint32_t XB, uint32_t e_l, uint32_t lim) {
+  uint32_t M = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+#define HBX_SDWA_PAIR(B)                                            \
+    {                                                               \
+      HBX_SDWA_STEP(XA, in[k], out[k], B);                          \
+      HBX_SDWA_STEP(XB, in[8 + k], out[8 + k], B);                  \
+      uint32_t DA = XA, DB = XB;                                    \
+      if (TAIL) {                                                   \
+        DA = (e_l + 4u * k + B < lim) ? DA : 0u;                    \
+        DB = (e_l + 32u + 4u * k + B < lim) ? DB : 0u;              \
+      }                                                             \
+      M = max(M, max(DA, DB));                                      \
+    }
+    HBX_SDWA_PAIR(0) HBX_SDWA_PAIR(1) HBX_SDWA_PAIR(2) HBX_SDWA_PAIR(3)
+#undef HBX_SDWA_PAIR
+  }
+  return M;
+}
+
 }  // namespace
 
+// Rollsum state carried between K1 iterations.
+struct K1State {
+  uint32_t S1c, s2c;  // state before the iteration's first position
+  RunAgg pa;          // in-aggregates of the previous run (= this run's "out")
+};
+
+// Priming: the state at q0-1 is the digest state of the MIN bytes before q0
+// (`halo`, this thread's 64-byte run of it); at q0 == 0 the window is all
+// virtual zeros.
+__device__ __forceinline__ K1State k1_prime(const uint32_t (&halo)[16], bool at_start,
+                                            uint2 (&wtot)[2][16], uint32_t w, uint32_t l,
+                                            uint32_t e_l) {
+  K1State st;
+  if (at_start) {
+    st.pa = RunAgg{0u, 0u, 0u, 0u};
+    st.S1c = 0u;
+    st.s2c = 0x8000u;
+    return st;
+  }
+  st.pa = run_aggregates(halo);
+  const uint32_t iA = wave_incl_sum(st.pa.af);
+  const uint32_t iC = wave_incl_sum(e_l * st.pa.af + st.pa.jf);
+  if (l == 63u) wtot[1][w] = make_uint2(iA, iC);
+  __syncthreads();
+  const uint2 t = (l < 16u) ? wtot[1][l] : make_uint2(0u, 0u);
+  const uint32_t sA = row_incl_sum(t.x), sC = row_incl_sum(t.y);
+  st.S1c = readlane(sA, 15);
+  st.s2c = 0x8000u - readlane(sC, 15);  // virtual-zero start: s2 = 2^15 - sum k*x_k
+  return st;
+}
+
+// One 64 KiB iteration: thread (w, l) owns positions e_l .. e_l+63 of it;
+// `cur` are their bytes, `out` the bytes MIN earlier.  Returns, wave-uniform,
+// the slice's max digest and the digest just before the slice (= state).
+__device__ __forceinline__ void k1_iteration(const uint32_t (&cur)[16], const uint32_t (&out)[16],
+                                             K1State& st, uint2 (&wtot)[2][16], uint32_t it,
+                                             uint32_t w, uint32_t l, uint32_t e_l, uint64_t qs,
+                                             uint64_t N, uint32_t& smax, uint32_t& sprev) {
+  const RunAgg ca = run_aggregates(cur);
+  const uint32_t A_hA = ca.ah - st.pa.ah, J_hA = ca.jh - st.pa.jh;
+  const uint32_t A_l = ca.af - st.pa.af, J_l = ca.jf - st.pa.jf;
+  const uint32_t C_l = e_l * A_l + J_l;
+  const uint32_t iA = wave_incl_sum(A_l);
+  const uint32_t iC = wave_incl_sum(C_l);
+  if (l == 63u) wtot[it & 1u][w] = make_uint2(iA, iC);
+  __syncthreads();
+  const uint2 t = (l < 16u) ? wtot[it & 1u][l] : make_uint2(0u, 0u);
+  const uint32_t sA = row_incl_sum(t.x), sC = row_incl_sum(t.y);
+  const uint32_t WA = w ? readlane(sA, (int)w - 1) : 0u;
+  const uint32_t WC = w ? readlane(sC, (int)w - 1) : 0u;
+  const uint32_t totA = readlane(sA, 15), totC = readlane(sC, 15);
+
+  // state before the lane's first position (*), then before position 32
+  const uint32_t A_pre = WA + (iA - A_l), C_pre = WC + (iC - C_l);
+  const uint32_t S1_t = st.S1c + A_pre;
+  const uint32_t s2_t = st.s2c + e_l * S1_t - C_pre;
+  const uint32_t A_pre2 = A_pre + A_hA, C_pre2 = C_pre + e_l * A_hA + J_hA;
+  const uint32_t S1_b = st.S1c + A_pre2;
+  const uint32_t s2_b = st.s2c + (e_l + 32u) * S1_b - C_pre2;
+  const uint32_t S1p = (S1_t & 0xffffu) | (S1_b << 16);
+  const uint32_t S2p = (s2_t & 0xffffu) | (s2_b << 16);
+  sprev = readlane((s2_t << 16) | (S1_t & 0xffffu), 0);
+
+  uint32_t M;
+#if HBX_K1_SDWA
+  const uint32_t XA = (s2_t << 16) | (S1_t & 0xffffu), XB = (s2_b << 16) | (S1_b & 0xffffu);
+  if (qs + kMinBlock <= N) {
+    M = digest_pass_sdwa<false>(cur, out, XA, XB, e_l, 0u);
+  } else {
+    M = digest_pass_sdwa<true>(cur, out, XA, XB, e_l, (uint32_t)(N - qs));
+  }
+  (void)S1p;
+  (void)S2p;
+#else
+  if (qs + kMinBlock <= N) {
+    M = digest_pass<false>(cur, out, S1p, S2p, e_l, 0u);
+  } else {
+    M = digest_pass<true>(cur, out, S1p, S2p, e_l, (uint32_t)(N - qs));
+  }
+#endif
+  smax = readlane(wave_max_to_lane63(M), 63);
+
+  st.S1c += totA;
+  st.s2c -= totC;  // 65536*(...) vanishes mod 2^16
+  st.pa = ca;
+}
+
+// Slice summary {max, prev} of one wave-iteration: ONE store instruction
+// (lanes 0 and 1), always issued — slices past the file end go to the dummy
+// slot — so K1-DMA can count its outstanding vector-memory ops exactly.
+__device__ __forceinline__ void k1_store_slice(uint2* __restrict__ ssum, uint64_t idx, uint32_t l,
+                                               uint32_t smax, uint32_t sprev) {
+  if (l < 2u) reinterpret_cast<uint32_t*>(ssum + idx)[l] = l ? sprev : smax;
+}
+
 // tiles[t] = {file index, tile index within file}; a tile is tile_iters
-// consecutive 64 KiB iterations of one file.
+// consecutive 64 KiB iterations of one file.  ssum[slice_base[f] + j] =
+// {max digest of slice j, digest before slice j}; ssum[dummy] absorbs the
+// writes of slices past a file's end.
 extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan(
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
     const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ slice_base,
-    const uint2* __restrict__ tiles, uint32_t tile_iters, uint32_t* __restrict__ slice_max,
-    uint32_t* __restrict__ slice_prev) {
+    const uint2* __restrict__ tiles, uint32_t tile_iters, uint2* __restrict__ ssum,
+    uint64_t dummy) {
   __shared__ uint2 wtot[2][16];
   const uint2 td = tiles[blockIdx.x];
   const uint32_t f = td.x;
@@ -108,83 +249,145 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan(
   const uint32_t nbytes = (uint32_t)((umin64(rem, (uint64_t)n_it * kMinBlock) + 15ull) & ~15ull);
   const __amdgpu_buffer_rsrc_t rs = make_rsrc_u(fb + q0, nbytes);
 
-  // ---- priming: "out" bytes of iteration 0 = the MIN bytes before q0, and
-  //      the rollsum state at q0-1 = digest state of exactly that window.
   uint32_t out[16];
-  RunAgg pa;
-  uint32_t S1c, s2c;
-  if (q0 == 0) {
 #pragma unroll
-    for (int k = 0; k < 16; k++) out[k] = 0u;
-    pa = RunAgg{0u, 0u, 0u, 0u};
-    S1c = 0u;
-    s2c = 0x8000u;
-  } else {
-    const __amdgpu_buffer_rsrc_t rh = make_rsrc_u(fb + q0 - kMinBlock, kMinBlock);
-    load_run64(rh, e_l, 0u, out);
-    pa = run_aggregates(out);
-    const uint32_t iA = wave_incl_sum(pa.af);
-    const uint32_t iC = wave_incl_sum(e_l * pa.af + pa.jf);
-    if (l == 63u) wtot[1][w] = make_uint2(iA, iC);
-    __syncthreads();
-    const uint2 t = (l < 16u) ? wtot[1][l] : make_uint2(0u, 0u);
-    const uint32_t sA = row_incl_sum(t.x), sC = row_incl_sum(t.y);
-    S1c = readlane(sA, 15);
-    s2c = 0x8000u - readlane(sC, 15);  // virtual-zero start: s2 = 2^15 - sum k*x_k
-  }
+  for (int k = 0; k < 16; k++) out[k] = 0u;
+  if (q0 != 0) load_run64(make_rsrc_u(fb + q0 - kMinBlock, kMinBlock), e_l, 0u, out);
+  K1State st = k1_prime(out, q0 == 0, wtot, w, l, e_l);
 
   uint32_t cur[16], nxt[16];
   load_run64(rs, e_l, 0u, cur);
   for (uint32_t it = 0; it < n_it; it++) {
     if (it + 1 < n_it) load_run64(rs, e_l, (it + 1) * kMinBlock, nxt);
-
-    const RunAgg ca = run_aggregates(cur);
-    const uint32_t A_hA = ca.ah - pa.ah, J_hA = ca.jh - pa.jh;
-    const uint32_t A_l = ca.af - pa.af, J_l = ca.jf - pa.jf;
-    const uint32_t C_l = e_l * A_l + J_l;
-    const uint32_t iA = wave_incl_sum(A_l);
-    const uint32_t iC = wave_incl_sum(C_l);
-    if (l == 63u) wtot[it & 1u][w] = make_uint2(iA, iC);
-    __syncthreads();
-    const uint2 t = (l < 16u) ? wtot[it & 1u][l] : make_uint2(0u, 0u);
-    const uint32_t sA = row_incl_sum(t.x), sC = row_incl_sum(t.y);
-    const uint32_t WA = w ? readlane(sA, (int)w - 1) : 0u;
-    const uint32_t WC = w ? readlane(sC, (int)w - 1) : 0u;
-    const uint32_t totA = readlane(sA, 15), totC = readlane(sC, 15);
-
-    // state before the lane's first position (*), then before position 32
-    const uint32_t A_pre = WA + (iA - A_l), C_pre = WC + (iC - C_l);
-    const uint32_t S1_t = S1c + A_pre;
-    const uint32_t s2_t = s2c + e_l * S1_t - C_pre;
-    const uint32_t A_pre2 = A_pre + A_hA, C_pre2 = C_pre + e_l * A_hA + J_hA;
-    const uint32_t S1_b = S1c + A_pre2;
-    const uint32_t s2_b = s2c + (e_l + 32u) * S1_b - C_pre2;
-    const uint32_t S1p = (S1_t & 0xffffu) | (S1_b << 16);
-    const uint32_t S2p = (s2_t & 0xffffu) | (s2_b << 16);
-
     const uint64_t qs = q0 + (uint64_t)it * kMinBlock;  // iteration start position
-    const bool slice_ok = qs + (uint64_t)w * kSlice < N;
-    const uint64_t sidx = sb + ((qs >> kSliceShift) + w);
-    if (l == 0u && slice_ok) slice_prev[sidx] = (s2_t << 16) | (S1_t & 0xffffu);
-
-    uint32_t M;
-    if (qs + kMinBlock <= N) {
-      M = digest_pass<false>(cur, out, S1p, S2p, e_l, 0u);
-    } else {
-      M = digest_pass<true>(cur, out, S1p, S2p, e_l, (uint32_t)(N - qs));
-    }
-    M = wave_max_to_lane63(M);
-    if (l == 63u && slice_ok) slice_max[sidx] = M;
-
-    S1c += totA;
-    s2c -= totC;  // 65536*(...) vanishes mod 2^16
+    uint32_t smax, sprev;
+    k1_iteration(cur, out, st, wtot, it, w, l, e_l, qs, N, smax, sprev);
+    const bool ok = qs + (uint64_t)w * kSlice < N;
+    k1_store_slice(ssum, ok ? sb + ((qs >> kSliceShift) + w) : dummy, l, smax, sprev);
 #pragma unroll
     for (int k = 0; k < 16; k++) {
       out[k] = cur[k];
       cur[k] = nxt[k];
     }
-    pa = ca;
   }
+}
+
+// ---------------------------------------------------------- K1 (LDS-DMA) --
+// Same scan; the runs land in LDS by buffer_load ... lds (no VGPR staging),
+// two iterations in flight per CU (128 KiB), instead of one in registers.
+// Each wave owns 2 private 4 KiB slots (it reads only what it loaded itself,
+// so no barrier guards the data); a slot holds 4 pieces of 1 KiB, piece k
+// lane l = bytes 16k..16k+15 of lane l's run, so every ds_read_b128 is
+// conflict-free.  Vector-memory ops per wave per iteration are exactly 4 DMA
+// + 1 slice store, which makes the hand-counted vmcnt waits exact.
+typedef uint32_t s32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ s32x4 make_srd(const void* base, uint32_t nbytes) {
+  const uint64_t p = reinterpret_cast<uint64_t>(base);
+  s32x4 r;
+  r.x = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)p);
+  r.y = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(p >> 32)) & 0xffffu;
+  r.z = (uint32_t)__builtin_amdgcn_readfirstlane((int)nbytes);
+  r.w = 0x00020000u;
+  return r;
+}
+
+// 64 lanes x 16 B from srd[voff + soff] into LDS [lds, lds + 1 KiB).
+__device__ __forceinline__ void dma16(s32x4 srd, uint32_t voff, uint32_t soff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(srd), "s"(lds), "s"(soff)
+      : "memory");
+}
+
+constexpr uint32_t kDmaSlot = 4096;  // bytes per wave per iteration
+
+extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_dma(
+    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
+    const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ slice_base,
+    const uint2* __restrict__ tiles, uint32_t tile_iters, uint2* __restrict__ ssum,
+    uint64_t dummy) {
+  __shared__ uint2 wtot[2][16];
+  __shared__ __attribute__((aligned(1024))) uint8_t land[kK1Threads / 64][2][kDmaSlot];
+  const uint2 td = tiles[blockIdx.x];
+  const uint32_t f = td.x;
+  const uint64_t N = file_len[f];
+  const uint64_t q0 = (uint64_t)td.y * tile_iters * kMinBlock;
+  const uint8_t* fb = arena + file_off[f];
+  const uint64_t sb = slice_base[f];
+
+  const uint32_t tid = threadIdx.x;
+  const uint32_t l = tid & 63u;
+  const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+  const uint32_t e_l = w * kSlice + l * 64u;
+
+  const uint64_t rem = N - q0;
+  const uint32_t n_it = (uint32_t)umin64(tile_iters, (rem + kMinBlock - 1) / kMinBlock);
+  const uint32_t nbytes = (uint32_t)((umin64(rem, (uint64_t)n_it * kMinBlock) + 15ull) & ~15ull);
+  const s32x4 srd = make_srd(fb + q0, nbytes);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)&land[w][0][0];
+  const uint32_t lds1 = (uint32_t)(uintptr_t)&land[w][1][0];
+  // HBX_K1_COALESCED: each DMA instruction reads 1 KiB contiguous (lane l:
+  // bytes 16l..16l+15 of the piece) so the LDS slot holds the wave's 4 KiB in
+  // file order; the per-lane 64-byte reads then take a 4-way bank conflict.
+  // Otherwise lane l of piece k reads bytes 16k.. of its own run (strided
+  // global access, conflict-free LDS reads).
+  auto issue = [&](uint32_t it, uint32_t lds) {  // 4 DMA ops, always issued
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t voff = HBX_K1_COALESCED ? (w * kSlice + 1024u * k + 16u * l) : (e_l + 16u * k);
+      dma16(srd, voff, it * kMinBlock, lds + 1024u * k);
+    }
+  };
+  auto land_read = [&](uint32_t slot, uint32_t (&v)[16]) {
+    const u32x4* p = reinterpret_cast<const u32x4*>(&land[w][slot][0]);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const u32x4 t = HBX_K1_COALESCED ? p[4 * l + k] : p[64 * k + l];
+      v[4 * k + 0] = t.x;
+      v[4 * k + 1] = t.y;
+      v[4 * k + 2] = t.z;
+      v[4 * k + 3] = t.w;
+    }
+  };
+
+  uint32_t out[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) out[k] = 0u;
+  if (q0 != 0) load_run64(make_rsrc_u(fb + q0 - kMinBlock, kMinBlock), e_l, 0u, out);
+  K1State st = k1_prime(out, q0 == 0, wtot, w, l, e_l);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  issue(0u, lds0);
+  issue(1u, lds1);  // past the tile end: out-of-range reads land zeros, never read
+  uint32_t cur[16];
+  for (uint32_t it = 0; it < n_it; it++) {
+    // outstanding, oldest first: DMA(it), store(it-2), DMA(it+1), store(it-1)
+    if (it == 0)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (it == 1)
+      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    land_read(it & 1u, cur);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot consumed before it is refilled
+    issue(it + 2u, (it & 1u) ? lds1 : lds0);
+    const uint64_t qs = q0 + (uint64_t)it * kMinBlock;
+    uint32_t smax, sprev;
+    k1_iteration(cur, out, st, wtot, it, w, l, e_l, qs, N, smax, sprev);
+    const bool ok = qs + (uint64_t)w * kSlice < N;
+    k1_store_slice(ssum, ok ? sb + ((qs >> kSliceShift) + w) : dummy, l, smax, sprev);
+#pragma unroll
+    for (int k = 0; k < 16; k++) out[k] = cur[k];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup exits
 }
 
 // ------------------------------------------------------------------ K2 --
@@ -231,7 +434,7 @@ __device__ void slice_argmax(const uint8_t* fb, uint64_t N, uint64_t j, uint32_t
 extern "C" __global__ __launch_bounds__(64) void hbx_k2_cut_chain(
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
     const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ slice_base,
-    const uint32_t* __restrict__ slice_max, const uint32_t* __restrict__ slice_prev,
+    const uint2* __restrict__ ssum,
     const uint64_t* __restrict__ cut_base, uint64_t* __restrict__ cut_ends,
     uint32_t* __restrict__ cut_count) {
   const uint32_t f = blockIdx.x;
@@ -255,7 +458,7 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k2_cut_chain(
       uint32_t bv = 0u;
       int64_t bj = -1;
       for (uint64_t j = ja + 1 + l; j < jb; j += 64) {
-        const uint32_t v = slice_max[sb + j];
+        const uint32_t v = ssum[sb + j].x;
         if (v >= bv) {
           bv = v;
           bj = (int64_t)j;
@@ -269,10 +472,10 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k2_cut_chain(
       uint64_t qwin = 0;
       int src = 1;  // 0 = first edge slice, 1 = interior, 2 = last edge slice
       // last (partial) slice: wins ties
-      if (slice_max[sb + jb] >= Mbest) {
+      if (ssum[sb + jb].x >= Mbest) {
         uint32_t D;
         int P;
-        slice_argmax(fb, N, jb, slice_prev[sb + jb], 0, (int)(qb - (jb << kSliceShift)), D, P);
+        slice_argmax(fb, N, jb, ssum[sb + jb].y, 0, (int)(qb - (jb << kSliceShift)), D, P);
         if (P >= 0 && D >= Mbest) {
           Mbest = D;
           qwin = (jb << kSliceShift) + (uint64_t)P;
@@ -280,10 +483,10 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k2_cut_chain(
         }
       }
       // first (partial) slice: must be strictly greater
-      if (slice_max[sb + ja] > Mbest) {
+      if (ssum[sb + ja].x > Mbest) {
         uint32_t D;
         int P;
-        slice_argmax(fb, N, ja, slice_prev[sb + ja], (int)(qa - (ja << kSliceShift)),
+        slice_argmax(fb, N, ja, ssum[sb + ja].y, (int)(qa - (ja << kSliceShift)),
                      (int)kSlice - 1, D, P);
         if (P >= 0 && D > Mbest) {
           Mbest = D;
@@ -294,7 +497,7 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k2_cut_chain(
       if (src == 1) {
         uint32_t D;
         int P;
-        slice_argmax(fb, N, jI, slice_prev[sb + jI], 0, (int)kSlice - 1, D, P);
+        slice_argmax(fb, N, jI, ssum[sb + jI].y, 0, (int)kSlice - 1, D, P);
         qwin = (jI << kSliceShift) + (uint64_t)P;
       }
       cut = qwin + 1;

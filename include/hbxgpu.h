@@ -133,7 +133,7 @@ int hbx_free_pinned(void *p);
  * [0] K1 window-digest scan, [1] K2 cut chain, [2] K3 block MD5,
  * [3] K4 content id, [4] whole batch on the stream. */
 int hbx_stage_times(hbx_ctx *ctx, float ms[5]);
-/* Tile length of K1 in 64 KiB iterations (default 32 = 2 MiB tiles). */
+/* Tile length of K1 in 64 KiB iterations (default 64 = 4 MiB tiles). */
 int hbx_set_tile_iters(hbx_ctx *ctx, uint32_t iters);
 
 #ifdef __cplusplus
