@@ -9,7 +9,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libhbxgpu.so")
+# HBX_LIB overrides the in-tree library (A/B experiments with variant builds).
+LIB_PATH = os.environ.get("HBX_LIB") or os.path.join(HERE, "libhbxgpu.so")
 
 HBX_OK = 0
 ERRORS = {-1: "HBX_ERR_ARG", -2: "HBX_ERR_HIP", -3: "HBX_ERR_CAPACITY", -4: "HBX_ERR_IO",
@@ -19,7 +20,7 @@ ERRORS = {-1: "HBX_ERR_ARG", -2: "HBX_ERR_HIP", -3: "HBX_ERR_CAPACITY", -4: "HBX
 EXPORTS = [
     "hbx_version", "hbx_device_count", "hbx_max_chunks", "hbx_ctx_create", "hbx_ctx_destroy",
     "hbx_last_error", "hbx_chunk_hash", "hbx_chunk_hash_batch", "hbx_chunk_hash_device",
-    "hbx_submit_device", "hbx_wait", "hbx_block_id", "hbx_arena_alloc", "hbx_arena_free",
+    "hbx_submit_device", "hbx_wait", "hbx_store_paths", "hbx_block_id", "hbx_arena_alloc", "hbx_arena_free",
     "hbx_memcpy_h2d", "hbx_memcpy_h2d_async", "hbx_alloc_pinned", "hbx_free_pinned", "hbx_stage_times",
     "hbx_set_tile_iters",
 ]
@@ -66,6 +67,7 @@ def load() -> ctypes.CDLL:
     L.hbx_chunk_hash_device.argtypes = [P, P, U64, P, P, P, P, P, P, P]
     L.hbx_submit_device.argtypes = [P, P, U64, P, P, P, P, P, P, P]
     L.hbx_wait.argtypes = [P]
+    L.hbx_store_paths.argtypes = [P, U64, P, P, P, P, P, P, P, ctypes.c_uint32, U64]
     L.hbx_block_id.argtypes = [P, P, ctypes.c_uint32, P, U64, P]
     L.hbx_arena_alloc.argtypes = [P, U64, ctypes.POINTER(P)]
     L.hbx_arena_free.argtypes = [P, P]

@@ -12,12 +12,17 @@
 // 556-560 + block.go:96-111 (StoreData -> HashData).
 #include <hip/hip_runtime.h>
 
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/hbxgpu.h"
@@ -114,6 +119,8 @@ struct hbx_ctx {
   DevBuf d_stage;  // host-input arena
   DevBuf d_msg;    // hbx_block_id message
   PinBuf h_meta, h_res;
+  PinBuf h_stage;           // hbx_store_paths: pinned landing buffer for file reads
+  hbx_ctx* twin = nullptr;  // hbx_store_paths: second context (double buffering)
   Pending pend;
 
   int fail(int code, const std::string& m) {
@@ -361,6 +368,8 @@ void hbx_ctx_destroy(hbx_ctx* c) {
     b->release();
   c->h_meta.release();
   c->h_res.release();
+  c->h_stage.release();
+  if (c->twin) hbx_ctx_destroy(c->twin);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -519,6 +528,120 @@ int hbx_memcpy_h2d(hbx_ctx* c, void* d, const void* h, uint64_t n) {
   HBX_TRY(c, hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, c->stream));
   HBX_TRY(c, hipStreamSynchronize(c->stream));
   return HBX_OK;
+}
+
+// ---- files on disk -> pinned -> HBM -> results (BASELINE configs[4]) ----
+namespace {
+
+// Read whole files into dst + offs[i] with `threads` threads (files are
+// independent).  Returns 0 or HBX_ERR_IO with the offending path in err.
+int read_files(uint64_t n, const char* const* paths, const uint64_t* lens, const uint64_t* offs,
+               uint8_t* dst, uint32_t threads, std::string& err) {
+  std::atomic<uint64_t> next{0};
+  std::atomic<int> failed{0};
+  std::mutex emu;
+  auto worker = [&]() {
+    for (;;) {
+      const uint64_t i = next.fetch_add(1);
+      if (i >= n || failed.load()) return;
+      const int fd = ::open(paths[i], O_RDONLY | O_CLOEXEC);
+      bool ok = fd >= 0;
+      uint64_t got = 0;
+      while (ok && got < lens[i]) {
+        const ssize_t r = ::pread(fd, dst + offs[i] + got, lens[i] - got, (off_t)got);
+        if (r <= 0) ok = false;
+        else got += (uint64_t)r;
+      }
+      if (fd >= 0) ::close(fd);
+      if (!ok) {
+        failed.store(1);
+        std::lock_guard<std::mutex> g(emu);
+        err = std::string("cannot read ") + std::to_string(lens[i]) + " bytes of " + paths[i];
+        return;
+      }
+    }
+  };
+  const uint32_t nt = std::max<uint32_t>(1, std::min<uint64_t>(threads, n));
+  std::vector<std::thread> pool;
+  for (uint32_t t = 1; t < nt; t++) pool.emplace_back(worker);
+  worker();
+  for (auto& t : pool) t.join();
+  return failed.load() ? HBX_ERR_IO : HBX_OK;
+}
+
+}  // namespace
+
+int hbx_store_paths(hbx_ctx* c, uint64_t n, const char* const* paths, const uint64_t* lens,
+                    uint64_t* cut_ends, uint8_t* ids, const uint64_t* out_base,
+                    const uint64_t* caps, hbx_file_summary* sums, uint32_t io_threads,
+                    uint64_t batch_bytes) {
+  if (!c) return HBX_ERR_ARG;
+  if (n && (!paths || !lens || !out_base || !caps)) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->pend.active) return c->fail(HBX_ERR_STATE, "a submitted batch is still pending");
+  HBX_TRY(c, hipSetDevice(c->device));
+  if (!c->twin) {
+    int rc = hbx_ctx_create(c->device, &c->twin);
+    if (rc) return c->fail(rc, "cannot create the second context");
+    c->twin->tile_iters = c->tile_iters;
+    c->twin->md5_wgs = c->md5_wgs;
+    c->twin->k1_dma = c->k1_dma;
+  }
+  if (batch_bytes < (64ull << 20)) batch_bytes = 64ull << 20;
+  hbx_ctx* X[2] = {c, c->twin};
+  struct Batch {
+    uint64_t first = 0, count = 0, total = 0, cap = 0;
+    std::vector<uint64_t> offs;
+  } B[2];
+  auto finish = [&](int s) -> int {  // wait for slot s's batch and scatter its results
+    Batch& b = B[s];
+    if (!b.count) return HBX_OK;
+    HBX_TRY(X[s], hipStreamSynchronize(X[s]->stream));
+    int rc = collect_batch(X[s], b.count, b.cap, cut_ends, ids, out_base + b.first,
+                           caps + b.first, sums ? sums + b.first : nullptr);
+    b.count = 0;
+    if (rc) c->err = X[s]->err;
+    return rc;
+  };
+  uint64_t f = 0;
+  int slot = 0;
+  while (f < n) {
+    int rc = finish(slot);  // the slot's buffers are free again
+    if (rc) return rc;
+    Batch& b = B[slot];
+    b.first = f;
+    b.offs.clear();
+    uint64_t tot = 0;
+    while (f < n && (b.offs.empty() || tot + lens[f] <= batch_bytes) && b.offs.size() < 65536) {
+      b.offs.push_back(tot);
+      tot += (lens[f] + 255) & ~uint64_t(255);
+      f++;
+    }
+    b.count = f - b.first;
+    b.total = tot;
+    hbx_ctx* x = X[slot];
+    HBX_TRY(c, x->h_stage.ensure(tot + 65536));
+    HBX_TRY(c, x->d_stage.ensure(tot + 65536));
+    rc = read_files(b.count, paths + b.first, lens + b.first, b.offs.data(), x->h_stage.as<uint8_t>(),
+                    io_threads, c->err);
+    if (rc) {
+      b.count = 0;
+      (void)finish(slot ^ 1);
+      return rc;
+    }
+    HBX_TRY(c, hipMemcpyAsync(x->d_stage.p, x->h_stage.p, tot, hipMemcpyHostToDevice, x->stream));
+    rc = enqueue_batch(x, x->d_stage.p, b.count, b.offs.data(), lens + b.first, &b.cap);
+    if (rc) {
+      c->err = x->err;
+      b.count = 0;
+      (void)finish(slot ^ 1);
+      return rc;
+    }
+    slot ^= 1;
+  }
+  int rc0 = finish(slot);
+  int rc1 = finish(slot ^ 1);
+  return rc0 ? rc0 : rc1;
 }
 
 int hbx_memcpy_h2d_async(hbx_ctx* c, void* d, const void* h, uint64_t n) {

@@ -627,7 +627,11 @@ __device__ __forceinline__ uint32_t msg_word(uint32_t widx, uint32_t lo, uint32_
 // 64 chunks per wave, one per lane).  `c` is the lane's chunk start.  Reads
 // stay within the chunk + 64 bytes (HBX_ARENA_SLACK): every dword that holds
 // chunk bytes, and never more than 63 bytes past the chunk end.
+#ifndef HBX_MD5_RING
+#define HBX_MD5_RING 8
+#endif
 __device__ void md5_block_id(const uint8_t* c, uint32_t len, uint32_t (&h)[4]) {
+  constexpr int RING = HBX_MD5_RING;  // blocks of prefetch (16 VGPRs each)
   md5_init(h);
   const uint32_t sh = (uint32_t)reinterpret_cast<uintptr_t>(c) & 3u;
   const uint32_t* va = reinterpret_cast<const uint32_t*>(c - sh);  // raw R[r] = va[r]
@@ -636,15 +640,15 @@ __device__ void md5_block_id(const uint8_t* c, uint32_t len, uint32_t (&h)[4]) {
   const uint32_t nlast = nfull ? nfull - 1u : 0u;  // clamp prefetches to this block
   // Full blocks.  Block b needs raw dwords R[16b-2 .. 16b+15]: 16 loaded with
   // it (4 x dwordx4 at va+64b, never below the chunk start) plus 2 carried.
-  // Loads run 4 blocks ahead through a 4-deep register ring.  The loop is
+  // Loads run RING blocks ahead through a register ring.  The loop is
   // wave-uniform (bound = the wave's longest chunk, lanes past their own end
   // compute and discard) so the compiler keeps exact vmcnt counting and never
   // drains the ring at a divergent join.
   const uint32_t nmax = wave_max_all(nfull);
   uint32_t c0 = 0u, c1 = 0u;  // R[16b-2], R[16b-1]
-  u32x4 ring[4][4];
+  u32x4 ring[RING][4];
 #pragma unroll
-  for (int r = 0; r < 4; r++) {
+  for (int r = 0; r < RING; r++) {
     const u32x4* src = reinterpret_cast<const u32x4*>(va + 16u * min((uint32_t)r, nlast));
 #pragma unroll
     for (int i = 0; i < 4; i++) ring[r][i] = __builtin_nontemporal_load(src + i);
@@ -673,7 +677,7 @@ __device__ void md5_block_id(const uint8_t* c, uint32_t len, uint32_t (&h)[4]) {
     // refill only after the slot's registers are consumed: the load then
     // reuses them and the ring needs no copies at the loop back-edge
     if (refill) {
-      const u32x4* src = reinterpret_cast<const u32x4*>(va + 16u * min(b + 4u, nlast));
+      const u32x4* src = reinterpret_cast<const u32x4*>(va + 16u * min(b + (uint32_t)RING, nlast));
 #pragma unroll
       for (int i = 0; i < 4; i++) ring[r][i] = __builtin_nontemporal_load(src + i);
     }
@@ -685,12 +689,12 @@ __device__ void md5_block_id(const uint8_t* c, uint32_t len, uint32_t (&h)[4]) {
     for (int i = 0; i < 4; i++) h[i] = live ? t[i] : h[i];
   };
   uint32_t b = 0;
-  for (; b + 4u <= nmax; b += 4u) {
+  for (; b + (uint32_t)RING <= nmax; b += (uint32_t)RING) {
 #pragma unroll
-    for (int r = 0; r < 4; r++) block(r, b + (uint32_t)r, true);
+    for (int r = 0; r < RING; r++) block(r, b + (uint32_t)r, true);
   }
 #pragma unroll
-  for (int r = 0; r < 3; r++) {
+  for (int r = 0; r < RING - 1; r++) {
     if (b + (uint32_t)r < nmax) block(r, b + (uint32_t)r, false);
   }
   // tail: remaining message bytes + 0x80 + zeros + 64-bit bit length

@@ -190,6 +190,20 @@ class Engine:
                                                  ctypes.c_void_p(int(h_src)), int(nbytes)),
                     "hbx_memcpy_h2d_async")
 
+    def store_paths(self, paths: Sequence[Union[str, os.PathLike]], io_threads: int = 16,
+                    batch_bytes: int = 1 << 30) -> List[FileChunks]:
+        """storeFile for many files on disk, end to end: the library reads them
+        into pinned memory on ``io_threads`` threads and overlaps reading the
+        next batch with the copy + kernels of the current one."""
+        enc = [os.fsencode(p) for p in paths]
+        lens = np.array([os.stat(p).st_size for p in enc], np.uint64)
+        arr = (ctypes.c_char_p * max(len(enc), 1))(*enc)
+        caps, base, cuts, ids, sums = self._alloc_out(lens)
+        self._check(self._L.hbx_store_paths(self._ctx, len(enc), ctypes.cast(arr, ctypes.c_void_p),
+                                            _p(lens), _p(cuts), _p(ids), _p(base), _p(caps), sums,
+                                            int(io_threads), int(batch_bytes)), "hbx_store_paths")
+        return self._unpack(lens, caps, base, cuts, ids, sums)
+
     def store_file(self, path: Union[str, os.PathLike]) -> FileChunks:
         """storeFile(path) for a regular file on disk (store.go:84-199)."""
         with open(path, "rb") as fh:

@@ -14,6 +14,7 @@
  *   hbx_chunk_hash_device the same, files already resident in device memory
  *   hbx_submit_device /   asynchronous form (one batch in flight per context)
  *   hbx_wait
+ *   hbx_store_paths       storeFile(path) for many files on disk, end to end
  *   hbx_block_id          HashboxBlock.HashData for an arbitrary block with
  *                         links (pkg/core/block.go:96-111), e.g. the
  *                         FileChainBlock of store.go:187-188
@@ -111,6 +112,18 @@ int hbx_submit_device(hbx_ctx *ctx, const void *d_arena, uint64_t n_files,
                       uint8_t *ids, const uint64_t *out_base, const uint64_t *caps,
                       hbx_file_summary *summaries);
 int hbx_wait(hbx_ctx *ctx);
+
+/* Files on disk, end to end (storeFile over a list of paths, store.go:84-199
+ * with the tree walk left to the caller): io_threads read the files straight
+ * into pinned staging, batches of up to batch_bytes alternate between two
+ * HIP streams so reading batch b+1 overlaps the H2D copy and kernels of
+ * batch b.  lens[i] must be the file sizes (stat); a file that cannot be
+ * read in full fails the call with HBX_ERR_IO.  Outputs as
+ * hbx_chunk_hash_batch. */
+int hbx_store_paths(hbx_ctx *ctx, uint64_t n_files, const char *const *paths,
+                    const uint64_t *lens, uint64_t *cut_ends, uint8_t *ids,
+                    const uint64_t *out_base, const uint64_t *caps, hbx_file_summary *summaries,
+                    uint32_t io_threads, uint64_t batch_bytes);
 
 /* MD5(BE32(n_links) || links || BE32(len) || data) on the device. */
 int hbx_block_id(hbx_ctx *ctx, const uint8_t *links, uint32_t n_links, const uint8_t *data,

@@ -135,3 +135,24 @@ def test_kat_block_ids_on_device(engine):
     for r, g in zip(kat["block_id"], got):
         assert g.ids[0].tobytes().hex() == r["id"] if g.n_chunks else r["data_hex"] == ""
         assert engine.block_id(bytes.fromhex(r["data_hex"])).hex() == r["id"]
+
+
+def test_store_paths_end_to_end(engine, oracle, tmp_path):
+    """Files on disk -> pinned -> HBM -> results, in small batches so the
+    two-stream double buffering and batch boundaries are exercised."""
+    sizes = [0, 1, 4096, 2 * MIN + 1, 3 * MAXB + 7, 700_001, 5 * MIN, 12345, 9 * 1024 * 1024]
+    paths, datas = [], []
+    for i, n in enumerate(sizes * 3):
+        x = oracle.random_bytes(n, 900 + i)
+        p = tmp_path / f"f{i:03d}.bin"
+        p.write_bytes(x.tobytes())
+        paths.append(str(p))
+        datas.append(x)
+    got = engine.store_paths(paths, io_threads=4, batch_bytes=64 << 20)
+    for x, g in zip(datas, got):
+        _check(g, oracle.store_file(x, fast=True))
+    # a missing file fails loudly
+    import pytest as _pt
+    from hashbox_amd import HbxError
+    with _pt.raises((HbxError, FileNotFoundError)):
+        engine.store_paths([str(tmp_path / "missing.bin")])

@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""BASELINE config 5: 100 k mixed small files (log-uniform 4 KiB-4 MiB, seed 5)
+end to end: files on disk (tmpfs, resident) -> pinned host memory (16 reader
+threads) -> H2D -> K1..K4 -> D2H, with reading of batch b+1 overlapped with
+the copy + kernels of batch b (hbx_store_paths).  CPU beside it: the oracle's
+literal storeFile loop on 16 threads over a sample of the same files (read
+from the same tmpfs).  Spot-checks the GPU results against the oracle.
+
+Run on the GPU box:  python tools/bench_config5.py [--files 100000] [--dir /dev/shm/hbx5]
+Prints one JSON line.
+"""
+import argparse
+import json
+import os
+import shutil
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+
+def make_files(d, n, seed):
+    g = np.random.Generator(np.random.PCG64(seed))
+    sizes = np.exp(g.uniform(np.log(4096), np.log(4 << 20), n)).astype(np.int64)
+    pool = g.integers(0, 256, 512 << 20, dtype=np.uint8)
+    offs = g.integers(0, pool.size - (4 << 20), n)
+    os.makedirs(d, exist_ok=True)
+    paths = []
+    for i in range(n):
+        p = os.path.join(d, f"{i // 1000:03d}_{i:06d}.bin")
+        with open(p, "wb") as fh:
+            fh.write(pool[offs[i]:offs[i] + sizes[i]].tobytes())
+        paths.append(p)
+    return paths, sizes
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--files", type=int, default=100_000)
+    ap.add_argument("--dir", default="/dev/shm/hbx_config5")
+    ap.add_argument("--io-threads", type=int, default=16)
+    ap.add_argument("--batch-mib", type=int, default=1024)
+    ap.add_argument("--cpu-sample", type=int, default=10_000)
+    ap.add_argument("--keep", action="store_true")
+    a = ap.parse_args()
+    import torch  # noqa: F401  (one HIP runtime per process: see hashbox_amd/_lib.py)
+    from hashbox_amd import Engine
+    from oracle import oracle as O
+
+    t0 = time.time()
+    paths, sizes = make_files(a.dir, a.files, 5)
+    t_make = time.time() - t0
+    total = int(sizes.sum())
+    eng = Engine(0)
+    try:
+        eng.store_paths(paths[:2000], a.io_threads, a.batch_mib << 20)  # warm-up
+        t0 = time.time()
+        res = eng.store_paths(paths, a.io_threads, a.batch_mib << 20)
+        t_gpu = time.time() - t0
+        # CPU oracle on a sample (files read from the same tmpfs, 16 threads)
+        rng = np.random.Generator(np.random.PCG64(6))
+        pick = np.sort(rng.choice(a.files, min(a.cpu_sample, a.files), replace=False))
+        t0 = time.time()
+        datas = [np.fromfile(paths[i], dtype=np.uint8) for i in pick]
+        ref = O.store_batch_mt(datas, a.io_threads)
+        t_cpu = time.time() - t0
+        sample_bytes = int(sizes[pick].sum())
+        bad = sum(1 for i, r in zip(pick, ref)
+                  if not (np.array_equal(res[i].cut_ends, r.cut_ends)
+                          and np.array_equal(res[i].ids, r.ids)))
+        n_chunks = sum(r.n_chunks for r in res)
+        print(json.dumps({
+            "config": "BASELINE configs[4]: 100k mixed small files end to end",
+            "files": a.files, "bytes": total, "chunks": n_chunks,
+            "storage": f"{a.dir} (tmpfs: page-cache resident, no device IO)",
+            "e2e_seconds": round(t_gpu, 3), "e2e_gibs": round(total / t_gpu / (1 << 30), 3),
+            "e2e_files_per_s": round(a.files / t_gpu, 1),
+            "io_threads": a.io_threads, "batch_mib": a.batch_mib,
+            "cpu_oracle": {"files": len(pick), "bytes": sample_bytes, "threads": a.io_threads,
+                           "seconds": round(t_cpu, 3),
+                           "gibs": round(sample_bytes / t_cpu / (1 << 30), 3),
+                           "includes": "file reads + literal storeFile loop + MD5"},
+            "sample_mismatches": bad, "make_seconds": round(t_make, 1)}), flush=True)
+    finally:
+        eng.close()
+        if not a.keep:
+            shutil.rmtree(a.dir, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()
