@@ -1,12 +1,19 @@
 #!/usr/bin/env python3
 """Benchmark: device-resident rollsum split + block-ID hashing on MI355X.
 
-Workload (BASELINE.json configs[1]): 64 x 128 MiB uniform random buffers per
-GPU, resident in HBM before the timed region.  One step = one pass of the hot
-path over that batch: K1 window-digest scan -> K2 cut chain -> K3 block MD5 ->
-K4 content ids -> D2H of cut lists + block IDs.  Files shard by GPU (weak
-scaling: each rank owns its own 64-file batch, no collective on the data path;
-the only collectives are the start/end barrier and the max-time reduction).
+Workload (BASELINE.json configs[1]): batches of 64 x 128 MiB uniform random
+buffers per GPU, resident in HBM before the timed region.  One step = one
+batch through the whole hot path: K1 window-digest scan -> K2 cut chain ->
+K3 block MD5 -> K4 content ids -> D2H of cut lists + block IDs.  Steps
+pipeline on one engine context: K3 is time-sliced (--md5-slice blocks per
+chain per launch), so each step's chunks join the MD5 chains still in flight
+and no batch waits behind another's longest chunk.  The timed region runs K
+steps from an empty pipeline to a fully drained one (every batch's results
+collected); `value` = K batches / that time.  --md5-slice 0 runs every batch
+alone (one K3 launch per batch: the single-batch latency path).  Files shard
+by GPU (weak scaling: each rank owns its own batches, no collective on the
+data path; the only collectives are the start/end barrier and the max-time
+reduction).
 
 Prints ONE JSON line on rank 0.  Multi-GPU:
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -34,8 +41,8 @@ GIB = 1 << 30
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--files", type=int, default=64)
     ap.add_argument("--file-mib", type=int, default=128)
     ap.add_argument("--seed", type=int, default=1000)
@@ -43,15 +50,35 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-files", type=int, default=32,
                     help="files of the batch timed on the CPU oracle (bounded sample)")
-    ap.add_argument("--inflight", type=int, default=1,
-                    help="batches in flight (one engine context + one resident batch each); "
-                         "1 = every step runs alone")
+    ap.add_argument("--md5-slice", type=int, default=16384,
+                    help="K3 time slice in 64-B MD5 blocks per chain per launch (0 = each batch "
+                         "hashed alone in one launch)")
+    ap.add_argument("--arenas", type=int, default=0,
+                    help="distinct resident batches (default: the pipeline depth the slice "
+                         "schedule needs, so no step forces a drain)")
     ap.add_argument("--e2e", action="store_true",
                     help="host-inclusive mode: files in pinned host memory, H2D of batch i+1 "
                          "overlapped with the kernels of batch i (two contexts)")
     ap.add_argument("--check", action="store_true",
                     help="verify the first file of the batch against the oracle")
     return ap.parse_args()
+
+
+def measured_traffic(kernel, nf, fbytes):
+    """HBM bytes per launch of `kernel` from the newest committed PMC pass of
+    this same workload (profiles/*_traffic.json, written by
+    tools/pmc_traffic.py from a separate rocprofv3 --pmc FETCH_SIZE run: PMC
+    counters cannot be read inside this timed run)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
+    if not files or (nf, fbytes) != (64, 128 << 20):
+        return None, None
+    d = json.load(open(files[-1]))
+    k = d.get("kernels", {}).get(kernel)
+    if not k:
+        return None, None
+    return int(k["hbm_bytes"]), (os.path.relpath(files[-1], ROOT) +
+                                 ("" if k.get("calibrated") else " (uncalibrated access width)"))
 
 
 def cpu_baseline(host_files, threads):
@@ -84,7 +111,7 @@ def run_e2e(a, local):
     nf, fbytes = a.files, a.file_mib << 20
     lens = [fbytes] * nf
     offs, total = pack_arena_layout(lens)
-    engs = [Engine(local), Engine(local)]
+    engs = [Engine(local, md5_slice=0), Engine(local, md5_slice=0)]
     arenas = [torch.empty(total, dtype=torch.uint8, device=f"cuda:{local}") for _ in range(2)]
     hp = ctypes.c_void_p()
     assert engs[0]._L.hbx_alloc_pinned(total, ctypes.byref(hp)) == 0
@@ -148,44 +175,48 @@ def main():
     nf, fbytes = a.files, a.file_mib << 20
     lens = [fbytes] * nf
     offs, total = pack_arena_layout(lens)
-    D = max(1, a.inflight)
+    B = max(0, a.md5_slice)
+    # launches a batch needs before its chains are all hashed; a batch can be
+    # collected without a forced drain once `need` newer steps have launched
+    nfull = (min(fbytes, 8 << 20) + 8) >> 6
+    need = 1 if B == 0 else -(-nfull // B)
+    R = a.arenas if a.arenas > 0 else need + 1
     # synthetic uniform random bytes, generated on the device (per-rank seed);
-    # one resident batch per in-flight context
+    # R distinct resident batches, batch j reads arena j % R
     g = torch.Generator(device=dev)
     g.manual_seed(a.seed + 7919 * rank)
     arenas = []
-    for _ in range(D):
+    for _ in range(R):
         t = torch.empty(total, dtype=torch.uint8, device=dev)
         t.random_(0, 256, generator=g)
         arenas.append(t)
     arena = arenas[0]
     torch.cuda.synchronize()
 
-    engs = [Engine(local) for _ in range(D)]
-    eng = engs[0]
+    eng = Engine(local, md5_slice=B)
+    # single-batch latency (one batch alone, synchronous call), untimed
+    for _ in range(2):
+        eng.chunk_hash_device(arena.data_ptr(), offs, lens)
+    latency = eng.stage_times()
 
-    res = None
-    for i in range(a.warmup):
-        engs[i % D].submit_device(arenas[i % D].data_ptr(), offs, lens)
-        res = engs[i % D].wait()
+    def run(steps):
+        """steps batches through the pipeline, fully drained; last result."""
+        last = None
+        for j in range(steps):
+            if eng.pending() >= R:  # arena j % R is free once its batch is collected
+                last = eng.wait()
+            eng.submit_device(arenas[j % R].data_ptr(), offs, lens)
+        while eng.pending():
+            last = eng.wait()
+        return last
 
-    stage = np.zeros(5)
+    run(a.warmup)
+    eng.stage_totals(reset=True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    results = {}
-    for j in range(a.steps):
-        e = engs[j % D]
-        if j >= D:  # this context's previous batch must be collected first
-            results[j - D] = e.wait()
-            stage += e.stage_times()
-        e.submit_device(arenas[j % D].data_ptr(), offs, lens)
-    for j in range(max(0, a.steps - D), a.steps):
-        e = engs[j % D]
-        results[j] = e.wait()
-        stage += e.stage_times()
-    res = results[a.steps - 1] if a.steps else res
+    res = run(a.steps)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist:
@@ -195,7 +226,7 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    stage /= max(a.steps, 1)
+    tot_ms, tot_n = eng.stage_totals()
     n_chunks = sum(r.n_chunks for r in res)
     longest = max(int(np.max(np.diff(np.concatenate([[0], r.cut_ends]).astype(np.int64))))
                   for r in res if r.n_chunks)
@@ -203,7 +234,7 @@ def main():
     check = None
     if a.check and rank == 0:
         from oracle import oracle as O
-        h0 = arenas[(a.steps - 1) % D][int(offs[0]):int(offs[0]) + fbytes].cpu().numpy()
+        h0 = arenas[(a.steps - 1) % R][int(offs[0]):int(offs[0]) + fbytes].cpu().numpy()
         ref = O.store_file(h0, fast=True)
         check = bool(np.array_equal(ref.cut_ends, res[0].cut_ends)
                      and np.array_equal(ref.ids, res[0].ids))
@@ -218,10 +249,21 @@ def main():
     batch_bytes = nf * fbytes
     total_bytes = batch_bytes * world * a.steps
     value = total_bytes / el / GIB
-    names = ["k1_digest_scan", "k2_cut_chain", "k3_block_md5", "k4_content_id"]
-    dom = int(np.argmax(stage[:4]))
-    achieved = batch_bytes / (stage[dom] * 1e-3) / 1e9  # GB/s, algorithmic bytes = input bytes
-    k1_gbs = batch_bytes / (stage[0] * 1e-3) / 1e9 if stage[0] > 0 else 0.0
+    names = ["k1_digest_scan", "k2_cut_chain", "k2c_chain_plan", "k3_block_md5", "k4_content_id"]
+    kernel_of = {"k1_digest_scan": "hbx_k1_digest_scan_dma", "k2_cut_chain": "hbx_k2_cut_chain",
+                 "k2c_chain_plan": "hbx_k2c_plan", "k3_block_md5": "hbx_k3_block_md5",
+                 "k4_content_id": "hbx_k4_content_id"}
+    avg_ms = tot_ms / np.maximum(tot_n, 1)
+    dom = int(np.argmax(tot_ms))
+    # algorithmic bytes per launch: every input byte is scanned once by K1 and
+    # MD5-hashed once by K3, so a kernel's average launch covers
+    # (bytes of the K batches) / (its launches); K2/K2c/K4 are priced the same
+    per_launch = a.steps * batch_bytes / max(int(tot_n[dom]), 1)
+    achieved = per_launch / (avg_ms[dom] * 1e-3) / 1e9
+    traffic, traffic_src = measured_traffic(kernel_of[names[dom]], nf, fbytes)
+    k1_gbs = (a.steps * batch_bytes / max(int(tot_n[0]), 1)) / (avg_ms[0] * 1e-3) / 1e9 \
+        if tot_ms[0] > 0 else 0.0
+    k3_bps = a.steps * batch_bytes / (tot_ms[3] * 1e-3) if tot_ms[3] > 0 else 0.0
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -234,29 +276,40 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic: uniform random bytes generated on the device (torch Generator), "
-                "resident in HBM before timing",
-        "config": {"workload": f"{nf} x {a.file_mib} MiB random buffers per GPU, rollsum split + "
-                               "MD5 block IDs + file content ids, device-resident (configs[1])",
-                   "files_per_gpu": nf, "file_bytes": fbytes, "chunks_per_gpu": n_chunks,
-                   "longest_chunk_bytes": longest,
+        "data": f"synthetic: uniform random bytes generated on the device (torch Generator), "
+                f"{R} distinct resident batches, resident in HBM before timing",
+        "config": {"workload": f"{nf} x {a.file_mib} MiB random buffers per GPU per step, rollsum "
+                               "split + MD5 block IDs + file content ids, device-resident "
+                               "(configs[1])",
+                   "files_per_step": nf, "file_bytes": fbytes, "chunks_per_step": n_chunks,
+                   "longest_chunk_bytes": longest, "md5_slice_blocks": B,
+                   "pipeline_depth": R, "launches_per_batch": need,
                    "parallelism": f"file-sharded x{world} (independent HIP streams, no data-path "
-                                  "collective)",
-                   "batches_in_flight": D},
+                                  "collective)"},
         "roofline": {"kernel": names[dom], "bound": "hbm", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                     "traffic": None},
-        "stages_ms": {n: round(float(v), 4) for n, v in zip(names + ["batch"], stage)},
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "launches": int(tot_n[dom]), "avg_launch_ms": round(float(avg_ms[dom]), 4),
+                     "algorithmic_bytes_per_launch": int(per_launch)},
+        # K3's real limit is VALU issue of the serial MD5 chains (~5.55 lane-ops
+        # per byte, 355 VALU per 64-B block); peak = 256 CU x 4 SIMD x 16 lanes x 2.4 GHz
+        "k3_valu": {"achieved_tops": round(k3_bps * 355 / 64 / 1e12, 3),
+                    "peak_tops": round(256 * 4 * 16 * 2.4e9 / 1e12, 2),
+                    "frac": round(k3_bps * 355 / 64 / (256 * 4 * 16 * 2.4e9), 4)},
+        "kernel_ms_per_step": {n: round(float(v) / a.steps, 4) for n, v in zip(names, tot_ms)},
+        "kernel_launches": {n: int(v) for n, v in zip(names, tot_n)},
         "k1_roofline": {"achieved": round(k1_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(k1_gbs / HBM_PEAK_GBS, 4)},
+        "single_batch": {"ms": round(float(latency[4]), 3),
+                         "gibs": round(batch_bytes / GIB / (float(latency[4]) * 1e-3), 3),
+                         "stages_ms": [round(float(x), 3) for x in latency]},
         "cpu_baseline": cpu,
     }
     if check is not None:
         out["check_vs_oracle"] = check
     if rank == 0:
         print(json.dumps(out), flush=True)
-    for e in engs:
-        e.close()
+    eng.close()
     if dist:
         dist.destroy_process_group()
 

@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -85,16 +86,35 @@ struct PinBuf {
   }
 };
 
-struct Pending {
-  bool active = false;
-  uint64_t n_files = 0;
-  uint64_t total_cap = 0;
+// Per-kernel cumulative timing: one event pair per launch, harvested once the
+// end event has completed (hbx_stage_totals).
+struct TimedLaunch {
+  hipEvent_t a, b;
+  int stage;
+};
+
+// One submitted batch.  Its device buffers live until its results are
+// collected: K3 writes BlockIDs into d_ids across several launches when the
+// MD5 stage is time-sliced.
+struct Batch {
+  uint64_t n = 0, caps = 0;
+  std::vector<uint64_t> cut_base;
+  DevBuf d_meta, d_cuts, d_count, d_ids, d_cid, d_ctype;
+  PinBuf h_meta, h_res;
   uint64_t* cut_ends = nullptr;
   uint8_t* ids = nullptr;
-  const uint64_t* out_base = nullptr;
-  const uint64_t* caps = nullptr;
-  hbx_file_summary* summaries = nullptr;
-  std::vector<uint64_t> out_base_copy, caps_copy;
+  hbx_file_summary* sums = nullptr;
+  std::vector<uint64_t> out_base, capv;
+  uint32_t need = 1, done = 0;  // K3 launches its chains need / have had
+  bool finalized = false;
+  hipEvent_t ev[5] = {};  // K1 start | K1 end | K2 end | plan+K3 end (first) | results ready
+  void release() {
+    for (DevBuf* d : {&d_meta, &d_cuts, &d_count, &d_ids, &d_cid, &d_ctype}) d->release();
+    h_meta.release();
+    h_res.release();
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+  }
 };
 
 }  // namespace
@@ -102,26 +122,32 @@ struct Pending {
 struct hbx_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev[5] = {};
   std::mutex mu;
   std::string err;
-  uint32_t tile_iters = 64;  // K1 tile = 64 x 64 KiB (measured best: fewer halo primes)
-  uint32_t k1_dma = 1;     // K1 lands tiles in LDS by DMA (HBX_K1_DMA=0: register prefetch)
-  uint32_t md5_wgs = 256;  // K3 grid: one 512-thread workgroup per CU (set from the device)
+  uint32_t tile_iters = 64;   // K1 tile = 64 x 64 KiB (measured best: fewer halo primes)
+  uint32_t k1_dma = 1;        // K1 lands tiles in LDS by DMA (HBX_K1_DMA=0: register prefetch)
+  uint32_t md5_wgs = 256;     // K3 grid: one 512-thread workgroup per CU (set from the device)
+  uint32_t md5_slice = 16384; // K3 time slice: full MD5 blocks per chain per launch (0 = unlimited)
   float stage_ms[5] = {0, 0, 0, 0, 0};
 
-  // host-side plan of the current batch
-  std::vector<uint64_t> h_slice_base, h_cut_base;
+  // host-side plan scratch
+  std::vector<uint64_t> h_slice_base;
   std::vector<uint2> h_tiles;
 
-  DevBuf d_meta;  // file_off | file_len | slice_base | cut_base | tiles
-  DevBuf d_ssum, d_cuts, d_count, d_ids, d_cid, d_ctype, d_work, d_ctl;
-  DevBuf d_stage;  // host-input arena
-  DevBuf d_msg;    // hbx_block_id message
-  PinBuf h_meta, h_res;
+  DevBuf d_ssum;            // K1 -> K2 slice summaries (shared: consumed in stream order)
+  DevBuf d_tab[2], d_tctl[2];  // MD5 chain tables (ping-pong) + their counts
+  int tab_cur = -1;         // table holding the last launch's chains (-1: none in flight)
+  DevBuf d_stage;           // host-input arena
+  DevBuf d_msg;             // hbx_block_id message
   PinBuf h_stage;           // hbx_store_paths: pinned landing buffer for file reads
   hbx_ctx* twin = nullptr;  // hbx_store_paths: second context (double buffering)
-  Pending pend;
+
+  std::deque<Batch*> pending;  // submitted, not yet collected (FIFO)
+  std::vector<Batch*> pool;
+  std::vector<TimedLaunch> open_t;
+  std::vector<hipEvent_t> ev_pool;
+  double tot_ms[5] = {0, 0, 0, 0, 0};
+  uint64_t tot_n[5] = {0, 0, 0, 0, 0};
 
   int fail(int code, const std::string& m) {
     err = m;
@@ -131,6 +157,15 @@ struct hbx_ctx {
     if (e == hipSuccess) return HBX_OK;
     err = std::string(what) + ": " + hipGetErrorString(e);
     return HBX_ERR_HIP;
+  }
+  hipEvent_t event() {
+    if (!ev_pool.empty()) {
+      hipEvent_t e = ev_pool.back();
+      ev_pool.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    return hipEventCreate(&e) == hipSuccess ? e : nullptr;
   }
 };
 
@@ -144,7 +179,52 @@ namespace {
 
 inline uint64_t max_chunks(uint64_t len) { return len / HBX_MIN_BLOCK_SIZE + 1; }
 
-// Layout of the pinned result block after a batch.
+// Grow a buffer the stream may still be using: drain the stream first.
+int ensure_shared(hbx_ctx* c, DevBuf& b, size_t n) {
+  if (n <= b.cap && b.p) return HBX_OK;
+  HBX_TRY(c, hipStreamSynchronize(c->stream));
+  HBX_TRY(c, b.ensure(n));
+  return HBX_OK;
+}
+
+// Bracket one launch with an event pair for hbx_stage_totals.
+struct StageTimer {
+  hbx_ctx* c;
+  TimedLaunch t;
+  StageTimer(hbx_ctx* ctx, int stage) : c(ctx) {
+    t.stage = stage;
+    t.a = c->event();
+    t.b = c->event();
+    if (t.a) (void)hipEventRecord(t.a, c->stream);
+  }
+  ~StageTimer() {
+    if (t.a && t.b && hipEventRecord(t.b, c->stream) == hipSuccess) {
+      c->open_t.push_back(t);
+    } else {
+      if (t.a) c->ev_pool.push_back(t.a);
+      if (t.b) c->ev_pool.push_back(t.b);
+    }
+  }
+};
+
+void harvest_timings(hbx_ctx* c) {
+  size_t keep = 0;
+  for (size_t i = 0; i < c->open_t.size(); i++) {
+    TimedLaunch& t = c->open_t[i];
+    float ms = 0.f;
+    if (hipEventQuery(t.b) == hipSuccess && hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) {
+      c->tot_ms[t.stage] += ms;
+      c->tot_n[t.stage] += 1;
+      c->ev_pool.push_back(t.a);
+      c->ev_pool.push_back(t.b);
+    } else {
+      c->open_t[keep++] = t;
+    }
+  }
+  c->open_t.resize(keep);
+}
+
+// Layout of the pinned result block of a batch.
 struct ResLayout {
   size_t counts, cuts, ids, cid, ctype, total;
 };
@@ -165,68 +245,198 @@ ResLayout res_layout(uint64_t n_files, uint64_t total_cap) {
   return r;
 }
 
-// Plan + enqueue one device batch.  Results land in ctx->h_res at the next
-// stream sync.
-int enqueue_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* offs,
-                  const uint64_t* lens, uint64_t* total_cap_out) {
-  if (n == 0) {
-    *total_cap_out = 0;
-    return HBX_OK;
+Batch* acquire_batch(hbx_ctx* c) {
+  Batch* b;
+  if (!c->pool.empty()) {
+    b = c->pool.back();
+    c->pool.pop_back();
+  } else {
+    b = new Batch();
+    for (auto& e : b->ev) {
+      if (hipEventCreate(&e) != hipSuccess) {
+        b->release();
+        delete b;
+        return nullptr;
+      }
+    }
   }
+  b->n = b->caps = 0;
+  b->need = 1;
+  b->done = 0;
+  b->finalized = false;
+  b->cut_ends = nullptr;
+  b->ids = nullptr;
+  b->sums = nullptr;
+  return b;
+}
+
+// K4 + D2H of one batch whose chains are all hashed.
+int finalize_batch(hbx_ctx* c, Batch* b) {
+  hipStream_t s = c->stream;
+  b->finalized = true;
+  if (b->n) {
+    const uint64_t n = b->n;
+    const uint64_t* d_cb = b->d_meta.as<uint64_t>() + 3 * n;
+    {
+      StageTimer t(c, 4);
+      hipLaunchKernelGGL(hbx_k4_content_id, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, s,
+                         (uint32_t)n, d_cb, b->d_count.as<uint32_t>(), b->d_ids.as<uint32_t>(),
+                         b->d_cid.as<uint32_t>(), b->d_ctype.as<int32_t>());
+    }
+    HBX_TRY(c, hipGetLastError());
+    const ResLayout rl = res_layout(n, b->caps);
+    uint8_t* hr = b->h_res.as<uint8_t>();
+    HBX_TRY(c, hipMemcpyAsync(hr + rl.counts, b->d_count.p, n * 4, hipMemcpyDeviceToHost, s));
+    HBX_TRY(c, hipMemcpyAsync(hr + rl.cuts, b->d_cuts.p, b->caps * 8, hipMemcpyDeviceToHost, s));
+    HBX_TRY(c, hipMemcpyAsync(hr + rl.ids, b->d_ids.p, b->caps * 16, hipMemcpyDeviceToHost, s));
+    HBX_TRY(c, hipMemcpyAsync(hr + rl.cid, b->d_cid.p, n * 16, hipMemcpyDeviceToHost, s));
+    HBX_TRY(c, hipMemcpyAsync(hr + rl.ctype, b->d_ctype.p, n * 4, hipMemcpyDeviceToHost, s));
+  }
+  HBX_TRY(c, hipEventRecord(b->ev[4], s));
+  return HBX_OK;
+}
+
+// One MD5 launch: plan (carried chains + the new batch's chunks, if any) and
+// K3 with `budget` blocks per chain.  Afterwards every pending batch has had
+// one more launch; those whose chains are now guaranteed complete are
+// finalized.  A budget of kBudgetAll completes every chain in flight.
+int md5_launch(hbx_ctx* c, Batch* nb, const uint8_t* arena, uint32_t budget) {
+  hipStream_t s = c->stream;
+  uint64_t bound = 0;  // chains alive after this plan <= chunks of unfinalized batches
+  for (Batch* b : c->pending)
+    if (!b->finalized) bound += b->caps;
+  const int src = c->tab_cur;
+  const int dst = src < 0 ? 0 : src ^ 1;
+  int rc = ensure_shared(c, c->d_tab[dst], std::max<uint64_t>(bound, 64) * sizeof(Chain));
+  if (rc) return rc;
+  if ((rc = ensure_shared(c, c->d_tctl[dst], 256))) return rc;
+  const Chain* prev = src < 0 ? nullptr : c->d_tab[src].as<Chain>();
+  const uint32_t* prev_ctl = src < 0 ? nullptr : c->d_tctl[src].as<uint32_t>();
+  Chain* cur = c->d_tab[dst].as<Chain>();
+  uint32_t* ctl = c->d_tctl[dst].as<uint32_t>();
+  {
+    StageTimer t(c, 2);
+    if (nb && nb->n) {
+      const uint64_t n = nb->n;
+      const uint64_t* d_off = nb->d_meta.as<uint64_t>();
+      hipLaunchKernelGGL(hbx_k2c_plan, dim3(1), dim3(kPlanThreads), 0, s, (uint32_t)n, arena,
+                         d_off, d_off + 3 * n,
+                         nb->d_cuts.as<uint64_t>(), nb->d_count.as<uint32_t>(),
+                         nb->d_ids.as<uint32_t>(), prev, prev_ctl, cur, ctl, budget);
+    } else {
+      hipLaunchKernelGGL(hbx_k2c_plan, dim3(1), dim3(kPlanThreads), 0, s, 0u,
+                         static_cast<const uint8_t*>(nullptr), static_cast<const uint64_t*>(nullptr),
+                         static_cast<const uint64_t*>(nullptr), static_cast<const uint64_t*>(nullptr),
+                         static_cast<const uint32_t*>(nullptr), static_cast<uint32_t*>(nullptr), prev,
+                         prev_ctl, cur, ctl, budget);
+    }
+  }
+  HBX_TRY(c, hipGetLastError());
+  {
+    StageTimer t(c, 3);
+    hipLaunchKernelGGL(hbx_k3_block_md5, dim3(c->md5_wgs), dim3(kK3Threads), 0, s, cur,
+                       static_cast<const uint32_t*>(ctl), budget);
+  }
+  HBX_TRY(c, hipGetLastError());
+  c->tab_cur = dst;
+  if (nb) HBX_TRY(c, hipEventRecord(nb->ev[3], s));
+  bool any_left = false;
+  for (Batch* b : c->pending) {
+    if (b->finalized) continue;
+    b->done++;
+    if (budget == kBudgetAll || b->done >= b->need) {
+      if ((rc = finalize_batch(c, b))) return rc;
+    } else {
+      any_left = true;
+    }
+  }
+  if (!any_left) c->tab_cur = -1;  // every chain in flight is hashed
+  return HBX_OK;
+}
+
+// Plan + enqueue one device batch (K1, K2, first MD5 launch).  Results are
+// collected by wait_oldest in submission order.
+int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* offs,
+                 const uint64_t* lens, uint64_t* cut_ends, uint8_t* ids, const uint64_t* out_base,
+                 const uint64_t* caps, hbx_file_summary* sums, uint32_t budget) {
   if (n > 0xFFFFFFFFull) return c->fail(HBX_ERR_ARG, "too many files");
+  for (uint64_t f = 0; f < n; f++)
+    if (offs[f] % HBX_ARENA_ALIGN) return c->fail(HBX_ERR_ARG, "file offset not 16-byte aligned");
+  Batch* b = acquire_batch(c);
+  if (!b) return c->fail(HBX_ERR_HIP, "cannot create batch events");
+  b->n = n;
+  b->cut_ends = cut_ends;
+  b->ids = ids;
+  b->sums = sums;
+  b->out_base.assign(out_base, out_base + n);
+  b->capv.assign(caps, caps + n);
+  b->cut_base.resize(n);
   c->h_slice_base.resize(n);
-  c->h_cut_base.resize(n);
   c->h_tiles.clear();
-  uint64_t slices = 0, caps = 0;
+  uint64_t slices = 0, tcaps = 0, longest = 0;
   const uint64_t tile_bytes = (uint64_t)c->tile_iters * HBX_MIN_BLOCK_SIZE;
   for (uint64_t f = 0; f < n; f++) {
-    if (offs[f] % HBX_ARENA_ALIGN) return c->fail(HBX_ERR_ARG, "file offset not 16-byte aligned");
     const uint64_t N = lens[f];
+    longest = std::max(longest, N);
     c->h_slice_base[f] = slices;
-    c->h_cut_base[f] = caps;
-    const uint64_t cap = max_chunks(N);
-    caps += cap;
+    b->cut_base[f] = tcaps;
+    tcaps += max_chunks(N);
     if (N > 2ull * HBX_MIN_BLOCK_SIZE) {  // only files with split candidates scan
       slices += (N + kSlice - 1) / kSlice;
       const uint64_t nt = (N + tile_bytes - 1) / tile_bytes;
-      if (nt > 0xFFFFFFFFull) return c->fail(HBX_ERR_ARG, "file too large");
+      if (nt > 0xFFFFFFFFull) {
+        c->pool.push_back(b);
+        return c->fail(HBX_ERR_ARG, "file too large");
+      }
       for (uint64_t t = 0; t < nt; t++) c->h_tiles.push_back(make_uint2((uint32_t)f, (uint32_t)t));
     }
+  }
+  b->caps = tcaps;
+  // launches this batch's chains need: a chunk is <= min(longest file, MAX)
+  // bytes, i.e. <= nfull full message blocks, and each launch advances it by
+  // min(remaining, budget) blocks, finishing it in the launch where the
+  // remainder fits
+  const uint64_t nfull = (std::min<uint64_t>(longest, HBX_MAX_BLOCK_SIZE) + 8) >> 6;
+  b->need = budget == kBudgetAll ? 1u : (uint32_t)std::max<uint64_t>(1, (nfull + budget - 1) / budget);
+  c->pending.push_back(b);
+  hipStream_t s = c->stream;
+  if (n == 0) {
+    for (int i = 0; i < 4; i++) HBX_TRY(c, hipEventRecord(b->ev[i], s));
+    b->finalized = true;
+    HBX_TRY(c, hipEventRecord(b->ev[4], s));
+    return HBX_OK;
   }
   const uint64_t nt = c->h_tiles.size();
   // meta block: off | len | slice_base | cut_base | tiles
   const size_t meta_bytes = n * 8 * 4 + nt * sizeof(uint2);
-  HBX_TRY(c, c->h_meta.ensure(meta_bytes));
-  HBX_TRY(c, c->d_meta.ensure(meta_bytes));
-  uint64_t* hm = c->h_meta.as<uint64_t>();
+  HBX_TRY(c, b->h_meta.ensure(meta_bytes));
+  HBX_TRY(c, b->d_meta.ensure(meta_bytes));
+  uint64_t* hm = b->h_meta.as<uint64_t>();
   std::memcpy(hm, offs, n * 8);
   std::memcpy(hm + n, lens, n * 8);
   std::memcpy(hm + 2 * n, c->h_slice_base.data(), n * 8);
-  std::memcpy(hm + 3 * n, c->h_cut_base.data(), n * 8);
+  std::memcpy(hm + 3 * n, b->cut_base.data(), n * 8);
   if (nt) std::memcpy(hm + 4 * n, c->h_tiles.data(), nt * sizeof(uint2));
+  int rc = ensure_shared(c, c->d_ssum, (slices + 1) * sizeof(uint2));  // +1: dummy slot
+  if (rc) return rc;
+  HBX_TRY(c, b->d_cuts.ensure(tcaps * 8));
+  HBX_TRY(c, b->d_count.ensure(n * 4));
+  HBX_TRY(c, b->d_ids.ensure(tcaps * 16));
+  HBX_TRY(c, b->d_cid.ensure(n * 16));
+  HBX_TRY(c, b->d_ctype.ensure(n * 4));
+  HBX_TRY(c, b->h_res.ensure(res_layout(n, tcaps).total));
 
-  HBX_TRY(c, c->d_ssum.ensure((slices + 1) * sizeof(uint2)));  // +1: dummy slot
-  HBX_TRY(c, c->d_cuts.ensure(caps * 8));
-  HBX_TRY(c, c->d_count.ensure(n * 4));
-  HBX_TRY(c, c->d_ids.ensure(caps * 16));
-  HBX_TRY(c, c->d_work.ensure(caps * 8));
-  HBX_TRY(c, c->d_ctl.ensure(64));
-  HBX_TRY(c, c->d_cid.ensure(n * 16));
-  HBX_TRY(c, c->d_ctype.ensure(n * 4));
-  const ResLayout rl = res_layout(n, caps);
-  HBX_TRY(c, c->h_res.ensure(rl.total));
-
-  hipStream_t s = c->stream;
-  HBX_TRY(c, hipMemcpyAsync(c->d_meta.p, hm, meta_bytes, hipMemcpyHostToDevice, s));
-  const uint64_t* d_off = c->d_meta.as<uint64_t>();
+  HBX_TRY(c, hipMemcpyAsync(b->d_meta.p, hm, meta_bytes, hipMemcpyHostToDevice, s));
+  const uint64_t* d_off = b->d_meta.as<uint64_t>();
   const uint64_t* d_len = d_off + n;
   const uint64_t* d_sb = d_off + 2 * n;
   const uint64_t* d_cb = d_off + 3 * n;
   const uint2* d_tiles = reinterpret_cast<const uint2*>(d_off + 4 * n);
   const uint8_t* arena = static_cast<const uint8_t*>(d_arena);
 
-  HBX_TRY(c, hipEventRecord(c->ev[0], s));
+  HBX_TRY(c, hipEventRecord(b->ev[0], s));
   if (nt) {
+    StageTimer t(c, 0);
     if (c->k1_dma)
       hipLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3((uint32_t)nt), dim3(kK1Threads), 0, s,
                          arena, d_off, d_len, d_sb, d_tiles, c->tile_iters, c->d_ssum.as<uint2>(),
@@ -235,44 +445,25 @@ int enqueue_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* o
       hipLaunchKernelGGL(hbx_k1_digest_scan, dim3((uint32_t)nt), dim3(kK1Threads), 0, s, arena,
                          d_off, d_len, d_sb, d_tiles, c->tile_iters, c->d_ssum.as<uint2>(),
                          slices);
-    HBX_TRY(c, hipGetLastError());
   }
-  HBX_TRY(c, hipEventRecord(c->ev[1], s));
-  hipLaunchKernelGGL(hbx_k2_cut_chain, dim3((uint32_t)n), dim3(64), 0, s, arena, d_off, d_len,
-                     d_sb, c->d_ssum.as<uint2>(), d_cb,
-                     c->d_cuts.as<uint64_t>(), c->d_count.as<uint32_t>());
   HBX_TRY(c, hipGetLastError());
-  HBX_TRY(c, hipEventRecord(c->ev[2], s));
-  hipLaunchKernelGGL(hbx_k2c_plan, dim3(1), dim3(kPlanThreads), 0, s, (uint32_t)n, d_cb,
-                     c->d_cuts.as<uint64_t>(), c->d_count.as<uint32_t>(), c->d_work.as<uint2>(),
-                     c->d_ctl.as<uint32_t>());
+  HBX_TRY(c, hipEventRecord(b->ev[1], s));
+  {
+    StageTimer t(c, 1);
+    hipLaunchKernelGGL(hbx_k2_cut_chain, dim3((uint32_t)n), dim3(64), 0, s, arena, d_off, d_len,
+                       d_sb, c->d_ssum.as<uint2>(), d_cb, b->d_cuts.as<uint64_t>(),
+                       b->d_count.as<uint32_t>());
+  }
   HBX_TRY(c, hipGetLastError());
-  hipLaunchKernelGGL(hbx_k3_block_md5, dim3(c->md5_wgs), dim3(kK3Threads), 0, s, arena, d_off, d_cb,
-                     c->d_cuts.as<uint64_t>(), c->d_work.as<uint2>(), c->d_ctl.as<uint32_t>(),
-                     c->d_ids.as<uint32_t>());
-  HBX_TRY(c, hipGetLastError());
-  HBX_TRY(c, hipEventRecord(c->ev[3], s));
-  hipLaunchKernelGGL(hbx_k4_content_id, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, s,
-                     (uint32_t)n, d_cb, c->d_count.as<uint32_t>(), c->d_ids.as<uint32_t>(),
-                     c->d_cid.as<uint32_t>(), c->d_ctype.as<int32_t>());
-  HBX_TRY(c, hipGetLastError());
-  HBX_TRY(c, hipEventRecord(c->ev[4], s));
-
-  uint8_t* hr = c->h_res.as<uint8_t>();
-  HBX_TRY(c, hipMemcpyAsync(hr + rl.counts, c->d_count.p, n * 4, hipMemcpyDeviceToHost, s));
-  HBX_TRY(c, hipMemcpyAsync(hr + rl.cuts, c->d_cuts.p, caps * 8, hipMemcpyDeviceToHost, s));
-  HBX_TRY(c, hipMemcpyAsync(hr + rl.ids, c->d_ids.p, caps * 16, hipMemcpyDeviceToHost, s));
-  HBX_TRY(c, hipMemcpyAsync(hr + rl.cid, c->d_cid.p, n * 16, hipMemcpyDeviceToHost, s));
-  HBX_TRY(c, hipMemcpyAsync(hr + rl.ctype, c->d_ctype.p, n * 4, hipMemcpyDeviceToHost, s));
-  *total_cap_out = caps;
-  return HBX_OK;
+  HBX_TRY(c, hipEventRecord(b->ev[2], s));
+  return md5_launch(c, b, arena, budget);
 }
 
-// After the stream sync: scatter pinned results into the caller's arrays.
-int collect_batch(hbx_ctx* c, uint64_t n, uint64_t total_cap, uint64_t* cut_ends, uint8_t* ids,
-                  const uint64_t* out_base, const uint64_t* caps, hbx_file_summary* sums) {
-  const ResLayout rl = res_layout(n, total_cap);
-  const uint8_t* hr = c->h_res.as<uint8_t>();
+// Scatter a collected batch's pinned results into the caller's arrays.
+int collect_batch(hbx_ctx* c, Batch* b) {
+  const uint64_t n = b->n;
+  const ResLayout rl = res_layout(n, b->caps);
+  const uint8_t* hr = b->h_res.as<uint8_t>();
   const uint32_t* counts = reinterpret_cast<const uint32_t*>(hr + rl.counts);
   const uint64_t* cuts = reinterpret_cast<const uint64_t*>(hr + rl.cuts);
   const uint8_t* hid = hr + rl.ids;
@@ -281,36 +472,51 @@ int collect_batch(hbx_ctx* c, uint64_t n, uint64_t total_cap, uint64_t* cut_ends
   int rc = HBX_OK;
   for (uint64_t f = 0; f < n; f++) {
     const uint64_t k = counts[f];
-    const uint64_t ib = c->h_cut_base[f];
-    if (sums) {
-      std::memcpy(sums[f].content_id, cid + 16 * f, 16);
-      sums[f].content_type = ctype[f];
-      sums[f].n_chunks = (uint32_t)k;
+    const uint64_t ib = b->cut_base[f];
+    if (b->sums) {
+      std::memcpy(b->sums[f].content_id, cid + 16 * f, 16);
+      b->sums[f].content_type = ctype[f];
+      b->sums[f].n_chunks = (uint32_t)k;
     }
-    if (k > caps[f]) {
+    if (k > b->capv[f]) {
       rc = c->fail(HBX_ERR_CAPACITY, "output capacity too small for file " + std::to_string(f));
       continue;
     }
-    if (cut_ends) std::memcpy(cut_ends + out_base[f], cuts + ib, k * 8);
-    if (ids) std::memcpy(ids + 16 * out_base[f], hid + 16 * ib, k * 16);
+    if (b->cut_ends) std::memcpy(b->cut_ends + b->out_base[f], cuts + ib, k * 8);
+    if (b->ids) std::memcpy(b->ids + 16 * b->out_base[f], hid + 16 * ib, k * 16);
   }
   float ms = 0.f;
   for (int i = 0; i < 4; i++) {
-    if (hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]) == hipSuccess) c->stage_ms[i] = ms;
+    c->stage_ms[i] = 0.f;
+    if (hipEventElapsedTime(&ms, b->ev[i], b->ev[i + 1]) == hipSuccess) c->stage_ms[i] = ms;
   }
-  if (hipEventElapsedTime(&ms, c->ev[0], c->ev[4]) == hipSuccess) c->stage_ms[4] = ms;
+  if (hipEventElapsedTime(&ms, b->ev[0], b->ev[4]) == hipSuccess) c->stage_ms[4] = ms;
+  return rc;
+}
+
+// Complete the oldest pending batch (draining the MD5 chains first if its
+// chains are not yet guaranteed hashed) and collect it.
+int wait_oldest(hbx_ctx* c) {
+  if (c->pending.empty()) return HBX_OK;
+  Batch* b = c->pending.front();
+  if (!b->finalized) {
+    int rc = md5_launch(c, nullptr, nullptr, kBudgetAll);
+    if (rc) return rc;
+  }
+  HBX_TRY(c, hipEventSynchronize(b->ev[4]));
+  c->pending.pop_front();
+  int rc = collect_batch(c, b);
+  c->pool.push_back(b);
+  harvest_timings(c);
   return rc;
 }
 
 int run_device_sync(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* offs,
                     const uint64_t* lens, uint64_t* cut_ends, uint8_t* ids,
                     const uint64_t* out_base, const uint64_t* caps, hbx_file_summary* sums) {
-  uint64_t total_cap = 0;
-  int rc = enqueue_batch(c, d_arena, n, offs, lens, &total_cap);
+  int rc = submit_batch(c, d_arena, n, offs, lens, cut_ends, ids, out_base, caps, sums, kBudgetAll);
   if (rc) return rc;
-  if (n == 0) return HBX_OK;
-  HBX_TRY(c, hipStreamSynchronize(c->stream));
-  return collect_batch(c, n, total_cap, cut_ends, ids, out_base, caps, sums);
+  return wait_oldest(c);
 }
 
 }  // namespace
@@ -344,16 +550,11 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = std::getenv("HBX_K1_DMA")) c->k1_dma = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("HBX_MD5_WGS")) c->md5_wgs = (uint32_t)std::max(1, std::atoi(v));
   if (const char* v = std::getenv("HBX_TILE_ITERS")) c->tile_iters = (uint32_t)std::min(1024, std::max(1, std::atoi(v)));
+  if (const char* v = std::getenv("HBX_MD5_SLICE")) c->md5_slice = (uint32_t)std::max(0, std::atoi(v));
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return HBX_ERR_HIP;
-  }
-  for (auto& e : c->ev) {
-    if (hipEventCreate(&e) != hipSuccess) {
-      delete c;
-      return HBX_ERR_HIP;
-    }
   }
   *out = c;
   return HBX_OK;
@@ -363,15 +564,21 @@ void hbx_ctx_destroy(hbx_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (DevBuf* b : {&c->d_meta, &c->d_ssum, &c->d_cuts, &c->d_count, &c->d_ids,
-                    &c->d_cid, &c->d_ctype, &c->d_work, &c->d_ctl, &c->d_stage, &c->d_msg})
+  for (DevBuf* b : {&c->d_ssum, &c->d_tab[0], &c->d_tab[1], &c->d_tctl[0], &c->d_tctl[1],
+                    &c->d_stage, &c->d_msg})
     b->release();
-  c->h_meta.release();
-  c->h_res.release();
   c->h_stage.release();
   if (c->twin) hbx_ctx_destroy(c->twin);
-  for (auto& e : c->ev)
-    if (e) (void)hipEventDestroy(e);
+  for (Batch* b : c->pending) c->pool.push_back(b);
+  for (Batch* b : c->pool) {
+    b->release();
+    delete b;
+  }
+  for (TimedLaunch& t : c->open_t) {
+    (void)hipEventDestroy(t.a);
+    (void)hipEventDestroy(t.b);
+  }
+  for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -392,6 +599,28 @@ int hbx_stage_times(hbx_ctx* c, float ms[5]) {
   return HBX_OK;
 }
 
+int hbx_set_md5_slice(hbx_ctx* c, uint32_t blocks) {
+  if (!c) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->md5_slice = blocks;
+  return HBX_OK;
+}
+
+int hbx_stage_totals(hbx_ctx* c, double ms[5], uint64_t launches[5], int reset) {
+  if (!c) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  harvest_timings(c);
+  for (int i = 0; i < 5; i++) {
+    if (ms) ms[i] = c->tot_ms[i];
+    if (launches) launches[i] = c->tot_n[i];
+    if (reset) {
+      c->tot_ms[i] = 0.0;
+      c->tot_n[i] = 0;
+    }
+  }
+  return HBX_OK;
+}
+
 int hbx_chunk_hash_device(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* offs,
                           const uint64_t* lens, uint64_t* cut_ends, uint8_t* ids,
                           const uint64_t* out_base, const uint64_t* caps,
@@ -399,7 +628,7 @@ int hbx_chunk_hash_device(hbx_ctx* c, const void* d_arena, uint64_t n, const uin
   if (!c) return HBX_ERR_ARG;
   if (n && (!d_arena || !offs || !lens || !out_base || !caps)) return HBX_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->pend.active) return c->fail(HBX_ERR_STATE, "a submitted batch is still pending");
+  if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
   HBX_TRY(c, hipSetDevice(c->device));
   return run_device_sync(c, d_arena, n, offs, lens, cut_ends, ids, out_base, caps, sums);
 }
@@ -410,34 +639,22 @@ int hbx_submit_device(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_
   if (!c) return HBX_ERR_ARG;
   if (n && (!d_arena || !offs || !lens || !out_base || !caps)) return HBX_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->pend.active) return c->fail(HBX_ERR_STATE, "a submitted batch is still pending");
   HBX_TRY(c, hipSetDevice(c->device));
-  uint64_t total_cap = 0;
-  int rc = enqueue_batch(c, d_arena, n, offs, lens, &total_cap);
-  if (rc) return rc;
-  Pending& p = c->pend;
-  p.active = true;
-  p.n_files = n;
-  p.total_cap = total_cap;
-  p.cut_ends = cut_ends;
-  p.ids = ids;
-  p.summaries = sums;
-  p.out_base_copy.assign(out_base, out_base + n);
-  p.caps_copy.assign(caps, caps + n);
-  return HBX_OK;
+  return submit_batch(c, d_arena, n, offs, lens, cut_ends, ids, out_base, caps, sums,
+                      c->md5_slice ? c->md5_slice : kBudgetAll);
 }
 
 int hbx_wait(hbx_ctx* c) {
   if (!c) return HBX_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
-  Pending& p = c->pend;
-  if (!p.active) return HBX_OK;
-  p.active = false;
   HBX_TRY(c, hipSetDevice(c->device));
-  HBX_TRY(c, hipStreamSynchronize(c->stream));
-  if (p.n_files == 0) return HBX_OK;
-  return collect_batch(c, p.n_files, p.total_cap, p.cut_ends, p.ids, p.out_base_copy.data(),
-                       p.caps_copy.data(), p.summaries);
+  return wait_oldest(c);
+}
+
+int hbx_pending(hbx_ctx* c) {
+  if (!c) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  return (int)c->pending.size();
 }
 
 int hbx_chunk_hash_batch(hbx_ctx* c, uint64_t n, const uint8_t* const* datas,
@@ -447,7 +664,7 @@ int hbx_chunk_hash_batch(hbx_ctx* c, uint64_t n, const uint8_t* const* datas,
   if (!c) return HBX_ERR_ARG;
   if (n && (!datas || !lens || !out_base || !caps)) return HBX_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->pend.active) return c->fail(HBX_ERR_STATE, "a submitted batch is still pending");
+  if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
   HBX_TRY(c, hipSetDevice(c->device));
   std::vector<uint64_t> offs(n);
   uint64_t total = 0;
@@ -578,7 +795,7 @@ int hbx_store_paths(hbx_ctx* c, uint64_t n, const char* const* paths, const uint
   if (!c) return HBX_ERR_ARG;
   if (n && (!paths || !lens || !out_base || !caps)) return HBX_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->pend.active) return c->fail(HBX_ERR_STATE, "a submitted batch is still pending");
+  if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
   HBX_TRY(c, hipSetDevice(c->device));
   if (!c->twin) {
     int rc = hbx_ctx_create(c->device, &c->twin);
@@ -590,15 +807,13 @@ int hbx_store_paths(hbx_ctx* c, uint64_t n, const char* const* paths, const uint
   if (batch_bytes < (64ull << 20)) batch_bytes = 64ull << 20;
   hbx_ctx* X[2] = {c, c->twin};
   struct Batch {
-    uint64_t first = 0, count = 0, total = 0, cap = 0;
+    uint64_t first = 0, count = 0, total = 0;
     std::vector<uint64_t> offs;
   } B[2];
   auto finish = [&](int s) -> int {  // wait for slot s's batch and scatter its results
     Batch& b = B[s];
     if (!b.count) return HBX_OK;
-    HBX_TRY(X[s], hipStreamSynchronize(X[s]->stream));
-    int rc = collect_batch(X[s], b.count, b.cap, cut_ends, ids, out_base + b.first,
-                           caps + b.first, sums ? sums + b.first : nullptr);
+    int rc = wait_oldest(X[s]);
     b.count = 0;
     if (rc) c->err = X[s]->err;
     return rc;
@@ -630,7 +845,8 @@ int hbx_store_paths(hbx_ctx* c, uint64_t n, const char* const* paths, const uint
       return rc;
     }
     HBX_TRY(c, hipMemcpyAsync(x->d_stage.p, x->h_stage.p, tot, hipMemcpyHostToDevice, x->stream));
-    rc = enqueue_batch(x, x->d_stage.p, b.count, b.offs.data(), lens + b.first, &b.cap);
+    rc = submit_batch(x, x->d_stage.p, b.count, b.offs.data(), lens + b.first, cut_ends, ids,
+                      out_base + b.first, caps + b.first, sums ? sums + b.first : nullptr, kBudgetAll);
     if (rc) {
       c->err = x->err;
       b.count = 0;

@@ -623,96 +623,103 @@ __device__ __forceinline__ uint32_t msg_word(uint32_t widx, uint32_t lo, uint32_
   return (raw & mask) | (0x80u << (8u * nv));
 }
 
-// MD5( BE32(0) || BE32(len) || data[0..len) ) for one lane ("lane mode":
-// 64 chunks per wave, one per lane).  `c` is the lane's chunk start.  Reads
-// stay within the chunk + 64 bytes (HBX_ARENA_SLACK): every dword that holds
-// chunk bytes, and never more than 63 bytes past the chunk end.
+// Resumable lane-mode MD5 of M = BE32(0) || BE32(len) || data[0..len) (64
+// chains per wave, one per lane).  The lane compresses full message blocks
+// [b0, b0+cnt) into h and, when `finish`, the 1-2 padded tail blocks after the
+// last full block.  `c` is the chunk start.  Reads stay within the chunk +
+// 64 bytes (HBX_ARENA_SLACK): every dword holding chunk bytes and never more
+// than 63 bytes past the chunk end.
 #ifndef HBX_MD5_RING
 #define HBX_MD5_RING 8
 #endif
-__device__ void md5_block_id(const uint8_t* c, uint32_t len, uint32_t (&h)[4]) {
+__device__ void md5_run(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32_t b0, uint32_t cnt,
+                        bool finish) {
   constexpr int RING = HBX_MD5_RING;  // blocks of prefetch (16 VGPRs each)
-  md5_init(h);
   const uint32_t sh = (uint32_t)reinterpret_cast<uintptr_t>(c) & 3u;
   const uint32_t* va = reinterpret_cast<const uint32_t*>(c - sh);  // raw R[r] = va[r]
   const uint32_t T = len + 8u;  // message bytes (prefix + data)
   const uint32_t nfull = T >> 6;
-  const uint32_t nlast = nfull ? nfull - 1u : 0u;  // clamp prefetches to this block
-  // Full blocks.  Block b needs raw dwords R[16b-2 .. 16b+15]: 16 loaded with
-  // it (4 x dwordx4 at va+64b, never below the chunk start) plus 2 carried.
-  // Loads run RING blocks ahead through a register ring.  The loop is
-  // wave-uniform (bound = the wave's longest chunk, lanes past their own end
-  // compute and discard) so the compiler keeps exact vmcnt counting and never
-  // drains the ring at a divergent join.
-  const uint32_t nmax = wave_max_all(nfull);
+  const uint32_t last = cnt ? b0 + cnt - 1u : b0;  // prefetches clamp to this block
+  // Block b needs raw dwords R[16b-2 .. 16b+15]: 16 loaded with it (4 x
+  // dwordx4 at va+64b, never below the chunk start) plus 2 carried.  Loads
+  // run RING blocks ahead through a register ring.  The loop is wave-uniform
+  // (bound = the wave's largest cnt; lanes past their own cnt compute and
+  // discard) so the compiler keeps exact vmcnt counting and never drains the
+  // ring at a divergent join.
+  const uint32_t nmax = wave_max_all(cnt);
+  const bool any_first = __builtin_amdgcn_ballot_w64(cnt != 0u && b0 == 0u) != 0ull;
   uint32_t c0 = 0u, c1 = 0u;  // R[16b-2], R[16b-1]
+  if (b0 != 0u) {
+    c0 = va[16u * b0 - 2u];
+    c1 = va[16u * b0 - 1u];
+  }
   u32x4 ring[RING][4];
 #pragma unroll
   for (int r = 0; r < RING; r++) {
-    const u32x4* src = reinterpret_cast<const u32x4*>(va + 16u * min((uint32_t)r, nlast));
+    const u32x4* src = reinterpret_cast<const u32x4*>(va + 16u * min(b0 + (uint32_t)r, last));
 #pragma unroll
     for (int i = 0; i < 4; i++) ring[r][i] = __builtin_nontemporal_load(src + i);
   }
-  auto block = [&](int r, uint32_t b, bool refill) {
+  auto block = [&](int r, uint32_t i, bool refill) {
     uint32_t R[16];
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-      R[4 * i + 0] = ring[r][i].x;
-      R[4 * i + 1] = ring[r][i].y;
-      R[4 * i + 2] = ring[r][i].z;
-      R[4 * i + 3] = ring[r][i].w;
+    for (int q = 0; q < 4; q++) {
+      R[4 * q + 0] = ring[r][q].x;
+      R[4 * q + 1] = ring[r][q].y;
+      R[4 * q + 2] = ring[r][q].z;
+      R[4 * q + 3] = ring[r][q].w;
     }
-    // message word i = data word 16b+i-2 = bytes of R[16b+i-2], R[16b+i-1]
+    // message word j = data word 16b+j-2 = bytes of R[16b+j-2], R[16b+j-1]
     uint32_t m[16];
     m[0] = alignbyte(c1, c0, sh);
     m[1] = alignbyte(R[0], c1, sh);
 #pragma unroll
-    for (int i = 2; i < 16; i++) m[i] = alignbyte(R[i - 1], R[i - 2], sh);
-    if (b == 0) {  // wave-uniform
-      m[0] = 0u;
-      m[1] = bswap32(len);
+    for (int j = 2; j < 16; j++) m[j] = alignbyte(R[j - 1], R[j - 2], sh);
+    if (i == 0u && any_first) {  // wave-uniform; block 0 carries the framing
+      m[0] = b0 == 0u ? 0u : m[0];
+      m[1] = b0 == 0u ? bswap32(len) : m[1];
     }
     c0 = R[14];
     c1 = R[15];
     // refill only after the slot's registers are consumed: the load then
     // reuses them and the ring needs no copies at the loop back-edge
     if (refill) {
-      const u32x4* src = reinterpret_cast<const u32x4*>(va + 16u * min(b + (uint32_t)RING, nlast));
+      const u32x4* src = reinterpret_cast<const u32x4*>(va + 16u * min(b0 + i + (uint32_t)RING, last));
 #pragma unroll
-      for (int i = 0; i < 4; i++) ring[r][i] = __builtin_nontemporal_load(src + i);
+      for (int q = 0; q < 4; q++) ring[r][q] = __builtin_nontemporal_load(src + q);
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the refill ahead of this block's compression
     uint32_t t[4] = {h[0], h[1], h[2], h[3]};
     md5_compress(t, m);
-    const bool live = b < nfull;
+    const bool live = i < cnt;
 #pragma unroll
-    for (int i = 0; i < 4; i++) h[i] = live ? t[i] : h[i];
+    for (int q = 0; q < 4; q++) h[q] = live ? t[q] : h[q];
   };
-  uint32_t b = 0;
-  for (; b + (uint32_t)RING <= nmax; b += (uint32_t)RING) {
+  uint32_t i = 0;
+  for (; i + (uint32_t)RING <= nmax; i += (uint32_t)RING) {
 #pragma unroll
-    for (int r = 0; r < RING; r++) block(r, b + (uint32_t)r, true);
+    for (int r = 0; r < RING; r++) block(r, i + (uint32_t)r, true);
   }
 #pragma unroll
   for (int r = 0; r < RING - 1; r++) {
-    if (b + (uint32_t)r < nmax) block(r, b + (uint32_t)r, false);
+    if (i + (uint32_t)r < nmax) block(r, i + (uint32_t)r, false);
   }
   // tail: remaining message bytes + 0x80 + zeros + 64-bit bit length
   const uint32_t rem = T - 64u * nfull;  // 0..63
-  const uint32_t ntail = (rem + 9u > 64u) ? 2u : 1u;
+  const uint32_t ntail = finish ? ((rem + 9u > 64u) ? 2u : 1u) : 0u;
   for (uint32_t tb = 0; tb < ntail; tb++) {
     const uint32_t bb = nfull + tb;
     uint32_t m[16];
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
-      const uint32_t widx = 16u * bb + (uint32_t)i;
+    for (int j = 0; j < 16; j++) {
+      const uint32_t widx = 16u * bb + (uint32_t)j;
       uint32_t lo = 0u, hi = 0u;
       const uint32_t dpos = 4u * (widx - 2u);
       if (widx >= 2u && dpos < len) {
         lo = va[dpos >> 2];
         hi = va[(dpos >> 2) + 1u];
       }
-      m[i] = msg_word(widx, lo, hi, sh, len);
+      m[j] = msg_word(widx, lo, hi, sh, len);
     }
     if (tb + 1 == ntail) {
       const uint64_t bits = (uint64_t)T * 8ull;
@@ -725,72 +732,116 @@ __device__ void md5_block_id(const uint8_t* c, uint32_t len, uint32_t (&h)[4]) {
 
 }  // namespace
 
+// ------------------------------------------------------ MD5 chain table --
+// K3 is time-sliced: one launch advances every chain in flight by at most
+// `budget` full message blocks (HBX: hbx_set_md5_slice), carrying the MD5
+// state in this table between launches.  Chunks of a new batch join the
+// table as fresh chains, so several batches pipeline through one stream and
+// no batch waits for another's longest chunk (DESIGN.md §4 "K3").
+struct alignas(16) Chain {
+  uint64_t src;   // device address of the chunk's first byte
+  uint32_t len;   // chunk bytes
+  uint32_t next;  // full message blocks already compressed; kChainDone once hashed
+  uint32_t h[4];  // MD5 state after `next` blocks
+  uint64_t out;   // device address of the chunk's 16-byte BlockID
+  uint64_t pad;
+};
+constexpr uint32_t kChainDone = 0xFFFFFFFFu;
+constexpr uint32_t kBudgetAll = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t chain_cnt(uint32_t len, uint32_t next, uint32_t budget) {
+  const uint32_t nfull = (len + 8u) >> 6;
+  return min(nfull - next, budget);
+}
+__device__ __forceinline__ uint32_t chain_bucket(uint32_t cnt) { return 31u - __builtin_clz(cnt + 1u); }
+
 // ----------------------------------------------------------- K2c plan --
-// Orders all chunks of the batch by length bucket (floor(log2 len)),
-// longest first, so each K3 wave gets 64 chunks of similar length (a wave
-// runs as long as its longest lane) and the longest chunks — the serial MD5
-// critical path — start first.
+// Builds the chain table for one K3 launch: the unfinished chains of the
+// previous launch (`prev`, count prev_ctl[1]; nullptr = none) plus one fresh
+// chain per chunk of the new batch (n_files may be 0), ordered by this
+// launch's block count (log2 buckets, largest first) so each K3 wave gets 64
+// chains of similar length and the longest start first.  ctl[1] = entries.
 constexpr int kPlanThreads = 1024;
 
 extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
-    uint32_t n_files, const uint64_t* __restrict__ cut_base, const uint64_t* __restrict__ cut_ends,
-    const uint32_t* __restrict__ cut_count, uint2* __restrict__ work, uint32_t* __restrict__ ctl) {
-  __shared__ uint32_t hist[32], cur[32];
+    uint32_t n_files, const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
+    const uint64_t* __restrict__ cut_base, const uint64_t* __restrict__ cut_ends,
+    const uint32_t* __restrict__ cut_count, uint32_t* __restrict__ ids, const Chain* __restrict__ prev,
+    const uint32_t* __restrict__ prev_ctl, Chain* __restrict__ cur, uint32_t* __restrict__ ctl,
+    uint32_t budget) {
+  __shared__ uint32_t hist[32], pos[32];
   const uint32_t tid = threadIdx.x;
+  const uint32_t n_prev = prev ? prev_ctl[1] : 0u;
   if (tid < 32) hist[tid] = 0u;
   __syncthreads();
+  for (uint32_t e = tid; e < n_prev; e += kPlanThreads) {
+    const Chain ch = prev[e];
+    if (ch.next != kChainDone) atomicAdd(&hist[chain_bucket(chain_cnt(ch.len, ch.next, budget))], 1u);
+  }
   for (uint32_t f = tid; f < n_files; f += kPlanThreads) {
     const uint64_t cb = cut_base[f];
     const uint32_t k = cut_count[f];
-    uint64_t prev = 0;
+    uint64_t start = 0;
     for (uint32_t i = 0; i < k; i++) {
       const uint64_t e = cut_ends[cb + i];
-      atomicAdd(&hist[31 - __builtin_clz((uint32_t)(e - prev))], 1u);
-      prev = e;
+      atomicAdd(&hist[chain_bucket(chain_cnt((uint32_t)(e - start), 0u, budget))], 1u);
+      start = e;
     }
   }
   __syncthreads();
   if (tid == 0) {
-    uint32_t pos = 0;
+    uint32_t p = 0;
     for (int bk = 31; bk >= 0; bk--) {
-      cur[bk] = pos;
-      pos += hist[bk];
+      pos[bk] = p;
+      p += hist[bk];
     }
     ctl[0] = 0u;
-    ctl[1] = pos;  // all chunks
+    ctl[1] = p;
   }
   __syncthreads();
+  for (uint32_t e = tid; e < n_prev; e += kPlanThreads) {
+    const Chain ch = prev[e];
+    if (ch.next != kChainDone)
+      cur[atomicAdd(&pos[chain_bucket(chain_cnt(ch.len, ch.next, budget))], 1u)] = ch;
+  }
   for (uint32_t f = tid; f < n_files; f += kPlanThreads) {
     const uint64_t cb = cut_base[f];
     const uint32_t k = cut_count[f];
-    uint64_t prev = 0;
+    const uint64_t base = reinterpret_cast<uint64_t>(arena + file_off[f]);
+    uint64_t start = 0;
     for (uint32_t i = 0; i < k; i++) {
       const uint64_t e = cut_ends[cb + i];
-      const uint32_t p = atomicAdd(&cur[31 - __builtin_clz((uint32_t)(e - prev))], 1u);
-      work[p] = make_uint2(f, i);
-      prev = e;
+      Chain ch;
+      ch.src = base + start;
+      ch.len = (uint32_t)(e - start);
+      ch.next = 0u;
+      ch.h[0] = 0x67452301u;
+      ch.h[1] = 0xefcdab89u;
+      ch.h[2] = 0x98badcfeu;
+      ch.h[3] = 0x10325476u;
+      ch.out = reinterpret_cast<uint64_t>(ids + 4u * (cb + i));
+      ch.pad = 0ull;
+      cur[atomicAdd(&pos[chain_bucket(chain_cnt(ch.len, 0u, budget))], 1u)] = ch;
+      start = e;
     }
   }
 }
 
 // ---------------------------------------------------------- K3 block MD5 --
-namespace {
-
-}  // namespace
-
-// Block-ID kernel (lane mode: lane = chunk, 64 similar-length chunks per
-// wave in the planner's longest-first order).  grid = one 512-thread
-// workgroup per CU; group g runs on wave (g / grid) % 8 of workgroup
-// g % grid, so the first 4 x grid groups (the longest chunks) each get a SIMD
-// of their own.  The MD5 chain is bound by its 4 dependent VALU per step;
-// lane mode runs 64 such chains in one instruction stream at that bound
-// (DESIGN.md "K3"; tools/experiments/md5_wave_mode.hip for what did not pay).
+// Block-ID kernel (lane mode: lane = chain, 64 similar-length chains per
+// wave in the planner's order).  Each lane resumes its chain at `next`,
+// compresses up to `budget` full blocks and either finishes (tail blocks,
+// BlockID stored at `out`, entry marked done) or saves the state for the
+// next launch.  grid = one 512-thread workgroup per CU; group g runs on wave
+// (g / grid) % 8 of workgroup g % grid, so the first 4 x grid groups each get
+// a SIMD of their own.  The MD5 chain is bound by its 4 dependent VALU per
+// step; lane mode runs 64 such chains in one instruction stream at that
+// bound (DESIGN.md "K3"; tools/experiments/md5_wave_mode.hip for what did
+// not pay).
 constexpr int kK3Threads = 512;
 
 extern "C" __global__ __launch_bounds__(kK3Threads) void hbx_k3_block_md5(
-    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
-    const uint64_t* __restrict__ cut_base, const uint64_t* __restrict__ cut_ends,
-    const uint2* __restrict__ work, const uint32_t* __restrict__ ctl, uint32_t* __restrict__ ids) {
+    Chain* __restrict__ tab, const uint32_t* __restrict__ ctl, uint32_t budget) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t n_total = ctl[1];
@@ -799,16 +850,22 @@ extern "C" __global__ __launch_bounds__(kK3Threads) void hbx_k3_block_md5(
   for (uint32_t g = wave * gridDim.x + blockIdx.x; g < groups; g += nwaves) {
     const uint32_t k = 64u * g + lane;
     const bool active = k < n_total;
-    const uint2 wk = work[active ? k : 64u * g];
-    const uint64_t cb = cut_base[wk.x];
-    const uint64_t start = wk.y ? cut_ends[cb + wk.y - 1] : 0ull;
-    const uint64_t end = cut_ends[cb + wk.y];
-    // every lane stays alive for the wave-wide loop bound; idle lanes hash
-    // an empty message and store nothing
-    const uint32_t len = active ? (uint32_t)(end - start) : 0u;
-    uint32_t h[4];
-    md5_block_id(arena + file_off[wk.x] + start, len, h);
-    if (active) reinterpret_cast<uint4*>(ids)[cb + wk.y] = make_uint4(h[0], h[1], h[2], h[3]);
+    // idle lanes stay alive for the wave-wide loop bound: they run an empty
+    // slice over the group's first chunk and store nothing
+    const Chain ch = tab[active ? k : 64u * g];
+    const uint32_t len = active ? ch.len : 0u;
+    const uint32_t b0 = active ? ch.next : 0u;
+    const uint32_t cnt = active ? chain_cnt(len, b0, budget) : 0u;
+    const bool finish = active && b0 + cnt == ((len + 8u) >> 6);
+    uint32_t h[4] = {ch.h[0], ch.h[1], ch.h[2], ch.h[3]};
+    md5_run(reinterpret_cast<const uint8_t*>(ch.src), len, h, b0, cnt, finish);
+    if (finish) {
+      *reinterpret_cast<uint4*>(ch.out) = make_uint4(h[0], h[1], h[2], h[3]);
+      tab[k].next = kChainDone;
+    } else if (active) {
+      *reinterpret_cast<uint4*>(&tab[k].h[0]) = make_uint4(h[0], h[1], h[2], h[3]);
+      tab[k].next = b0 + cnt;
+    }
   }
 }
 

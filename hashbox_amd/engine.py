@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+from collections import deque
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Union
 
@@ -74,16 +75,19 @@ def _p(a: np.ndarray) -> int:
 class Engine:
     """One MI355X (one HIP stream) running the chunk + block-ID path."""
 
-    def __init__(self, device: int = 0, tile_iters: Optional[int] = None):
+    def __init__(self, device: int = 0, tile_iters: Optional[int] = None,
+                 md5_slice: Optional[int] = None):
         self._L = _lib.load()
         self._ctx = ctypes.c_void_p()
         rc = self._L.hbx_ctx_create(int(device), ctypes.byref(self._ctx))
         if rc != 0:
             raise HbxError(f"hbx_ctx_create(device={device}) failed: {_lib.ERRORS.get(rc, rc)}")
         self.device = device
-        self._pending = None
+        self._pending = deque()
         if tile_iters is not None:
             self._check(self._L.hbx_set_tile_iters(self._ctx, int(tile_iters)), "set_tile_iters")
+        if md5_slice is not None:
+            self.set_md5_slice(md5_slice)
 
     # ----------------------------------------------------------- plumbing --
     def close(self):
@@ -152,27 +156,50 @@ class Engine:
         """Files resident in device memory (pointer ``d_arena``, e.g. a torch
         uint8 tensor's ``data_ptr()``).  Offsets 16-B aligned; each file must be
         followed by >= 64 readable bytes."""
-        self.submit_device(d_arena, offs, lens)
-        return self.wait()
+        offs = np.ascontiguousarray(offs, np.uint64)
+        lens = np.ascontiguousarray(lens, np.uint64)
+        caps, base, cuts, ids, sums = self._alloc_out(lens)
+        self._check(self._L.hbx_chunk_hash_device(self._ctx, ctypes.c_void_p(int(d_arena)), len(lens),
+                                                  _p(offs), _p(lens), _p(cuts), _p(ids), _p(base),
+                                                  _p(caps), sums), "hbx_chunk_hash_device")
+        return self._unpack(lens, caps, base, cuts, ids, sums)
 
     def submit_device(self, d_arena: int, offs: Sequence[int], lens: Sequence[int]):
-        if self._pending is not None:
-            raise HbxError("a batch is already pending on this engine")
+        """Enqueue a device-resident batch and return at once.  Any number of
+        batches may be in flight; :meth:`wait` completes the oldest.  The
+        arena must stay untouched until then."""
         offs = np.ascontiguousarray(offs, np.uint64)
         lens = np.ascontiguousarray(lens, np.uint64)
         caps, base, cuts, ids, sums = self._alloc_out(lens)
         self._check(self._L.hbx_submit_device(self._ctx, ctypes.c_void_p(int(d_arena)), len(lens),
                                               _p(offs), _p(lens), _p(cuts), _p(ids), _p(base),
                                               _p(caps), sums), "hbx_submit_device")
-        self._pending = (offs, lens, caps, base, cuts, ids, sums)
+        self._pending.append((offs, lens, caps, base, cuts, ids, sums))
 
     def wait(self) -> List[FileChunks]:
-        if self._pending is None:
+        """Results of the oldest submitted batch ([] if none is pending)."""
+        if not self._pending:
             return []
-        offs, lens, caps, base, cuts, ids, sums = self._pending
-        self._pending = None
+        offs, lens, caps, base, cuts, ids, sums = self._pending.popleft()
         self._check(self._L.hbx_wait(self._ctx), "hbx_wait")
         return self._unpack(lens, caps, base, cuts, ids, sums)
+
+    def pending(self) -> int:
+        n = self._L.hbx_pending(self._ctx)
+        if n < 0:
+            self._check(n, "hbx_pending")
+        return int(n)
+
+    def set_md5_slice(self, blocks: int):
+        """MD5 blocks per chain per K3 launch (0 = unlimited)."""
+        self._check(self._L.hbx_set_md5_slice(self._ctx, int(blocks)), "hbx_set_md5_slice")
+
+    def stage_totals(self, reset: bool = False):
+        """Cumulative device ms and launch counts per kernel: K1, K2, plan, K3, K4."""
+        ms = (ctypes.c_double * 5)()
+        n = (ctypes.c_uint64 * 5)()
+        self._check(self._L.hbx_stage_totals(self._ctx, ms, n, int(bool(reset))), "hbx_stage_totals")
+        return np.array(list(ms), np.float64), np.array(list(n), np.int64)
 
     def block_id(self, data: BytesLike, links: Sequence[bytes] = ()) -> bytes:
         """HashboxBlock.HashData (pkg/core/block.go:96-111) on the device."""
@@ -211,7 +238,9 @@ class Engine:
         return self.chunk_hash(data)
 
     def stage_times(self) -> np.ndarray:
-        """Device ms of the last batch: K1, K2, K3, K4, total."""
+        """Device ms of the last collected batch: K1, K2, plan + first K3
+        launch, later K3 launches + K4, total (synchronous calls: K3 in [2],
+        K4 in [3])."""
         ms = (ctypes.c_float * 5)()
         self._check(self._L.hbx_stage_times(self._ctx, ms), "hbx_stage_times")
         return np.array(list(ms), np.float64)

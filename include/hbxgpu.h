@@ -12,8 +12,8 @@
  *   hbx_chunk_hash_batch  the same, for many files at once (tree walk order
  *                         store.go:201-397 is the caller's business)
  *   hbx_chunk_hash_device the same, files already resident in device memory
- *   hbx_submit_device /   asynchronous form (one batch in flight per context)
- *   hbx_wait
+ *   hbx_submit_device /   asynchronous, pipelined form: any number of batches
+ *   hbx_wait              in flight per context, completed in FIFO order
  *   hbx_store_paths       storeFile(path) for many files on disk, end to end
  *   hbx_block_id          HashboxBlock.HashData for an arbitrary block with
  *                         links (pkg/core/block.go:96-111), e.g. the
@@ -28,9 +28,10 @@
  *     into core.Abort, pkg/core/utils.go:22-37).
  *   - The caller owns every buffer passed in.  The library never frees caller
  *     memory and never keeps a caller pointer after the call returns, except
- *     between hbx_submit_device and hbx_wait, where the output arrays must
- *     stay valid (use hbx_alloc_pinned memory from cgo: cgo forbids C from
- *     retaining Go pointers).
+ *     between hbx_submit_device and the hbx_wait that completes the batch,
+ *     where the device arena and the output arrays must stay valid (use
+ *     hbx_alloc_pinned memory from cgo: cgo forbids C from retaining Go
+ *     pointers).
  *   - One context = one GPU + one HIP stream.  Calls on one context are
  *     serialised by an internal lock; use one context per GPU (or per
  *     goroutine) to run in parallel.
@@ -105,13 +106,28 @@ int hbx_chunk_hash_device(hbx_ctx *ctx, const void *d_arena, uint64_t n_files,
                           uint64_t *cut_ends, uint8_t *ids, const uint64_t *out_base,
                           const uint64_t *caps, hbx_file_summary *summaries);
 
-/* Asynchronous device form: enqueue on the context's stream, return at once;
- * hbx_wait completes the batch and fills the output arrays given here. */
+/* Asynchronous device form: enqueue on the context's stream and return at
+ * once.  Batches pipeline: the block-MD5 stage is time-sliced
+ * (hbx_set_md5_slice), so the chunks of a new batch join the chains of the
+ * batches still in flight instead of waiting behind their longest chunk.
+ * hbx_wait completes the OLDEST pending batch and fills the output arrays
+ * given at its submit (it first drains every chain in flight if that batch's
+ * chains are not yet guaranteed hashed).  The synchronous calls
+ * (hbx_chunk_hash*, hbx_store_paths) fail with HBX_ERR_STATE while batches
+ * are pending. */
 int hbx_submit_device(hbx_ctx *ctx, const void *d_arena, uint64_t n_files,
                       const uint64_t *file_offs, const uint64_t *file_lens, uint64_t *cut_ends,
                       uint8_t *ids, const uint64_t *out_base, const uint64_t *caps,
                       hbx_file_summary *summaries);
 int hbx_wait(hbx_ctx *ctx);
+/* Number of submitted batches not yet completed by hbx_wait. */
+int hbx_pending(hbx_ctx *ctx);
+/* Time slice of the block-MD5 stage: full 64-byte MD5 blocks each chain in
+ * flight advances per launch (default 16384 = 1 MiB; 0 = unlimited, one
+ * launch per batch).  A submitted batch is complete after
+ * ceil(min(longest file, 8 MiB)/64 / blocks) further launches; results are
+ * identical for every setting. */
+int hbx_set_md5_slice(hbx_ctx *ctx, uint32_t blocks);
 
 /* Files on disk, end to end (storeFile over a list of paths, store.go:84-199
  * with the tree walk left to the caller): io_threads read the files straight
@@ -143,9 +159,15 @@ int hbx_alloc_pinned(uint64_t bytes, void **out);
 int hbx_free_pinned(void *p);
 
 /* Device time (ms) of the last completed batch per stage:
- * [0] K1 window-digest scan, [1] K2 cut chain, [2] K3 block MD5,
- * [3] K4 content id, [4] whole batch on the stream. */
+ * [0] K1 window-digest scan, [1] K2 cut chain, [2] chain plan + first K3
+ * launch, [3] later K3 launches + K4 content id, [4] whole batch on the
+ * stream.  For a synchronous call [2] is all of K3 and [3] is K4. */
 int hbx_stage_times(hbx_ctx *ctx, float ms[5]);
+/* Cumulative device time (ms) and launch count per kernel since the context
+ * was created (or last reset), for completed launches:
+ * [0] K1 scan, [1] K2 cut chain, [2] K2c chain plan, [3] K3 block MD5,
+ * [4] K4 content id.  reset != 0 zeroes the totals after reading. */
+int hbx_stage_totals(hbx_ctx *ctx, double ms[5], uint64_t launches[5], int reset);
 /* Tile length of K1 in 64 KiB iterations (default 64 = 4 MiB tiles). */
 int hbx_set_tile_iters(hbx_ctx *ctx, uint32_t iters);
 

@@ -156,3 +156,75 @@ def test_store_paths_end_to_end(engine, oracle, tmp_path):
     from hashbox_amd import HbxError
     with _pt.raises((HbxError, FileNotFoundError)):
         engine.store_paths([str(tmp_path / "missing.bin")])
+
+
+def _device_batches(oracle, nb, seed):
+    """nb device-resident batches of mixed files (edge lengths, long chunks,
+    constant runs) plus their oracle results."""
+    import torch
+    from hashbox_amd import pack_arena_layout
+    rng = np.random.default_rng(seed)
+    out = []
+    for b in range(nb):
+        sizes = [int(rng.integers(0, 3 * MAXB)) for _ in range(5)] + [0, 57, 2 * MIN + 1, MAXB + 9]
+        files = [oracle.random_bytes(n, seed * 100 + 10 * b + i) for i, n in enumerate(sizes)]
+        files[1] = np.full(sizes[1], 0x5A, np.uint8)  # constant run: 8 MiB max-length chunks
+        offs, total = pack_arena_layout(sizes)
+        host = np.zeros(total, np.uint8)
+        for o, f in zip(offs, files):
+            host[int(o):int(o) + f.size] = f
+        dev = torch.from_numpy(host).to("cuda:0")
+        out.append((dev, offs, sizes, [oracle.store_file(f, fast=True) for f in files]))
+    torch.cuda.synchronize()
+    return out
+
+
+@pytest.mark.parametrize("md5_slice", [1, 3, 64, 16384])
+def test_pipelined_batches_time_sliced(oracle, md5_slice):
+    """Several batches in flight on one context with the block-MD5 stage
+    time-sliced: chains resume across many K3 launches, new batches' chunks
+    join carried chains, results come back in FIFO order, bit-exact."""
+    from hashbox_amd import Engine
+    batches = _device_batches(oracle, 4, 31 + md5_slice % 7)
+    with Engine(0, md5_slice=md5_slice) as e:
+        for dev, offs, sizes, _ in batches[:3]:
+            e.submit_device(dev.data_ptr(), offs, sizes)
+        assert e.pending() == 3
+        first = e.wait()  # may force a drain of every chain in flight
+        e.submit_device(batches[3][0].data_ptr(), batches[3][1], batches[3][2])
+        rest = [e.wait() for _ in range(3)]
+        assert e.pending() == 0 and e.wait() == []
+        for (_, _, _, ref), got in zip(batches, [first] + rest):
+            for g, r in zip(got, ref):
+                _check(g, r)
+        # the synchronous path is refused while batches are pending
+        from hashbox_amd import HbxError
+        e.submit_device(batches[0][0].data_ptr(), batches[0][1], batches[0][2])
+        with pytest.raises(HbxError):
+            e.chunk_hash(b"x")
+        for g, r in zip(e.wait(), batches[0][3]):
+            _check(g, r)
+        ms, n = e.stage_totals()
+        assert n[3] >= 1 and ms[3] > 0
+
+
+def test_pipelined_steady_state(oracle):
+    """A deep pipeline as bench.py drives it: submit, and wait only once
+    `depth` batches are pending, so batches complete through the slice
+    schedule rather than a forced drain."""
+    from hashbox_amd import Engine
+    batches = _device_batches(oracle, 3, 57)
+    got = []
+    with Engine(0, md5_slice=4096) as e:  # 256 KiB per chain per launch: 32 launches per 8 MiB
+        order = [i % 3 for i in range(40)]
+        for i in order:
+            dev, offs, sizes, _ = batches[i]
+            e.submit_device(dev.data_ptr(), offs, sizes)
+            if e.pending() > 34:
+                got.append(e.wait())
+        while e.pending():
+            got.append(e.wait())
+    assert len(got) == len(order)
+    for i, g in zip(order, got):
+        for a, r in zip(g, batches[i][3]):
+            _check(a, r)
