@@ -121,7 +121,8 @@ struct Batch {
 
 struct hbx_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;   // scan stream: input copies, K1, K2 (and hbx_block_id)
+  hipStream_t hstream = nullptr;  // hash stream: chain plan, K3, K4, result D2H
   std::mutex mu;
   std::string err;
   uint32_t tile_iters = 64;   // K1 tile = 64 x 64 KiB (measured best: fewer halo primes)
@@ -183,6 +184,7 @@ inline uint64_t max_chunks(uint64_t len) { return len / HBX_MIN_BLOCK_SIZE + 1; 
 int ensure_shared(hbx_ctx* c, DevBuf& b, size_t n) {
   if (n <= b.cap && b.p) return HBX_OK;
   HBX_TRY(c, hipStreamSynchronize(c->stream));
+  HBX_TRY(c, hipStreamSynchronize(c->hstream));
   HBX_TRY(c, b.ensure(n));
   return HBX_OK;
 }
@@ -190,15 +192,16 @@ int ensure_shared(hbx_ctx* c, DevBuf& b, size_t n) {
 // Bracket one launch with an event pair for hbx_stage_totals.
 struct StageTimer {
   hbx_ctx* c;
+  hipStream_t s;
   TimedLaunch t;
-  StageTimer(hbx_ctx* ctx, int stage) : c(ctx) {
+  StageTimer(hbx_ctx* ctx, hipStream_t st, int stage) : c(ctx), s(st) {
     t.stage = stage;
     t.a = c->event();
     t.b = c->event();
-    if (t.a) (void)hipEventRecord(t.a, c->stream);
+    if (t.a) (void)hipEventRecord(t.a, s);
   }
   ~StageTimer() {
-    if (t.a && t.b && hipEventRecord(t.b, c->stream) == hipSuccess) {
+    if (t.a && t.b && hipEventRecord(t.b, s) == hipSuccess) {
       c->open_t.push_back(t);
     } else {
       if (t.a) c->ev_pool.push_back(t.a);
@@ -272,13 +275,13 @@ Batch* acquire_batch(hbx_ctx* c) {
 
 // K4 + D2H of one batch whose chains are all hashed.
 int finalize_batch(hbx_ctx* c, Batch* b) {
-  hipStream_t s = c->stream;
+  hipStream_t s = c->hstream;
   b->finalized = true;
   if (b->n) {
     const uint64_t n = b->n;
     const uint64_t* d_cb = b->d_meta.as<uint64_t>() + 3 * n;
     {
-      StageTimer t(c, 4);
+      StageTimer t(c, s, 4);
       hipLaunchKernelGGL(hbx_k4_content_id, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, s,
                          (uint32_t)n, d_cb, b->d_count.as<uint32_t>(), b->d_ids.as<uint32_t>(),
                          b->d_cid.as<uint32_t>(), b->d_ctype.as<int32_t>());
@@ -301,7 +304,7 @@ int finalize_batch(hbx_ctx* c, Batch* b) {
 // one more launch; those whose chains are now guaranteed complete are
 // finalized.  A budget of kBudgetAll completes every chain in flight.
 int md5_launch(hbx_ctx* c, Batch* nb, const uint8_t* arena, uint32_t budget) {
-  hipStream_t s = c->stream;
+  hipStream_t s = c->hstream;
   uint64_t bound = 0;  // chains alive after this plan <= chunks of unfinalized batches
   for (Batch* b : c->pending)
     if (!b->finalized) bound += b->caps;
@@ -315,7 +318,7 @@ int md5_launch(hbx_ctx* c, Batch* nb, const uint8_t* arena, uint32_t budget) {
   Chain* cur = c->d_tab[dst].as<Chain>();
   uint32_t* ctl = c->d_tctl[dst].as<uint32_t>();
   {
-    StageTimer t(c, 2);
+    StageTimer t(c, s, 2);
     if (nb && nb->n) {
       const uint64_t n = nb->n;
       const uint64_t* d_off = nb->d_meta.as<uint64_t>();
@@ -333,7 +336,7 @@ int md5_launch(hbx_ctx* c, Batch* nb, const uint8_t* arena, uint32_t budget) {
   }
   HBX_TRY(c, hipGetLastError());
   {
-    StageTimer t(c, 3);
+    StageTimer t(c, s, 3);
     hipLaunchKernelGGL(hbx_k3_block_md5, dim3(c->md5_wgs), dim3(kK3Threads), 0, s, cur,
                        static_cast<const uint32_t*>(ctl), budget);
   }
@@ -436,7 +439,7 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
 
   HBX_TRY(c, hipEventRecord(b->ev[0], s));
   if (nt) {
-    StageTimer t(c, 0);
+    StageTimer t(c, s, 0);
     if (c->k1_dma)
       hipLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3((uint32_t)nt), dim3(kK1Threads), 0, s,
                          arena, d_off, d_len, d_sb, d_tiles, c->tile_iters, c->d_ssum.as<uint2>(),
@@ -449,13 +452,16 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(b->ev[1], s));
   {
-    StageTimer t(c, 1);
+    StageTimer t(c, s, 1);
     hipLaunchKernelGGL(hbx_k2_cut_chain, dim3((uint32_t)n), dim3(64), 0, s, arena, d_off, d_len,
                        d_sb, c->d_ssum.as<uint2>(), d_cb, b->d_cuts.as<uint64_t>(),
                        b->d_count.as<uint32_t>());
   }
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(b->ev[2], s));
+  // the hash stream picks the batch up once its cuts exist; the scan stream
+  // is free for the next batch's K1/K2 while K3 runs
+  if (c->hstream != s) HBX_TRY(c, hipStreamWaitEvent(c->hstream, b->ev[2], 0));
   return md5_launch(c, b, arena, budget);
 }
 
@@ -556,6 +562,14 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
     delete c;
     return HBX_ERR_HIP;
   }
+  const char* one = std::getenv("HBX_ONE_STREAM");  // A/B: scan and hash on one stream
+  if (one && std::atoi(one)) {
+    c->hstream = c->stream;
+  } else if (hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return HBX_ERR_HIP;
+  }
   *out = c;
   return HBX_OK;
 }
@@ -564,6 +578,7 @@ void hbx_ctx_destroy(hbx_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->hstream) (void)hipStreamSynchronize(c->hstream);
   for (DevBuf* b : {&c->d_ssum, &c->d_tab[0], &c->d_tab[1], &c->d_tctl[0], &c->d_tctl[1],
                     &c->d_stage, &c->d_msg})
     b->release();
@@ -579,6 +594,7 @@ void hbx_ctx_destroy(hbx_ctx* c) {
     (void)hipEventDestroy(t.b);
   }
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+  if (c->hstream && c->hstream != c->stream) (void)hipStreamDestroy(c->hstream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
