@@ -520,7 +520,7 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, int s) {
 }
 #define HBX_F(b, c, d) ((((c) ^ (d)) & (b)) ^ (d))
 #define HBX_G(b, c, d) ((((b) ^ (c)) & (d)) ^ (c))
-#define HBX_H(b, c, d) ((b) ^ (c) ^ (d))
+#define HBX_H(b, c, d) __builtin_amdgcn_bitop3_b32((b), (c), (d), 0x96)  // b ^ c ^ d in one op
 #define HBX_I(b, c, d) ((c) ^ ((b) | ~(d)))
 #define HBX_STEP(FN, a, b, c, d, x, t, s) a = (b) + rotl((a) + (FN(b, c, d)) + (x) + (t), s)
 
@@ -632,6 +632,11 @@ __device__ __forceinline__ uint32_t msg_word(uint32_t widx, uint32_t lo, uint32_
 #ifndef HBX_MD5_RING
 #define HBX_MD5_RING 8
 #endif
+// 1: load each block's 16 message words straight from their (unaligned) byte
+// address instead of aligned dwords + 16 v_alignbyte per block
+#ifndef HBX_MD5_UNALIGNED
+#define HBX_MD5_UNALIGNED 0
+#endif
 __device__ void md5_run(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32_t b0, uint32_t cnt,
                         bool finish) {
   constexpr int RING = HBX_MD5_RING;  // blocks of prefetch (16 VGPRs each)
@@ -653,10 +658,19 @@ __device__ void md5_run(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32
     c0 = va[16u * b0 - 2u];
     c1 = va[16u * b0 - 1u];
   }
+#if HBX_MD5_UNALIGNED
+  // message block b >= 1 = data bytes [64b-8, 64b+56); block 0 loads data
+  // bytes [0, 64) and shifts by two words (its first two are the framing)
+  auto blk_src = [&](uint32_t b) {
+    return reinterpret_cast<const u32x4*>(b ? c + 64u * b - 8u : c);
+  };
+#else
+  auto blk_src = [&](uint32_t b) { return reinterpret_cast<const u32x4*>(va + 16u * b); };
+#endif
   u32x4 ring[RING][4];
 #pragma unroll
   for (int r = 0; r < RING; r++) {
-    const u32x4* src = reinterpret_cast<const u32x4*>(va + 16u * min(b0 + (uint32_t)r, last));
+    const u32x4* src = blk_src(min(b0 + (uint32_t)r, last));
 #pragma unroll
     for (int i = 0; i < 4; i++) ring[r][i] = __builtin_nontemporal_load(src + i);
   }
@@ -669,8 +683,19 @@ __device__ void md5_run(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32
       R[4 * q + 2] = ring[r][q].z;
       R[4 * q + 3] = ring[r][q].w;
     }
-    // message word j = data word 16b+j-2 = bytes of R[16b+j-2], R[16b+j-1]
     uint32_t m[16];
+#if HBX_MD5_UNALIGNED
+#pragma unroll
+    for (int j = 0; j < 16; j++) m[j] = R[j];
+    if (i == 0u && any_first) {  // wave-uniform; block 0 carries the framing
+      const bool f = b0 == 0u;
+#pragma unroll
+      for (int j = 15; j >= 2; j--) m[j] = f ? R[j - 2] : R[j];
+      m[0] = f ? 0u : R[0];
+      m[1] = f ? bswap32(len) : R[1];
+    }
+#else
+    // message word j = data word 16b+j-2 = bytes of R[16b+j-2], R[16b+j-1]
     m[0] = alignbyte(c1, c0, sh);
     m[1] = alignbyte(R[0], c1, sh);
 #pragma unroll
@@ -681,16 +706,27 @@ __device__ void md5_run(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32
     }
     c0 = R[14];
     c1 = R[15];
-    // refill only after the slot's registers are consumed: the load then
-    // reuses them and the ring needs no copies at the loop back-edge
-    if (refill) {
-      const u32x4* src = reinterpret_cast<const u32x4*>(va + 16u * min(b0 + i + (uint32_t)RING, last));
+#endif
+    auto do_refill = [&]() {
+      const u32x4* src = blk_src(min(b0 + i + (uint32_t)RING, last));
 #pragma unroll
       for (int q = 0; q < 4; q++) ring[r][q] = __builtin_nontemporal_load(src + q);
-    }
+    };
+#if HBX_MD5_UNALIGNED
+    // the message words ARE the slot's registers: refill once compressed
+    uint32_t t[4] = {h[0], h[1], h[2], h[3]};
+    md5_compress(t, m);
+    __builtin_amdgcn_sched_barrier(0);
+    if (refill) do_refill();
+#else
+    // refill only after the slot's registers are consumed (the aligned
+    // words feed v_alignbyte): the load then reuses them and the ring needs
+    // no copies at the loop back-edge
+    if (refill) do_refill();
     __builtin_amdgcn_sched_barrier(0);  // keep the refill ahead of this block's compression
     uint32_t t[4] = {h[0], h[1], h[2], h[3]};
     md5_compress(t, m);
+#endif
     const bool live = i < cnt;
 #pragma unroll
     for (int q = 0; q < 4; q++) h[q] = live ? t[q] : h[q];
