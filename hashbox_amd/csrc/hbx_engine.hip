@@ -140,8 +140,9 @@ struct hbx_ctx {
   int tab_cur = -1;         // table holding the last launch's chains (-1: none in flight)
   DevBuf d_stage;           // host-input arena
   DevBuf d_msg;             // hbx_block_id message
-  PinBuf h_stage;           // hbx_store_paths: pinned landing buffer for file reads
-  hbx_ctx* twin = nullptr;  // hbx_store_paths: second context (double buffering)
+  PinBuf h_read[2];         // hbx_store_paths: pinned landing slots for file reads
+  hipEvent_t h2d_done[2] = {nullptr, nullptr};  // slot's H2D copy has completed
+  std::vector<DevBuf> d_ring;  // hbx_store_paths: device arenas of the batches in flight
 
   std::deque<Batch*> pending;  // submitted, not yet collected (FIFO)
   std::vector<Batch*> pool;
@@ -582,8 +583,10 @@ void hbx_ctx_destroy(hbx_ctx* c) {
   for (DevBuf* b : {&c->d_ssum, &c->d_tab[0], &c->d_tab[1], &c->d_tctl[0], &c->d_tctl[1],
                     &c->d_stage, &c->d_msg})
     b->release();
-  c->h_stage.release();
-  if (c->twin) hbx_ctx_destroy(c->twin);
+  for (PinBuf& h : c->h_read) h.release();
+  for (DevBuf& d : c->d_ring) d.release();
+  for (hipEvent_t e : c->h2d_done)
+    if (e) (void)hipEventDestroy(e);
   for (Batch* b : c->pending) c->pool.push_back(b);
   for (Batch* b : c->pool) {
     b->release();
@@ -813,67 +816,59 @@ int hbx_store_paths(hbx_ctx* c, uint64_t n, const char* const* paths, const uint
   std::lock_guard<std::mutex> g(c->mu);
   if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
   HBX_TRY(c, hipSetDevice(c->device));
-  if (!c->twin) {
-    int rc = hbx_ctx_create(c->device, &c->twin);
-    if (rc) return c->fail(rc, "cannot create the second context");
-    c->twin->tile_iters = c->tile_iters;
-    c->twin->md5_wgs = c->md5_wgs;
-    c->twin->k1_dma = c->k1_dma;
-  }
   if (batch_bytes < (64ull << 20)) batch_bytes = 64ull << 20;
-  hbx_ctx* X[2] = {c, c->twin};
-  struct Batch {
-    uint64_t first = 0, count = 0, total = 0;
-    std::vector<uint64_t> offs;
-  } B[2];
-  auto finish = [&](int s) -> int {  // wait for slot s's batch and scatter its results
-    Batch& b = B[s];
-    if (!b.count) return HBX_OK;
-    int rc = wait_oldest(X[s]);
-    b.count = 0;
-    if (rc) c->err = X[s]->err;
-    return rc;
-  };
-  uint64_t f = 0;
-  int slot = 0;
-  while (f < n) {
-    int rc = finish(slot);  // the slot's buffers are free again
-    if (rc) return rc;
-    Batch& b = B[slot];
-    b.first = f;
-    b.offs.clear();
+  for (hipEvent_t& e : c->h2d_done)
+    if (!e) HBX_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  // Pipeline: files of batch k are read (io_threads) into pinned slot k % 2
+  // while earlier batches copy and hash; the H2D copy runs on the scan
+  // stream into device arena k % depth, and the batch joins the time-sliced
+  // MD5 chains.  A pinned slot is free once its copy has completed, a device
+  // arena once its batch has been collected.
+  const uint32_t budget = c->md5_slice ? c->md5_slice : kBudgetAll;
+  const uint64_t nfull_max = (HBX_MAX_BLOCK_SIZE + 8ull) >> 6;
+  const size_t depth = budget == kBudgetAll ? 2 : (size_t)std::min<uint64_t>(
+      64, (nfull_max + budget - 1) / budget + 1);
+  if (c->d_ring.size() < depth) c->d_ring.resize(depth);
+  bool slot_used[2] = {false, false};
+  std::vector<uint64_t> offs;
+  uint64_t f = 0, k = 0;
+  int rc = HBX_OK;
+  while (f < n && rc == HBX_OK) {
+    const uint64_t first = f;
+    offs.clear();
     uint64_t tot = 0;
-    while (f < n && (b.offs.empty() || tot + lens[f] <= batch_bytes) && b.offs.size() < 65536) {
-      b.offs.push_back(tot);
+    while (f < n && (offs.empty() || tot + lens[f] <= batch_bytes) && offs.size() < 65536) {
+      offs.push_back(tot);
       tot += (lens[f] + 255) & ~uint64_t(255);
       f++;
     }
-    b.count = f - b.first;
-    b.total = tot;
-    hbx_ctx* x = X[slot];
-    HBX_TRY(c, x->h_stage.ensure(tot + 65536));
-    HBX_TRY(c, x->d_stage.ensure(tot + 65536));
-    rc = read_files(b.count, paths + b.first, lens + b.first, b.offs.data(), x->h_stage.as<uint8_t>(),
+    const int p = (int)(k & 1);
+    DevBuf& arena = c->d_ring[k % depth];
+    if (c->pending.size() >= depth && (rc = wait_oldest(c))) break;  // frees arena k % depth
+    if (slot_used[p] && (rc = c->hip(hipEventSynchronize(c->h2d_done[p]), "h2d wait"))) break;
+    if ((rc = c->hip(c->h_read[p].ensure(tot + 65536), "pinned staging"))) break;
+    if ((rc = ensure_shared(c, arena, tot + 65536))) break;
+    rc = read_files(f - first, paths + first, lens + first, offs.data(), c->h_read[p].as<uint8_t>(),
                     io_threads, c->err);
-    if (rc) {
-      b.count = 0;
-      (void)finish(slot ^ 1);
-      return rc;
-    }
-    HBX_TRY(c, hipMemcpyAsync(x->d_stage.p, x->h_stage.p, tot, hipMemcpyHostToDevice, x->stream));
-    rc = submit_batch(x, x->d_stage.p, b.count, b.offs.data(), lens + b.first, cut_ends, ids,
-                      out_base + b.first, caps + b.first, sums ? sums + b.first : nullptr, kBudgetAll);
-    if (rc) {
-      c->err = x->err;
-      b.count = 0;
-      (void)finish(slot ^ 1);
-      return rc;
-    }
-    slot ^= 1;
+    if (rc) break;
+    if ((rc = c->hip(hipMemcpyAsync(arena.p, c->h_read[p].p, tot, hipMemcpyHostToDevice, c->stream),
+                     "hipMemcpyAsync")))
+      break;
+    if ((rc = c->hip(hipEventRecord(c->h2d_done[p], c->stream), "hipEventRecord"))) break;
+    slot_used[p] = true;
+    rc = submit_batch(c, arena.p, f - first, offs.data(), lens + first, cut_ends, ids,
+                      out_base + first, caps + first, sums ? sums + first : nullptr, budget);
+    k++;
   }
-  int rc0 = finish(slot);
-  int rc1 = finish(slot ^ 1);
-  return rc0 ? rc0 : rc1;
+  // collect everything in flight (also after a failure: the caller's arrays
+  // must not be written once this call has returned)
+  while (!c->pending.empty()) {
+    const std::string keep = c->err;
+    const int r2 = wait_oldest(c);
+    if (rc == HBX_OK) rc = r2;
+    else c->err = keep;
+  }
+  return rc;
 }
 
 int hbx_memcpy_h2d_async(hbx_ctx* c, void* d, const void* h, uint64_t n) {

@@ -130,10 +130,11 @@ int hbx_pending(hbx_ctx *ctx);
 int hbx_set_md5_slice(hbx_ctx *ctx, uint32_t blocks);
 
 /* Files on disk, end to end (storeFile over a list of paths, store.go:84-199
- * with the tree walk left to the caller): io_threads read the files straight
- * into pinned staging, batches of up to batch_bytes alternate between two
- * HIP streams so reading batch b+1 overlaps the H2D copy and kernels of
- * batch b.  lens[i] must be the file sizes (stat); a file that cannot be
+ * with the tree walk left to the caller): io_threads read batches of up to
+ * batch_bytes straight into two pinned slots; each batch is copied into a
+ * ring of device arenas and pipelined like hbx_submit_device, so reading
+ * batch b+1 overlaps the copy of batch b and the hashing of every batch
+ * still in flight.  lens[i] must be the file sizes (stat); a file that cannot be
  * read in full fails the call with HBX_ERR_IO.  Outputs as
  * hbx_chunk_hash_batch. */
 int hbx_store_paths(hbx_ctx *ctx, uint64_t n_files, const char *const *paths,
