@@ -50,12 +50,16 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-files", type=int, default=32,
                     help="files of the batch timed on the CPU oracle (bounded sample)")
-    ap.add_argument("--md5-slice", type=int, default=16384,
+    ap.add_argument("--md5-slice", type=int, default=-1,
                     help="K3 time slice in 64-B MD5 blocks per chain per launch (0 = each batch "
-                         "hashed alone in one launch)")
+                         "hashed alone in one launch; -1 = sized from HBM, see --hbm-frac)")
     ap.add_argument("--arenas", type=int, default=0,
                     help="distinct resident batches (default: the pipeline depth the slice "
                          "schedule needs, so no step forces a drain)")
+    ap.add_argument("--hbm-frac", type=float, default=0.7,
+                    help="with --md5-slice -1: fraction of free HBM given to resident batches; "
+                         "throughput ~ resident bytes / batch latency (the longest chunk's "
+                         "serial MD5), so the pipeline is made as deep as this allows")
     ap.add_argument("--e2e", action="store_true",
                     help="host-inclusive mode: files in pinned host memory, H2D of batch i+1 "
                          "overlapped with the kernels of batch i (two contexts)")
@@ -175,12 +179,21 @@ def main():
     nf, fbytes = a.files, a.file_mib << 20
     lens = [fbytes] * nf
     offs, total = pack_arena_layout(lens)
-    B = max(0, a.md5_slice)
     # launches a batch needs before its chains are all hashed; a batch can be
     # collected without a forced drain once `need` newer steps have launched
     nfull = (min(fbytes, 8 << 20) + 8) >> 6
+    if a.md5_slice < 0:
+        free, _ = torch.cuda.mem_get_info(dev)
+        r_fit = max(2, int(free * a.hbm_frac) // (total + (64 << 20)))
+        R = a.arenas if a.arenas > 0 else r_fit
+        B = -(-nfull // max(1, R - 1))
+    else:
+        B = a.md5_slice
     need = 1 if B == 0 else -(-nfull // B)
-    R = a.arenas if a.arenas > 0 else need + 1
+    if a.arenas > 0:
+        R = a.arenas
+    elif a.md5_slice >= 0:
+        R = need + 1
     # synthetic uniform random bytes, generated on the device (per-rank seed);
     # R distinct resident batches, batch j reads arena j % R
     g = torch.Generator(device=dev)
