@@ -637,6 +637,18 @@ __device__ __forceinline__ uint32_t msg_word(uint32_t widx, uint32_t lo, uint32_
 #ifndef HBX_MD5_UNALIGNED
 #define HBX_MD5_UNALIGNED 0
 #endif
+// 1: chunk bytes are loaded nontemporal (streamed past the caches)
+#ifndef HBX_MD5_NT
+#define HBX_MD5_NT 1
+#endif
+template <class T>
+__device__ __forceinline__ T md5_load(const T* p) {
+#if HBX_MD5_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
 __device__ void md5_run(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32_t b0, uint32_t cnt,
                         bool finish) {
   constexpr int RING = HBX_MD5_RING;  // blocks of prefetch (16 VGPRs each)
@@ -672,7 +684,7 @@ __device__ void md5_run(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32
   for (int r = 0; r < RING; r++) {
     const u32x4* src = blk_src(min(b0 + (uint32_t)r, last));
 #pragma unroll
-    for (int i = 0; i < 4; i++) ring[r][i] = __builtin_nontemporal_load(src + i);
+    for (int i = 0; i < 4; i++) ring[r][i] = md5_load(src + i);
   }
   auto block = [&](int r, uint32_t i, bool refill) {
     uint32_t R[16];
@@ -710,7 +722,7 @@ __device__ void md5_run(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32
     auto do_refill = [&]() {
       const u32x4* src = blk_src(min(b0 + i + (uint32_t)RING, last));
 #pragma unroll
-      for (int q = 0; q < 4; q++) ring[r][q] = __builtin_nontemporal_load(src + q);
+      for (int q = 0; q < 4; q++) ring[r][q] = md5_load(src + q);
     };
 #if HBX_MD5_UNALIGNED
     // the message words ARE the slot's registers: refill once compressed
