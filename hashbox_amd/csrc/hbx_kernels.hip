@@ -637,9 +637,9 @@ __device__ __forceinline__ uint32_t msg_word(uint32_t widx, uint32_t lo, uint32_
 #ifndef HBX_MD5_UNALIGNED
 #define HBX_MD5_UNALIGNED 0
 #endif
-// 1: chunk bytes are loaded nontemporal (streamed past the caches)
+// 1: chunk bytes are loaded nontemporal (measured slower: 99 vs 88 ms per batch)
 #ifndef HBX_MD5_NT
-#define HBX_MD5_NT 1
+#define HBX_MD5_NT 0
 #endif
 template <class T>
 __device__ __forceinline__ T md5_load(const T* p) {
@@ -880,15 +880,21 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
 // wave in the planner's order).  Each lane resumes its chain at `next`,
 // compresses up to `budget` full blocks and either finishes (tail blocks,
 // BlockID stored at `out`, entry marked done) or saves the state for the
-// next launch.  grid = one 512-thread workgroup per CU; group g runs on wave
-// (g / grid) % 8 of workgroup g % grid, so the first 4 x grid groups each get
+// next launch.  grid = one 256-thread workgroup per CU; group g runs on wave
+// (g / grid) % 4 of workgroup g % grid, so the first 4 x grid groups each get
 // a SIMD of their own.  The MD5 chain is bound by its 4 dependent VALU per
 // step; lane mode runs 64 such chains in one instruction stream at that
 // bound (DESIGN.md "K3"; tools/experiments/md5_wave_mode.hip for what did
 // not pay).
-constexpr int kK3Threads = 512;
+// 256 threads = one wave per SIMD: a single wave saturates its SIMD's issue
+// slots, and one wave per SIMD lets the compiler use the whole register file
+// (VGPR + AGPR) for the prefetch ring without spilling.
+#ifndef HBX_K3_THREADS
+#define HBX_K3_THREADS 256
+#endif
+constexpr int kK3Threads = HBX_K3_THREADS;
 
-extern "C" __global__ __launch_bounds__(kK3Threads) void hbx_k3_block_md5(
+extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
     Chain* __restrict__ tab, const uint32_t* __restrict__ ctl, uint32_t budget) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
