@@ -892,6 +892,9 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
 #ifndef HBX_K3_THREADS
 #define HBX_K3_THREADS 256
 #endif
+#ifndef HBX_K3_DENSE
+#define HBX_K3_DENSE 0
+#endif
 constexpr int kK3Threads = HBX_K3_THREADS;
 
 extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
@@ -901,7 +904,14 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
   const uint32_t n_total = ctl[1];
   const uint32_t groups = (n_total + 63u) / 64u;
   const uint32_t nwaves = gridDim.x * (kK3Threads / 64);
-  for (uint32_t g = wave * gridDim.x + blockIdx.x; g < groups; g += nwaves) {
+#if HBX_K3_DENSE
+  // dense: group g on wave g % W of workgroup g / W, so the busy waves fill
+  // the fewest CUs and whole CUs stay free for the scan stream's K1/K2
+  const uint32_t g0 = blockIdx.x * (kK3Threads / 64) + wave;
+#else
+  const uint32_t g0 = wave * gridDim.x + blockIdx.x;
+#endif
+  for (uint32_t g = g0; g < groups; g += nwaves) {
     const uint32_t k = 64u * g + lane;
     const bool active = k < n_total;
     // idle lanes stay alive for the wave-wide loop bound: they run an empty
