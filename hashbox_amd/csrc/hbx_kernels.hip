@@ -16,6 +16,8 @@
 //                          (hashback/hashback.go:162-170) with links = ids
 //                          (type 3).
 // No MFMA anywhere: this is a byte scan plus an integer hash.
+#include <type_traits>
+
 #include "hbx_device.h"
 
 using namespace hbx;
@@ -629,6 +631,8 @@ __device__ __forceinline__ uint32_t msg_word(uint32_t widx, uint32_t lo, uint32_
 // last full block.  `c` is the chunk start.  Reads stay within the chunk +
 // 64 bytes (HBX_ARENA_SLACK): every dword holding chunk bytes and never more
 // than 63 bytes past the chunk end.
+__device__ void md5_tail(const uint8_t* c, uint32_t len, uint32_t (&h)[4], bool finish);
+
 #ifndef HBX_MD5_RING
 #define HBX_MD5_RING 8
 #endif
@@ -654,8 +658,6 @@ __device__ void md5_run(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32
   constexpr int RING = HBX_MD5_RING;  // blocks of prefetch (16 VGPRs each)
   const uint32_t sh = (uint32_t)reinterpret_cast<uintptr_t>(c) & 3u;
   const uint32_t* va = reinterpret_cast<const uint32_t*>(c - sh);  // raw R[r] = va[r]
-  const uint32_t T = len + 8u;  // message bytes (prefix + data)
-  const uint32_t nfull = T >> 6;
   const uint32_t last = cnt ? b0 + cnt - 1u : b0;  // prefetches clamp to this block
   // Block b needs raw dwords R[16b-2 .. 16b+15]: 16 loaded with it (4 x
   // dwordx4 at va+64b, never below the chunk start) plus 2 carried.  Loads
@@ -752,6 +754,15 @@ __device__ void md5_run(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32
   for (int r = 0; r < RING - 1; r++) {
     if (i + (uint32_t)r < nmax) block(r, i + (uint32_t)r, false);
   }
+  md5_tail(c, len, h, finish);
+}
+
+// The 1-2 padded tail blocks after the last full block (lanes with `finish`).
+__device__ void md5_tail(const uint8_t* c, uint32_t len, uint32_t (&h)[4], bool finish) {
+  const uint32_t sh = (uint32_t)reinterpret_cast<uintptr_t>(c) & 3u;
+  const uint32_t* va = reinterpret_cast<const uint32_t*>(c - sh);
+  const uint32_t T = len + 8u;
+  const uint32_t nfull = T >> 6;
   // tail: remaining message bytes + 0x80 + zeros + 64-bit bit length
   const uint32_t rem = T - 64u * nfull;  // 0..63
   const uint32_t ntail = finish ? ((rem + 9u > 64u) ? 2u : 1u) : 0u;
@@ -778,6 +789,115 @@ __device__ void md5_run(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32
   }
 }
 
+// One full message block b of a lane's chain through plain per-lane loads
+// (the prologue of the cooperative path below: it puts every lane of the
+// wave at a block >= 1, where the message words are data words).
+__device__ void md5_block_at(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32_t b) {
+  const uint32_t sh = (uint32_t)reinterpret_cast<uintptr_t>(c) & 3u;
+  const uint32_t* va = reinterpret_cast<const uint32_t*>(c - sh);
+  const uint32_t base = b ? 16u * b - 2u : 0u;
+  uint32_t v[17];
+#pragma unroll
+  for (int j = 0; j < 17; j++) v[j] = va[base + (uint32_t)j];
+  uint32_t m[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const uint32_t dw = alignbyte(v[j + 1], v[j], sh);                    // b >= 1: word j
+    const uint32_t d0 = j >= 2 ? alignbyte(v[j - 1], v[j - 2], sh) : 0u;  // b == 0
+    m[j] = b ? dw : (j == 0 ? 0u : j == 1 ? bswap32(len) : d0);
+  }
+  md5_compress(h, m);
+}
+
+// Cooperative streaming for a wave whose 64 lanes all advance exactly R
+// blocks, lane j from block b1_j >= 1 of its own chain.  Lane-mode loads put
+// 64 chains (64 pages) in every load instruction and the per-CU address
+// translation thrashes (89 % UTCL1 misses); here load
+// instruction q fetches 256 contiguous bytes of each of 4 chains, so it
+// touches ~4 pages.  Each chain's message stream is read dword-aligned from
+// S_j = chunk + 64*b1 - 8 - (chunk & 3), staged 4 blocks (16 granules of 16
+// B) at a time through registers into LDS (rows of 272 B: conflict-free, all
+// offsets immediate), two stages resident (the current one and the next),
+// and each lane reads its own row with 4 aligned ds_read_b128 per block.
+constexpr uint32_t kCoopRow = 272u;              // 256 B of one chain's stage + 16 B pad
+constexpr uint32_t kCoopHalf = 64u * kCoopRow;   // one stage of the wave's 64 chains
+constexpr uint32_t kCoopWaveLds = 2u * kCoopHalf;
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src_lane) {
+  const int lo = __builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)(uint32_t)v);
+  const int hi = __builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)(uint32_t)(v >> 32));
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+template <int HALF>
+__device__ __forceinline__ void coop_write(uint8_t* wl, uint32_t wr, const u32x4 (&G)[16]) {
+#pragma unroll
+  for (int q = 0; q < 16; q++)
+    *reinterpret_cast<u32x4*>(wl + wr + (uint32_t)HALF * kCoopHalf + 1088u * (uint32_t)q) = G[q];
+}
+
+// Loads of stage `st` (granules 16*st .. 16*st+15 of every chain) into G;
+// granules >= ngr (past the last needed dword) are not read.
+__device__ __forceinline__ void coop_load(u32x4 (&G)[16], const uint64_t (&Q)[16], uint32_t st,
+                                          uint32_t t, uint32_t ngr) {
+  const uint64_t off = 256ull * st;
+  if (16u * st + 16u <= ngr) {
+#pragma unroll
+    for (int q = 0; q < 16; q++) G[q] = md5_load(reinterpret_cast<const u32x4*>(Q[q] + off));
+  } else if (16u * st + t < ngr) {
+#pragma unroll
+    for (int q = 0; q < 16; q++) G[q] = md5_load(reinterpret_cast<const u32x4*>(Q[q] + off));
+  }
+}
+
+__device__ void md5_coop(uint8_t* wl, const uint8_t* c, uint32_t (&h)[4], uint32_t b1, uint32_t R) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t sh = (uint32_t)reinterpret_cast<uintptr_t>(c) & 3u;
+  const uint64_t S = reinterpret_cast<uint64_t>(c) + 64ull * b1 - 8ull - sh;
+  const uint32_t t = lane & 15u, sub = lane >> 4;
+  uint64_t Q[16];  // role q: chain 4q+sub, granule t of each stage
+#pragma unroll
+  for (int q = 0; q < 16; q++) Q[q] = shfl64(S, 4u * (uint32_t)q + sub) + 16ull * t;
+  const uint32_t wr = sub * kCoopRow + 16u * t;  // + 1088 q: row 4q+sub, granule t
+  const uint32_t rd = lane * kCoopRow;           // this lane's row
+  const uint32_t ngr = 4u * R + 1u;              // granules holding dwords 0 .. 16R
+  const uint32_t nst = (ngr + 15u) / 16u;
+  u32x4 G[16];
+  coop_load(G, Q, 0u, t, ngr);
+  coop_write<0>(wl, wr, G);
+  if (nst > 1u) coop_load(G, Q, 1u, t, ngr);
+  // window: granules g..g+4 of the current block (W[0] carried)
+  u32x4 W0 = *reinterpret_cast<const u32x4*>(wl + rd);
+  auto stage_pair = [&](auto half_c, uint32_t s) {
+    constexpr int HALF = decltype(half_c)::value;
+    // start of stage s: stage s+1 into the other half, loads of s+2 issued
+    if (s + 1u < nst) coop_write<HALF ^ 1>(wl, wr, G);
+    if (s + 2u < nst) coop_load(G, Q, s + 2u, t, ngr);
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t blk = 4u * s + (uint32_t)u;
+      if (blk >= R) break;  // wave-uniform
+      const uint8_t* hb = wl + rd + (uint32_t)HALF * kCoopHalf;
+      const u32x4 W1 = *reinterpret_cast<const u32x4*>(hb + 16u * (4u * u + 1u));
+      const u32x4 W2 = *reinterpret_cast<const u32x4*>(hb + 16u * (4u * u + 2u));
+      const u32x4 W3 = *reinterpret_cast<const u32x4*>(hb + 16u * (4u * u + 3u));
+      const u32x4 W4 = u < 3 ? *reinterpret_cast<const u32x4*>(hb + 16u * (4u * u + 4u))
+                             : *reinterpret_cast<const u32x4*>(wl + rd + (uint32_t)(HALF ^ 1) * kCoopHalf);
+      const uint32_t D[17] = {W0.x, W0.y, W0.z, W0.w, W1.x, W1.y, W1.z, W1.w, W2.x,
+                              W2.y, W2.z, W2.w, W3.x, W3.y, W3.z, W3.w, W4.x};
+      uint32_t m[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) m[i] = alignbyte(D[i + 1], D[i], sh);
+      md5_compress(h, m);
+      W0 = W4;
+    }
+  };
+  for (uint32_t s = 0; 4u * s < R; s += 2u) {
+    stage_pair(std::integral_constant<int, 0>{}, s);
+    if (4u * (s + 1u) < R) stage_pair(std::integral_constant<int, 1>{}, s + 1u);
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------ MD5 chain table --
@@ -801,7 +921,11 @@ __device__ __forceinline__ uint32_t chain_cnt(uint32_t len, uint32_t next, uint3
   const uint32_t nfull = (len + 8u) >> 6;
   return min(nfull - next, budget);
 }
-__device__ __forceinline__ uint32_t chain_bucket(uint32_t cnt) { return 31u - __builtin_clz(cnt + 1u); }
+// Planner order key: chains advancing exactly `budget` blocks (the
+// cooperative K3 path's waves) first, then log2 buckets of the block count.
+__device__ __forceinline__ uint32_t chain_bucket(uint32_t cnt, uint32_t budget) {
+  return (cnt == budget) ? 32u : 31u - __builtin_clz(cnt + 1u);
+}
 
 // ----------------------------------------------------------- K2c plan --
 // Builds the chain table for one K3 launch: the unfinished chains of the
@@ -817,14 +941,14 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
     const uint32_t* __restrict__ cut_count, uint32_t* __restrict__ ids, const Chain* __restrict__ prev,
     const uint32_t* __restrict__ prev_ctl, Chain* __restrict__ cur, uint32_t* __restrict__ ctl,
     uint32_t budget) {
-  __shared__ uint32_t hist[32], pos[32];
+  __shared__ uint32_t hist[33], pos[33];
   const uint32_t tid = threadIdx.x;
   const uint32_t n_prev = prev ? prev_ctl[1] : 0u;
-  if (tid < 32) hist[tid] = 0u;
+  if (tid < 33) hist[tid] = 0u;
   __syncthreads();
   for (uint32_t e = tid; e < n_prev; e += kPlanThreads) {
     const Chain ch = prev[e];
-    if (ch.next != kChainDone) atomicAdd(&hist[chain_bucket(chain_cnt(ch.len, ch.next, budget))], 1u);
+    if (ch.next != kChainDone) atomicAdd(&hist[chain_bucket(chain_cnt(ch.len, ch.next, budget), budget)], 1u);
   }
   for (uint32_t f = tid; f < n_files; f += kPlanThreads) {
     const uint64_t cb = cut_base[f];
@@ -832,25 +956,26 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
     uint64_t start = 0;
     for (uint32_t i = 0; i < k; i++) {
       const uint64_t e = cut_ends[cb + i];
-      atomicAdd(&hist[chain_bucket(chain_cnt((uint32_t)(e - start), 0u, budget))], 1u);
+      atomicAdd(&hist[chain_bucket(chain_cnt((uint32_t)(e - start), 0u, budget), budget)], 1u);
       start = e;
     }
   }
   __syncthreads();
   if (tid == 0) {
     uint32_t p = 0;
-    for (int bk = 31; bk >= 0; bk--) {
+    for (int bk = 32; bk >= 0; bk--) {
       pos[bk] = p;
       p += hist[bk];
     }
     ctl[0] = 0u;
     ctl[1] = p;
+    ctl[2] = hist[32];  // leading chains that advance exactly `budget` blocks
   }
   __syncthreads();
   for (uint32_t e = tid; e < n_prev; e += kPlanThreads) {
     const Chain ch = prev[e];
     if (ch.next != kChainDone)
-      cur[atomicAdd(&pos[chain_bucket(chain_cnt(ch.len, ch.next, budget))], 1u)] = ch;
+      cur[atomicAdd(&pos[chain_bucket(chain_cnt(ch.len, ch.next, budget), budget)], 1u)] = ch;
   }
   for (uint32_t f = tid; f < n_files; f += kPlanThreads) {
     const uint64_t cb = cut_base[f];
@@ -869,7 +994,7 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
       ch.h[3] = 0x10325476u;
       ch.out = reinterpret_cast<uint64_t>(ids + 4u * (cb + i));
       ch.pad = 0ull;
-      cur[atomicAdd(&pos[chain_bucket(chain_cnt(ch.len, 0u, budget))], 1u)] = ch;
+      cur[atomicAdd(&pos[chain_bucket(chain_cnt(ch.len, 0u, budget), budget)], 1u)] = ch;
       start = e;
     }
   }
@@ -895,6 +1020,11 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
 #ifndef HBX_K3_DENSE
 #define HBX_K3_DENSE 0
 #endif
+// cooperative (page-local) loads for waves of full-slice chains
+#ifndef HBX_K3_COOP
+#define HBX_K3_COOP 1
+#endif
+constexpr uint32_t kCoopMinBudget = 8u;
 constexpr int kK3Threads = HBX_K3_THREADS;
 
 extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
@@ -902,6 +1032,13 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t n_total = ctl[1];
+#if HBX_K3_COOP
+  static_assert(kK3Threads == 256, "cooperative K3 path sized for 4 waves per workgroup");
+  __shared__ __attribute__((aligned(16))) uint8_t k3_lds[kK3Threads / 64][kCoopWaveLds];
+  // the planner puts chains advancing exactly `budget` blocks first
+  const uint32_t coop_groups =
+      (budget >= kCoopMinBudget && budget != kBudgetAll) ? ctl[2] / 64u : 0u;
+#endif
   const uint32_t groups = (n_total + 63u) / 64u;
   const uint32_t nwaves = gridDim.x * (kK3Threads / 64);
 #if HBX_K3_DENSE
@@ -912,6 +1049,26 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
   const uint32_t g0 = wave * gridDim.x + blockIdx.x;
 #endif
   for (uint32_t g = g0; g < groups; g += nwaves) {
+#if HBX_K3_COOP
+    if (g < coop_groups) {  // wave-uniform: 64 chains, each advancing exactly `budget` blocks
+      const uint32_t k = 64u * g + lane;
+      const Chain ch = tab[k];
+      const uint8_t* src = reinterpret_cast<const uint8_t*>(ch.src);
+      uint32_t h[4] = {ch.h[0], ch.h[1], ch.h[2], ch.h[3]};
+      md5_block_at(src, ch.len, h, ch.next);  // every lane now at a block >= 1
+      md5_coop(k3_lds[wave], src, h, ch.next + 1u, budget - 1u);
+      const bool finish = ch.next + budget == ((ch.len + 8u) >> 6);
+      md5_tail(src, ch.len, h, finish);
+      if (finish) {
+        *reinterpret_cast<uint4*>(ch.out) = make_uint4(h[0], h[1], h[2], h[3]);
+        tab[k].next = kChainDone;
+      } else {
+        *reinterpret_cast<uint4*>(&tab[k].h[0]) = make_uint4(h[0], h[1], h[2], h[3]);
+        tab[k].next = ch.next + budget;
+      }
+      continue;
+    }
+#endif
     const uint32_t k = 64u * g + lane;
     const bool active = k < n_total;
     // idle lanes stay alive for the wave-wide loop bound: they run an empty
