@@ -75,7 +75,7 @@ def measured_traffic(kernel, nf, fbytes):
     counters cannot be read inside this timed run)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
-    if not files or (nf, fbytes) != (64, 128 << 20):
+    if not files or (nf, fbytes) != (64, 128 << 20):  # measured on the default workload only
         return None, None
     d = json.load(open(files[-1]))
     k = d.get("kernels", {}).get(kernel)
