@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -143,6 +144,7 @@ struct hbx_ctx {
   PinBuf h_read[2];         // hbx_store_paths: pinned landing slots for file reads
   hipEvent_t h2d_done[2] = {nullptr, nullptr};  // slot's H2D copy has completed
   std::vector<DevBuf> d_ring;  // hbx_store_paths: device arenas of the batches in flight
+  double io_s[3] = {0, 0, 0};  // hbx_store_paths: reading files | waiting for an arena | waiting for a copy
 
   std::deque<Batch*> pending;  // submitted, not yet collected (FIFO)
   std::vector<Batch*> pool;
@@ -829,6 +831,24 @@ int hbx_store_paths(hbx_ctx* c, uint64_t n, const char* const* paths, const uint
   const size_t depth = budget == kBudgetAll ? 2 : (size_t)std::min<uint64_t>(
       64, (nfull_max + budget - 1) / budget + 1);
   if (c->d_ring.size() < depth) c->d_ring.resize(depth);
+  // size every staging buffer once, for the largest batch this call forms
+  // (growing one later would re-pin host memory or drain the streams)
+  uint64_t biggest = 0;
+  for (uint64_t i = 0; i < n;) {
+    uint64_t tot = 0, cnt = 0;
+    while (i < n && (cnt == 0 || tot + lens[i] <= batch_bytes) && cnt < 65536) {
+      tot += (lens[i] + 255) & ~uint64_t(255);
+      i++;
+      cnt++;
+    }
+    biggest = std::max(biggest, tot);
+  }
+  for (PinBuf& h : c->h_read) HBX_TRY(c, h.ensure(biggest + 65536));
+  for (size_t i = 0; i < depth; i++) {
+    int r0 = ensure_shared(c, c->d_ring[i], biggest + 65536);
+    if (r0) return r0;
+  }
+  auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   bool slot_used[2] = {false, false};
   std::vector<uint64_t> offs;
   uint64_t f = 0, k = 0;
@@ -844,12 +864,16 @@ int hbx_store_paths(hbx_ctx* c, uint64_t n, const char* const* paths, const uint
     }
     const int p = (int)(k & 1);
     DevBuf& arena = c->d_ring[k % depth];
+    double t0 = now();
     if (c->pending.size() >= depth && (rc = wait_oldest(c))) break;  // frees arena k % depth
+    double t1 = now();
     if (slot_used[p] && (rc = c->hip(hipEventSynchronize(c->h2d_done[p]), "h2d wait"))) break;
-    if ((rc = c->hip(c->h_read[p].ensure(tot + 65536), "pinned staging"))) break;
-    if ((rc = ensure_shared(c, arena, tot + 65536))) break;
+    double t2 = now();
     rc = read_files(f - first, paths + first, lens + first, offs.data(), c->h_read[p].as<uint8_t>(),
                     io_threads, c->err);
+    c->io_s[0] += now() - t2;
+    c->io_s[1] += t1 - t0;
+    c->io_s[2] += t2 - t1;
     if (rc) break;
     if ((rc = c->hip(hipMemcpyAsync(arena.p, c->h_read[p].p, tot, hipMemcpyHostToDevice, c->stream),
                      "hipMemcpyAsync")))
@@ -869,6 +893,16 @@ int hbx_store_paths(hbx_ctx* c, uint64_t n, const char* const* paths, const uint
     else c->err = keep;
   }
   return rc;
+}
+
+int hbx_io_times(hbx_ctx* c, double s[3], int reset) {
+  if (!c || !s) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  for (int i = 0; i < 3; i++) {
+    s[i] = c->io_s[i];
+    if (reset) c->io_s[i] = 0.0;
+  }
+  return HBX_OK;
 }
 
 int hbx_memcpy_h2d_async(hbx_ctx* c, void* d, const void* h, uint64_t n) {

@@ -231,6 +231,13 @@ class Engine:
                                             int(io_threads), int(batch_bytes)), "hbx_store_paths")
         return self._unpack(lens, caps, base, cuts, ids, sums)
 
+    def io_times(self, reset: bool = False) -> np.ndarray:
+        """store_paths host seconds: reading files, waiting for an arena,
+        waiting for a pinned slot's copy (cumulative)."""
+        s = (ctypes.c_double * 3)()
+        self._check(self._L.hbx_io_times(self._ctx, s, int(bool(reset))), "hbx_io_times")
+        return np.array(list(s), np.float64)
+
     def store_file(self, path: Union[str, os.PathLike]) -> FileChunks:
         """storeFile(path) for a regular file on disk (store.go:84-199)."""
         with open(path, "rb") as fh:

@@ -142,6 +142,11 @@ int hbx_store_paths(hbx_ctx *ctx, uint64_t n_files, const char *const *paths,
                     const uint64_t *out_base, const uint64_t *caps, hbx_file_summary *summaries,
                     uint32_t io_threads, uint64_t batch_bytes);
 
+/* Host seconds hbx_store_paths spent, cumulative per context: [0] reading
+ * files into pinned memory, [1] waiting for a device arena (its batch's
+ * hashing), [2] waiting for a pinned slot's H2D copy.  reset != 0 zeroes them. */
+int hbx_io_times(hbx_ctx *ctx, double s[3], int reset);
+
 /* MD5(BE32(n_links) || links || BE32(len) || data) on the device. */
 int hbx_block_id(hbx_ctx *ctx, const uint8_t *links, uint32_t n_links, const uint8_t *data,
                  uint64_t len, uint8_t out[16]);

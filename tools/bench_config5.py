@@ -57,9 +57,11 @@ def main():
     eng = Engine(0)
     try:
         eng.store_paths(paths[:2000], a.io_threads, a.batch_mib << 20)  # warm-up
+        eng.io_times(reset=True)
         t0 = time.time()
         res = eng.store_paths(paths, a.io_threads, a.batch_mib << 20)
         t_gpu = time.time() - t0
+        io = eng.io_times()
         # CPU oracle on a sample (files read from the same tmpfs, 16 threads)
         rng = np.random.Generator(np.random.PCG64(6))
         pick = np.sort(rng.choice(a.files, min(a.cpu_sample, a.files), replace=False))
@@ -78,6 +80,8 @@ def main():
             "storage": f"{a.dir} (tmpfs: page-cache resident, no device IO)",
             "e2e_seconds": round(t_gpu, 3), "e2e_gibs": round(total / t_gpu / (1 << 30), 3),
             "e2e_files_per_s": round(a.files / t_gpu, 1),
+            "host_seconds": {"read_files": round(float(io[0]), 3), "wait_arena": round(float(io[1]), 3),
+                             "wait_h2d": round(float(io[2]), 3)},
             "io_threads": a.io_threads, "batch_mib": a.batch_mib,
             "cpu_oracle": {"files": len(pick), "bytes": sample_bytes, "threads": a.io_threads,
                            "seconds": round(t_cpu, 3),
