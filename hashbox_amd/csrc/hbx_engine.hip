@@ -127,7 +127,7 @@ struct hbx_ctx {
   std::mutex mu;
   std::string err;
   uint32_t tile_iters = 64;   // K1 tile = 64 x 64 KiB (measured best: fewer halo primes)
-  uint32_t k1_dma = 1;        // K1 lands tiles in LDS by DMA (HBX_K1_DMA=0: register prefetch)
+  uint32_t k1_mode = 1;       // K1: 0 register prefetch, 1 LDS-DMA landing, 2 K1-lite (co-resides with K3)
   uint32_t md5_wgs = 256;     // K3 grid: one 512-thread workgroup per CU (set from the device)
   uint32_t md5_slice = 16384; // K3 time slice: full MD5 blocks per chain per launch (0 = unlimited)
   float stage_ms[5] = {0, 0, 0, 0, 0};
@@ -443,7 +443,12 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
   HBX_TRY(c, hipEventRecord(b->ev[0], s));
   if (nt) {
     StageTimer t(c, s, 0);
-    if (c->k1_dma)
+    if (c->k1_mode == 2)
+      hipLaunchKernelGGL(hbx_k1_digest_scan_lite, dim3((uint32_t)nt), dim3(kK1LThreads), 0, s,
+                         arena, d_off, d_len, d_sb, d_tiles,
+                         c->tile_iters * (HBX_MIN_BLOCK_SIZE / kK1LSpan), c->d_ssum.as<uint2>(),
+                         slices);
+    else if (c->k1_mode == 1)
       hipLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3((uint32_t)nt), dim3(kK1Threads), 0, s,
                          arena, d_off, d_len, d_sb, d_tiles, c->tile_iters, c->d_ssum.as<uint2>(),
                          slices);
@@ -556,7 +561,8 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->md5_wgs = (uint32_t)prop.multiProcessorCount;
-  if (const char* v = std::getenv("HBX_K1_DMA")) c->k1_dma = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("HBX_K1_DMA")) c->k1_mode = std::atoi(v) ? 1u : 0u;
+  if (const char* v = std::getenv("HBX_K1_MODE")) c->k1_mode = (uint32_t)std::min(2, std::max(0, std::atoi(v)));
   if (const char* v = std::getenv("HBX_MD5_WGS")) c->md5_wgs = (uint32_t)std::max(1, std::atoi(v));
   if (const char* v = std::getenv("HBX_TILE_ITERS")) c->tile_iters = (uint32_t)std::min(1024, std::max(1, std::atoi(v)));
   if (const char* v = std::getenv("HBX_MD5_SLICE")) c->md5_slice = (uint32_t)std::max(0, std::atoi(v));
