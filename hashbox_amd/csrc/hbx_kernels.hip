@@ -787,7 +787,10 @@ __device__ void md5_run(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32
   constexpr int RING = HBX_MD5_RING;  // blocks of prefetch (16 VGPRs each)
   const uint32_t sh = (uint32_t)reinterpret_cast<uintptr_t>(c) & 3u;
   const uint32_t* va = reinterpret_cast<const uint32_t*>(c - sh);  // raw R[r] = va[r]
-  const uint32_t last = cnt ? b0 + cnt - 1u : b0;  // prefetches clamp to this block
+  // prefetches clamp to the last block this lane compresses; a lane with
+  // nothing to compress reads block b0-1 (always whole data), never block
+  // b0 (which may be the tail, up to 72 bytes past the chunk)
+  const uint32_t last = cnt ? b0 + cnt - 1u : (b0 ? b0 - 1u : 0u);
   // Block b needs raw dwords R[16b-2 .. 16b+15]: 16 loaded with it (4 x
   // dwordx4 at va+64b, never below the chunk start) plus 2 carried.  Loads
   // run RING blocks ahead through a register ring.  The loop is wave-uniform
@@ -1050,19 +1053,24 @@ __device__ __forceinline__ uint32_t chain_cnt(uint32_t len, uint32_t next, uint3
   const uint32_t nfull = (len + 8u) >> 6;
   return min(nfull - next, budget);
 }
-// Planner order key: chains advancing exactly `budget` blocks (the
-// cooperative K3 path's waves) first, then log2 buckets of the block count.
-__device__ __forceinline__ uint32_t chain_bucket(uint32_t cnt, uint32_t budget) {
-  return (cnt == budget) ? 32u : 31u - __builtin_clz(cnt + 1u);
+// Planner order: this launch's block count, descending, in 1024 bins (bin 0
+// = a full slice), so the 64 chains of a K3 wave have nearly equal counts
+// and the wave can advance them together by its minimum (the cooperative
+// path) with only a small per-lane remainder.
+constexpr uint32_t kPlanBins = 1024u;
+__device__ __forceinline__ uint32_t chain_bin(uint32_t cnt, uint32_t budget) {
+  const uint32_t ref = min(budget, (uint32_t)(kMaxBlock >> 6));  // largest possible count
+  const uint32_t c = min(cnt, ref);
+  return (ref - c) * (kPlanBins - 1u) / ref;
 }
 
 // ----------------------------------------------------------- K2c plan --
 // Builds the chain table for one K3 launch: the unfinished chains of the
 // previous launch (`prev`, count prev_ctl[1]; nullptr = none) plus one fresh
-// chain per chunk of the new batch (n_files may be 0), ordered by this
-// launch's block count (log2 buckets, largest first) so each K3 wave gets 64
-// chains of similar length and the longest start first.  ctl[1] = entries.
+// chain per chunk of the new batch (n_files may be 0), ordered as above.
+// ctl[1] = entries.
 constexpr int kPlanThreads = 1024;
+static_assert(kPlanThreads == (int)kPlanBins, "one planner thread per bin");
 
 extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
     uint32_t n_files, const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
@@ -1070,14 +1078,14 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
     const uint32_t* __restrict__ cut_count, uint32_t* __restrict__ ids, const Chain* __restrict__ prev,
     const uint32_t* __restrict__ prev_ctl, Chain* __restrict__ cur, uint32_t* __restrict__ ctl,
     uint32_t budget) {
-  __shared__ uint32_t hist[33], pos[33];
+  __shared__ uint32_t hist[kPlanBins], pos[kPlanBins], wsum[kPlanThreads / 64];
   const uint32_t tid = threadIdx.x;
   const uint32_t n_prev = prev ? prev_ctl[1] : 0u;
-  if (tid < 33) hist[tid] = 0u;
+  hist[tid] = 0u;
   __syncthreads();
   for (uint32_t e = tid; e < n_prev; e += kPlanThreads) {
     const Chain ch = prev[e];
-    if (ch.next != kChainDone) atomicAdd(&hist[chain_bucket(chain_cnt(ch.len, ch.next, budget), budget)], 1u);
+    if (ch.next != kChainDone) atomicAdd(&hist[chain_bin(chain_cnt(ch.len, ch.next, budget), budget)], 1u);
   }
   for (uint32_t f = tid; f < n_files; f += kPlanThreads) {
     const uint64_t cb = cut_base[f];
@@ -1085,26 +1093,29 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
     uint64_t start = 0;
     for (uint32_t i = 0; i < k; i++) {
       const uint64_t e = cut_ends[cb + i];
-      atomicAdd(&hist[chain_bucket(chain_cnt((uint32_t)(e - start), 0u, budget), budget)], 1u);
+      atomicAdd(&hist[chain_bin(chain_cnt((uint32_t)(e - start), 0u, budget), budget)], 1u);
       start = e;
     }
   }
   __syncthreads();
-  if (tid == 0) {
-    uint32_t p = 0;
-    for (int bk = 32; bk >= 0; bk--) {
-      pos[bk] = p;
-      p += hist[bk];
+  {  // exclusive scan of the bins: one bin per thread
+    const uint32_t v = hist[tid];
+    const uint32_t inc = wave_incl_sum(v);
+    if ((tid & 63u) == 63u) wsum[tid >> 6] = inc;
+    __syncthreads();
+    uint32_t before = 0u;
+    for (uint32_t wv = 0; wv < (tid >> 6); wv++) before += wsum[wv];
+    pos[tid] = before + inc - v;
+    if (tid == kPlanThreads - 1) {
+      ctl[0] = 0u;
+      ctl[1] = before + inc;
     }
-    ctl[0] = 0u;
-    ctl[1] = p;
-    ctl[2] = hist[32];  // leading chains that advance exactly `budget` blocks
   }
   __syncthreads();
   for (uint32_t e = tid; e < n_prev; e += kPlanThreads) {
     const Chain ch = prev[e];
     if (ch.next != kChainDone)
-      cur[atomicAdd(&pos[chain_bucket(chain_cnt(ch.len, ch.next, budget), budget)], 1u)] = ch;
+      cur[atomicAdd(&pos[chain_bin(chain_cnt(ch.len, ch.next, budget), budget)], 1u)] = ch;
   }
   for (uint32_t f = tid; f < n_files; f += kPlanThreads) {
     const uint64_t cb = cut_base[f];
@@ -1123,7 +1134,7 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
       ch.h[3] = 0x10325476u;
       ch.out = reinterpret_cast<uint64_t>(ids + 4u * (cb + i));
       ch.pad = 0ull;
-      cur[atomicAdd(&pos[chain_bucket(chain_cnt(ch.len, 0u, budget), budget)], 1u)] = ch;
+      cur[atomicAdd(&pos[chain_bin(chain_cnt(ch.len, 0u, budget), budget)], 1u)] = ch;
       start = e;
     }
   }
@@ -1167,9 +1178,6 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
 #if HBX_K3_COOP
   static_assert(kK3Threads == 256, "cooperative K3 path sized for 4 waves per workgroup");
   __shared__ __attribute__((aligned(16))) uint8_t k3_lds[kK3Threads / 64][kCoopWaveLds];
-  // the planner puts chains advancing exactly `budget` blocks first
-  const uint32_t coop_groups =
-      (budget >= kCoopMinBudget && budget != kBudgetAll) ? ctl[2] / 64u : 0u;
 #endif
   const uint32_t groups = (n_total + 63u) / 64u;
   const uint32_t nwaves = gridDim.x * (kK3Threads / 64);
@@ -1181,26 +1189,6 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
   const uint32_t g0 = wave * gridDim.x + blockIdx.x;
 #endif
   for (uint32_t g = g0; g < groups; g += nwaves) {
-#if HBX_K3_COOP
-    if (g < coop_groups) {  // wave-uniform: 64 chains, each advancing exactly `budget` blocks
-      const uint32_t k = 64u * g + lane;
-      const Chain ch = tab[k];
-      const uint8_t* src = reinterpret_cast<const uint8_t*>(ch.src);
-      uint32_t h[4] = {ch.h[0], ch.h[1], ch.h[2], ch.h[3]};
-      md5_block_at(src, ch.len, h, ch.next);  // every lane now at a block >= 1
-      md5_coop(k3_lds[wave], src, h, ch.next + 1u, budget - 1u);
-      const bool finish = ch.next + budget == ((ch.len + 8u) >> 6);
-      md5_tail(src, ch.len, h, finish);
-      if (finish) {
-        *reinterpret_cast<uint4*>(ch.out) = make_uint4(h[0], h[1], h[2], h[3]);
-        tab[k].next = kChainDone;
-      } else {
-        *reinterpret_cast<uint4*>(&tab[k].h[0]) = make_uint4(h[0], h[1], h[2], h[3]);
-        tab[k].next = ch.next + budget;
-      }
-      continue;
-    }
-#endif
     const uint32_t k = 64u * g + lane;
     const bool active = k < n_total;
     // idle lanes stay alive for the wave-wide loop bound: they run an empty
@@ -1211,7 +1199,22 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
     const uint32_t cnt = active ? chain_cnt(len, b0, budget) : 0u;
     const bool finish = active && b0 + cnt == ((len + 8u) >> 6);
     uint32_t h[4] = {ch.h[0], ch.h[1], ch.h[2], ch.h[3]};
-    md5_run(reinterpret_cast<const uint8_t*>(ch.src), len, h, b0, cnt, finish);
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(ch.src);
+#if HBX_K3_COOP
+    // R = the wave's smallest count: all 64 chains advance R blocks together
+    // through page-local cooperative loads (idle lanes shadow the group's
+    // first chain, whose count is >= R), then each lane its own remainder
+    const uint32_t R = ~wave_max_all(active ? ~cnt : 0u);
+    if (R >= kCoopMinBudget) {  // wave-uniform
+      md5_block_at(src, ch.len, h, ch.next);  // every lane now at a block >= 1
+      md5_coop(k3_lds[wave], src, h, ch.next + 1u, R - 1u);
+      md5_run(src, len, h, b0 + R, active ? cnt - R : 0u, finish);
+    } else {
+      md5_run(src, len, h, b0, cnt, finish);
+    }
+#else
+    md5_run(src, len, h, b0, cnt, finish);
+#endif
     if (finish) {
       *reinterpret_cast<uint4*>(ch.out) = make_uint4(h[0], h[1], h[2], h[3]);
       tab[k].next = kChainDone;
