@@ -60,6 +60,9 @@ def parse():
                     help="with --md5-slice -1: fraction of free HBM given to resident batches; "
                          "throughput ~ resident bytes / batch latency (the longest chunk's "
                          "serial MD5), so the pipeline is made as deep as this allows")
+    ap.add_argument("--lead", type=int, default=2,
+                    help="steps the scan stream (K1/K2 of a new batch) may run ahead of the hash "
+                         "stream: the pipeline holds launches-per-batch + lead batches")
     ap.add_argument("--e2e", action="store_true",
                     help="host-inclusive mode: files in pinned host memory, H2D of batch i+1 "
                          "overlapped with the kernels of batch i (two contexts)")
@@ -182,18 +185,21 @@ def main():
     # launches a batch needs before its chains are all hashed; a batch can be
     # collected without a forced drain once `need` newer steps have launched
     nfull = (min(fbytes, 8 << 20) + 8) >> 6
+    # a batch holds its arena from its K1 until its last K3 launch; with
+    # `lead` more arenas than launches per batch, the scan stream runs `lead`
+    # steps ahead of the hash stream and never waits for a collect
     if a.md5_slice < 0:
         free, _ = torch.cuda.mem_get_info(dev)
-        r_fit = max(2, int(free * a.hbm_frac) // (total + (64 << 20)))
+        r_fit = max(a.lead + 1, int(free * a.hbm_frac) // (total + (64 << 20)))
         R = a.arenas if a.arenas > 0 else r_fit
-        B = -(-nfull // max(1, R - 1))
+        B = -(-nfull // max(1, R - a.lead))
     else:
         B = a.md5_slice
     need = 1 if B == 0 else -(-nfull // B)
     if a.arenas > 0:
         R = a.arenas
     elif a.md5_slice >= 0:
-        R = need + 1
+        R = need + a.lead
     # synthetic uniform random bytes, generated on the device (per-rank seed);
     # R distinct resident batches, batch j reads arena j % R
     g = torch.Generator(device=dev)
@@ -207,6 +213,10 @@ def main():
     torch.cuda.synchronize()
 
     eng = Engine(local, md5_slice=B)
+    # every batch slot, chain table and summary buffer of the pipeline is
+    # allocated now: an allocation inside the timed region would drain both
+    # streams
+    eng.reserve(R + 1, nf, nf * fbytes)
     # single-batch latency (one batch alone, synchronous call), untimed
     for _ in range(2):
         eng.chunk_hash_device(arena.data_ptr(), offs, lens)
@@ -296,7 +306,8 @@ def main():
                                "(configs[1])",
                    "files_per_step": nf, "file_bytes": fbytes, "chunks_per_step": n_chunks,
                    "longest_chunk_bytes": longest, "md5_slice_blocks": B,
-                   "pipeline_depth": R, "launches_per_batch": need,
+                   "pipeline_depth": R, "launches_per_batch": need, "scan_lead": a.lead,
+                   "k1_kernel": os.environ.get("HBX_K1_MODE", "default"),
                    "parallelism": f"file-sharded x{world} (independent HIP streams, no data-path "
                                   "collective)"},
         "roofline": {"kernel": names[dom], "bound": "hbm", "achieved": round(achieved, 2),

@@ -123,12 +123,19 @@ struct Batch {
 struct hbx_ctx {
   int device = 0;
   hipStream_t stream = nullptr;   // scan stream: input copies, K1, K2 (and hbx_block_id)
-  hipStream_t hstream = nullptr;  // hash stream: chain plan, K3, K4, result D2H
+  hipStream_t cstream = nullptr;  // cut stream: K2 (after its batch's K1 on the scan stream)
+  hipStream_t hstream = nullptr;  // hash stream: chain plan, K3
+  hipStream_t rstream = nullptr;  // result stream: K4 + result D2H of batches whose chains are done
+  hipEvent_t k3_done = nullptr;   // recorded on the hash stream after a K3 launch that completes batches
   std::mutex mu;
   std::string err;
   uint32_t tile_iters = 64;   // K1 tile = 64 x 64 KiB (measured best: fewer halo primes)
   uint32_t k1_mode = 1;       // K1: 0 register prefetch, 1 LDS-DMA landing, 2 K1-lite (co-resides with K3)
-  uint32_t md5_wgs = 256;     // K3 grid: one 512-thread workgroup per CU (set from the device)
+  uint32_t md5_wgs = 256;     // K3 grid: one 256-thread workgroup per CU (set from the device)
+  // K3 wave placement: 1 packs the busy waves into the fewest CUs (4 per CU,
+  // one per SIMD), leaving whole CUs to the next batch's K1 (measured 1510 vs
+  // 1255 GiB/s spread, 100 steps); 0 spreads them one per CU first
+  uint32_t k3_dense = 1;
   uint32_t md5_slice = 16384; // K3 time slice: full MD5 blocks per chain per launch (0 = unlimited)
   float stage_ms[5] = {0, 0, 0, 0, 0};
 
@@ -136,7 +143,12 @@ struct hbx_ctx {
   std::vector<uint64_t> h_slice_base;
   std::vector<uint2> h_tiles;
 
-  DevBuf d_ssum;            // K1 -> K2 slice summaries (shared: consumed in stream order)
+  // K1 -> K2 slice summaries, two slots used by alternate batches: K1 of
+  // batch i+1 (scan stream) overlaps K2 of batch i (cut stream)
+  DevBuf d_ssum[2];
+  int ssum_slot = 0;
+  hipEvent_t ssum_free[2] = {nullptr, nullptr};  // recorded after the K2 that last read the slot
+  bool ssum_used[2] = {false, false};
   DevBuf d_tab[2], d_tctl[2];  // MD5 chain tables (ping-pong) + their counts
   int tab_cur = -1;         // table holding the last launch's chains (-1: none in flight)
   DevBuf d_stage;           // host-input arena
@@ -183,12 +195,16 @@ namespace {
 
 inline uint64_t max_chunks(uint64_t len) { return len / HBX_MIN_BLOCK_SIZE + 1; }
 
-// Grow a buffer the stream may still be using: drain the stream first.
+// Grow a buffer the streams may still be using: drain both streams first.  A
+// drain stalls the pipeline, so growth is geometric (and hbx_reserve sizes
+// everything up front for a known workload).
 int ensure_shared(hbx_ctx* c, DevBuf& b, size_t n) {
   if (n <= b.cap && b.p) return HBX_OK;
   HBX_TRY(c, hipStreamSynchronize(c->stream));
+  HBX_TRY(c, hipStreamSynchronize(c->cstream));
   HBX_TRY(c, hipStreamSynchronize(c->hstream));
-  HBX_TRY(c, b.ensure(n));
+  HBX_TRY(c, hipStreamSynchronize(c->rstream));
+  HBX_TRY(c, b.ensure(b.p ? std::max(n, b.cap + b.cap / 2) : n));
   return HBX_OK;
 }
 
@@ -276,9 +292,11 @@ Batch* acquire_batch(hbx_ctx* c) {
   return b;
 }
 
-// K4 + D2H of one batch whose chains are all hashed.
+// K4 + D2H of one batch whose chains are all hashed, on the result stream
+// (after c->k3_done), so the hash stream goes straight on with the next plan
+// and K3 launch.
 int finalize_batch(hbx_ctx* c, Batch* b) {
-  hipStream_t s = c->hstream;
+  hipStream_t s = c->rstream;
   b->finalized = true;
   if (b->n) {
     const uint64_t n = b->n;
@@ -341,16 +359,21 @@ int md5_launch(hbx_ctx* c, Batch* nb, const uint8_t* arena, uint32_t budget) {
   {
     StageTimer t(c, s, 3);
     hipLaunchKernelGGL(hbx_k3_block_md5, dim3(c->md5_wgs), dim3(kK3Threads), 0, s, cur,
-                       static_cast<const uint32_t*>(ctl), budget);
+                       static_cast<const uint32_t*>(ctl), budget, c->k3_dense);
   }
   HBX_TRY(c, hipGetLastError());
   c->tab_cur = dst;
   if (nb) HBX_TRY(c, hipEventRecord(nb->ev[3], s));
-  bool any_left = false;
+  bool any_left = false, forked = false;
   for (Batch* b : c->pending) {
     if (b->finalized) continue;
     b->done++;
     if (budget == kBudgetAll || b->done >= b->need) {
+      if (!forked && c->rstream != s) {  // the result stream picks up after this K3
+        HBX_TRY(c, hipEventRecord(c->k3_done, s));
+        HBX_TRY(c, hipStreamWaitEvent(c->rstream, c->k3_done, 0));
+        forked = true;
+      }
       if ((rc = finalize_batch(c, b))) return rc;
     } else {
       any_left = true;
@@ -423,7 +446,10 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
   std::memcpy(hm + 2 * n, c->h_slice_base.data(), n * 8);
   std::memcpy(hm + 3 * n, b->cut_base.data(), n * 8);
   if (nt) std::memcpy(hm + 4 * n, c->h_tiles.data(), nt * sizeof(uint2));
-  int rc = ensure_shared(c, c->d_ssum, (slices + 1) * sizeof(uint2));  // +1: dummy slot
+  const int slot = c->ssum_slot;
+  c->ssum_slot ^= 1;
+  DevBuf& ssum = c->d_ssum[slot];
+  int rc = ensure_shared(c, ssum, (slices + 1) * sizeof(uint2));  // +1: dummy slot
   if (rc) return rc;
   HBX_TRY(c, b->d_cuts.ensure(tcaps * 8));
   HBX_TRY(c, b->d_count.ensure(n * 4));
@@ -440,36 +466,41 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
   const uint2* d_tiles = reinterpret_cast<const uint2*>(d_off + 4 * n);
   const uint8_t* arena = static_cast<const uint8_t*>(d_arena);
 
+  // the K2 that last read this summary slot (two batches back) must be done
+  if (c->ssum_used[slot] && c->cstream != s) HBX_TRY(c, hipStreamWaitEvent(s, c->ssum_free[slot], 0));
   HBX_TRY(c, hipEventRecord(b->ev[0], s));
   if (nt) {
     StageTimer t(c, s, 0);
     if (c->k1_mode == 2)
       hipLaunchKernelGGL(hbx_k1_digest_scan_lite, dim3((uint32_t)nt), dim3(kK1LThreads), 0, s,
                          arena, d_off, d_len, d_sb, d_tiles,
-                         c->tile_iters * (HBX_MIN_BLOCK_SIZE / kK1LSpan), c->d_ssum.as<uint2>(),
-                         slices);
+                         c->tile_iters * (HBX_MIN_BLOCK_SIZE / kK1LSpan), ssum.as<uint2>(), slices);
     else if (c->k1_mode == 1)
       hipLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3((uint32_t)nt), dim3(kK1Threads), 0, s,
-                         arena, d_off, d_len, d_sb, d_tiles, c->tile_iters, c->d_ssum.as<uint2>(),
-                         slices);
+                         arena, d_off, d_len, d_sb, d_tiles, c->tile_iters, ssum.as<uint2>(), slices);
     else
       hipLaunchKernelGGL(hbx_k1_digest_scan, dim3((uint32_t)nt), dim3(kK1Threads), 0, s, arena,
-                         d_off, d_len, d_sb, d_tiles, c->tile_iters, c->d_ssum.as<uint2>(),
-                         slices);
+                         d_off, d_len, d_sb, d_tiles, c->tile_iters, ssum.as<uint2>(), slices);
   }
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(b->ev[1], s));
+  // K2 on the cut stream: the scan stream goes straight on with the next
+  // batch's K1 (into the other summary slot)
+  hipStream_t s2 = c->cstream;
+  if (s2 != s) HBX_TRY(c, hipStreamWaitEvent(s2, b->ev[1], 0));
   {
-    StageTimer t(c, s, 1);
-    hipLaunchKernelGGL(hbx_k2_cut_chain, dim3((uint32_t)n), dim3(64), 0, s, arena, d_off, d_len,
-                       d_sb, c->d_ssum.as<uint2>(), d_cb, b->d_cuts.as<uint64_t>(),
+    StageTimer t(c, s2, 1);
+    hipLaunchKernelGGL(hbx_k2_cut_chain, dim3((uint32_t)n), dim3(64), 0, s2, arena, d_off, d_len,
+                       d_sb, ssum.as<uint2>(), d_cb, b->d_cuts.as<uint64_t>(),
                        b->d_count.as<uint32_t>());
   }
   HBX_TRY(c, hipGetLastError());
-  HBX_TRY(c, hipEventRecord(b->ev[2], s));
+  HBX_TRY(c, hipEventRecord(b->ev[2], s2));
+  HBX_TRY(c, hipEventRecord(c->ssum_free[slot], s2));
+  c->ssum_used[slot] = true;
   // the hash stream picks the batch up once its cuts exist; the scan stream
   // is free for the next batch's K1/K2 while K3 runs
-  if (c->hstream != s) HBX_TRY(c, hipStreamWaitEvent(c->hstream, b->ev[2], 0));
+  if (c->hstream != s2) HBX_TRY(c, hipStreamWaitEvent(c->hstream, b->ev[2], 0));
   return md5_launch(c, b, arena, budget);
 }
 
@@ -564,6 +595,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = std::getenv("HBX_K1_DMA")) c->k1_mode = std::atoi(v) ? 1u : 0u;
   if (const char* v = std::getenv("HBX_K1_MODE")) c->k1_mode = (uint32_t)std::min(2, std::max(0, std::atoi(v)));
   if (const char* v = std::getenv("HBX_MD5_WGS")) c->md5_wgs = (uint32_t)std::max(1, std::atoi(v));
+  if (const char* v = std::getenv("HBX_K3_DENSE")) c->k3_dense = std::atoi(v) ? 1u : 0u;
   if (const char* v = std::getenv("HBX_TILE_ITERS")) c->tile_iters = (uint32_t)std::min(1024, std::max(1, std::atoi(v)));
   if (const char* v = std::getenv("HBX_MD5_SLICE")) c->md5_slice = (uint32_t)std::max(0, std::atoi(v));
   if (hipSetDevice(device) != hipSuccess ||
@@ -571,12 +603,24 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
     delete c;
     return HBX_ERR_HIP;
   }
-  const char* one = std::getenv("HBX_ONE_STREAM");  // A/B: scan and hash on one stream
+  const char* one = std::getenv("HBX_ONE_STREAM");  // A/B: scan, hash and results on one stream
+  // K2 on its own stream is optional: with GPU_MAX_HW_QUEUES = 4 a fourth
+  // stream of ours shares a hardware queue (measured: +0.2 ms hash-stream gap)
+  const char* k2s = std::getenv("HBX_K2_STREAM");
+  const bool own_k2 = k2s && std::atoi(k2s);
   if (one && std::atoi(one)) {
-    c->hstream = c->stream;
-  } else if (hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking) != hipSuccess) {
-    (void)hipStreamDestroy(c->stream);
-    delete c;
+    c->cstream = c->hstream = c->rstream = c->stream;
+  } else if ((own_k2 ? hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking)
+                     : (c->cstream = c->stream, hipSuccess)) != hipSuccess ||
+             hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking) != hipSuccess ||
+             hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking) != hipSuccess) {
+    hbx_ctx_destroy(c);
+    return HBX_ERR_HIP;
+  }
+  if (hipEventCreateWithFlags(&c->k3_done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ssum_free[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ssum_free[1], hipEventDisableTiming) != hipSuccess) {
+    hbx_ctx_destroy(c);
     return HBX_ERR_HIP;
   }
   *out = c;
@@ -586,9 +630,11 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
 void hbx_ctx_destroy(hbx_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
-  if (c->hstream) (void)hipStreamSynchronize(c->hstream);
-  for (DevBuf* b : {&c->d_ssum, &c->d_tab[0], &c->d_tab[1], &c->d_tctl[0], &c->d_tctl[1],
+  for (hipStream_t s : {c->stream, c->cstream, c->hstream, c->rstream})
+    if (s) (void)hipStreamSynchronize(s);
+  for (hipEvent_t e : {c->k3_done, c->ssum_free[0], c->ssum_free[1]})
+    if (e) (void)hipEventDestroy(e);
+  for (DevBuf* b : {&c->d_ssum[0], &c->d_ssum[1], &c->d_tab[0], &c->d_tab[1], &c->d_tctl[0], &c->d_tctl[1],
                     &c->d_stage, &c->d_msg})
     b->release();
   for (PinBuf& h : c->h_read) h.release();
@@ -605,7 +651,8 @@ void hbx_ctx_destroy(hbx_ctx* c) {
     (void)hipEventDestroy(t.b);
   }
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
-  if (c->hstream && c->hstream != c->stream) (void)hipStreamDestroy(c->hstream);
+  for (hipStream_t s : {c->cstream, c->hstream, c->rstream})
+    if (s && s != c->stream) (void)hipStreamDestroy(s);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -631,6 +678,40 @@ int hbx_set_md5_slice(hbx_ctx* c, uint32_t blocks) {
   std::lock_guard<std::mutex> g(c->mu);
   c->md5_slice = blocks;
   return HBX_OK;
+}
+
+int hbx_reserve(hbx_ctx* c, uint32_t batches, uint64_t files, uint64_t bytes) {
+  if (!c || files > 0xFFFFFFFFull) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
+  HBX_TRY(c, hipSetDevice(c->device));
+  const uint64_t tile_bytes = (uint64_t)c->tile_iters * HBX_MIN_BLOCK_SIZE;
+  const uint64_t caps = bytes / HBX_MIN_BLOCK_SIZE + files;  // >= sum of max_chunks over the files
+  const uint64_t tiles = bytes / tile_bytes + files;
+  const uint64_t slices = bytes / kSlice + files;
+  const size_t meta_bytes = files * 8 * 4 + tiles * sizeof(uint2);
+  int rc = HBX_OK;
+  for (int t = 0; t < 2 && !rc; t++) {
+    rc = ensure_shared(c, c->d_ssum[t], (slices + 1) * sizeof(uint2));
+    if (rc) break;
+    rc = ensure_shared(c, c->d_tab[t], std::max<uint64_t>((uint64_t)batches * caps, 64) * sizeof(Chain));
+    if (!rc) rc = ensure_shared(c, c->d_tctl[t], 256);
+  }
+  if (rc) return rc;
+  std::vector<Batch*> ready;
+  while (ready.size() < batches) {
+    Batch* b = acquire_batch(c);  // pooled first, then new
+    if (!b) break;
+    ready.push_back(b);
+    for (auto r : {b->h_meta.ensure(meta_bytes), b->d_meta.ensure(meta_bytes), b->d_cuts.ensure(caps * 8),
+                   b->d_count.ensure(files * 4), b->d_ids.ensure(caps * 16), b->d_cid.ensure(files * 16),
+                   b->d_ctype.ensure(files * 4), b->h_res.ensure(res_layout(files, caps).total)})
+      if (r != hipSuccess && !rc) rc = c->hip(r, "hbx_reserve");
+    if (rc) break;
+  }
+  for (Batch* b : ready) c->pool.push_back(b);
+  if (!rc && ready.size() < batches) rc = c->fail(HBX_ERR_HIP, "cannot create batch events");
+  return rc;
 }
 
 int hbx_stage_totals(hbx_ctx* c, double ms[5], uint64_t launches[5], int reset) {

@@ -562,6 +562,10 @@ __device__ void slice_argmax(const uint8_t* fb, uint64_t N, uint64_t j, uint32_t
 
 }  // namespace
 
+// interior summaries per lane per round: 32 x 64 lanes covers the 2048
+// slices of a MAX-sized candidate range in one round
+constexpr int kK2Loads = 32;
+
 extern "C" __global__ __launch_bounds__(64) void hbx_k2_cut_chain(
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
     const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ slice_base,
@@ -585,28 +589,45 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k2_cut_chain(
       // candidates p in [s+MIN, s+L]  <=>  q = p-1 in [qa, qb]
       const uint64_t qa = s + kMinBlock - 1, qb = s + L - 1;
       const uint64_t ja = qa >> kSliceShift, jb = qb >> kSliceShift;  // jb - ja >= 16
-      // interior slices (ja, jb): max + last slice holding it
-      uint32_t bv = 0u;
+      // interior slices (ja, jb): max + last slice holding it (and the
+      // state before it).  A lane's summary loads, and the two edge slices'
+      // summaries, are all issued before the first is used: one memory round
+      // trip per cut instead of a chain of up to 32.
+      const uint2 sA = ssum[sb + ja], sB = ssum[sb + jb];
+      uint32_t bv = 0u, by = 0u;
       int64_t bj = -1;
-      for (uint64_t j = ja + 1 + l; j < jb; j += 64) {
-        const uint32_t v = ssum[sb + j].x;
-        if (v >= bv) {
-          bv = v;
-          bj = (int64_t)j;
+      for (uint64_t j0 = ja + 1; j0 < jb; j0 += 64u * kK2Loads) {
+        uint2 v[kK2Loads];
+#pragma unroll
+        for (int u = 0; u < kK2Loads; u++) {
+          const uint64_t j = j0 + 64u * (uint32_t)u + l;
+          v[u] = ssum[sb + (j < jb ? j : jb)];  // jb is in the file: a valid slot
+        }
+#pragma unroll
+        for (int u = 0; u < kK2Loads; u++) {
+          const uint64_t j = j0 + 64u * (uint32_t)u + l;
+          if (j < jb && v[u].x >= bv) {
+            bv = v[u].x;
+            by = v[u].y;
+            bj = (int64_t)j;
+          }
         }
       }
       const uint32_t MI = wave_max_all(bj >= 0 ? bv : 0u);
       const uint32_t jrel = wave_max_all((bj >= 0 && bv == MI) ? (uint32_t)(bj - (int64_t)ja) : 0u);
       const uint64_t jI = ja + jrel;
+      // the state before slice jI, from the lane that holds it
+      const uint64_t hold = __builtin_amdgcn_ballot_w64(bj == (int64_t)jI);
+      const uint32_t yI = readlane(by, hold ? (int)__builtin_ctzll(hold) : 0);
 
       uint32_t Mbest = MI;
       uint64_t qwin = 0;
       int src = 1;  // 0 = first edge slice, 1 = interior, 2 = last edge slice
       // last (partial) slice: wins ties
-      if (ssum[sb + jb].x >= Mbest) {
+      if (sB.x >= Mbest) {
         uint32_t D;
         int P;
-        slice_argmax(fb, N, jb, ssum[sb + jb].y, 0, (int)(qb - (jb << kSliceShift)), D, P);
+        slice_argmax(fb, N, jb, sB.y, 0, (int)(qb - (jb << kSliceShift)), D, P);
         if (P >= 0 && D >= Mbest) {
           Mbest = D;
           qwin = (jb << kSliceShift) + (uint64_t)P;
@@ -614,11 +635,10 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k2_cut_chain(
         }
       }
       // first (partial) slice: must be strictly greater
-      if (ssum[sb + ja].x > Mbest) {
+      if (sA.x > Mbest) {
         uint32_t D;
         int P;
-        slice_argmax(fb, N, ja, ssum[sb + ja].y, (int)(qa - (ja << kSliceShift)),
-                     (int)kSlice - 1, D, P);
+        slice_argmax(fb, N, ja, sA.y, (int)(qa - (ja << kSliceShift)), (int)kSlice - 1, D, P);
         if (P >= 0 && D > Mbest) {
           Mbest = D;
           qwin = (ja << kSliceShift) + (uint64_t)P;
@@ -628,7 +648,7 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k2_cut_chain(
       if (src == 1) {
         uint32_t D;
         int P;
-        slice_argmax(fb, N, jI, ssum[sb + jI].y, 0, (int)kSlice - 1, D, P);
+        slice_argmax(fb, N, jI, yI, 0, (int)kSlice - 1, D, P);
         qwin = (jI << kSliceShift) + (uint64_t)P;
       }
       cut = qwin + 1;
@@ -774,8 +794,16 @@ __device__ void md5_tail(const uint8_t* c, uint32_t len, uint32_t (&h)[4], bool 
 #ifndef HBX_MD5_NT
 #define HBX_MD5_NT 0
 #endif
-template <class T>
-__device__ __forceinline__ T md5_load(const T* p) {
+// Chunk bytes are read through explicit global (address space 1) pointers.
+// A pointer rebuilt from an integer address is generic to the compiler, and a
+// generic (flat) load counts against lgkmcnt as well as vmcnt: every wait for
+// an LDS read would then also wait for the prefetches still in flight.
+typedef __attribute__((address_space(1))) const uint32_t g_u32;
+typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
+__device__ __forceinline__ g_u32* gptr32(const void* p) { return (g_u32*)(uintptr_t)p; }
+__device__ __forceinline__ g_u32x4* gptr128(uint64_t a) { return (g_u32x4*)a; }
+
+__device__ __forceinline__ u32x4 md5_load(g_u32x4* p) {
 #if HBX_MD5_NT
   return __builtin_nontemporal_load(p);
 #else
@@ -786,7 +814,7 @@ __device__ void md5_run(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32
                         bool finish) {
   constexpr int RING = HBX_MD5_RING;  // blocks of prefetch (16 VGPRs each)
   const uint32_t sh = (uint32_t)reinterpret_cast<uintptr_t>(c) & 3u;
-  const uint32_t* va = reinterpret_cast<const uint32_t*>(c - sh);  // raw R[r] = va[r]
+  g_u32* va = gptr32(c - sh);  // raw R[r] = va[r]
   // prefetches clamp to the last block this lane compresses; a lane with
   // nothing to compress reads block b0-1 (always whole data), never block
   // b0 (which may be the tail, up to 72 bytes past the chunk)
@@ -808,15 +836,15 @@ __device__ void md5_run(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32
   // message block b >= 1 = data bytes [64b-8, 64b+56); block 0 loads data
   // bytes [0, 64) and shifts by two words (its first two are the framing)
   auto blk_src = [&](uint32_t b) {
-    return reinterpret_cast<const u32x4*>(b ? c + 64u * b - 8u : c);
+    return gptr128(reinterpret_cast<uint64_t>(b ? c + 64u * b - 8u : c));
   };
 #else
-  auto blk_src = [&](uint32_t b) { return reinterpret_cast<const u32x4*>(va + 16u * b); };
+  auto blk_src = [&](uint32_t b) { return reinterpret_cast<g_u32x4*>(va + 16u * b); };
 #endif
   u32x4 ring[RING][4];
 #pragma unroll
   for (int r = 0; r < RING; r++) {
-    const u32x4* src = blk_src(min(b0 + (uint32_t)r, last));
+    g_u32x4* src = blk_src(min(b0 + (uint32_t)r, last));
 #pragma unroll
     for (int i = 0; i < 4; i++) ring[r][i] = md5_load(src + i);
   }
@@ -854,7 +882,7 @@ __device__ void md5_run(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32
     c1 = R[15];
 #endif
     auto do_refill = [&]() {
-      const u32x4* src = blk_src(min(b0 + i + (uint32_t)RING, last));
+      g_u32x4* src = blk_src(min(b0 + i + (uint32_t)RING, last));
 #pragma unroll
       for (int q = 0; q < 4; q++) ring[r][q] = md5_load(src + q);
     };
@@ -892,7 +920,7 @@ __device__ void md5_run(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32
 // The 1-2 padded tail blocks after the last full block (lanes with `finish`).
 __device__ void md5_tail(const uint8_t* c, uint32_t len, uint32_t (&h)[4], bool finish) {
   const uint32_t sh = (uint32_t)reinterpret_cast<uintptr_t>(c) & 3u;
-  const uint32_t* va = reinterpret_cast<const uint32_t*>(c - sh);
+  g_u32* va = gptr32(c - sh);
   const uint32_t T = len + 8u;
   const uint32_t nfull = T >> 6;
   // tail: remaining message bytes + 0x80 + zeros + 64-bit bit length
@@ -926,7 +954,7 @@ __device__ void md5_tail(const uint8_t* c, uint32_t len, uint32_t (&h)[4], bool 
 // wave at a block >= 1, where the message words are data words).
 __device__ void md5_block_at(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32_t b) {
   const uint32_t sh = (uint32_t)reinterpret_cast<uintptr_t>(c) & 3u;
-  const uint32_t* va = reinterpret_cast<const uint32_t*>(c - sh);
+  g_u32* va = gptr32(c - sh);
   const uint32_t base = b ? 16u * b - 2u : 0u;
   uint32_t v[17];
 #pragma unroll
@@ -975,10 +1003,10 @@ __device__ __forceinline__ void coop_load(u32x4 (&G)[16], const uint64_t (&Q)[16
   const uint64_t off = 256ull * st;
   if (16u * st + 16u <= ngr) {
 #pragma unroll
-    for (int q = 0; q < 16; q++) G[q] = md5_load(reinterpret_cast<const u32x4*>(Q[q] + off));
+    for (int q = 0; q < 16; q++) G[q] = md5_load(gptr128(Q[q] + off));
   } else if (16u * st + t < ngr) {
 #pragma unroll
-    for (int q = 0; q < 16; q++) G[q] = md5_load(reinterpret_cast<const u32x4*>(Q[q] + off));
+    for (int q = 0; q < 16; q++) G[q] = md5_load(gptr128(Q[q] + off));
   }
 }
 
@@ -1071,6 +1099,8 @@ __device__ __forceinline__ uint32_t chain_bin(uint32_t cnt, uint32_t budget) {
 // ctl[1] = entries.
 constexpr int kPlanThreads = 1024;
 static_assert(kPlanThreads == (int)kPlanBins, "one planner thread per bin");
+constexpr int kPlanUnroll = 4;               // carried-chain loads in flight per thread
+constexpr uint32_t kPlanLanesPerFile = 16u;  // threads sharing one file's new chunks
 
 extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
     uint32_t n_files, const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
@@ -1083,18 +1113,27 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
   const uint32_t n_prev = prev ? prev_ctl[1] : 0u;
   hist[tid] = 0u;
   __syncthreads();
-  for (uint32_t e = tid; e < n_prev; e += kPlanThreads) {
-    const Chain ch = prev[e];
-    if (ch.next != kChainDone) atomicAdd(&hist[chain_bin(chain_cnt(ch.len, ch.next, budget), budget)], 1u);
+  // carried chains: kPlanUnroll entries per thread per round, loads first
+  for (uint32_t e0 = 0; e0 < n_prev; e0 += kPlanThreads * kPlanUnroll) {
+    uint2 ln[kPlanUnroll];  // {len, next}
+#pragma unroll
+    for (int u = 0; u < kPlanUnroll; u++) {
+      const uint32_t e = e0 + (uint32_t)u * kPlanThreads + tid;
+      ln[u] = e < n_prev ? *reinterpret_cast<const uint2*>(&prev[e].len) : make_uint2(0u, kChainDone);
+    }
+#pragma unroll
+    for (int u = 0; u < kPlanUnroll; u++)
+      if (ln[u].y != kChainDone) atomicAdd(&hist[chain_bin(chain_cnt(ln[u].x, ln[u].y, budget), budget)], 1u);
   }
-  for (uint32_t f = tid; f < n_files; f += kPlanThreads) {
+  // new chunks: kPlanLanesPerFile threads per file, chunk i on thread i % L
+  for (uint32_t w = tid; w < n_files * kPlanLanesPerFile; w += kPlanThreads) {
+    const uint32_t f = w / kPlanLanesPerFile;
     const uint64_t cb = cut_base[f];
     const uint32_t k = cut_count[f];
-    uint64_t start = 0;
-    for (uint32_t i = 0; i < k; i++) {
+    for (uint32_t i = w % kPlanLanesPerFile; i < k; i += kPlanLanesPerFile) {
+      const uint64_t start = i ? cut_ends[cb + i - 1] : 0ull;
       const uint64_t e = cut_ends[cb + i];
       atomicAdd(&hist[chain_bin(chain_cnt((uint32_t)(e - start), 0u, budget), budget)], 1u);
-      start = e;
     }
   }
   __syncthreads();
@@ -1112,17 +1151,29 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
     }
   }
   __syncthreads();
-  for (uint32_t e = tid; e < n_prev; e += kPlanThreads) {
-    const Chain ch = prev[e];
-    if (ch.next != kChainDone)
-      cur[atomicAdd(&pos[chain_bin(chain_cnt(ch.len, ch.next, budget), budget)], 1u)] = ch;
+  for (uint32_t e0 = 0; e0 < n_prev; e0 += kPlanThreads * kPlanUnroll) {
+    Chain ch[kPlanUnroll];
+#pragma unroll
+    for (int u = 0; u < kPlanUnroll; u++) {
+      const uint32_t e = e0 + (uint32_t)u * kPlanThreads + tid;
+      if (e < n_prev) {
+        ch[u] = prev[e];
+      } else {
+        ch[u].next = kChainDone;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kPlanUnroll; u++)
+      if (ch[u].next != kChainDone)
+        cur[atomicAdd(&pos[chain_bin(chain_cnt(ch[u].len, ch[u].next, budget), budget)], 1u)] = ch[u];
   }
-  for (uint32_t f = tid; f < n_files; f += kPlanThreads) {
+  for (uint32_t w = tid; w < n_files * kPlanLanesPerFile; w += kPlanThreads) {
+    const uint32_t f = w / kPlanLanesPerFile;
     const uint64_t cb = cut_base[f];
     const uint32_t k = cut_count[f];
     const uint64_t base = reinterpret_cast<uint64_t>(arena + file_off[f]);
-    uint64_t start = 0;
-    for (uint32_t i = 0; i < k; i++) {
+    for (uint32_t i = w % kPlanLanesPerFile; i < k; i += kPlanLanesPerFile) {
+      const uint64_t start = i ? cut_ends[cb + i - 1] : 0ull;
       const uint64_t e = cut_ends[cb + i];
       Chain ch;
       ch.src = base + start;
@@ -1135,7 +1186,6 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
       ch.out = reinterpret_cast<uint64_t>(ids + 4u * (cb + i));
       ch.pad = 0ull;
       cur[atomicAdd(&pos[chain_bin(chain_cnt(ch.len, 0u, budget), budget)], 1u)] = ch;
-      start = e;
     }
   }
 }
@@ -1157,9 +1207,6 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
 #ifndef HBX_K3_THREADS
 #define HBX_K3_THREADS 256
 #endif
-#ifndef HBX_K3_DENSE
-#define HBX_K3_DENSE 0
-#endif
 // cooperative (page-local) loads for waves of full-slice chains
 #ifndef HBX_K3_COOP
 #define HBX_K3_COOP 1
@@ -1168,7 +1215,7 @@ constexpr uint32_t kCoopMinBudget = 8u;
 constexpr int kK3Threads = HBX_K3_THREADS;
 
 extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
-    Chain* __restrict__ tab, const uint32_t* __restrict__ ctl, uint32_t budget) {
+    Chain* __restrict__ tab, const uint32_t* __restrict__ ctl, uint32_t budget, uint32_t dense) {
   // the MD5 chains are issue-bound: win the SIMD's issue arbitration against
   // co-resident K1-lite waves of the next batch
   __builtin_amdgcn_s_setprio(3);
@@ -1181,13 +1228,11 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
 #endif
   const uint32_t groups = (n_total + 63u) / 64u;
   const uint32_t nwaves = gridDim.x * (kK3Threads / 64);
-#if HBX_K3_DENSE
-  // dense: group g on wave g % W of workgroup g / W, so the busy waves fill
-  // the fewest CUs and whole CUs stay free for the scan stream's K1/K2
-  const uint32_t g0 = blockIdx.x * (kK3Threads / 64) + wave;
-#else
-  const uint32_t g0 = wave * gridDim.x + blockIdx.x;
-#endif
+  // spread: group g on wave (g / grid) % W of workgroup g % grid (one busy
+  // wave per CU first); dense: group g on wave g % W of workgroup g / W, so
+  // the busy waves fill the fewest CUs and whole CUs stay free for the scan
+  // stream's K1/K2
+  const uint32_t g0 = dense ? blockIdx.x * (kK3Threads / 64) + wave : wave * gridDim.x + blockIdx.x;
   for (uint32_t g = g0; g < groups; g += nwaves) {
     const uint32_t k = 64u * g + lane;
     const bool active = k < n_total;
@@ -1216,7 +1261,7 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
     md5_run(src, len, h, b0, cnt, finish);
 #endif
     if (finish) {
-      *reinterpret_cast<uint4*>(ch.out) = make_uint4(h[0], h[1], h[2], h[3]);
+      *(__attribute__((address_space(1))) u32x4*)ch.out = u32x4{h[0], h[1], h[2], h[3]};
       tab[k].next = kChainDone;
     } else if (active) {
       *reinterpret_cast<uint4*>(&tab[k].h[0]) = make_uint4(h[0], h[1], h[2], h[3]);

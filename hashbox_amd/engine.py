@@ -194,6 +194,13 @@ class Engine:
         """MD5 blocks per chain per K3 launch (0 = unlimited)."""
         self._check(self._L.hbx_set_md5_slice(self._ctx, int(blocks)), "hbx_set_md5_slice")
 
+    def reserve(self, batches: int, files: int, nbytes: int):
+        """Pre-size the pipeline for ``batches`` batches in flight of up to
+        ``files`` files / ``nbytes`` bytes each, so the steady state never
+        allocates (an allocation drains both streams)."""
+        self._check(self._L.hbx_reserve(self._ctx, int(batches), int(files), int(nbytes)),
+                    "hbx_reserve")
+
     def stage_totals(self, reset: bool = False):
         """Cumulative device ms and launch counts per kernel: K1, K2, plan, K3, K4."""
         ms = (ctypes.c_double * 5)()

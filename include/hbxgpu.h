@@ -128,6 +128,12 @@ int hbx_pending(hbx_ctx *ctx);
  * ceil(min(longest file, 8 MiB)/64 / blocks) further launches; results are
  * identical for every setting. */
 int hbx_set_md5_slice(hbx_ctx *ctx, uint32_t blocks);
+/* Optional: pre-size the pipeline for `batches` batches in flight of up to
+ * `files` files and `bytes` bytes each.  The batch pool, the MD5 chain tables
+ * and the slice summaries are allocated now, so the steady state never
+ * allocates (growing a buffer the streams share drains both streams).  Fails
+ * with HBX_ERR_STATE while batches are pending. */
+int hbx_reserve(hbx_ctx *ctx, uint32_t batches, uint64_t files, uint64_t bytes);
 
 /* Files on disk, end to end (storeFile over a list of paths, store.go:84-199
  * with the tree walk left to the caller): io_threads read batches of up to
