@@ -41,7 +41,7 @@ GIB = 1 << 30
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--files", type=int, default=64)
     ap.add_argument("--file-mib", type=int, default=128)
@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--arenas", type=int, default=0,
                     help="distinct resident batches (default: the pipeline depth the slice "
                          "schedule needs, so no step forces a drain)")
-    ap.add_argument("--hbm-frac", type=float, default=0.8,
+    ap.add_argument("--hbm-frac", type=float, default=0.95,
                     help="with --md5-slice -1: fraction of free HBM given to resident batches; "
                          "throughput ~ resident bytes / batch latency (the longest chunk's "
                          "serial MD5), so the pipeline is made as deep as this allows")

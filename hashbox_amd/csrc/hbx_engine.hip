@@ -153,6 +153,7 @@ struct hbx_ctx {
   int tab_cur = -1;         // table holding the last launch's chains (-1: none in flight)
   DevBuf d_stage;           // host-input arena
   DevBuf d_msg;             // hbx_block_id message
+  DevBuf d_plan;            // chain planner: global bin counts + cursors
   PinBuf h_read[2];         // hbx_store_paths: pinned landing slots for file reads
   hipEvent_t h2d_done[2] = {nullptr, nullptr};  // slot's H2D copy has completed
   std::vector<DevBuf> d_ring;  // hbx_store_paths: device arenas of the batches in flight
@@ -338,22 +339,20 @@ int md5_launch(hbx_ctx* c, Batch* nb, const uint8_t* arena, uint32_t budget) {
   const uint32_t* prev_ctl = src < 0 ? nullptr : c->d_tctl[src].as<uint32_t>();
   Chain* cur = c->d_tab[dst].as<Chain>();
   uint32_t* ctl = c->d_tctl[dst].as<uint32_t>();
+  if ((rc = ensure_shared(c, c->d_plan, 2 * kPlanBins * sizeof(uint32_t)))) return rc;
   {
     StageTimer t(c, s, 2);
-    if (nb && nb->n) {
-      const uint64_t n = nb->n;
-      const uint64_t* d_off = nb->d_meta.as<uint64_t>();
-      hipLaunchKernelGGL(hbx_k2c_plan, dim3(1), dim3(kPlanThreads), 0, s, (uint32_t)n, arena,
-                         d_off, d_off + 3 * n,
-                         nb->d_cuts.as<uint64_t>(), nb->d_count.as<uint32_t>(),
-                         nb->d_ids.as<uint32_t>(), prev, prev_ctl, cur, ctl, budget);
-    } else {
-      hipLaunchKernelGGL(hbx_k2c_plan, dim3(1), dim3(kPlanThreads), 0, s, 0u,
-                         static_cast<const uint8_t*>(nullptr), static_cast<const uint64_t*>(nullptr),
-                         static_cast<const uint64_t*>(nullptr), static_cast<const uint64_t*>(nullptr),
-                         static_cast<const uint32_t*>(nullptr), static_cast<uint32_t*>(nullptr), prev,
-                         prev_ctl, cur, ctl, budget);
-    }
+    HBX_TRY(c, hipMemsetAsync(c->d_plan.p, 0, 2 * kPlanBins * sizeof(uint32_t), s));
+    const bool fresh = nb && nb->n;
+    const uint64_t n = fresh ? nb->n : 0;
+    const uint64_t* d_off = fresh ? nb->d_meta.as<uint64_t>() : nullptr;
+    for (uint32_t phase = 0; phase < 2; phase++)
+      hipLaunchKernelGGL(hbx_k2c_plan, dim3(kPlanGroups), dim3(kPlanThreads), 0, s, (uint32_t)n,
+                         fresh ? arena : nullptr, d_off, fresh ? d_off + 3 * n : nullptr,
+                         fresh ? nb->d_cuts.as<uint64_t>() : nullptr,
+                         fresh ? nb->d_count.as<uint32_t>() : nullptr,
+                         fresh ? nb->d_ids.as<uint32_t>() : nullptr, prev, prev_ctl, cur, ctl, budget,
+                         c->d_plan.as<uint32_t>(), phase);
   }
   HBX_TRY(c, hipGetLastError());
   {
@@ -635,7 +634,7 @@ void hbx_ctx_destroy(hbx_ctx* c) {
   for (hipEvent_t e : {c->k3_done, c->ssum_free[0], c->ssum_free[1]})
     if (e) (void)hipEventDestroy(e);
   for (DevBuf* b : {&c->d_ssum[0], &c->d_ssum[1], &c->d_tab[0], &c->d_tab[1], &c->d_tctl[0], &c->d_tctl[1],
-                    &c->d_stage, &c->d_msg})
+                    &c->d_stage, &c->d_msg, &c->d_plan})
     b->release();
   for (PinBuf& h : c->h_read) h.release();
   for (DevBuf& d : c->d_ring) d.release();

@@ -996,48 +996,77 @@ __device__ __forceinline__ void coop_write(uint8_t* wl, uint32_t wr, const u32x4
     *reinterpret_cast<u32x4*>(wl + wr + (uint32_t)HALF * kCoopHalf + 1088u * (uint32_t)q) = G[q];
 }
 
-// Loads of stage `st` (granules 16*st .. 16*st+15 of every chain) into G;
-// granules >= ngr (past the last needed dword) are not read.
+// Loads of stage `st` (granules 16*st .. 16*st+15 of every chain) into G.
+// Branch-free, so the compiler's vmcnt bookkeeping stays exact through the
+// stage loop and a wait covers only the register set it needs: a granule
+// past the last needed one (>= ngr) re-reads granule ngr-1, which every
+// chain holds.
 __device__ __forceinline__ void coop_load(u32x4 (&G)[16], const uint64_t (&Q)[16], uint32_t st,
                                           uint32_t t, uint32_t ngr) {
-  const uint64_t off = 256ull * st;
-  if (16u * st + 16u <= ngr) {
+  const uint32_t g = min(16u * st + t, ngr - 1u);  // this lane's granule
+  const uint64_t off = 16ull * (g - t);            // Q[q] already holds + 16 t
 #pragma unroll
-    for (int q = 0; q < 16; q++) G[q] = md5_load(gptr128(Q[q] + off));
-  } else if (16u * st + t < ngr) {
-#pragma unroll
-    for (int q = 0; q < 16; q++) G[q] = md5_load(gptr128(Q[q] + off));
-  }
+  for (int q = 0; q < 16; q++) G[q] = md5_load(gptr128(Q[q] + off));
 }
+
+// 1: each chain's message stream is read from its exact byte address (16-B
+// loads at any byte offset; the hardware splits them), so the words land in
+// LDS aligned and a block needs no v_alignbyte.  0: dword-aligned reads plus
+// 16 v_alignbyte per block.
+#ifndef HBX_COOP_BYTE
+#define HBX_COOP_BYTE 1
+#endif
 
 __device__ void md5_coop(uint8_t* wl, const uint8_t* c, uint32_t (&h)[4], uint32_t b1, uint32_t R) {
   const uint32_t lane = threadIdx.x & 63u;
+#if HBX_COOP_BYTE
+  const uint64_t S = reinterpret_cast<uint64_t>(c) + 64ull * b1 - 8ull;  // message block b1
+  const uint32_t ngr = 4u * R;                                           // granules of R blocks
+#else
   const uint32_t sh = (uint32_t)reinterpret_cast<uintptr_t>(c) & 3u;
   const uint64_t S = reinterpret_cast<uint64_t>(c) + 64ull * b1 - 8ull - sh;
+  const uint32_t ngr = 4u * R + 1u;  // granules holding dwords 0 .. 16R
+#endif
   const uint32_t t = lane & 15u, sub = lane >> 4;
   uint64_t Q[16];  // role q: chain 4q+sub, granule t of each stage
 #pragma unroll
   for (int q = 0; q < 16; q++) Q[q] = shfl64(S, 4u * (uint32_t)q + sub) + 16ull * t;
   const uint32_t wr = sub * kCoopRow + 16u * t;  // + 1088 q: row 4q+sub, granule t
   const uint32_t rd = lane * kCoopRow;           // this lane's row
-  const uint32_t ngr = 4u * R + 1u;              // granules holding dwords 0 .. 16R
   const uint32_t nst = (ngr + 15u) / 16u;
-  u32x4 G[16];
-  coop_load(G, Q, 0u, t, ngr);
-  coop_write<0>(wl, wr, G);
-  if (nst > 1u) coop_load(G, Q, 1u, t, ngr);
+  // Two register sets of loads in flight (stages s+1 and s+2 while stage s
+  // is hashed), so a load has two stages (~8 blocks) to land.  Stages past
+  // the last re-read it (coop_load clamps).
+  u32x4 GA[16], GB[16];
+  coop_load(GA, Q, 0u, t, ngr);
+  coop_load(GB, Q, 1u, t, ngr);
+  coop_write<0>(wl, wr, GA);
+  coop_load(GA, Q, 2u, t, ngr);
+#if !HBX_COOP_BYTE
   // window: granules g..g+4 of the current block (W[0] carried)
   u32x4 W0 = *reinterpret_cast<const u32x4*>(wl + rd);
-  auto stage_pair = [&](auto half_c, uint32_t s) {
+#endif
+  auto stage_pair = [&](auto half_c, uint32_t s, u32x4(&Gn)[16]) {
     constexpr int HALF = decltype(half_c)::value;
-    // start of stage s: stage s+1 into the other half, loads of s+2 issued
-    if (s + 1u < nst) coop_write<HALF ^ 1>(wl, wr, G);
-    if (s + 2u < nst) coop_load(G, Q, s + 2u, t, ngr);
+    // start of stage s: stage s+1 (in Gn) into the other half, then Gn's
+    // registers take the loads of stage s+3.  Unconditional: past the last
+    // stage the loads repeat it and the write lands in a half never read
+    // again.
+    coop_write<HALF ^ 1>(wl, wr, Gn);
+    coop_load(Gn, Q, min(s + 3u, nst - 1u), t, ngr);
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       const uint32_t blk = 4u * s + (uint32_t)u;
       if (blk >= R) break;  // wave-uniform
       const uint8_t* hb = wl + rd + (uint32_t)HALF * kCoopHalf;
+#if HBX_COOP_BYTE
+      u32x4 W[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) W[i] = *reinterpret_cast<const u32x4*>(hb + 16u * (4u * u + (uint32_t)i));
+      const uint32_t m[16] = {W[0].x, W[0].y, W[0].z, W[0].w, W[1].x, W[1].y, W[1].z, W[1].w,
+                              W[2].x, W[2].y, W[2].z, W[2].w, W[3].x, W[3].y, W[3].z, W[3].w};
+      md5_compress(h, m);
+#else
       const u32x4 W1 = *reinterpret_cast<const u32x4*>(hb + 16u * (4u * u + 1u));
       const u32x4 W2 = *reinterpret_cast<const u32x4*>(hb + 16u * (4u * u + 2u));
       const u32x4 W3 = *reinterpret_cast<const u32x4*>(hb + 16u * (4u * u + 3u));
@@ -1050,11 +1079,12 @@ __device__ void md5_coop(uint8_t* wl, const uint8_t* c, uint32_t (&h)[4], uint32
       for (int i = 0; i < 16; i++) m[i] = alignbyte(D[i + 1], D[i], sh);
       md5_compress(h, m);
       W0 = W4;
+#endif
     }
   };
   for (uint32_t s = 0; 4u * s < R; s += 2u) {
-    stage_pair(std::integral_constant<int, 0>{}, s);
-    if (4u * (s + 1u) < R) stage_pair(std::integral_constant<int, 1>{}, s + 1u);
+    stage_pair(std::integral_constant<int, 0>{}, s, GB);
+    stage_pair(std::integral_constant<int, 1>{}, s + 1u, GA);  // hashes nothing past block R
   }
 }
 
@@ -1096,37 +1126,38 @@ __device__ __forceinline__ uint32_t chain_bin(uint32_t cnt, uint32_t budget) {
 // Builds the chain table for one K3 launch: the unfinished chains of the
 // previous launch (`prev`, count prev_ctl[1]; nullptr = none) plus one fresh
 // chain per chunk of the new batch (n_files may be 0), ordered as above.
-// ctl[1] = entries.
+// ctl[1] = entries.  Two launches of the same grid over the same partition
+// of the entries (carried chains by global thread, new chunks by
+// (file, lane) work items):
+//   phase 0: per-workgroup histogram of the bins, added into gh[0, 1024)
+//   phase 1: every workgroup scans gh into bin bases, reserves its own range
+//            in each bin (one atomic per bin on gh[1024 + bin]) and scatters
+//            its entries with LDS atomics.
+// gh (2 x 1024 u32) is zeroed before phase 0.  Order inside a bin is
+// arbitrary; results never depend on it (each chain is independent).
 constexpr int kPlanThreads = 1024;
 static_assert(kPlanThreads == (int)kPlanBins, "one planner thread per bin");
-constexpr int kPlanUnroll = 4;               // carried-chain loads in flight per thread
-constexpr uint32_t kPlanLanesPerFile = 16u;  // threads sharing one file's new chunks
+constexpr uint32_t kPlanLanesPerFile = 16u;  // work items sharing one file's new chunks
+constexpr uint32_t kPlanGroups = 32u;        // grid of both phases
 
 extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
     uint32_t n_files, const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
     const uint64_t* __restrict__ cut_base, const uint64_t* __restrict__ cut_ends,
     const uint32_t* __restrict__ cut_count, uint32_t* __restrict__ ids, const Chain* __restrict__ prev,
     const uint32_t* __restrict__ prev_ctl, Chain* __restrict__ cur, uint32_t* __restrict__ ctl,
-    uint32_t budget) {
+    uint32_t budget, uint32_t* __restrict__ gh, uint32_t phase) {
   __shared__ uint32_t hist[kPlanBins], pos[kPlanBins], wsum[kPlanThreads / 64];
   const uint32_t tid = threadIdx.x;
+  const uint32_t gt = blockIdx.x * kPlanThreads + tid, gn = gridDim.x * kPlanThreads;
   const uint32_t n_prev = prev ? prev_ctl[1] : 0u;
+  const uint32_t n_work = n_files * kPlanLanesPerFile;
   hist[tid] = 0u;
   __syncthreads();
-  // carried chains: kPlanUnroll entries per thread per round, loads first
-  for (uint32_t e0 = 0; e0 < n_prev; e0 += kPlanThreads * kPlanUnroll) {
-    uint2 ln[kPlanUnroll];  // {len, next}
-#pragma unroll
-    for (int u = 0; u < kPlanUnroll; u++) {
-      const uint32_t e = e0 + (uint32_t)u * kPlanThreads + tid;
-      ln[u] = e < n_prev ? *reinterpret_cast<const uint2*>(&prev[e].len) : make_uint2(0u, kChainDone);
-    }
-#pragma unroll
-    for (int u = 0; u < kPlanUnroll; u++)
-      if (ln[u].y != kChainDone) atomicAdd(&hist[chain_bin(chain_cnt(ln[u].x, ln[u].y, budget), budget)], 1u);
+  for (uint32_t e = gt; e < n_prev; e += gn) {
+    const uint2 ln = *reinterpret_cast<const uint2*>(&prev[e].len);  // {len, next}
+    if (ln.y != kChainDone) atomicAdd(&hist[chain_bin(chain_cnt(ln.x, ln.y, budget), budget)], 1u);
   }
-  // new chunks: kPlanLanesPerFile threads per file, chunk i on thread i % L
-  for (uint32_t w = tid; w < n_files * kPlanLanesPerFile; w += kPlanThreads) {
+  for (uint32_t w = gt; w < n_work; w += gn) {
     const uint32_t f = w / kPlanLanesPerFile;
     const uint64_t cb = cut_base[f];
     const uint32_t k = cut_count[f];
@@ -1137,37 +1168,32 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
     }
   }
   __syncthreads();
-  {  // exclusive scan of the bins: one bin per thread
-    const uint32_t v = hist[tid];
+  if (phase == 0u) {
+    if (hist[tid]) atomicAdd(&gh[tid], hist[tid]);
+    return;
+  }
+  {  // exclusive scan of the global bins (one per thread), then this
+     // workgroup's range inside each bin
+    const uint32_t v = gh[tid];
     const uint32_t inc = wave_incl_sum(v);
     if ((tid & 63u) == 63u) wsum[tid >> 6] = inc;
     __syncthreads();
     uint32_t before = 0u;
     for (uint32_t wv = 0; wv < (tid >> 6); wv++) before += wsum[wv];
-    pos[tid] = before + inc - v;
-    if (tid == kPlanThreads - 1) {
+    const uint32_t mine = hist[tid];
+    pos[tid] = before + inc - v + (mine ? atomicAdd(&gh[kPlanBins + tid], mine) : 0u);
+    if (blockIdx.x == 0 && tid == kPlanThreads - 1) {
       ctl[0] = 0u;
       ctl[1] = before + inc;
     }
   }
   __syncthreads();
-  for (uint32_t e0 = 0; e0 < n_prev; e0 += kPlanThreads * kPlanUnroll) {
-    Chain ch[kPlanUnroll];
-#pragma unroll
-    for (int u = 0; u < kPlanUnroll; u++) {
-      const uint32_t e = e0 + (uint32_t)u * kPlanThreads + tid;
-      if (e < n_prev) {
-        ch[u] = prev[e];
-      } else {
-        ch[u].next = kChainDone;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kPlanUnroll; u++)
-      if (ch[u].next != kChainDone)
-        cur[atomicAdd(&pos[chain_bin(chain_cnt(ch[u].len, ch[u].next, budget), budget)], 1u)] = ch[u];
+  for (uint32_t e = gt; e < n_prev; e += gn) {
+    const Chain ch = prev[e];
+    if (ch.next != kChainDone)
+      cur[atomicAdd(&pos[chain_bin(chain_cnt(ch.len, ch.next, budget), budget)], 1u)] = ch;
   }
-  for (uint32_t w = tid; w < n_files * kPlanLanesPerFile; w += kPlanThreads) {
+  for (uint32_t w = gt; w < n_work; w += gn) {
     const uint32_t f = w / kPlanLanesPerFile;
     const uint64_t cb = cut_base[f];
     const uint32_t k = cut_count[f];

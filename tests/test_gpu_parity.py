@@ -228,3 +228,30 @@ def test_pipelined_steady_state(oracle):
     for i, g in zip(order, got):
         for a, r in zip(g, batches[i][3]):
             _check(a, r)
+
+
+@pytest.mark.parametrize("dense", ["0", "1"])
+def test_reserved_pipeline_placements(oracle, monkeypatch, dense):
+    """hbx_reserve pre-sizes the pool, chain tables and summaries; both K3
+    wave placements (HBX_K3_DENSE) give the same bit-exact results through a
+    pipeline that runs its scan stream two steps ahead."""
+    from hashbox_amd import Engine
+    monkeypatch.setenv("HBX_K3_DENSE", dense)
+    batches = _device_batches(oracle, 2, 43)
+    got, order = [], [i % 2 for i in range(12)]
+    with Engine(0, md5_slice=2048) as e:
+        e.reserve(10, max(len(b[2]) for b in batches), max(int(sum(b[2])) for b in batches))
+        for i in order:
+            dev, offs, sizes, _ = batches[i]
+            e.submit_device(dev.data_ptr(), offs, sizes)
+            if e.pending() >= 8:
+                got.append(e.wait())
+        while e.pending():
+            got.append(e.wait())
+        with pytest.raises(Exception):  # reserve is refused while batches are pending
+            e.submit_device(batches[0][0].data_ptr(), batches[0][1], batches[0][2])
+            e.reserve(2, 1, 1)
+        got_last = e.wait()
+    for i, g in zip(order + [0], got + [got_last]):
+        for a, r in zip(g, batches[i][3]):
+            _check(a, r)
