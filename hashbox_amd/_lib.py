@@ -23,7 +23,7 @@ EXPORTS = [
     "hbx_submit_device", "hbx_wait", "hbx_store_paths", "hbx_block_id", "hbx_arena_alloc", "hbx_arena_free",
     "hbx_memcpy_h2d", "hbx_memcpy_h2d_async", "hbx_alloc_pinned", "hbx_free_pinned", "hbx_stage_times",
     "hbx_set_tile_iters", "hbx_pending", "hbx_set_md5_slice", "hbx_stage_totals", "hbx_io_times",
-    "hbx_reserve",
+    "hbx_reserve", "hbx_verify_blocks", "hbx_verify_blocks_device",
 ]
 
 
@@ -83,6 +83,8 @@ def load() -> ctypes.CDLL:
     L.hbx_stage_totals.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64), I]
     L.hbx_io_times.argtypes = [P, ctypes.POINTER(ctypes.c_double), I]
     L.hbx_reserve.argtypes = [P, ctypes.c_uint32, U64, U64]
+    L.hbx_verify_blocks.argtypes = [P, U64, P, P, P, P, P, P, P, P, ctypes.POINTER(U64)]
+    L.hbx_verify_blocks_device.argtypes = [P, P, U64, P, P, P, P, P, P, P, P, ctypes.POINTER(U64)]
     for name in EXPORTS:
         if name not in ("hbx_ctx_destroy", "hbx_last_error", "hbx_max_chunks"):
             getattr(L, name).restype = I

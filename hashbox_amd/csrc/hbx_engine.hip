@@ -154,6 +154,7 @@ struct hbx_ctx {
   DevBuf d_stage;           // host-input arena
   DevBuf d_msg;             // hbx_block_id message
   DevBuf d_plan;            // chain planner: global bin counts + cursors
+  DevBuf d_vdesc, d_vlinks, d_vout, d_vexp, d_zeros;  // hbx_verify_blocks*
   PinBuf h_read[2];         // hbx_store_paths: pinned landing slots for file reads
   hipEvent_t h2d_done[2] = {nullptr, nullptr};  // slot's H2D copy has completed
   std::vector<DevBuf> d_ring;  // hbx_store_paths: device arenas of the batches in flight
@@ -634,7 +635,8 @@ void hbx_ctx_destroy(hbx_ctx* c) {
   for (hipEvent_t e : {c->k3_done, c->ssum_free[0], c->ssum_free[1]})
     if (e) (void)hipEventDestroy(e);
   for (DevBuf* b : {&c->d_ssum[0], &c->d_ssum[1], &c->d_tab[0], &c->d_tab[1], &c->d_tctl[0], &c->d_tctl[1],
-                    &c->d_stage, &c->d_msg, &c->d_plan})
+                    &c->d_stage, &c->d_msg, &c->d_plan, &c->d_vdesc, &c->d_vlinks,
+                    &c->d_vout, &c->d_vexp, &c->d_zeros})
     b->release();
   for (PinBuf& h : c->h_read) h.release();
   for (DevBuf& d : c->d_ring) d.release();
@@ -828,6 +830,107 @@ int hbx_block_id(hbx_ctx* c, const uint8_t* links, uint32_t n_links, const uint8
   HBX_TRY(c, hipMemcpyAsync(out, dm, 16, hipMemcpyDeviceToHost, c->stream));
   HBX_TRY(c, hipStreamSynchronize(c->stream));
   return HBX_OK;
+}
+
+namespace {
+// K6 over n blocks whose data is already on the device (block i at
+// arena + offs[i]); lanes are ordered longest first so each wave's 64 chains
+// are about equally long.
+int verify_device(hbx_ctx* c, const uint8_t* arena, uint64_t n, const uint64_t* offs,
+                  const uint64_t* lens, const uint8_t* links, const uint64_t* link_base,
+                  const uint32_t* n_links, uint8_t* ids, const uint8_t* expect, uint8_t* ok,
+                  uint64_t* n_bad) {
+  if (n_bad) *n_bad = 0;
+  if (n == 0) return HBX_OK;
+  if (n > 0xFFFFFFFFull) return c->fail(HBX_ERR_ARG, "too many blocks");
+  uint64_t nlinks_total = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    const uint32_t nl = n_links ? n_links[i] : 0u;
+    if (nl && (!links || !link_base)) return c->fail(HBX_ERR_ARG, "links missing");
+    if (lens[i] + 8ull + 16ull * nl + 128ull > 0xFFFFFFFFull) return c->fail(HBX_ERR_ARG, "block too large");
+    if (nl) nlinks_total = std::max(nlinks_total, link_base[i] + nl);
+  }
+  std::vector<uint32_t> perm(n);
+  for (uint64_t i = 0; i < n; i++) perm[i] = (uint32_t)i;
+  std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) { return lens[a] > lens[b]; });
+  HBX_TRY(c, c->d_vdesc.ensure(n * sizeof(VerifyDesc)));
+  HBX_TRY(c, c->d_vlinks.ensure(std::max<uint64_t>(16 * nlinks_total, 16)));
+  HBX_TRY(c, c->d_vout.ensure(n * 17));
+  HBX_TRY(c, c->d_zeros.ensure(256));
+  if (expect) HBX_TRY(c, c->d_vexp.ensure(n * 16));
+  const uint8_t* dl = c->d_vlinks.as<uint8_t>();
+  std::vector<VerifyDesc> desc(n);
+  std::vector<uint8_t> exp_p(expect ? n * 16 : 0);
+  for (uint64_t k = 0; k < n; k++) {
+    const uint32_t i = perm[k];
+    const uint32_t nl = n_links ? n_links[i] : 0u;
+    desc[k].src = reinterpret_cast<uint64_t>(arena + offs[i]);
+    desc[k].links = reinterpret_cast<uint64_t>(dl + (nl ? 16 * link_base[i] : 0));
+    desc[k].len = (uint32_t)lens[i];
+    desc[k].n_links = nl;
+    desc[k].pad = 0;
+    if (expect) std::memcpy(&exp_p[16 * k], expect + 16ull * i, 16);
+  }
+  hipStream_t s = c->stream;
+  HBX_TRY(c, hipMemsetAsync(c->d_zeros.p, 0, 256, s));
+  HBX_TRY(c, hipMemcpyAsync(c->d_vdesc.p, desc.data(), n * sizeof(VerifyDesc), hipMemcpyHostToDevice, s));
+  if (nlinks_total) HBX_TRY(c, hipMemcpyAsync(c->d_vlinks.p, links, 16 * nlinks_total, hipMemcpyHostToDevice, s));
+  if (expect) HBX_TRY(c, hipMemcpyAsync(c->d_vexp.p, exp_p.data(), n * 16, hipMemcpyHostToDevice, s));
+  uint8_t* dout = c->d_vout.as<uint8_t>();
+  hipLaunchKernelGGL(hbx_k6_hash_blocks, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, s,
+                     c->d_vdesc.as<VerifyDesc>(), (uint32_t)n, c->d_zeros.as<uint8_t>(),
+                     reinterpret_cast<uint32_t*>(dout), expect ? c->d_vexp.as<uint32_t>() : nullptr,
+                     dout + 16 * n);
+  HBX_TRY(c, hipGetLastError());
+  std::vector<uint8_t> out(n * 17);
+  HBX_TRY(c, hipMemcpyAsync(out.data(), dout, n * 17, hipMemcpyDeviceToHost, s));
+  HBX_TRY(c, hipStreamSynchronize(s));
+  uint64_t bad = 0;
+  for (uint64_t k = 0; k < n; k++) {
+    const uint32_t i = perm[k];
+    if (ids) std::memcpy(ids + 16ull * i, &out[16 * k], 16);
+    if (expect) {
+      const uint8_t good = out[16 * n + k];
+      if (ok) ok[i] = good;
+      bad += good ? 0 : 1;
+    }
+  }
+  if (n_bad) *n_bad = bad;
+  return HBX_OK;
+}
+}  // namespace
+
+int hbx_verify_blocks_device(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* offs,
+                             const uint64_t* lens, const uint8_t* links, const uint64_t* link_base,
+                             const uint32_t* n_links, uint8_t* ids, const uint8_t* expect, uint8_t* ok,
+                             uint64_t* n_bad) {
+  if (!c || (n && (!d_arena || !offs || !lens))) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
+  HBX_TRY(c, hipSetDevice(c->device));
+  return verify_device(c, static_cast<const uint8_t*>(d_arena), n, offs, lens, links, link_base, n_links,
+                       ids, expect, ok, n_bad);
+}
+
+int hbx_verify_blocks(hbx_ctx* c, uint64_t n, const uint8_t* const* datas, const uint64_t* lens,
+                      const uint8_t* links, const uint64_t* link_base, const uint32_t* n_links,
+                      uint8_t* ids, const uint8_t* expect, uint8_t* ok, uint64_t* n_bad) {
+  if (!c || (n && (!datas || !lens))) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
+  HBX_TRY(c, hipSetDevice(c->device));
+  std::vector<uint64_t> offs(n);
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    if (lens[i] && !datas[i]) return c->fail(HBX_ERR_ARG, "null block data");
+    offs[i] = total;
+    total += (lens[i] + 255) & ~uint64_t(255);
+  }
+  HBX_TRY(c, c->d_stage.ensure(total + 65536));
+  uint8_t* arena = c->d_stage.as<uint8_t>();
+  for (uint64_t i = 0; i < n; i++)
+    if (lens[i]) HBX_TRY(c, hipMemcpyAsync(arena + offs[i], datas[i], lens[i], hipMemcpyHostToDevice, c->stream));
+  return verify_device(c, arena, n, offs.data(), lens, links, link_base, n_links, ids, expect, ok, n_bad);
 }
 
 int hbx_arena_alloc(hbx_ctx* c, uint64_t bytes, void** d_ptr) {

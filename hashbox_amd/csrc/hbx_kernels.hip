@@ -1401,3 +1401,91 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k5_md5_raw(const uint8_t* _
   out[2] = h[2];
   out[3] = h[3];
 }
+
+// ------------------------------------------------------------ K6 verify --
+// Batched HashboxBlock.HashData / VerifyBlock (pkg/core/block.go:96-111,
+// 152-174) for uncompressed blocks: lane per block, message =
+// BE32(n_links) || links || BE32(len) || data.  The message blocks that hold
+// prefix bytes are built byte by byte (a short message entirely so); the
+// data-only rest runs through the streaming path (md5_run, md5_tail), whose
+// framing is an 8-byte prefix, on a virtual start shifted back by
+// (prefix - 8) bytes: from block ceil(prefix/64) on, every byte it reads lies
+// inside the block's data.
+struct VerifyDesc {
+  uint64_t src;      // device address of the block's data
+  uint64_t links;    // device address of its n_links 16-byte link IDs
+  uint32_t len;      // data bytes
+  uint32_t n_links;
+  uint64_t pad;
+};
+static_assert(sizeof(VerifyDesc) == 32, "descriptor layout shared with the host");
+
+namespace {
+__device__ __forceinline__ uint32_t k6_byte(uint64_t o, uint32_t nl, uint32_t len, uint32_t p, uint64_t T,
+                                            const uint8_t* links, const uint8_t* data) {
+  if (o < 4u) return (nl >> (8u * (3u - (uint32_t)o))) & 0xffu;
+  if (o < 4u + 16ull * nl) return links[o - 4u];
+  if (o < p) return (len >> (8u * (3u - (uint32_t)(o - 4u - 16ull * nl)))) & 0xffu;
+  if (o < T) return data[o - p];
+  return o == T ? 0x80u : 0u;
+}
+}  // namespace
+
+// One wave per workgroup (the waves of a launch spread over the CUs, as K3's
+// spread placement); blocks arrive sorted longest first, so a wave's 64
+// chains are about equally long and advance their common count through the
+// cooperative path.
+extern "C" __global__ __launch_bounds__(64, 1) void hbx_k6_hash_blocks(
+    const VerifyDesc* __restrict__ desc, uint32_t n, const uint8_t* __restrict__ zeros,
+    uint32_t* __restrict__ ids, const uint32_t* __restrict__ expect, uint8_t* __restrict__ ok) {
+  __shared__ __attribute__((aligned(16))) uint8_t k6_lds[kCoopWaveLds];
+  const uint32_t i = blockIdx.x * 64u + threadIdx.x;
+  const bool active = i < n;
+  const VerifyDesc v = desc[active ? i : 0u];  // n >= 1: idle lanes shadow block 0 and store nothing
+  const uint32_t len = v.len, nl = v.n_links;
+  const uint32_t p = 8u + 16u * nl;       // prefix bytes
+  const uint64_t T = (uint64_t)len + p;   // message bytes (< 2^32 - 128, checked by the host)
+  const uint32_t nfull = (uint32_t)(T >> 6);
+  const uint32_t hb = (p + 63u) >> 6;     // message blocks holding prefix bytes
+  const bool fast = nfull >= hb;          // the tail holds no prefix byte
+  const uint32_t nslow = fast ? hb : (uint32_t)((T + 8u) >> 6) + 1u;
+  const uint8_t* data = reinterpret_cast<const uint8_t*>(v.src);
+  const uint8_t* links = reinterpret_cast<const uint8_t*>(v.links);
+  uint32_t h[4];
+  md5_init(h);
+  for (uint32_t b = 0; b < nslow; b++) {
+    uint32_t m[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint64_t o = 64ull * b + 4u * (uint32_t)j;
+      m[j] = k6_byte(o, nl, len, p, T, links, data) | (k6_byte(o + 1u, nl, len, p, T, links, data) << 8) |
+             (k6_byte(o + 2u, nl, len, p, T, links, data) << 16) |
+             (k6_byte(o + 3u, nl, len, p, T, links, data) << 24);
+    }
+    if (!fast && b + 1u == nslow) {
+      const uint64_t bits = T * 8ull;
+      m[14] = (uint32_t)bits;
+      m[15] = (uint32_t)(bits >> 32);
+    }
+    md5_compress(h, m);
+  }
+  // data-only full blocks (wave-uniform call; a lane with none streams an
+  // empty range over a zero page), then the tail
+  const uint32_t cnt = fast ? nfull - hb : 0u;
+  const uint8_t* vs = data - (p - 8u);
+  // every lane is at block hb >= 1 of its message: the wave's smallest
+  // count R goes through the cooperative loads (idle lanes shadow block 0,
+  // the longest), the per-lane remainder through the lane path
+  const uint32_t R = ~wave_max_all(active ? ~cnt : 0u);
+  const uint32_t Rc = R >= kCoopMinBudget ? R : 0u;  // wave-uniform
+  if (Rc) md5_coop(k6_lds, vs, h, hb, Rc);
+  const uint32_t rest = cnt - Rc;
+  md5_run(rest ? vs : zeros + 64, rest ? len + p - 8u : 0u, h, rest ? hb + Rc : 1u, rest, false);
+  if (fast) md5_tail(vs, len + p - 8u, h, true);
+  if (active) {
+    *reinterpret_cast<uint4*>(ids + 4u * i) = make_uint4(h[0], h[1], h[2], h[3]);
+    if (expect)
+      ok[i] = (uint8_t)(h[0] == expect[4u * i] && h[1] == expect[4u * i + 1u] && h[2] == expect[4u * i + 2u] &&
+                        h[3] == expect[4u * i + 3u]);
+  }
+}

@@ -218,6 +218,58 @@ class Engine:
                     "hbx_block_id")
         return out.tobytes()
 
+    @staticmethod
+    def _links_arrays(links_per_block: Optional[Sequence[Sequence[bytes]]], n: int):
+        if not links_per_block or not any(len(x) for x in links_per_block):
+            return None, None, None
+        counts = np.array([len(x) for x in links_per_block], np.uint32)
+        base = np.zeros(n, np.uint64)
+        base[1:] = np.cumsum(counts.astype(np.uint64))[:-1]
+        flat = np.frombuffer(b"".join(bytes(l) for x in links_per_block for l in x), np.uint8)
+        if flat.size != 16 * int(counts.sum()):
+            raise ValueError("every link must be a 16-byte block ID")
+        return np.ascontiguousarray(flat), base, counts
+
+    def _verify(self, fn, lead_args, n, links, expect):
+        links_a, base, counts = self._links_arrays(links, n)
+        ids = np.zeros((max(n, 1), 16), np.uint8)
+        exp = None
+        if expect is not None:
+            exp = np.ascontiguousarray(np.frombuffer(b"".join(bytes(e) for e in expect), np.uint8))
+            if exp.size != 16 * n:
+                raise ValueError("expect must hold one 16-byte ID per block")
+        ok = np.zeros(max(n, 1), np.uint8)
+        bad = ctypes.c_uint64(0)
+        self._check(fn(self._ctx, *lead_args,
+                       _p(links_a) if links_a is not None else None,
+                       _p(base) if base is not None else None,
+                       _p(counts) if counts is not None else None,
+                       _p(ids), _p(exp) if exp is not None else None, _p(ok), ctypes.byref(bad)),
+                    fn.__name__)
+        return ids[:n], (ok[:n].astype(bool) if expect is not None else None), int(bad.value)
+
+    def verify_blocks(self, blocks: Sequence[BytesLike], links: Optional[Sequence[Sequence[bytes]]] = None,
+                      expect: Optional[Sequence[bytes]] = None):
+        """HashboxBlock.HashData / VerifyBlock (pkg/core/block.go:96-111,
+        152-174) for many uncompressed blocks at once.  Returns (ids [n,16],
+        ok [n] bool or None, number of mismatches)."""
+        arrs = [_u8(b) for b in blocks]
+        n = len(arrs)
+        lens = np.array([a.size for a in arrs], np.uint64)
+        ptrs = np.array([_p(a) for a in arrs], np.uint64)
+        return self._verify(self._L.hbx_verify_blocks, (n, _p(ptrs), _p(lens)), n, links, expect)
+
+    def verify_blocks_device(self, d_arena: int, offs: Sequence[int], lens: Sequence[int],
+                             links: Optional[Sequence[Sequence[bytes]]] = None,
+                             expect: Optional[Sequence[bytes]] = None):
+        """The same for blocks resident in device memory (each followed by
+        >= 64 readable bytes)."""
+        offs = np.ascontiguousarray(offs, np.uint64)
+        lens = np.ascontiguousarray(lens, np.uint64)
+        n = int(lens.size)
+        return self._verify(self._L.hbx_verify_blocks_device,
+                            (ctypes.c_void_p(int(d_arena)), n, _p(offs), _p(lens)), n, links, expect)
+
     def memcpy_h2d_async(self, d_dst: int, h_src: int, nbytes: int):
         """Enqueue an H2D copy on this engine's stream (pinned source)."""
         self._check(self._L.hbx_memcpy_h2d_async(self._ctx, ctypes.c_void_p(int(d_dst)),

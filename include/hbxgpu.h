@@ -157,6 +157,29 @@ int hbx_io_times(hbx_ctx *ctx, double s[3], int reset);
 int hbx_block_id(hbx_ctx *ctx, const uint8_t *links, uint32_t n_links, const uint8_t *data,
                  uint64_t len, uint8_t out[16]);
 
+/* Batched HashboxBlock.HashData / VerifyBlock (pkg/core/block.go:96-111,
+ * 152-174) for uncompressed blocks (BlockDataTypeRaw, or data already
+ * inflated).  Block i's ID is MD5(BE32(n_links[i]) || links || BE32(lens[i])
+ * || data), its links being the n_links[i] 16-byte IDs at
+ * links[16*link_base[i] ..] (host memory; links, link_base and n_links may
+ * be NULL when no block has links).  ids (16*n bytes, may be NULL) receives
+ * the IDs.  With expect != NULL (16*n bytes), ok[i] (may be NULL) = 1 where
+ * the ID equals expect[16*i ..], 0 elsewhere, and *n_bad (may be NULL)
+ * counts the mismatches.  Callers in the reference: restore
+ * (hashback/restore.go:52, 256), the server's write check
+ * (server/server.go:182), verify -content (pkg/storagedb/integrity.go:117,
+ * 282), show-block (util/commands.go:212).  Refused (HBX_ERR_STATE) while
+ * batches are pending. */
+int hbx_verify_blocks(hbx_ctx *ctx, uint64_t n, const uint8_t *const *datas, const uint64_t *lens,
+                      const uint8_t *links, const uint64_t *link_base, const uint32_t *n_links,
+                      uint8_t *ids, const uint8_t *expect, uint8_t *ok, uint64_t *n_bad);
+/* The same for blocks in device memory: block i is d_arena[offs[i] ..
+ * +lens[i]), followed by HBX_ARENA_SLACK readable bytes. */
+int hbx_verify_blocks_device(hbx_ctx *ctx, const void *d_arena, uint64_t n, const uint64_t *offs,
+                             const uint64_t *lens, const uint8_t *links, const uint64_t *link_base,
+                             const uint32_t *n_links, uint8_t *ids, const uint8_t *expect,
+                             uint8_t *ok, uint64_t *n_bad);
+
 /* Device arena helpers (allocations include HBX_ARENA_SLACK). */
 int hbx_arena_alloc(hbx_ctx *ctx, uint64_t bytes, void **d_ptr);
 int hbx_arena_free(hbx_ctx *ctx, void *d_ptr);

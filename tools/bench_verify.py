@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Batch VerifyBlock throughput: the chunks of one configs[1]
+batch (64 x 128 MiB random, ~2,050 chunks of 64 KiB - 8 MiB) re-verified
+device-resident with hbx_verify_blocks_device, and a many-small-blocks case
+(16,384 blocks of 4-64 KiB with 0-3 links).  Spot-checks against the oracle.
+Prints one JSON line."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from hashbox_amd import Engine, pack_arena_layout  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+GIB = 1 << 30
+
+
+def timed(fn, reps=3):
+    fn()
+    torch.cuda.synchronize()
+    best = 1e9
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        r = fn()
+        best = min(best, time.perf_counter() - t0)
+    return best, r
+
+
+def main():
+    O.lib()
+    eng = Engine(0)
+    nf, fb = 64, 128 << 20
+    offs, total = pack_arena_layout([fb] * nf)
+    arena = torch.empty(total, dtype=torch.uint8, device="cuda:0")
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(1000)
+    arena.random_(0, 256, generator=g)
+    res = eng.chunk_hash_device(arena.data_ptr(), offs, [fb] * nf)
+    c_offs, c_lens, expect = [], [], []
+    for f, r in enumerate(res):
+        s = 0
+        for e, i in zip(r.cut_ends, r.ids):
+            c_offs.append(int(offs[f]) + s)
+            c_lens.append(int(e) - s)
+            expect.append(i.tobytes())
+            s = int(e)
+    big_bytes = sum(c_lens)
+    t_big, (ids, ok, bad) = timed(lambda: eng.verify_blocks_device(arena.data_ptr(), c_offs, c_lens,
+                                                                    expect=expect))
+    assert bad == 0 and ok.all()
+    # many small blocks with links
+    rng = np.random.default_rng(5)
+    sizes = [int(x) for x in rng.integers(4096, 65536, 16384)]
+    s_offs, s_total = pack_arena_layout(sizes)
+    links = [[rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(int(k))]
+             for k in rng.integers(0, 4, len(sizes))]
+    small = torch.empty(s_total, dtype=torch.uint8, device="cuda:0")
+    small.random_(0, 256, generator=g)
+    host = small.cpu().numpy()
+    sample = list(range(0, len(sizes), 97))
+    exp_small = [O.block_id(host[int(s_offs[i]):int(s_offs[i]) + sizes[i]], links[i]) for i in sample]
+    t_small, (ids_s, _, _) = timed(lambda: eng.verify_blocks_device(small.data_ptr(), s_offs, sizes, links))
+    assert all(ids_s[i].tobytes() == e for i, e in zip(sample, exp_small))
+    out = {
+        "metric": "batch VerifyBlock GiB/s, device-resident (hbx_verify_blocks_device, K6)",
+        "chunks_of_one_batch": {"blocks": len(c_lens), "bytes": big_bytes, "seconds": round(t_big, 4),
+                                "gibs": round(big_bytes / t_big / GIB, 2),
+                                "longest_block": max(c_lens)},
+        "small_blocks": {"blocks": len(sizes), "bytes": sum(sizes), "seconds": round(t_small, 4),
+                         "gibs": round(sum(sizes) / t_small / GIB, 2),
+                         "blocks_per_s": round(len(sizes) / t_small)},
+        "oracle_checked": {"chunks": "all (expect ids from the chunking path)", "small": len(sample)},
+    }
+    print(json.dumps(out), flush=True)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
