@@ -101,6 +101,7 @@ struct Batch {
   uint64_t n = 0, caps = 0;
   std::vector<uint64_t> cut_base;
   DevBuf d_meta, d_cuts, d_count, d_ids, d_cid, d_ctype;
+  DevBuf d_run, d_fresh, d_fcnt;  // the batch's MD5 chains (K2r), their order entries, count
   PinBuf h_meta, h_res;
   uint64_t* cut_ends = nullptr;
   uint8_t* ids = nullptr;
@@ -110,7 +111,7 @@ struct Batch {
   bool finalized = false;
   hipEvent_t ev[5] = {};  // K1 start | K1 end | K2 end | plan+K3 end (first) | results ready
   void release() {
-    for (DevBuf* d : {&d_meta, &d_cuts, &d_count, &d_ids, &d_cid, &d_ctype}) d->release();
+    for (DevBuf* d : {&d_meta, &d_cuts, &d_count, &d_ids, &d_cid, &d_ctype, &d_run, &d_fresh, &d_fcnt}) d->release();
     h_meta.release();
     h_res.release();
     for (auto& e : ev)
@@ -149,8 +150,14 @@ struct hbx_ctx {
   int ssum_slot = 0;
   hipEvent_t ssum_free[2] = {nullptr, nullptr};  // recorded after the K2 that last read the slot
   bool ssum_used[2] = {false, false};
-  DevBuf d_tab[2], d_tctl[2];  // MD5 chain tables (ping-pong) + their counts
-  int tab_cur = -1;         // table holding the last launch's chains (-1: none in flight)
+  // K3 launch orders (triple-buffered by launch index % 3): plan j (scan
+  // stream) writes order[j%3] from order[(j-1)%3]; K3 j (hash stream) reads it
+  DevBuf d_order[3], d_octl[3];
+  hipEvent_t plan_done[3] = {nullptr, nullptr, nullptr};   // plan j%3 written
+  hipEvent_t order_free[3] = {nullptr, nullptr, nullptr};  // K3 that read slot j%3 done
+  bool order_used[3] = {false, false, false};
+  uint64_t launches = 0;    // K3 launches planned so far
+  uint32_t last_budget = 0; // budget of the last planned launch
   DevBuf d_stage;           // host-input arena
   DevBuf d_msg;             // hbx_block_id message
   DevBuf d_plan;            // chain planner: global bin counts + cursors
@@ -326,45 +333,61 @@ int finalize_batch(hbx_ctx* c, Batch* b) {
 // K3 with `budget` blocks per chain.  Afterwards every pending batch has had
 // one more launch; those whose chains are now guaranteed complete are
 // finalized.  A budget of kBudgetAll completes every chain in flight.
-int md5_launch(hbx_ctx* c, Batch* nb, const uint8_t* arena, uint32_t budget) {
-  hipStream_t s = c->hstream;
-  uint64_t bound = 0;  // chains alive after this plan <= chunks of unfinalized batches
+// Plan launch j = c->launches on the scan stream: order[j%3] from
+// order[(j-1)%3] (advanced by the budget of launch j-1) plus the fresh chains
+// of batch nb (if any).  Needs no result of any K3 launch.
+int plan_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
+  hipStream_t s = c->stream;
+  const int slot = (int)(c->launches % 3), ps = (int)((c->launches + 2) % 3);
+  uint64_t bound = 64;  // entries <= chains of the unfinalized batches
   for (Batch* b : c->pending)
     if (!b->finalized) bound += b->caps;
-  const int src = c->tab_cur;
-  const int dst = src < 0 ? 0 : src ^ 1;
-  int rc = ensure_shared(c, c->d_tab[dst], std::max<uint64_t>(bound, 64) * sizeof(Chain));
+  int rc = ensure_shared(c, c->d_order[slot], bound * sizeof(OrderEntry));
+  if (!rc) rc = ensure_shared(c, c->d_octl[slot], 256);
+  if (!rc) rc = ensure_shared(c, c->d_plan, 2 * kPlanBins * sizeof(uint32_t));
   if (rc) return rc;
-  if ((rc = ensure_shared(c, c->d_tctl[dst], 256))) return rc;
-  const Chain* prev = src < 0 ? nullptr : c->d_tab[src].as<Chain>();
-  const uint32_t* prev_ctl = src < 0 ? nullptr : c->d_tctl[src].as<uint32_t>();
-  Chain* cur = c->d_tab[dst].as<Chain>();
-  uint32_t* ctl = c->d_tctl[dst].as<uint32_t>();
-  if ((rc = ensure_shared(c, c->d_plan, 2 * kPlanBins * sizeof(uint32_t)))) return rc;
+  // the K3 launch that read this slot three launches ago must be done
+  if (c->order_used[slot] && c->hstream != s) HBX_TRY(c, hipStreamWaitEvent(s, c->order_free[slot], 0));
+  const bool has_prev = c->launches > 0;
+  const bool fresh = nb && nb->n;
   {
     StageTimer t(c, s, 2);
     HBX_TRY(c, hipMemsetAsync(c->d_plan.p, 0, 2 * kPlanBins * sizeof(uint32_t), s));
-    const bool fresh = nb && nb->n;
-    const uint64_t n = fresh ? nb->n : 0;
-    const uint64_t* d_off = fresh ? nb->d_meta.as<uint64_t>() : nullptr;
     for (uint32_t phase = 0; phase < 2; phase++)
-      hipLaunchKernelGGL(hbx_k2c_plan, dim3(kPlanGroups), dim3(kPlanThreads), 0, s, (uint32_t)n,
-                         fresh ? arena : nullptr, d_off, fresh ? d_off + 3 * n : nullptr,
-                         fresh ? nb->d_cuts.as<uint64_t>() : nullptr,
-                         fresh ? nb->d_count.as<uint32_t>() : nullptr,
-                         fresh ? nb->d_ids.as<uint32_t>() : nullptr, prev, prev_ctl, cur, ctl, budget,
+      hipLaunchKernelGGL(hbx_k2c_plan, dim3(kPlanGroups), dim3(kPlanThreads), 0, s,
+                         has_prev ? c->d_order[ps].as<OrderEntry>() : nullptr,
+                         has_prev ? c->d_octl[ps].as<uint32_t>() : nullptr, c->last_budget,
+                         fresh ? nb->d_fresh.as<OrderEntry>() : nullptr,
+                         fresh ? nb->d_fcnt.as<uint32_t>() : nullptr, budget,
+                         c->d_order[slot].as<OrderEntry>(), c->d_octl[slot].as<uint32_t>(),
                          c->d_plan.as<uint32_t>(), phase);
   }
   HBX_TRY(c, hipGetLastError());
+  HBX_TRY(c, hipEventRecord(c->plan_done[slot], s));
+  c->last_budget = budget;
+  return HBX_OK;
+}
+
+// One MD5 launch (planned by plan_launch just before): K3 with `budget`
+// blocks per chain.  Afterwards every pending batch has had one more launch;
+// those whose chains are now guaranteed complete are finalized.  A budget of
+// kBudgetAll completes every chain in flight.
+int md5_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
+  hipStream_t s = c->hstream;
+  const int slot = (int)(c->launches % 3);
+  if (s != c->stream) HBX_TRY(c, hipStreamWaitEvent(s, c->plan_done[slot], 0));
   {
     StageTimer t(c, s, 3);
-    hipLaunchKernelGGL(hbx_k3_block_md5, dim3(c->md5_wgs), dim3(kK3Threads), 0, s, cur,
-                       static_cast<const uint32_t*>(ctl), budget, c->k3_dense);
+    hipLaunchKernelGGL(hbx_k3_block_md5, dim3(c->md5_wgs), dim3(kK3Threads), 0, s,
+                       c->d_order[slot].as<OrderEntry>(), static_cast<const uint32_t*>(c->d_octl[slot].as<uint32_t>()),
+                       budget, c->k3_dense);
   }
   HBX_TRY(c, hipGetLastError());
-  c->tab_cur = dst;
+  HBX_TRY(c, hipEventRecord(c->order_free[slot], s));
+  c->order_used[slot] = true;
+  c->launches++;
   if (nb) HBX_TRY(c, hipEventRecord(nb->ev[3], s));
-  bool any_left = false, forked = false;
+  bool forked = false;
   for (Batch* b : c->pending) {
     if (b->finalized) continue;
     b->done++;
@@ -374,12 +397,10 @@ int md5_launch(hbx_ctx* c, Batch* nb, const uint8_t* arena, uint32_t budget) {
         HBX_TRY(c, hipStreamWaitEvent(c->rstream, c->k3_done, 0));
         forked = true;
       }
-      if ((rc = finalize_batch(c, b))) return rc;
-    } else {
-      any_left = true;
+      int rc = finalize_batch(c, b);
+      if (rc) return rc;
     }
   }
-  if (!any_left) c->tab_cur = -1;  // every chain in flight is hashed
   return HBX_OK;
 }
 
@@ -456,7 +477,11 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
   HBX_TRY(c, b->d_ids.ensure(tcaps * 16));
   HBX_TRY(c, b->d_cid.ensure(n * 16));
   HBX_TRY(c, b->d_ctype.ensure(n * 4));
+  HBX_TRY(c, b->d_run.ensure(tcaps * sizeof(Chain)));
+  HBX_TRY(c, b->d_fresh.ensure(tcaps * sizeof(OrderEntry)));
+  HBX_TRY(c, b->d_fcnt.ensure(256));
   HBX_TRY(c, b->h_res.ensure(res_layout(n, tcaps).total));
+  if ((rc = ensure_shared(c, c->d_plan, 2 * kPlanBins * sizeof(uint32_t)))) return rc;
 
   HBX_TRY(c, hipMemcpyAsync(b->d_meta.p, hm, meta_bytes, hipMemcpyHostToDevice, s));
   const uint64_t* d_off = b->d_meta.as<uint64_t>();
@@ -495,13 +520,21 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
                        b->d_count.as<uint32_t>());
   }
   HBX_TRY(c, hipGetLastError());
-  HBX_TRY(c, hipEventRecord(b->ev[2], s2));
   HBX_TRY(c, hipEventRecord(c->ssum_free[slot], s2));
   c->ssum_used[slot] = true;
+  // K2r: the batch's chains and their order entries
+  HBX_TRY(c, hipMemsetAsync(b->d_fcnt.p, 0, 4, s2));
+  hipLaunchKernelGGL(hbx_k2r_new_chains, dim3((uint32_t)((n * kPlanLanesPerFile + 255) / 256)), dim3(256), 0, s2,
+                     (uint32_t)n, arena, d_off, d_cb, b->d_cuts.as<uint64_t>(), b->d_count.as<uint32_t>(),
+                     b->d_ids.as<uint32_t>(), b->d_run.as<Chain>(), b->d_fresh.as<OrderEntry>(),
+                     b->d_fcnt.as<uint32_t>());
+  HBX_TRY(c, hipGetLastError());
+  HBX_TRY(c, hipEventRecord(b->ev[2], s2));
   // the hash stream picks the batch up once its cuts exist; the scan stream
   // is free for the next batch's K1/K2 while K3 runs
-  if (c->hstream != s2) HBX_TRY(c, hipStreamWaitEvent(c->hstream, b->ev[2], 0));
-  return md5_launch(c, b, arena, budget);
+  if (s2 != s) HBX_TRY(c, hipStreamWaitEvent(s, b->ev[2], 0));  // the plan reads K2r's entries
+  if ((rc = plan_launch(c, b, budget))) return rc;
+  return md5_launch(c, b, budget);
 }
 
 // Scatter a collected batch's pinned results into the caller's arrays.
@@ -545,7 +578,8 @@ int wait_oldest(hbx_ctx* c) {
   if (c->pending.empty()) return HBX_OK;
   Batch* b = c->pending.front();
   if (!b->finalized) {
-    int rc = md5_launch(c, nullptr, nullptr, kBudgetAll);
+    int rc = plan_launch(c, nullptr, kBudgetAll);
+    if (!rc) rc = md5_launch(c, nullptr, kBudgetAll);
     if (rc) return rc;
   }
   HBX_TRY(c, hipEventSynchronize(b->ev[4]));
@@ -623,6 +657,13 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
     hbx_ctx_destroy(c);
     return HBX_ERR_HIP;
   }
+  for (int t = 0; t < 3; t++) {
+    if (hipEventCreateWithFlags(&c->plan_done[t], hipEventDisableTiming) == hipSuccess &&
+        hipEventCreateWithFlags(&c->order_free[t], hipEventDisableTiming) == hipSuccess)
+      continue;
+    hbx_ctx_destroy(c);
+    return HBX_ERR_HIP;
+  }
   *out = c;
   return HBX_OK;
 }
@@ -632,9 +673,11 @@ void hbx_ctx_destroy(hbx_ctx* c) {
   (void)hipSetDevice(c->device);
   for (hipStream_t s : {c->stream, c->cstream, c->hstream, c->rstream})
     if (s) (void)hipStreamSynchronize(s);
-  for (hipEvent_t e : {c->k3_done, c->ssum_free[0], c->ssum_free[1]})
+  for (hipEvent_t e : {c->k3_done, c->ssum_free[0], c->ssum_free[1], c->plan_done[0], c->plan_done[1],
+                       c->plan_done[2], c->order_free[0], c->order_free[1], c->order_free[2]})
     if (e) (void)hipEventDestroy(e);
-  for (DevBuf* b : {&c->d_ssum[0], &c->d_ssum[1], &c->d_tab[0], &c->d_tab[1], &c->d_tctl[0], &c->d_tctl[1],
+  for (DevBuf* b : {&c->d_ssum[0], &c->d_ssum[1], &c->d_order[0], &c->d_order[1], &c->d_order[2],
+                    &c->d_octl[0], &c->d_octl[1], &c->d_octl[2],
                     &c->d_stage, &c->d_msg, &c->d_plan, &c->d_vdesc, &c->d_vlinks,
                     &c->d_vout, &c->d_vexp, &c->d_zeros})
     b->release();
@@ -692,11 +735,11 @@ int hbx_reserve(hbx_ctx* c, uint32_t batches, uint64_t files, uint64_t bytes) {
   const uint64_t slices = bytes / kSlice + files;
   const size_t meta_bytes = files * 8 * 4 + tiles * sizeof(uint2);
   int rc = HBX_OK;
-  for (int t = 0; t < 2 && !rc; t++) {
-    rc = ensure_shared(c, c->d_ssum[t], (slices + 1) * sizeof(uint2));
-    if (rc) break;
-    rc = ensure_shared(c, c->d_tab[t], std::max<uint64_t>((uint64_t)batches * caps, 64) * sizeof(Chain));
-    if (!rc) rc = ensure_shared(c, c->d_tctl[t], 256);
+  for (int t = 0; t < 2 && !rc; t++) rc = ensure_shared(c, c->d_ssum[t], (slices + 1) * sizeof(uint2));
+  if (!rc) rc = ensure_shared(c, c->d_plan, 2 * kPlanBins * sizeof(uint32_t));
+  for (int t = 0; t < 3 && !rc; t++) {
+    rc = ensure_shared(c, c->d_order[t], ((uint64_t)batches * caps + 64) * sizeof(OrderEntry));
+    if (!rc) rc = ensure_shared(c, c->d_octl[t], 256);
   }
   if (rc) return rc;
   std::vector<Batch*> ready;
@@ -706,7 +749,8 @@ int hbx_reserve(hbx_ctx* c, uint32_t batches, uint64_t files, uint64_t bytes) {
     ready.push_back(b);
     for (auto r : {b->h_meta.ensure(meta_bytes), b->d_meta.ensure(meta_bytes), b->d_cuts.ensure(caps * 8),
                    b->d_count.ensure(files * 4), b->d_ids.ensure(caps * 16), b->d_cid.ensure(files * 16),
-                   b->d_ctype.ensure(files * 4), b->h_res.ensure(res_layout(files, caps).total)})
+                   b->d_ctype.ensure(files * 4), b->d_run.ensure(caps * sizeof(Chain)),
+                   b->d_fresh.ensure(caps * sizeof(OrderEntry)), b->d_fcnt.ensure(256), b->h_res.ensure(res_layout(files, caps).total)})
       if (r != hipSuccess && !rc) rc = c->hip(r, "hbx_reserve");
     if (rc) break;
   }

@@ -1111,61 +1111,113 @@ __device__ __forceinline__ uint32_t chain_cnt(uint32_t len, uint32_t next, uint3
   const uint32_t nfull = (len + 8u) >> 6;
   return min(nfull - next, budget);
 }
-// Planner order: this launch's block count, descending, in 1024 bins (bin 0
-// = a full slice), so the 64 chains of a K3 wave have nearly equal counts
-// and the wave can advance them together by its minimum (the cooperative
-// path) with only a small per-lane remainder.
+// ------------------------------------------------------- chain schedule --
+// A batch's chains live in the batch's own array for their whole life (K2r
+// writes them; K3 updates `next` and the MD5 state in place).  What changes
+// from launch to launch is the ORDER in which K3 takes them: a list of
+// {chain pointer, full blocks still to hash}, sorted by this launch's block
+// count descending in 1024 bins (bin 0 = a full slice), pooled over every
+// batch in flight, so the 64 chains of a K3 wave have nearly equal counts and
+// the wave advances them together by its minimum (the cooperative path) with
+// only a small per-lane remainder.  A chain's progress is deterministic (it
+// advances min(remaining, budget) blocks per launch), so the planner builds
+// the order of launch j from the order of launch j-1 without waiting for K3
+// j-1: it runs on the scan stream, beside the hash stream's K3 launches.
+struct OrderEntry {
+  uint64_t chain;  // Chain* in its batch's array
+  uint32_t rem;    // 1 + full message blocks still to hash before this launch (0 = finished)
+  uint32_t pad;
+};
 constexpr uint32_t kPlanBins = 1024u;
-__device__ __forceinline__ uint32_t chain_bin(uint32_t cnt, uint32_t budget) {
-  const uint32_t ref = min(budget, (uint32_t)(kMaxBlock >> 6));  // largest possible count
+__device__ __forceinline__ uint32_t order_bin(uint32_t cnt, uint32_t budget) {
+  const uint32_t ref = min(budget, (uint32_t)(kMaxBlock >> 6) + 1u);  // largest possible count
   const uint32_t c = min(cnt, ref);
   return (ref - c) * (kPlanBins - 1u) / ref;
 }
 
+// ------------------------------------------------------- K2r new chains --
+// One chain per chunk of a new batch, in any order, into the batch's array;
+// one order entry per chain into `fresh`; count in cnt[0] (zeroed before).
+constexpr uint32_t kPlanLanesPerFile = 16u;  // work items sharing one file's chunks
+
+extern "C" __global__ __launch_bounds__(256) void hbx_k2r_new_chains(
+    uint32_t n_files, const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
+    const uint64_t* __restrict__ cut_base, const uint64_t* __restrict__ cut_ends,
+    const uint32_t* __restrict__ cut_count, uint32_t* __restrict__ ids, Chain* __restrict__ run,
+    OrderEntry* __restrict__ fresh, uint32_t* __restrict__ cnt) {
+  const uint32_t w = blockIdx.x * 256u + threadIdx.x;
+  if (w >= n_files * kPlanLanesPerFile) return;
+  const uint32_t f = w / kPlanLanesPerFile;
+  const uint64_t cb = cut_base[f];
+  const uint32_t k = cut_count[f];
+  const uint64_t base = reinterpret_cast<uint64_t>(arena + file_off[f]);
+  for (uint32_t i = w % kPlanLanesPerFile; i < k; i += kPlanLanesPerFile) {
+    const uint64_t start = i ? cut_ends[cb + i - 1] : 0ull;
+    const uint64_t e = cut_ends[cb + i];
+    Chain ch;
+    ch.src = base + start;
+    ch.len = (uint32_t)(e - start);
+    ch.next = 0u;
+    ch.h[0] = 0x67452301u;
+    ch.h[1] = 0xefcdab89u;
+    ch.h[2] = 0x98badcfeu;
+    ch.h[3] = 0x10325476u;
+    ch.out = reinterpret_cast<uint64_t>(ids + 4u * (cb + i));
+    ch.pad = 0ull;
+    const uint32_t slot = atomicAdd(cnt, 1u);
+    run[slot] = ch;
+    OrderEntry o;
+    o.chain = reinterpret_cast<uint64_t>(run + slot);
+    o.rem = ((ch.len + 8u) >> 6) + 1u;
+    o.pad = 0u;
+    fresh[slot] = o;
+  }
+}
+
 // ----------------------------------------------------------- K2c plan --
-// Builds the chain table for one K3 launch: the unfinished chains of the
-// previous launch (`prev`, count prev_ctl[1]; nullptr = none) plus one fresh
-// chain per chunk of the new batch (n_files may be 0), ordered as above.
-// ctl[1] = entries.  Two launches of the same grid over the same partition
-// of the entries (carried chains by global thread, new chunks by
-// (file, lane) work items):
+// The order of one K3 launch: the entries of the previous launch's order
+// (`prev`, count *n_prev; their rem less what that launch, with budget
+// `bprev`, hashed; the ones it finished dropped) plus the `fresh` entries of a new
+// batch (count *n_fresh; either may be absent), binned by this launch's
+// count min(rem, budget).  Two launches of the same grid over the same
+// partition:
 //   phase 0: per-workgroup histogram of the bins, added into gh[0, 1024)
 //   phase 1: every workgroup scans gh into bin bases, reserves its own range
 //            in each bin (one atomic per bin on gh[1024 + bin]) and scatters
-//            its entries with LDS atomics.
+//            with LDS atomics; workgroup 0 writes the count to *n_out.
 // gh (2 x 1024 u32) is zeroed before phase 0.  Order inside a bin is
 // arbitrary; results never depend on it (each chain is independent).
 constexpr int kPlanThreads = 1024;
 static_assert(kPlanThreads == (int)kPlanBins, "one planner thread per bin");
-constexpr uint32_t kPlanLanesPerFile = 16u;  // work items sharing one file's new chunks
-constexpr uint32_t kPlanGroups = 32u;        // grid of both phases
+constexpr uint32_t kPlanGroups = 32u;  // grid of both phases
 
 extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
-    uint32_t n_files, const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
-    const uint64_t* __restrict__ cut_base, const uint64_t* __restrict__ cut_ends,
-    const uint32_t* __restrict__ cut_count, uint32_t* __restrict__ ids, const Chain* __restrict__ prev,
-    const uint32_t* __restrict__ prev_ctl, Chain* __restrict__ cur, uint32_t* __restrict__ ctl,
-    uint32_t budget, uint32_t* __restrict__ gh, uint32_t phase) {
+    const OrderEntry* __restrict__ prev, const uint32_t* __restrict__ n_prev_p, uint32_t bprev,
+    const OrderEntry* __restrict__ fresh, const uint32_t* __restrict__ n_fresh_p, uint32_t budget,
+    OrderEntry* __restrict__ out, uint32_t* __restrict__ n_out, uint32_t* __restrict__ gh,
+    uint32_t phase) {
   __shared__ uint32_t hist[kPlanBins], pos[kPlanBins], wsum[kPlanThreads / 64];
   const uint32_t tid = threadIdx.x;
   const uint32_t gt = blockIdx.x * kPlanThreads + tid, gn = gridDim.x * kPlanThreads;
-  const uint32_t n_prev = prev ? prev_ctl[1] : 0u;
-  const uint32_t n_work = n_files * kPlanLanesPerFile;
+  const uint32_t n_prev = prev ? *n_prev_p : 0u;
+  const uint32_t n_fresh = fresh ? *n_fresh_p : 0u;
+  const uint32_t n_all = n_prev + n_fresh;
+  // entry e of the combined list, advanced to this launch (rem 0 = finished)
+  auto entry = [&](uint32_t e) {
+    OrderEntry o;
+    if (e < n_prev) {  // the launch with budget bprev finished it iff its full blocks fit
+      o = prev[e];
+      o.rem = o.rem - 1u <= bprev ? 0u : o.rem - bprev;
+    } else {
+      o = fresh[e - n_prev];
+    }
+    return o;
+  };
   hist[tid] = 0u;
   __syncthreads();
-  for (uint32_t e = gt; e < n_prev; e += gn) {
-    const uint2 ln = *reinterpret_cast<const uint2*>(&prev[e].len);  // {len, next}
-    if (ln.y != kChainDone) atomicAdd(&hist[chain_bin(chain_cnt(ln.x, ln.y, budget), budget)], 1u);
-  }
-  for (uint32_t w = gt; w < n_work; w += gn) {
-    const uint32_t f = w / kPlanLanesPerFile;
-    const uint64_t cb = cut_base[f];
-    const uint32_t k = cut_count[f];
-    for (uint32_t i = w % kPlanLanesPerFile; i < k; i += kPlanLanesPerFile) {
-      const uint64_t start = i ? cut_ends[cb + i - 1] : 0ull;
-      const uint64_t e = cut_ends[cb + i];
-      atomicAdd(&hist[chain_bin(chain_cnt((uint32_t)(e - start), 0u, budget), budget)], 1u);
-    }
+  for (uint32_t e = gt; e < n_all; e += gn) {
+    const OrderEntry o = entry(e);
+    if (o.rem) atomicAdd(&hist[order_bin(min(o.rem - 1u, budget), budget)], 1u);
   }
   __syncthreads();
   if (phase == 0u) {
@@ -1182,54 +1234,25 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
     for (uint32_t wv = 0; wv < (tid >> 6); wv++) before += wsum[wv];
     const uint32_t mine = hist[tid];
     pos[tid] = before + inc - v + (mine ? atomicAdd(&gh[kPlanBins + tid], mine) : 0u);
-    if (blockIdx.x == 0 && tid == kPlanThreads - 1) {
-      ctl[0] = 0u;
-      ctl[1] = before + inc;
-    }
+    if (blockIdx.x == 0 && tid == kPlanThreads - 1) *n_out = before + inc;
   }
   __syncthreads();
-  for (uint32_t e = gt; e < n_prev; e += gn) {
-    const Chain ch = prev[e];
-    if (ch.next != kChainDone)
-      cur[atomicAdd(&pos[chain_bin(chain_cnt(ch.len, ch.next, budget), budget)], 1u)] = ch;
-  }
-  for (uint32_t w = gt; w < n_work; w += gn) {
-    const uint32_t f = w / kPlanLanesPerFile;
-    const uint64_t cb = cut_base[f];
-    const uint32_t k = cut_count[f];
-    const uint64_t base = reinterpret_cast<uint64_t>(arena + file_off[f]);
-    for (uint32_t i = w % kPlanLanesPerFile; i < k; i += kPlanLanesPerFile) {
-      const uint64_t start = i ? cut_ends[cb + i - 1] : 0ull;
-      const uint64_t e = cut_ends[cb + i];
-      Chain ch;
-      ch.src = base + start;
-      ch.len = (uint32_t)(e - start);
-      ch.next = 0u;
-      ch.h[0] = 0x67452301u;
-      ch.h[1] = 0xefcdab89u;
-      ch.h[2] = 0x98badcfeu;
-      ch.h[3] = 0x10325476u;
-      ch.out = reinterpret_cast<uint64_t>(ids + 4u * (cb + i));
-      ch.pad = 0ull;
-      cur[atomicAdd(&pos[chain_bin(chain_cnt(ch.len, 0u, budget), budget)], 1u)] = ch;
-    }
+  for (uint32_t e = gt; e < n_all; e += gn) {
+    const OrderEntry o = entry(e);
+    if (o.rem) out[atomicAdd(&pos[order_bin(min(o.rem - 1u, budget), budget)], 1u)] = o;
   }
 }
 
 // ---------------------------------------------------------- K3 block MD5 --
-// Block-ID kernel (lane mode: lane = chain, 64 similar-length chains per
-// wave in the planner's order).  Each lane resumes its chain at `next`,
+// Block-ID kernel (lane mode: lane = chain, 64 similar-count chains per wave
+// in the planner's order).  Each lane resumes its chain at `next`,
 // compresses up to `budget` full blocks and either finishes (tail blocks,
 // BlockID stored at `out`, entry marked done) or saves the state for the
-// next launch.  grid = one 256-thread workgroup per CU; group g runs on wave
-// (g / grid) % 4 of workgroup g % grid, so the first 4 x grid groups each get
-// a SIMD of their own.  The MD5 chain is bound by its 4 dependent VALU per
-// step; lane mode runs 64 such chains in one instruction stream at that
-// bound (DESIGN.md "K3"; tools/experiments/md5_wave_mode.hip for what did
-// not pay).
-// 256 threads = one wave per SIMD: a single wave saturates its SIMD's issue
-// slots, and one wave per SIMD lets the compiler use the whole register file
-// (VGPR + AGPR) for the prefetch ring without spilling.
+// next launch.  grid = one 256-thread workgroup per CU; placement of groups
+// on waves: see `dense`.  The MD5 chain is bound by the issue rate of one
+// wave (DESIGN.md "K3"; tools/experiments/md5_wave_mode.hip for what did not
+// pay).  256 threads = one wave per SIMD, which lets the compiler use the
+// whole register file (VGPR + AGPR) for the prefetch ring without spilling.
 #ifndef HBX_K3_THREADS
 #define HBX_K3_THREADS 256
 #endif
@@ -1241,13 +1264,14 @@ constexpr uint32_t kCoopMinBudget = 8u;
 constexpr int kK3Threads = HBX_K3_THREADS;
 
 extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
-    Chain* __restrict__ tab, const uint32_t* __restrict__ ctl, uint32_t budget, uint32_t dense) {
+    const OrderEntry* __restrict__ order, const uint32_t* __restrict__ n_order, uint32_t budget,
+    uint32_t dense) {
   // the MD5 chains are issue-bound: win the SIMD's issue arbitration against
-  // co-resident K1-lite waves of the next batch
+  // co-resident waves of other kernels
   __builtin_amdgcn_s_setprio(3);
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const uint32_t n_total = ctl[1];
+  const uint32_t n_total = *n_order;
 #if HBX_K3_COOP
   static_assert(kK3Threads == 256, "cooperative K3 path sized for 4 waves per workgroup");
   __shared__ __attribute__((aligned(16))) uint8_t k3_lds[kK3Threads / 64][kCoopWaveLds];
@@ -1263,8 +1287,9 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
     const uint32_t k = 64u * g + lane;
     const bool active = k < n_total;
     // idle lanes stay alive for the wave-wide loop bound: they run an empty
-    // slice over the group's first chunk and store nothing
-    const Chain ch = tab[active ? k : 64u * g];
+    // slice over the group's first chain and store nothing
+    Chain* __restrict__ chp = reinterpret_cast<Chain*>(order[active ? k : 64u * g].chain);
+    const Chain ch = *chp;
     const uint32_t len = active ? ch.len : 0u;
     const uint32_t b0 = active ? ch.next : 0u;
     const uint32_t cnt = active ? chain_cnt(len, b0, budget) : 0u;
@@ -1288,10 +1313,10 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
 #endif
     if (finish) {
       *(__attribute__((address_space(1))) u32x4*)ch.out = u32x4{h[0], h[1], h[2], h[3]};
-      tab[k].next = kChainDone;
+      chp->next = kChainDone;
     } else if (active) {
-      *reinterpret_cast<uint4*>(&tab[k].h[0]) = make_uint4(h[0], h[1], h[2], h[3]);
-      tab[k].next = b0 + cnt;
+      *reinterpret_cast<uint4*>(&chp->h[0]) = make_uint4(h[0], h[1], h[2], h[3]);
+      chp->next = b0 + cnt;
     }
   }
 }
