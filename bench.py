@@ -255,12 +255,14 @@ def main():
                   for r in res if r.n_chunks)
 
     check = None
-    if a.check and rank == 0:
+    if a.check and rank == 0:  # every file of the last timed batch vs the oracle
         from oracle import oracle as O
-        h0 = arenas[(a.steps - 1) % R][int(offs[0]):int(offs[0]) + fbytes].cpu().numpy()
-        ref = O.store_file(h0, fast=True)
-        check = bool(np.array_equal(ref.cut_ends, res[0].cut_ends)
-                     and np.array_equal(ref.ids, res[0].ids))
+        last = arenas[(a.steps - 1) % R]
+        host = [last[int(o):int(o) + fbytes].cpu().numpy() for o in offs]
+        refs = O.store_batch_mt(host, a.cpu_threads)
+        check = all(np.array_equal(r.cut_ends, g.cut_ends) and np.array_equal(r.ids, g.ids)
+                    for r, g in zip(refs, res)) and len(res) == len(refs)
+        del host
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

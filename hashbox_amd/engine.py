@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 from collections import deque
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Union
@@ -70,6 +71,16 @@ def _u8(data: BytesLike) -> np.ndarray:
 
 def _p(a: np.ndarray) -> int:
     return a.ctypes.data if a.size else 0
+
+
+def _sync_producer():
+    """The engine's HIP streams do not wait for other streams: device data
+    written on torch's current stream (e.g. a tensor just filled) must be
+    complete before the engine reads it.  The device-pointer entry points
+    call this first."""
+    t = sys.modules.get("torch")
+    if t is not None and t.cuda.is_initialized():
+        t.cuda.current_stream().synchronize()
 
 
 class Engine:
@@ -156,6 +167,7 @@ class Engine:
         """Files resident in device memory (pointer ``d_arena``, e.g. a torch
         uint8 tensor's ``data_ptr()``).  Offsets 16-B aligned; each file must be
         followed by >= 64 readable bytes."""
+        _sync_producer()
         offs = np.ascontiguousarray(offs, np.uint64)
         lens = np.ascontiguousarray(lens, np.uint64)
         caps, base, cuts, ids, sums = self._alloc_out(lens)
@@ -168,6 +180,7 @@ class Engine:
         """Enqueue a device-resident batch and return at once.  Any number of
         batches may be in flight; :meth:`wait` completes the oldest.  The
         arena must stay untouched until then."""
+        _sync_producer()
         offs = np.ascontiguousarray(offs, np.uint64)
         lens = np.ascontiguousarray(lens, np.uint64)
         caps, base, cuts, ids, sums = self._alloc_out(lens)
@@ -264,6 +277,7 @@ class Engine:
                              expect: Optional[Sequence[bytes]] = None):
         """The same for blocks resident in device memory (each followed by
         >= 64 readable bytes)."""
+        _sync_producer()
         offs = np.ascontiguousarray(offs, np.uint64)
         lens = np.ascontiguousarray(lens, np.uint64)
         n = int(lens.size)

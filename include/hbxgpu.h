@@ -40,6 +40,9 @@
  *     starts at cut_ends[i-1] (0 for i = 0).
  *   - Capacity: every chunk except the last is >= 64 KiB, so a file of len
  *     bytes has at most hbx_max_chunks(len) = len/65536 + 1 chunks.
+ *   - Device inputs must be complete when the call is made: the library's
+ *     HIP streams are non-blocking and do not wait for the caller's streams
+ *     (synchronize the producing stream first).
  */
 #ifndef HBXGPU_H
 #define HBXGPU_H

@@ -74,6 +74,16 @@ def main():
     res = eng.chunk_hash_device(arena.data_ptr(), offs, lens)
     t_gpu = time.time() - t0
     st = eng.stage_times()
+    # the same corpus again through the pipelined path: batches of 64 files
+    # in flight together, time-sliced K3 (chains resume across launches)
+    pipe = Engine(0, md5_slice=2048)
+    per = max(1, a.files // 4)
+    for b0 in range(0, a.files, per):
+        pipe.submit_device(arena.data_ptr(), offs[b0:b0 + per], lens[b0:b0 + per])
+    res_pipe = []
+    while pipe.pending():
+        res_pipe.extend(pipe.wait())
+    pipe.close()
     host = arena[:total].cpu().numpy()
     files = [host[i * fbytes:(i + 1) * fbytes] for i in range(a.files)]
     t0 = time.time()
@@ -81,17 +91,22 @@ def main():
     t_cpu = time.time() - t0
     bad_cuts = bad_ids = 0
     n_chunks = 0
-    for g, r in zip(res, ref):
+    pipe_bad = 0
+    for g, gp, r in zip(res, res_pipe, ref):
         n_chunks += r.n_chunks
         if not np.array_equal(g.cut_ends, r.cut_ends):
             bad_cuts += 1
         elif not np.array_equal(g.ids, r.ids):
             bad_ids += 1
+        if not (np.array_equal(gp.cut_ends, r.cut_ends) and np.array_equal(gp.ids, r.ids)
+                and gp.content_id == g.content_id and gp.content_type == g.content_type):
+            pipe_bad += 1
     print(json.dumps({
         "config": "BASELINE configs[3]: Zipf-duplicated corpus, bit-exactness vs oracle",
         "bytes": total, "files": a.files, "segments": nseg, "repeat_fraction": round(rep, 4),
         "chunks": n_chunks, "files_cut_mismatch": bad_cuts, "files_id_mismatch": bad_ids,
-        "bit_exact": bad_cuts == 0 and bad_ids == 0,
+        "bit_exact": bad_cuts == 0 and bad_ids == 0 and pipe_bad == 0 and len(res_pipe) == a.files,
+        "pipelined_files_mismatch": pipe_bad,
         "gpu_seconds": round(t_gpu, 4), "gpu_gibs": round(a.gib / t_gpu, 2),
         "gpu_stage_ms": [round(float(x), 3) for x in st],
         "cpu_oracle_seconds": round(t_cpu, 2), "cpu_threads": a.threads,
