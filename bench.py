@@ -34,6 +34,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 METRIC = "device-resident GiB/s chunked+hashed at 1/2/4/8 MI355X; % HBM roofline"
+K3_VALU_PER_BLOCK = 325
+VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md), GB/s
 GIB = 1 << 30
 
@@ -317,11 +319,14 @@ def main():
                      "traffic": traffic, "traffic_source": traffic_src,
                      "launches": int(tot_n[dom]), "avg_launch_ms": round(float(avg_ms[dom]), 4),
                      "algorithmic_bytes_per_launch": int(per_launch)},
-        # K3's real limit is VALU issue of the serial MD5 chains (~5.55 lane-ops
-        # per byte, 355 VALU per 64-B block); peak = 256 CU x 4 SIMD x 16 lanes x 2.4 GHz
-        "k3_valu": {"achieved_tops": round(k3_bps * 355 / 64 / 1e12, 3),
-                    "peak_tops": round(256 * 4 * 16 * 2.4e9 / 1e12, 2),
-                    "frac": round(k3_bps * 355 / 64 / (256 * 4 * 16 * 2.4e9), 4)},
+        # K3 is VALU-issue work: ~325 VALU per 64-B block on the cooperative path
+        # (5 per MD5 step).  Chip peak = 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz;
+        # one wave alone issues at most one VALU per 4 cycles (MI355X_MICROARCH.md),
+        # so one serial chain is floored at 325 x 4 cycles per block.
+        "k3_valu": {"valu_per_block": K3_VALU_PER_BLOCK,
+                    "achieved_tops": round(k3_bps * K3_VALU_PER_BLOCK / 64 / 1e12, 3),
+                    "peak_tops": round(VALU_PEAK_LANE_OPS / 1e12, 2),
+                    "frac": round(k3_bps * K3_VALU_PER_BLOCK / 64 / VALU_PEAK_LANE_OPS, 4)},
         "kernel_ms_per_step": {n: round(float(v) / a.steps, 4) for n, v in zip(names, tot_ms)},
         "kernel_launches": {n: int(v) for n, v in zip(names, tot_n)},
         "k1_roofline": {"achieved": round(k1_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
