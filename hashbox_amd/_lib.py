@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("HBX_LIB") or os.path.join(HERE, "libhbxgpu.so")
 
 HBX_OK = 0
 ERRORS = {-1: "HBX_ERR_ARG", -2: "HBX_ERR_HIP", -3: "HBX_ERR_CAPACITY", -4: "HBX_ERR_IO",
-          -5: "HBX_ERR_NODEV", -6: "HBX_ERR_STATE"}
+          -5: "HBX_ERR_NODEV", -6: "HBX_ERR_STATE", -7: "HBX_ERR_FORMAT"}
 
 # Every symbol include/hbxgpu.h declares (checked by tests/test_abi.py).
 EXPORTS = [
@@ -24,7 +24,22 @@ EXPORTS = [
     "hbx_memcpy_h2d", "hbx_memcpy_h2d_async", "hbx_alloc_pinned", "hbx_free_pinned", "hbx_stage_times",
     "hbx_set_tile_iters", "hbx_pending", "hbx_set_md5_slice", "hbx_stage_totals", "hbx_io_times",
     "hbx_reserve", "hbx_verify_blocks", "hbx_verify_blocks_device",
+    "hbx_file_entry_size", "hbx_file_entry_serialize", "hbx_file_entry_parse",
+    "hbx_chain_block_serialize", "hbx_chain_block_parse", "hbx_directory_block_size",
+    "hbx_directory_block_serialize", "hbx_directory_block_parse", "hbx_directory_block_ids",
 ]
+# Functions returning something other than an int status.
+_NON_STATUS = ("hbx_ctx_destroy", "hbx_last_error", "hbx_max_chunks", "hbx_file_entry_size",
+               "hbx_directory_block_size")
+
+
+class FileEntry(ctypes.Structure):
+    """hbx_file_entry: hashback FileEntry (hashback/hashback.go:80-90)."""
+    _fields_ = [("name", ctypes.c_void_p), ("name_len", ctypes.c_uint32), ("file_mode", ctypes.c_uint32),
+                ("file_size", ctypes.c_int64), ("mod_time", ctypes.c_int64),
+                ("reference_id", ctypes.c_uint8 * 16), ("content_id", ctypes.c_uint8 * 16),
+                ("decrypt_key", ctypes.c_uint8 * 16), ("link", ctypes.c_void_p), ("link_len", ctypes.c_uint32),
+                ("content_type", ctypes.c_uint8), ("pad", ctypes.c_uint8 * 3)]
 
 
 class FileSummary(ctypes.Structure):
@@ -85,8 +100,21 @@ def load() -> ctypes.CDLL:
     L.hbx_reserve.argtypes = [P, ctypes.c_uint32, U64, U64]
     L.hbx_verify_blocks.argtypes = [P, U64, P, P, P, P, P, P, P, P, ctypes.POINTER(U64)]
     L.hbx_verify_blocks_device.argtypes = [P, P, U64, P, P, P, P, P, P, P, P, ctypes.POINTER(U64)]
+    PU64 = ctypes.POINTER(U64)
+    PU32 = ctypes.POINTER(ctypes.c_uint32)
+    L.hbx_file_entry_size.argtypes = [P]
+    L.hbx_file_entry_size.restype = U64
+    L.hbx_file_entry_serialize.argtypes = [P, P, U64, PU64]
+    L.hbx_file_entry_parse.argtypes = [P, U64, P, PU64]
+    L.hbx_chain_block_serialize.argtypes = [P, P, ctypes.c_uint32, P, U64, PU64]
+    L.hbx_chain_block_parse.argtypes = [P, U64, PU32, P, P, ctypes.c_uint32]
+    L.hbx_directory_block_size.argtypes = [P, ctypes.c_uint32]
+    L.hbx_directory_block_size.restype = U64
+    L.hbx_directory_block_serialize.argtypes = [P, ctypes.c_uint32, P, U64, PU64, P, PU32]
+    L.hbx_directory_block_parse.argtypes = [P, U64, P, ctypes.c_uint32, PU32]
+    L.hbx_directory_block_ids.argtypes = [P, ctypes.c_uint32, P, P, P, P]
     for name in EXPORTS:
-        if name not in ("hbx_ctx_destroy", "hbx_last_error", "hbx_max_chunks"):
+        if name not in _NON_STATUS:
             getattr(L, name).restype = I
     _lib = L
     return L

@@ -29,6 +29,7 @@
 
 #include "../../include/hbxgpu.h"
 #include "hbx_kernels.hip"
+#include "hbx_formats.h"
 
 namespace {
 
@@ -1155,6 +1156,120 @@ int hbx_alloc_pinned(uint64_t bytes, void** out) {
 int hbx_free_pinned(void* p) {
   if (!p) return HBX_OK;
   return hipHostFree(p) == hipSuccess ? HBX_OK : HBX_ERR_HIP;
+}
+
+// ---- block formats (hbx_formats.h) ----------------------------
+uint64_t hbx_file_entry_size(const hbx_file_entry* e) { return e ? hbxfmt::entry_size(*e) : 0; }
+
+int hbx_file_entry_serialize(const hbx_file_entry* e, uint8_t* out, uint64_t cap, uint64_t* n) {
+  if (!e || (cap && !out) || (e->name_len && !e->name) || (e->link_len && !e->link && e->content_type == 4))
+    return HBX_ERR_ARG;
+  hbxfmt::Writer w{out, cap};
+  hbxfmt::write_entry(w, *e);
+  if (!w.ok) return HBX_ERR_CAPACITY;
+  if (n) *n = w.n;
+  return HBX_OK;
+}
+
+int hbx_file_entry_parse(const uint8_t* in, uint64_t len, hbx_file_entry* e, uint64_t* used) {
+  if (!e || (len && !in)) return HBX_ERR_ARG;
+  hbxfmt::Reader r{in, len};
+  if (!hbxfmt::read_entry(r, *e).empty()) return HBX_ERR_FORMAT;
+  if (used) *used = r.n;
+  return HBX_OK;
+}
+
+int hbx_chain_block_serialize(const uint8_t* ids, const uint8_t* keys, uint32_t k, uint8_t* out,
+                              uint64_t cap, uint64_t* n) {
+  if ((k && !ids) || (cap && !out)) return HBX_ERR_ARG;
+  hbxfmt::Writer w{out, cap};
+  hbxfmt::write_chain(w, ids, keys, k);
+  if (!w.ok) return HBX_ERR_CAPACITY;
+  if (n) *n = w.n;
+  return HBX_OK;
+}
+
+int hbx_chain_block_parse(const uint8_t* in, uint64_t len, uint32_t* k, uint8_t* ids, uint8_t* keys,
+                          uint32_t cap) {
+  if (!k || (len && !in)) return HBX_ERR_ARG;
+  hbxfmt::Reader r{in, len};
+  const uint32_t magic = r.u32();
+  const uint32_t cnt = r.u32();
+  if (!r.ok) return HBX_ERR_FORMAT;
+  if (magic != hbxfmt::kMagicChain) return HBX_ERR_FORMAT;  // "corrupted FileChainBlock"
+  *k = cnt;
+  if ((uint64_t)cnt * 32ull > len - r.n) return HBX_ERR_FORMAT;
+  if (cnt > cap && (ids || keys)) return HBX_ERR_CAPACITY;
+  for (uint32_t i = 0; i < cnt && (ids || keys); i++) {
+    const uint8_t* pair = r.take(32);
+    if (ids) std::memcpy(ids + 16ull * i, pair, 16);
+    if (keys) std::memcpy(keys + 16ull * i, pair + 16, 16);
+  }
+  return HBX_OK;
+}
+
+uint64_t hbx_directory_block_size(const hbx_file_entry* es, uint32_t n) {
+  return (es || !n) ? hbxfmt::dir_size(es, n) : 0;
+}
+
+int hbx_directory_block_serialize(const hbx_file_entry* es, uint32_t n, uint8_t* out, uint64_t cap,
+                                  uint64_t* n_out, uint8_t* links, uint32_t* n_links) {
+  if ((n && !es) || (cap && !out)) return HBX_ERR_ARG;
+  hbxfmt::Writer w{out, cap};
+  const uint32_t nl = hbxfmt::write_dir(w, es, n, links);
+  if (!w.ok) return HBX_ERR_CAPACITY;
+  if (n_out) *n_out = w.n;
+  if (n_links) *n_links = nl;
+  return HBX_OK;
+}
+
+int hbx_directory_block_parse(const uint8_t* in, uint64_t len, hbx_file_entry* es, uint32_t cap,
+                              uint32_t* n) {
+  if (!n || (len && !in)) return HBX_ERR_ARG;
+  hbxfmt::Reader r{in, len};
+  const uint32_t magic = r.u32();
+  const uint32_t cnt = r.u32();
+  if (!r.ok || magic != hbxfmt::kMagicDir) return HBX_ERR_FORMAT;  // "corrupted DirectoryBlock"
+  *n = cnt;
+  for (uint32_t i = 0; i < cnt; i++) {
+    hbx_file_entry tmp;
+    if (!hbxfmt::read_entry(r, tmp).empty()) return HBX_ERR_FORMAT;
+    if (es && i < cap) es[i] = tmp;
+  }
+  return (es && cnt > cap) ? HBX_ERR_CAPACITY : HBX_OK;
+}
+
+int hbx_directory_block_ids(hbx_ctx* c, uint32_t n_dirs, const hbx_file_entry* entries,
+                            const uint64_t* entry_base, const uint32_t* n_entries, uint8_t* ids) {
+  if (!c || (n_dirs && (!entries || !entry_base || !n_entries || !ids))) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
+  if (n_dirs == 0) return HBX_OK;
+  HBX_TRY(c, hipSetDevice(c->device));
+  // every directory block into one host image (256-B aligned, as hbx_verify_blocks
+  // lays out its staging), one copy, one K6 launch
+  std::vector<uint64_t> offs(n_dirs), lens(n_dirs), link_base(n_dirs);
+  std::vector<uint32_t> nls(n_dirs);
+  uint64_t total = 0, nlinks = 0;
+  for (uint32_t d = 0; d < n_dirs; d++) {
+    const hbx_file_entry* es = entries + entry_base[d];
+    offs[d] = total;
+    lens[d] = hbxfmt::dir_size(es, n_entries[d]);
+    total += (lens[d] + 255) & ~uint64_t(255);
+    link_base[d] = nlinks;
+    for (uint32_t i = 0; i < n_entries[d]; i++) nlinks += hbxfmt::has_content(es[i].content_type) ? 1 : 0;
+  }
+  std::vector<uint8_t> img(total), links(16 * std::max<uint64_t>(nlinks, 1));
+  for (uint32_t d = 0; d < n_dirs; d++) {
+    hbxfmt::Writer w{img.data() + offs[d], lens[d]};
+    nls[d] = hbxfmt::write_dir(w, entries + entry_base[d], n_entries[d], links.data() + 16 * link_base[d]);
+    if (!w.ok) return c->fail(HBX_ERR_ARG, "directory " + std::to_string(d) + ": bad entry");
+  }
+  HBX_TRY(c, c->d_stage.ensure(total + 65536));
+  uint8_t* arena = c->d_stage.as<uint8_t>();
+  HBX_TRY(c, hipMemcpyAsync(arena, img.data(), total, hipMemcpyHostToDevice, c->stream));
+  return verify_device(c, arena, n_dirs, offs.data(), lens.data(), links.data(), link_base.data(),
+                       nls.data(), ids, nullptr, nullptr, nullptr);
 }
 
 }  // extern "C"

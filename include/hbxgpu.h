@@ -20,6 +20,10 @@
  *                         FileChainBlock of store.go:187-188
  *   hbx_file_summary      entry.ContentType / entry.ContentBlockID written by
  *                         store.go:187-196
+ *   hbx_verify_blocks     HashboxBlock.VerifyBlock (block.go:152-174), batched
+ *   hbx_file_entry_*,     FileEntry / FileChainBlock / DirectoryBlock
+ *   hbx_chain_block_*,    Serialize + Unserialize (hashback/hashback.go:80-214)
+ *   hbx_directory_block_* and storeDir's block id (store.go:201-234)
  *
  * Conventions
  *   - Every function returns an int status: 0 = OK, negative = error
@@ -182,6 +186,78 @@ int hbx_verify_blocks_device(hbx_ctx *ctx, const void *d_arena, uint64_t n, cons
                              const uint64_t *lens, const uint8_t *links, const uint64_t *link_base,
                              const uint32_t *n_links, uint8_t *ids, const uint8_t *expect,
                              uint8_t *ok, uint64_t *n_bad);
+
+/* ---- Per-file and per-directory block formats ------------
+ * hashback/hashback.go:80-214.  FileEntry is one directory entry; its
+ * ContentBlockID is a chunk id (type 2), a FileChainBlock id (type 3, see
+ * hbx_file_summary) or a DirectoryBlock id (type 1).  Strings are raw bytes
+ * (core.String, pkg/core/core.go:95-109); integers big-endian
+ * (pkg/core/utils.go:73-88); file_mode is Go's os.FileMode bit layout and
+ * mod_time is UnixNano (store.go:243-251).  These functions are pure host
+ * code and need no context. */
+#define HBX_CONTENT_EMPTY 0     /* ContentTypeEmpty,     hashback.go:94 */
+#define HBX_CONTENT_DIRECTORY 1 /* ContentTypeDirectory, hashback.go:95 */
+#define HBX_CONTENT_SYMLINK 4   /* ContentTypeSymLink,   hashback.go:98 */
+#define HBX_ERR_FORMAT (-7)     /* corrupted or truncated serialized block */
+
+typedef struct {
+  const char *name; /* FileName (not NUL-terminated) */
+  uint32_t name_len;
+  uint32_t file_mode;  /* FileMode */
+  int64_t file_size;   /* FileSize */
+  int64_t mod_time;    /* ModTime */
+  uint8_t reference_id[16];
+  uint8_t content_id[16];  /* written for types 1, 2, 3 */
+  uint8_t decrypt_key[16]; /* written for type 2 */
+  const char *link;        /* FileLink, written for type 4 */
+  uint32_t link_len;
+  uint8_t content_type; /* 0 empty, 1 dir, 2 file data, 3 file chain, 4 symlink */
+  uint8_t pad[3];
+} hbx_file_entry;
+
+/* Serialized size of FileEntry.Serialize (hashback.go:113-132). */
+uint64_t hbx_file_entry_size(const hbx_file_entry *e);
+/* FileEntry.Serialize into out[0..cap); *n = bytes written.
+ * HBX_ERR_CAPACITY if cap is too small (nothing useful written). */
+int hbx_file_entry_serialize(const hbx_file_entry *e, uint8_t *out, uint64_t cap, uint64_t *n);
+/* FileEntry.Unserialize (hashback.go:133-155) of in[0..len); *used = bytes
+ * consumed.  name/link point into `in`.  HBX_ERR_FORMAT for a wrong magic
+ * ("corrupted FileEntry") or a short buffer. */
+int hbx_file_entry_parse(const uint8_t *in, uint64_t len, hbx_file_entry *e, uint64_t *used);
+
+/* FileChainBlock.Serialize (hashback.go:162-170): "fchn", k, then k pairs
+ * (id, decrypt key); keys may be NULL (all zero, as store.go:175-184 writes
+ * them).  Size is 8 + 32k.  This is the block whose HashData with links =
+ * ids is hbx_file_summary.content_id for type 3. */
+int hbx_chain_block_serialize(const uint8_t *ids, const uint8_t *keys, uint32_t k, uint8_t *out,
+                              uint64_t cap, uint64_t *n);
+/* FileChainBlock.Unserialize (hashback.go:171-185): *k = chain length; ids
+ * and keys (each 16*cap bytes, may be NULL) receive up to cap entries
+ * (HBX_ERR_CAPACITY if *k > cap). */
+int hbx_chain_block_parse(const uint8_t *in, uint64_t len, uint32_t *k, uint8_t *ids, uint8_t *keys,
+                          uint32_t cap);
+
+/* DirectoryBlock.Serialize (hashback.go:192-199) of n entries in the order
+ * given (storeDir sorts by name, store.go:217).  links (16*n bytes, may be
+ * NULL) receives storeDir's link list: the content_id of every entry of type
+ * 1, 2 or 3, in order (store.go:221-228); *n_links its length.  Size:
+ * hbx_directory_block_size. */
+uint64_t hbx_directory_block_size(const hbx_file_entry *entries, uint32_t n);
+int hbx_directory_block_serialize(const hbx_file_entry *entries, uint32_t n, uint8_t *out,
+                                  uint64_t cap, uint64_t *n_out, uint8_t *links, uint32_t *n_links);
+/* DirectoryBlock.Unserialize (hashback.go:200-214): *n = entry count;
+ * entries[0..min(n, cap)) are filled (names/links point into `in`). */
+int hbx_directory_block_parse(const uint8_t *in, uint64_t len, hbx_file_entry *entries, uint32_t cap,
+                              uint32_t *n);
+
+/* The IDs of many DirectoryBlocks at once, on the device: directory d holds
+ * entries[entry_base[d] .. + n_entries[d]); ids[16*d ..] receives
+ * NewHashboxBlock(dblk bytes, links).BlockID (store.go:230-231).  A tree's
+ * directories are hashed level by level, deepest first, since a parent's
+ * entry carries its child directory's id.  Refused (HBX_ERR_STATE) while
+ * batches are pending. */
+int hbx_directory_block_ids(hbx_ctx *ctx, uint32_t n_dirs, const hbx_file_entry *entries,
+                            const uint64_t *entry_base, const uint32_t *n_entries, uint8_t *ids);
 
 /* Device arena helpers (allocations include HBX_ARENA_SLACK). */
 int hbx_arena_alloc(hbx_ctx *ctx, uint64_t bytes, void **d_ptr);
