@@ -20,6 +20,7 @@ from __future__ import annotations
 import ctypes
 import os
 import stat
+import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -81,22 +82,49 @@ def _check(rc: int, what: str):
         raise HbxError(f"{what}: {_lib.ERRORS.get(rc, rc)}")
 
 
+_ENTRY_DTYPE = np.dtype({"names": ["name", "name_len", "file_mode", "file_size", "mod_time", "reference_id",
+                                    "content_id", "decrypt_key", "link", "link_len", "content_type"],
+                          "formats": ["<u8", "<u4", "<u4", "<i8", "<i8", ("u1", 16), ("u1", 16), ("u1", 16),
+                                      "<u8", "<u4", "u1"],
+                          "offsets": [0, 8, 12, 16, 24, 32, 48, 64, 80, 88, 92], "itemsize": 96})
+
+
 def _c_entries(entries: Sequence[FileEntry]):
-    """ctypes array of hbx_file_entry; returns (array, keepalive)."""
-    arr = (_lib.FileEntry * max(len(entries), 1))()
-    keep = []
-    for c, e in zip(arr, entries):
-        name = ctypes.create_string_buffer(bytes(e.file_name), max(len(e.file_name), 1))
-        link = ctypes.create_string_buffer(bytes(e.file_link), max(len(e.file_link), 1))
-        keep += [name, link]
-        c.name, c.name_len = ctypes.cast(name, ctypes.c_void_p), len(e.file_name)
-        c.link, c.link_len = ctypes.cast(link, ctypes.c_void_p), len(e.file_link)
-        c.file_size, c.file_mode, c.mod_time = int(e.file_size), int(e.file_mode) & 0xFFFFFFFF, int(e.mod_time)
-        c.content_type = int(e.content_type)
-        for dst, src in ((c.reference_id, e.reference_id), (c.content_id, e.content_block_id),
-                         (c.decrypt_key, e.decrypt_key)):
-            ctypes.memmove(dst, bytes(src), 16)
-    return arr, keep
+    """hbx_file_entry[] for many entries, built column-wise (names and links
+    in one byte pool).  Returns (ctypes array view, keepalive)."""
+    n = len(entries)
+    rec = np.zeros(max(n, 1), _ENTRY_DTYPE)
+    if n:
+        names = [bytes(e.file_name) for e in entries]
+        links = [bytes(e.file_link) for e in entries]
+        nl = np.fromiter((len(x) for x in names), np.uint64, n)
+        ll = np.fromiter((len(x) for x in links), np.uint64, n)
+        pool = np.frombuffer(b"".join(names) + b"".join(links) + b"\0", np.uint8)
+        base = pool.ctypes.data
+        noff = np.zeros(n, np.uint64)
+        noff[1:] = np.cumsum(nl[:-1])
+        loff = np.zeros(n, np.uint64)
+        loff[1:] = np.cumsum(ll[:-1])
+        loff += np.uint64(nl.sum())
+        rec["name"] = np.uint64(base) + noff
+        rec["name_len"] = nl
+        rec["link"] = np.uint64(base) + loff
+        rec["link_len"] = ll
+        rec["file_mode"] = np.fromiter((int(e.file_mode) & 0xFFFFFFFF for e in entries), np.uint32, n)
+        rec["file_size"] = np.fromiter((int(e.file_size) for e in entries), np.int64, n)
+        rec["mod_time"] = np.fromiter((int(e.mod_time) for e in entries), np.int64, n)
+        rec["content_type"] = np.fromiter((int(e.content_type) for e in entries), np.uint8, n)
+        for col, attr in (("reference_id", "reference_id"), ("content_id", "content_block_id"),
+                          ("decrypt_key", "decrypt_key")):
+            rec[col] = np.frombuffer(b"".join(bytes(getattr(e, attr)) for e in entries), np.uint8).reshape(n, 16)
+    else:
+        pool = np.zeros(1, np.uint8)
+    arr = (_lib.FileEntry * max(n, 1)).from_address(rec.ctypes.data)
+    return arr, (rec, pool)
+
+
+def _entry_ptr(arr, i: int) -> ctypes.c_void_p:
+    return ctypes.c_void_p(ctypes.addressof(arr) + 96 * i)
 
 
 def _py_entry(c) -> FileEntry:
@@ -180,9 +208,11 @@ def parse_directory_block(buf: bytes) -> List[FileEntry]:
     return [_py_entry(arr[i]) for i in range(n.value)]
 
 
-def directory_block_ids(eng: Engine, dirs: Sequence[Sequence[FileEntry]]) -> List[bytes]:
+def directory_block_ids(eng: Engine, dirs: Sequence[Sequence[FileEntry]], with_blocks: bool = False):
     """storeDir's block id (store.go:230-231) for many directories at once, on
-    the device (one K6 launch)."""
+    the device (one K6 launch).  With ``with_blocks`` also returns each
+    directory's (dblk bytes, links)."""
+    L = _lib.load()
     flat = [e for d in dirs for e in d]
     arr, _keep = _c_entries(flat)
     counts = np.array([len(d) for d in dirs], np.uint32)
@@ -192,7 +222,20 @@ def directory_block_ids(eng: Engine, dirs: Sequence[Sequence[FileEntry]]) -> Lis
     ids = np.zeros((max(len(dirs), 1), 16), np.uint8)
     eng._check(eng._L.hbx_directory_block_ids(eng._ctx, len(dirs), arr, base.ctypes.data, counts.ctypes.data,
                                               ids.ctypes.data), "hbx_directory_block_ids")
-    return [bytes(r) for r in ids[:len(dirs)]]
+    out = [bytes(r) for r in ids[:len(dirs)]]
+    if not with_blocks:
+        return out
+    blocks = []
+    links = ctypes.create_string_buffer(16 * max(int(counts.max()) if len(dirs) else 1, 1))
+    used, nl = ctypes.c_uint64(), ctypes.c_uint32()
+    for d in range(len(dirs)):
+        p = _entry_ptr(arr, int(base[d]))
+        size = L.hbx_directory_block_size(p, int(counts[d]))
+        buf = ctypes.create_string_buffer(max(size, 1))
+        _check(L.hbx_directory_block_serialize(p, int(counts[d]), buf, size, ctypes.byref(used), links,
+                                               ctypes.byref(nl)), "hbx_directory_block_serialize")
+        blocks.append((buf.raw[:used.value], [links.raw[16 * i:16 * i + 16] for i in range(nl.value)]))
+    return out, blocks
 
 
 @dataclass
@@ -204,6 +247,7 @@ class TreeStore:
     directories: Dict[bytes, Tuple[bytes, List[bytes], bytes]] = field(default_factory=dict)  # path -> (dblk, links, id)
     files: Dict[bytes, FileChunks] = field(default_factory=dict)  # path -> chunks (FileSize > 0 only)
     skipped: List[bytes] = field(default_factory=list)
+    seconds: Dict[str, float] = field(default_factory=dict)  # walk, files, directories
 
 
 def store_tree(eng: Engine, root, reference_id: bytes = _ZERO16, io_threads: int = 16,
@@ -247,8 +291,10 @@ def store_tree(eng: Engine, root, reference_id: bytes = _ZERO16, io_threads: int
             file_entries[path] = entry
         return True
 
+    t0 = time.perf_counter()
     if not visit(root, out.root, st, 0):
         return out
+    t1 = time.perf_counter()
     paths = list(file_entries)
     if paths:
         res = eng.store_paths(paths, io_threads=io_threads, batch_bytes=batch_bytes)
@@ -256,6 +302,7 @@ def store_tree(eng: Engine, root, reference_id: bytes = _ZERO16, io_threads: int
             e = file_entries[p]
             e.content_type, e.content_block_id = r.content_type, r.content_id  # store.go:187-196
             out.files[p] = r
+    t2 = time.perf_counter()
     by_depth: Dict[int, List[bytes]] = {}
     for p, d in depth.items():
         by_depth.setdefault(d, []).append(p)
@@ -263,9 +310,9 @@ def store_tree(eng: Engine, root, reference_id: bytes = _ZERO16, io_threads: int
     dir_entry[root] = out.root
     for d in sorted(by_depth, reverse=True):
         level = by_depth[d]
-        ids = directory_block_ids(eng, [[e for _, e in dirs[p]] for p in level])
-        for p, i in zip(level, ids):
-            data, links = serialize_directory_block([e for _, e in dirs[p]])
+        ids, blocks = directory_block_ids(eng, [[e for _, e in dirs[p]] for p in level], with_blocks=True)
+        for p, i, (data, links) in zip(level, ids, blocks):
             out.directories[p] = (data, links, i)
             dir_entry[p].content_block_id = i
+    out.seconds = {"walk": t1 - t0, "files": t2 - t1, "directories": time.perf_counter() - t2}
     return out
