@@ -27,10 +27,11 @@ EXPORTS = [
     "hbx_file_entry_size", "hbx_file_entry_serialize", "hbx_file_entry_parse",
     "hbx_chain_block_serialize", "hbx_chain_block_parse", "hbx_directory_block_size",
     "hbx_directory_block_serialize", "hbx_directory_block_parse", "hbx_directory_block_ids",
+    "hbx_deflate_bound", "hbx_deflate_blocks_device", "hbx_deflate_blocks",
 ]
 # Functions returning something other than an int status.
 _NON_STATUS = ("hbx_ctx_destroy", "hbx_last_error", "hbx_max_chunks", "hbx_file_entry_size",
-               "hbx_directory_block_size")
+               "hbx_directory_block_size", "hbx_deflate_bound")
 
 
 class FileEntry(ctypes.Structure):
@@ -113,6 +114,10 @@ def load() -> ctypes.CDLL:
     L.hbx_directory_block_serialize.argtypes = [P, ctypes.c_uint32, P, U64, PU64, P, PU32]
     L.hbx_directory_block_parse.argtypes = [P, U64, P, ctypes.c_uint32, PU32]
     L.hbx_directory_block_ids.argtypes = [P, ctypes.c_uint32, P, P, P, P]
+    L.hbx_deflate_bound.argtypes = [U64]
+    L.hbx_deflate_bound.restype = U64
+    L.hbx_deflate_blocks_device.argtypes = [P, P, U64, P, P, P, P, P, P]
+    L.hbx_deflate_blocks.argtypes = [P, U64, P, P, P, P, P]
     for name in EXPORTS:
         if name not in _NON_STATUS:
             getattr(L, name).restype = I

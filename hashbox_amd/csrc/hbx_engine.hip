@@ -29,6 +29,7 @@
 
 #include "../../include/hbxgpu.h"
 #include "hbx_kernels.hip"
+#include "hbx_deflate.hip"
 #include "hbx_formats.h"
 
 namespace {
@@ -163,6 +164,7 @@ struct hbx_ctx {
   DevBuf d_msg;             // hbx_block_id message
   DevBuf d_plan;            // chain planner: global bin counts + cursors
   DevBuf d_vdesc, d_vlinks, d_vout, d_vexp, d_zeros;  // hbx_verify_blocks*
+  DevBuf d_zblk, d_zinfo, d_zoff, d_zlen, d_zout, d_zimg;  // hbx_deflate_blocks*
   PinBuf h_read[2];         // hbx_store_paths: pinned landing slots for file reads
   hipEvent_t h2d_done[2] = {nullptr, nullptr};  // slot's H2D copy has completed
   std::vector<DevBuf> d_ring;  // hbx_store_paths: device arenas of the batches in flight
@@ -680,7 +682,8 @@ void hbx_ctx_destroy(hbx_ctx* c) {
   for (DevBuf* b : {&c->d_ssum[0], &c->d_ssum[1], &c->d_order[0], &c->d_order[1], &c->d_order[2],
                     &c->d_octl[0], &c->d_octl[1], &c->d_octl[2],
                     &c->d_stage, &c->d_msg, &c->d_plan, &c->d_vdesc, &c->d_vlinks,
-                    &c->d_vout, &c->d_vexp, &c->d_zeros})
+                    &c->d_vout, &c->d_vexp, &c->d_zeros, &c->d_zblk, &c->d_zinfo, &c->d_zoff,
+                    &c->d_zlen, &c->d_zout, &c->d_zimg})
     b->release();
   for (PinBuf& h : c->h_read) h.release();
   for (DevBuf& d : c->d_ring) d.release();
@@ -1270,6 +1273,106 @@ int hbx_directory_block_ids(hbx_ctx* c, uint32_t n_dirs, const hbx_file_entry* e
   HBX_TRY(c, hipMemcpyAsync(arena, img.data(), total, hipMemcpyHostToDevice, c->stream));
   return verify_device(c, arena, n_dirs, offs.data(), lens.data(), links.data(), link_base.data(),
                        nls.data(), ids, nullptr, nullptr, nullptr);
+}
+
+// ---- zlib block compression (hbx_deflate.hip) -----------------
+uint64_t hbx_deflate_bound(uint64_t len) {
+  return 11ull + len + 5ull * ((len + hbxz::kSeg - 1) / hbxz::kSeg);
+}
+
+namespace {
+// K7a -> K7s -> K7b over n blocks at device addresses src[i] (len[i] bytes,
+// HBX_ARENA_SLACK readable after each) into device streams dst[i].
+int deflate_device(hbx_ctx* c, uint64_t n, const uint64_t* src, const uint64_t* lens, const uint64_t* dst,
+                   uint64_t* out_lens) {
+  if (n == 0) return HBX_OK;
+  if (n > 0xFFFFFFFFull) return c->fail(HBX_ERR_ARG, "too many blocks");
+  std::vector<hbxz::ZBlock> zb(n);
+  uint64_t nseg = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    const uint64_t ns = (lens[i] + hbxz::kSeg - 1) / hbxz::kSeg;
+    zb[i] = hbxz::ZBlock{src[i], dst[i], lens[i], (uint32_t)nseg, (uint32_t)ns};
+    nseg += ns;
+    if (nseg > 0x7FFFFFFFull) return c->fail(HBX_ERR_ARG, "too much data in one call");
+  }
+  hipStream_t s = c->stream;
+  HBX_TRY(c, c->d_zblk.ensure(n * sizeof(hbxz::ZBlock)));
+  HBX_TRY(c, c->d_zinfo.ensure(std::max<uint64_t>(nseg, 1) * sizeof(hbxz::SegInfo)));
+  HBX_TRY(c, c->d_zoff.ensure(std::max<uint64_t>(nseg, 1) * 8));
+  HBX_TRY(c, c->d_zlen.ensure(n * 8));
+  HBX_TRY(c, c->d_zimg.ensure(std::max<uint64_t>(nseg, 1) * hbxz::kSlot));
+  HBX_TRY(c, hipMemcpyAsync(c->d_zblk.p, zb.data(), n * sizeof(hbxz::ZBlock), hipMemcpyHostToDevice, s));
+  const hbxz::ZBlock* dz = c->d_zblk.as<hbxz::ZBlock>();
+  if (nseg) {
+    hipLaunchKernelGGL(hbx_k7_deflate_size, dim3((uint32_t)nseg), dim3(hbxz::kThreads), 0, s, dz, (uint32_t)n,
+                       (uint32_t)nseg, c->d_zinfo.as<hbxz::SegInfo>(), c->d_zimg.as<uint32_t>());
+    HBX_TRY(c, hipGetLastError());
+  }
+  hipLaunchKernelGGL(hbx_k7_deflate_plan, dim3((uint32_t)n), dim3(64), 0, s, dz, (uint32_t)n,
+                     c->d_zinfo.as<hbxz::SegInfo>(), c->d_zoff.as<uint64_t>(), c->d_zlen.as<uint64_t>());
+  HBX_TRY(c, hipGetLastError());
+  if (nseg) {
+    hipLaunchKernelGGL(hbx_k7_deflate_write, dim3((uint32_t)nseg), dim3(hbxz::kThreads), 0, s, (uint32_t)nseg,
+                       c->d_zinfo.as<hbxz::SegInfo>(), c->d_zimg.as<uint32_t>(), c->d_zoff.as<uint64_t>());
+    HBX_TRY(c, hipGetLastError());
+  }
+  HBX_TRY(c, hipMemcpyAsync(out_lens, c->d_zlen.p, n * 8, hipMemcpyDeviceToHost, s));
+  HBX_TRY(c, hipStreamSynchronize(s));
+  return HBX_OK;
+}
+}  // namespace
+
+int hbx_deflate_blocks_device(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* offs,
+                              const uint64_t* lens, void* d_out, const uint64_t* out_offs,
+                              const uint64_t* out_caps, uint64_t* out_lens) {
+  if (!c || (n && (!d_arena || !offs || !lens || !d_out || !out_offs || !out_caps || !out_lens)))
+    return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
+  HBX_TRY(c, hipSetDevice(c->device));
+  std::vector<uint64_t> src(n), dst(n);
+  for (uint64_t i = 0; i < n; i++) {
+    if (out_caps[i] < hbx_deflate_bound(lens[i]))
+      return c->fail(HBX_ERR_CAPACITY, "output capacity below hbx_deflate_bound for block " + std::to_string(i));
+    src[i] = reinterpret_cast<uint64_t>(d_arena) + offs[i];
+    dst[i] = reinterpret_cast<uint64_t>(d_out) + out_offs[i];
+  }
+  return deflate_device(c, n, src.data(), lens, dst.data(), out_lens);
+}
+
+int hbx_deflate_blocks(hbx_ctx* c, uint64_t n, const uint8_t* const* datas, const uint64_t* lens,
+                       uint8_t* const* outs, const uint64_t* caps, uint64_t* out_lens) {
+  if (!c || (n && (!datas || !lens || !outs || !caps || !out_lens))) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
+  if (n == 0) return HBX_OK;
+  HBX_TRY(c, hipSetDevice(c->device));
+  std::vector<uint64_t> soff(n), doff(n), src(n), dst(n);
+  uint64_t sin = 0, sout = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    if (lens[i] && !datas[i]) return c->fail(HBX_ERR_ARG, "null block data");
+    if (caps[i] < hbx_deflate_bound(lens[i]))
+      return c->fail(HBX_ERR_CAPACITY, "output capacity below hbx_deflate_bound for block " + std::to_string(i));
+    soff[i] = sin;
+    sin += (lens[i] + 255) & ~uint64_t(255);
+    doff[i] = sout;
+    sout += (hbx_deflate_bound(lens[i]) + 15) & ~uint64_t(15);
+  }
+  HBX_TRY(c, c->d_stage.ensure(sin + 65536));
+  HBX_TRY(c, c->d_zout.ensure(sout + 64));
+  uint8_t* arena = c->d_stage.as<uint8_t>();
+  uint8_t* zo = c->d_zout.as<uint8_t>();
+  for (uint64_t i = 0; i < n; i++) {
+    if (lens[i]) HBX_TRY(c, hipMemcpyAsync(arena + soff[i], datas[i], lens[i], hipMemcpyHostToDevice, c->stream));
+    src[i] = reinterpret_cast<uint64_t>(arena + soff[i]);
+    dst[i] = reinterpret_cast<uint64_t>(zo + doff[i]);
+  }
+  const int rc = deflate_device(c, n, src.data(), lens, dst.data(), out_lens);
+  if (rc) return rc;
+  std::vector<uint8_t> host(sout);
+  HBX_TRY(c, hipMemcpy(host.data(), zo, sout, hipMemcpyDeviceToHost));
+  for (uint64_t i = 0; i < n; i++) std::memcpy(outs[i], host.data() + doff[i], out_lens[i]);
+  return HBX_OK;
 }
 
 }  // extern "C"

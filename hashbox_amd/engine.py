@@ -284,6 +284,42 @@ class Engine:
         return self._verify(self._L.hbx_verify_blocks_device,
                             (ctypes.c_void_p(int(d_arena)), n, _p(offs), _p(lens)), n, links, expect)
 
+    def deflate_bound(self, n: int) -> int:
+        """Largest zlib stream hbx_deflate_blocks* produces for n bytes."""
+        return int(self._L.hbx_deflate_bound(int(n)))
+
+    def deflate_blocks(self, blocks: Sequence[BytesLike]) -> List[bytes]:
+        """HashboxBlock.CompressData (pkg/core/block.go:133-150, 176-184) for
+        many blocks at once: one zlib stream per block, coded on the device."""
+        arrs = [_u8(b) for b in blocks]
+        n = len(arrs)
+        if n == 0:
+            return []
+        lens = np.array([a.size for a in arrs], np.uint64)
+        caps = np.array([self.deflate_bound(int(x)) for x in lens], np.uint64)
+        outs = [np.empty(int(c), np.uint8) for c in caps]
+        dptr = (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrs])
+        optr = (ctypes.c_void_p * n)(*[o.ctypes.data for o in outs])
+        olen = np.zeros(n, np.uint64)
+        self._check(self._L.hbx_deflate_blocks(self._ctx, n, dptr, _p(lens), optr, _p(caps), _p(olen)),
+                    "hbx_deflate_blocks")
+        return [o[:int(k)].tobytes() for o, k in zip(outs, olen)]
+
+    def deflate_blocks_device(self, d_arena: int, offs: Sequence[int], lens: Sequence[int], d_out: int,
+                              out_offs: Sequence[int], out_caps: Sequence[int]) -> np.ndarray:
+        """Device form: block i = d_arena[offs[i] ..+lens[i]) -> zlib stream at
+        d_out[out_offs[i] ..]; returns the stream lengths."""
+        _sync_producer()
+        offs = np.ascontiguousarray(offs, np.uint64)
+        lens = np.ascontiguousarray(lens, np.uint64)
+        oo = np.ascontiguousarray(out_offs, np.uint64)
+        oc = np.ascontiguousarray(out_caps, np.uint64)
+        olen = np.zeros(max(lens.size, 1), np.uint64)
+        self._check(self._L.hbx_deflate_blocks_device(self._ctx, ctypes.c_void_p(int(d_arena)), lens.size,
+                                                      _p(offs), _p(lens), ctypes.c_void_p(int(d_out)), _p(oo),
+                                                      _p(oc), _p(olen)), "hbx_deflate_blocks_device")
+        return olen[:lens.size]
+
     def memcpy_h2d_async(self, d_dst: int, h_src: int, nbytes: int):
         """Enqueue an H2D copy on this engine's stream (pinned source)."""
         self._check(self._L.hbx_memcpy_h2d_async(self._ctx, ctypes.c_void_p(int(d_dst)),

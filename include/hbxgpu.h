@@ -24,6 +24,7 @@
  *   hbx_file_entry_*,     FileEntry / FileChainBlock / DirectoryBlock
  *   hbx_chain_block_*,    Serialize + Unserialize (hashback/hashback.go:80-214)
  *   hbx_directory_block_* and storeDir's block id (store.go:201-234)
+ *   hbx_deflate_blocks    HashboxBlock.CompressData, zlib (block.go:133-184)
  *
  * Conventions
  *   - Every function returns an int status: 0 = OK, negative = error
@@ -258,6 +259,30 @@ int hbx_directory_block_parse(const uint8_t *in, uint64_t len, hbx_file_entry *e
  * batches are pending. */
 int hbx_directory_block_ids(hbx_ctx *ctx, uint32_t n_dirs, const hbx_file_entry *entries,
                             const uint64_t *entry_base, const uint32_t *n_entries, uint8_t *ids);
+
+/* ---- zlib block compression ---------------------------------
+ * HashboxBlock.CompressData for BlockDataTypeZlib (pkg/core/block.go:133-150,
+ * 176-184; done by the client's workers before sending, client.go:249-258):
+ * each block's data becomes one zlib stream (RFC 1950: 78 9C header, deflate
+ * blocks, Adler-32).  Not byte-identical to Go's compress/zlib (the server
+ * inflates and re-hashes, block.go:159-166; DataType is not hashed,
+ * block.go:101) but every stream inflates to the block's data.  Each 32 KiB
+ * segment is coded independently on the device (LZ77 within the segment +
+ * fixed Huffman, or stored when that is not smaller), so any output is at
+ * most hbx_deflate_bound(len) bytes. */
+uint64_t hbx_deflate_bound(uint64_t len);
+/* Blocks in device memory: block i = d_arena[offs[i] .. +lens[i]) (followed
+ * by HBX_ARENA_SLACK readable bytes); its stream goes to d_out[out_offs[i] ..]
+ * (out_caps[i] >= hbx_deflate_bound(lens[i]), else HBX_ERR_CAPACITY), its
+ * length to out_lens[i] (host).  Synchronous.  Refused (HBX_ERR_STATE) while
+ * batches are pending. */
+int hbx_deflate_blocks_device(hbx_ctx *ctx, const void *d_arena, uint64_t n, const uint64_t *offs,
+                              const uint64_t *lens, void *d_out, const uint64_t *out_offs,
+                              const uint64_t *out_caps, uint64_t *out_lens);
+/* The same for host blocks: datas[i] (lens[i] bytes) -> outs[i] (caps[i]
+ * bytes), out_lens[i] = stream length. */
+int hbx_deflate_blocks(hbx_ctx *ctx, uint64_t n, const uint8_t *const *datas, const uint64_t *lens,
+                       uint8_t *const *outs, const uint64_t *caps, uint64_t *out_lens);
 
 /* Device arena helpers (allocations include HBX_ARENA_SLACK). */
 int hbx_arena_alloc(hbx_ctx *ctx, uint64_t bytes, void **d_ptr);

@@ -55,3 +55,25 @@ def test_no_cpu_fallback_in_product():
             if fn.endswith((".py", ".hip", ".h", ".cpp")):
                 txt = open(os.path.join(dirpath, fn)).read()
                 assert "oracle" not in txt.lower().replace("oracle-", ""), fn
+
+
+def test_deflate_bound_host_only():
+    from hashbox_amd import _lib
+    L = _lib.load()
+    assert L.hbx_deflate_bound(0) == 11
+    assert L.hbx_deflate_bound(1) == 17
+    assert L.hbx_deflate_bound(32768) == 11 + 32768 + 5
+    assert L.hbx_deflate_bound(32769) == 11 + 32769 + 10
+
+
+def test_oracle_inflate_strict_rejects_truncation():
+    import zlib
+    from oracle import deflate as OD
+    z = zlib.compress(b"hello world" * 100)
+    assert OD.inflate_strict(z) == b"hello world" * 100
+    for bad in (z[:-1], z + b"\0", z[:5]):
+        try:
+            OD.inflate_strict(bad)
+        except (ValueError, zlib.error):
+            continue
+        raise AssertionError("accepted a bad stream")

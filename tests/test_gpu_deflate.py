@@ -1,0 +1,109 @@
+"""GPU: zlib block compression on the device (hbx_deflate_blocks*, kernels
+K7a/K7s/K7b; HashboxBlock.CompressData, pkg/core/block.go:133-184).
+
+Parity bar for this path (the output need not be bit-identical,
+the server inflates and re-hashes, block.go:159-166): every stream must be a
+complete RFC 1950 stream that inflates to exactly the block's data with a
+correct Adler-32 (checked by CPython's zlib, oracle/deflate.py), within
+hbx_deflate_bound.  Compression must also be real on compressible data.
+"""
+import numpy as np
+import pytest
+
+from oracle import deflate as OD
+
+pytestmark = pytest.mark.gpu
+
+
+def _text(n, seed):
+    rng = np.random.default_rng(seed)
+    words = [bytes(rng.integers(97, 123, int(k), dtype=np.uint8)) for k in rng.integers(2, 10, 400)]
+    out = bytearray()
+    while len(out) < n:
+        out += words[int(rng.zipf(1.3)) % len(words)] + b" "
+    return bytes(out[:n])
+
+
+def _check(engine, blocks):
+    outs = engine.deflate_blocks(blocks)
+    assert len(outs) == len(blocks)
+    for b, z in zip(blocks, outs):
+        assert z[:2] == b"\x78\x9c"
+        assert len(z) <= engine.deflate_bound(len(b))
+        assert OD.inflate_strict(z) == bytes(b)
+    return outs
+
+
+@pytest.mark.parametrize("n", [0, 1, 3, 4, 5, 127, 128, 129, 1000, 32767, 32768, 32769, 65536, 100_001])
+def test_edge_lengths_random_text_zero(engine, n):
+    rng = np.random.default_rng(n)
+    _check(engine, [rng.integers(0, 256, n, dtype=np.uint8).tobytes(), _text(n, n), bytes(n), b"ab" * (n // 2)])
+
+
+def test_random_is_stored_and_text_compresses(engine):
+    rng = np.random.default_rng(1)
+    rnd = rng.integers(0, 256, 3 << 20, dtype=np.uint8).tobytes()
+    txt = _text(3 << 20, 2)
+    zr, zt, zz = _check(engine, [rnd, txt, bytes(1 << 20)])
+    assert len(zr) == len(rnd) + 5 * (len(rnd) // 32768) + 11  # all stored: +5 B per 32 KiB segment
+    ref = len(OD.compress_ref(txt))
+    assert len(zt) < 0.75 * len(txt), (len(zt), len(txt))
+    assert len(zt) < 1.7 * ref, (len(zt), ref)  # fixed Huffman, 32 KiB segments vs zlib -6
+    assert len(zz) < (1 << 20) // 16  # >= one match token per 64-byte parse range
+
+
+def test_mixed_batch(engine):
+    rng = np.random.default_rng(7)
+    blocks = []
+    for i in range(400):
+        n = int(rng.choice([0, 1, 17, 4096, 16384, 40000, 70000, 200000]))
+        kind = i % 4
+        if kind == 0:
+            blocks.append(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+        elif kind == 1:
+            blocks.append(_text(n, i))
+        elif kind == 2:
+            blocks.append(bytes([i & 255]) * n)
+        else:
+            per = rng.integers(0, 256, 37, dtype=np.uint8).tobytes()
+            blocks.append((per * (n // 37 + 1))[:n])
+    _check(engine, blocks)
+
+
+def test_device_odd_offsets(engine):
+    import torch
+    rng = np.random.default_rng(9)
+    datas = [_text(50_000, 1), rng.integers(0, 256, 70_000, dtype=np.uint8).tobytes(), bytes(33_333), b"x"]
+    offs, pos = [], 3
+    for d in datas:  # inputs at odd byte offsets, as chunks inside a file are
+        offs.append(pos)
+        pos += len(d) + 7
+    host = np.zeros(pos + 64, np.uint8)
+    for o, d in zip(offs, datas):
+        host[o:o + len(d)] = np.frombuffer(d, np.uint8)
+    src = torch.from_numpy(host).to("cuda:0")
+    caps = [engine.deflate_bound(len(d)) for d in datas]
+    out_offs, q = [], 1
+    for c in caps:  # outputs at odd offsets too
+        out_offs.append(q)
+        q += c + 5
+    dst = torch.zeros(q + 64, dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()
+    lens = engine.deflate_blocks_device(src.data_ptr(), offs, [len(d) for d in datas], dst.data_ptr(), out_offs, caps)
+    out = dst.cpu().numpy()
+    for d, o, k in zip(datas, out_offs, lens):
+        assert OD.inflate_strict(out[o:o + int(k)].tobytes()) == d
+    # nothing written outside the streams
+    mask = np.ones(out.size, bool)
+    for o, k in zip(out_offs, lens):
+        mask[o:o + int(k)] = False
+    assert not out[mask].any()
+
+
+def test_capacity_refused(engine):
+    import torch
+    from hashbox_amd import HbxError
+    src = torch.zeros(1024, dtype=torch.uint8, device="cuda:0")
+    dst = torch.zeros(1024, dtype=torch.uint8, device="cuda:0")
+    with pytest.raises(HbxError):
+        engine.deflate_blocks_device(src.data_ptr(), [0], [900], dst.data_ptr(), [0], [900])

@@ -1,0 +1,123 @@
+#!/usr/bin/env python3
+"""Device zlib block compression (HashboxBlock.CompressData) on
+the chunks the engine cuts, device-resident:
+
+  random   the configs[1] batch: 64 x 128 MiB uniform random, every chunk
+  text     1 GiB of Zipf-distributed words (a 64 MiB generated text tiled),
+           every chunk
+
+Per corpus: device time of hbx_deflate_blocks_device (all chunks of the
+batch in one call: K7a + K7s + K7b), GB/s of input, compressed / input ratio,
+and beside it CPython zlib level 6 (Go's DefaultCompression stand-in,
+oracle/deflate.py) on 16 threads over a sample of the same chunks.  Every
+stream of a sample is inflated by the oracle and compared (round trip).
+
+Run on the GPU box: python tools/bench_deflate.py     (prints one JSON line)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+
+def text_corpus(nbytes, seed):
+    rng = np.random.default_rng(seed)
+    vocab = [bytes(rng.integers(97, 123, int(k), dtype=np.uint8)) for k in rng.integers(2, 11, 5000)]
+    ids = rng.zipf(1.2, 12_000_000) % len(vocab)
+    base = b" ".join(vocab[i] for i in ids)[: 64 << 20]
+    reps = (nbytes + len(base) - 1) // len(base)
+    return np.frombuffer((base * reps)[:nbytes], np.uint8)
+
+
+def run_corpus(eng, torch, name, host_or_dev, file_bytes, nfiles, sample, threads):
+    from oracle import deflate as OD
+    if isinstance(host_or_dev, np.ndarray):
+        arena = torch.empty(host_or_dev.size + 65536, dtype=torch.uint8, device="cuda:0")
+        arena[: host_or_dev.size].copy_(torch.from_numpy(host_or_dev))
+    else:
+        arena = host_or_dev
+    torch.cuda.synchronize()
+    offs = np.arange(nfiles, dtype=np.uint64) * np.uint64(file_bytes)
+    res = eng.chunk_hash_device(arena.data_ptr(), offs, [file_bytes] * nfiles)
+    c_off, c_len = [], []
+    for f, r in enumerate(res):
+        starts, ends = r.chunk_bounds()
+        c_off += list(offs[f] + starts)
+        c_len += list(ends - starts)
+    c_off = np.array(c_off, np.uint64)
+    c_len = np.array(c_len, np.uint64)
+    caps = np.array([eng.deflate_bound(int(n)) for n in c_len], np.uint64)
+    o_off = np.zeros_like(caps)
+    o_off[1:] = np.cumsum(caps[:-1])
+    out = torch.empty(int(caps.sum()) + 64, dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()
+    eng.deflate_blocks_device(arena.data_ptr(), c_off[:8], c_len[:8], out.data_ptr(), o_off[:8], caps[:8])  # warm-up
+    times = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        lens = eng.deflate_blocks_device(arena.data_ptr(), c_off, c_len, out.data_ptr(), o_off, caps)
+        times.append(time.perf_counter() - t0)
+    t = min(times)
+    total_in = int(c_len.sum())
+    total_out = int(lens.sum())
+    # round trip + CPU zlib -6 on a sample of chunks
+    rng = np.random.default_rng(3)
+    pick = np.sort(rng.choice(c_off.size, min(sample, c_off.size), replace=False))
+    host_in = arena[: int(offs[-1]) + file_bytes].cpu().numpy()
+    host_out = out.cpu().numpy()
+    blocks = [host_in[int(c_off[i]): int(c_off[i] + c_len[i])].tobytes() for i in pick]
+    bad = 0
+    for i, b in zip(pick, blocks):
+        z = host_out[int(o_off[i]): int(o_off[i] + lens[i])].tobytes()
+        bad += OD.inflate_strict(z) != b
+    t0 = time.perf_counter()
+    ref = OD.compress_ref_mt(blocks, threads)
+    t_cpu = time.perf_counter() - t0
+    s_in = sum(len(b) for b in blocks)
+    s_gpu = sum(int(lens[i]) for i in pick)
+    return {
+        "chunks": int(c_off.size), "bytes_in": total_in, "bytes_out": total_out,
+        "ratio": round(total_out / total_in, 4), "seconds": round(t, 4),
+        "gbs": round(total_in / t / 1e9, 2), "gibs": round(total_in / t / 2**30, 2),
+        "sample_chunks": int(pick.size), "sample_roundtrip_mismatches": int(bad),
+        "sample_ratio_gpu": round(s_gpu / s_in, 4),
+        "cpu_zlib6": {"threads": threads, "ratio": round(sum(map(len, ref)) / s_in, 4),
+                      "gbs": round(s_in / t_cpu / 1e9, 3), "sample_bytes": s_in},
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--files", type=int, default=64)
+    ap.add_argument("--file-mib", type=int, default=128)
+    ap.add_argument("--sample", type=int, default=64)
+    ap.add_argument("--threads", type=int, default=16)
+    a = ap.parse_args()
+    import torch
+    from hashbox_amd import Engine
+    fb = a.file_mib << 20
+    eng = Engine(0)
+    out = {"workload": "device zlib (K7) over every chunk of a batch, device-resident"}
+    try:
+        g = torch.Generator(device="cuda:0")
+        g.manual_seed(1)
+        arena = torch.empty(a.files * fb + 65536, dtype=torch.uint8, device="cuda:0")
+        arena.random_(0, 256, generator=g)
+        out["random"] = run_corpus(eng, torch, "random", arena, fb, a.files, a.sample, a.threads)
+        del arena
+        torch.cuda.empty_cache()
+        txt = text_corpus(8 * fb, 5)
+        out["text"] = run_corpus(eng, torch, "text", txt, fb, 8, a.sample, a.threads)
+    finally:
+        eng.close()
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
