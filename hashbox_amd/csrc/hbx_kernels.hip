@@ -117,7 +117,7 @@ __device__ __forceinline__ uint32_t digest_pass_sdwa(const uint32_t (&in)[16],
         DA = (e_l + 4u * k + B < lim) ? DA : 0u;                    \
         DB = (e_l + 32u + 4u * k + B < lim) ? DB : 0u;              \
       }                                                             \
-      M = max(M, max(DA, DB));                                      \
+      asm("v_max3_u32 %0, %0, %1, %2" : "+v"(M) : "v"(DA), "v"(DB)); \
     }
     HBX_SDWA_PAIR(0) HBX_SDWA_PAIR(1) HBX_SDWA_PAIR(2) HBX_SDWA_PAIR(3)
 #undef HBX_SDWA_PAIR
@@ -369,8 +369,10 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_d
 
   issue(0u, lds0);
   issue(1u, lds1);  // past the tile end: out-of-range reads land zeros, never read
-  uint32_t cur[16];
-  for (uint32_t it = 0; it < n_it; it++) {
+  // two register sets swap roles each iteration (this run / the run MIN
+  // earlier), so no 16-register copy per iteration
+  uint32_t run_b[16];
+  auto step = [&](uint32_t it, uint32_t (&cur)[16], const uint32_t (&prev)[16]) {
     // outstanding, oldest first: DMA(it), store(it-2), DMA(it+1), store(it-1)
     if (it == 0)
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -383,11 +385,13 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_d
     issue(it + 2u, (it & 1u) ? lds1 : lds0);
     const uint64_t qs = q0 + (uint64_t)it * kMinBlock;
     uint32_t smax, sprev;
-    k1_iteration(cur, out, st, wtot, it, w, l, e_l, qs, N, smax, sprev);
+    k1_iteration(cur, prev, st, wtot, it, w, l, e_l, qs, N, smax, sprev);
     const bool ok = qs + (uint64_t)w * kSlice < N;
     k1_store_slice(ssum, ok ? sb + ((qs >> kSliceShift) + w) : dummy, l, smax, sprev);
-#pragma unroll
-    for (int k = 0; k < 16; k++) out[k] = cur[k];
+  };
+  for (uint32_t it = 0; it < n_it; it += 2u) {
+    step(it, run_b, out);
+    if (it + 1u < n_it) step(it + 1u, out, run_b);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup exits
 }
