@@ -101,11 +101,38 @@ __device__ __forceinline__ uint32_t digest_pass(const uint32_t (&in)[16], const 
       : "+v"(X)                                                                               \
       : "v"(IN), "v"(OUT))
 
+// Four positions (one dword of each stream) plus the running max, in ONE
+// asm block: the compiler pads the boundary between two inline-asm blocks
+// with an s_nop whenever the second reads a register the first wrote, which
+// cost one issue slot per position pair with a block per position.  The two
+// streams' ops are interleaved (independent neighbours).
+#define HBX_SDWA_POS(B)                                                                    \
+  "v_add_u16_sdwa %0, %0, %3 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 "   \
+  "src1_sel:BYTE_" #B "\n\t"                                                              \
+  "v_add_u16_sdwa %1, %1, %5 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 "   \
+  "src1_sel:BYTE_" #B "\n\t"                                                              \
+  "v_sub_u16_sdwa %0, %0, %4 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 "   \
+  "src1_sel:BYTE_" #B "\n\t"                                                              \
+  "v_sub_u16_sdwa %1, %1, %6 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 "   \
+  "src1_sel:BYTE_" #B "\n\t"                                                              \
+  "v_lshl_add_u32 %0, %0, 16, %0\n\t"                                                     \
+  "v_lshl_add_u32 %1, %1, 16, %1\n\t"                                                     \
+  "v_max3_u32 %2, %2, %0, %1\n\t"
+#define HBX_SDWA_DWORD(XA, XB, M, INA, OUTA, INB, OUTB)                              \
+  asm(HBX_SDWA_POS(0) HBX_SDWA_POS(1) HBX_SDWA_POS(2) HBX_SDWA_POS(3)               \
+      : "+v"(XA), "+v"(XB), "+v"(M)                                                  \
+      : "v"(INA), "v"(OUTA), "v"(INB), "v"(OUTB))
+
 template <bool TAIL>
 __device__ __forceinline__ uint32_t digest_pass_sdwa(const uint32_t (&in)[16],
                                                      const uint32_t (&out)[16], uint32_t XA,
                                                      uint32_t XB, uint32_t e_l, uint32_t lim) {
   uint32_t M = 0;
+  if (!TAIL) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) HBX_SDWA_DWORD(XA, XB, M, in[k], out[k], in[8 + k], out[8 + k]);
+    return M;
+  }
 #pragma unroll
   for (int k = 0; k < 8; k++) {
 #define HBX_SDWA_PAIR(B)                                            \
@@ -113,10 +140,8 @@ __device__ __forceinline__ uint32_t digest_pass_sdwa(const uint32_t (&in)[16],
       HBX_SDWA_STEP(XA, in[k], out[k], B);                          \
       HBX_SDWA_STEP(XB, in[8 + k], out[8 + k], B);                  \
       uint32_t DA = XA, DB = XB;                                    \
-      if (TAIL) {                                                   \
-        DA = (e_l + 4u * k + B < lim) ? DA : 0u;                    \
-        DB = (e_l + 32u + 4u * k + B < lim) ? DB : 0u;              \
-      }                                                             \
+      DA = (e_l + 4u * k + B < lim) ? DA : 0u;                      \
+      DB = (e_l + 32u + 4u * k + B < lim) ? DB : 0u;                \
       asm("v_max3_u32 %0, %0, %1, %2" : "+v"(M) : "v"(DA), "v"(DB)); \
     }
     HBX_SDWA_PAIR(0) HBX_SDWA_PAIR(1) HBX_SDWA_PAIR(2) HBX_SDWA_PAIR(3)
