@@ -70,7 +70,7 @@ constexpr uint32_t kLazy = 32;  // no look-ahead past a match this long
 
 struct SegInfo {
   uint32_t bytes;  // coded bytes of the segment (stored or fixed image)
-  uint32_t mode;   // 0 stored, 1 fixed Huffman
+  uint32_t mode;   // 0 stored, 1 fixed Huffman, 2 dynamic Huffman
   uint32_t a, b;   // Adler partials: sum x, sum (n - j) x_j  (mod 65521)
 };
 
@@ -175,15 +175,47 @@ __device__ __forceinline__ uint32_t match_len(const uint32_t* data, uint32_t sh,
   return min(len, limit);
 }
 
-// Steps 2/3: thread t's parse of [128t, 128t+128) ∩ [0, n) with the
-// candidate distances `cd` (0 = none).  EMIT = false counts bits; EMIT = true
-// ORs them into `img` from bit offset o.
-template <bool EMIT>
-__device__ __forceinline__ uint32_t parse_range(const uint32_t* data, const uint16_t* cd, uint32_t* img,
-                                                uint32_t sh, uint32_t n, uint32_t o) {
+// Length and distance symbols (RFC 1951 §3.2.5): symbol, extra-bit count,
+// extra-bit value.
+__device__ __forceinline__ void len_sym(uint32_t len, uint32_t& sym, uint32_t& ne, uint32_t& ex) {
+  ne = 0u;
+  ex = 0u;
+  if (len <= 10u) {
+    sym = 254u + len;
+  } else if (len == 258u) {
+    sym = 285u;
+  } else {
+    const uint32_t l = len - 3u;
+    ne = 31u - __builtin_clz(l) - 2u;
+    sym = 257u + 4u * (ne + 1u) + ((l >> ne) & 3u);
+    ex = l & ((1u << ne) - 1u);
+  }
+}
+__device__ __forceinline__ void dist_sym(uint32_t dist, uint32_t& sym, uint32_t& ne, uint32_t& ex) {
+  const uint32_t d = dist - 1u;
+  ne = 0u;
+  ex = 0u;
+  if (d < 4u) {
+    sym = d;
+  } else {
+    ne = 31u - __builtin_clz(d) - 1u;
+    sym = 2u * (ne + 1u) + ((d >> ne) & 1u);
+    ex = d & ((1u << ne) - 1u);
+  }
+}
+
+// Step 2: thread t's greedy parse of [64t, 64t+64) ∩ [0, n) with the
+// candidate distances in `cd`, one-step lazy.  The tokens overwrite the
+// candidate slots they cover (already consumed): a literal at p is
+// 0x8000 | byte in slot p; a match is len in slot p and dist in slot p+1.
+// Symbol frequencies go to hll/hd; returns the fixed-code bits, `extra` the
+// extra bits (the same under any code).
+__device__ __forceinline__ uint32_t tokenize(const uint32_t* data, uint16_t* cd, uint32_t* hll, uint32_t* hd,
+                                             uint32_t sh, uint32_t n, uint32_t& extra) {
   const uint32_t r0 = threadIdx.x * kSub;
   const uint32_t end = min(r0 + kSub, n);
   uint32_t bits = 0u, p = r0, len = 0u, d = 0u;
+  extra = 0u;
   bool have = false;  // (len, d) already hold the match at p
   while (p < end) {
     if (!have) {
@@ -191,35 +223,151 @@ __device__ __forceinline__ uint32_t parse_range(const uint32_t* data, const uint
       len = d ? match_len(data, sh, p, p - d, min(258u, end - p)) : 0u;
     }
     have = false;
-    uint32_t v, nb, step;
     bool defer = false;
+    uint32_t len1 = 0u, d1 = 0u;
     if (len >= 4u && len < kLazy && p + 1u < end) {
-      const uint32_t d1 = cd[cphys(p + 1u)];
-      const uint32_t len1 = d1 ? match_len(data, sh, p + 1u, p + 1u - d1, min(258u, end - p - 1u)) : 0u;
-      if (len1 > len) {  // lazy: p becomes a literal, the longer match starts at p + 1
-        defer = true;
+      d1 = cd[cphys(p + 1u)];
+      len1 = d1 ? match_len(data, sh, p + 1u, p + 1u - d1, min(258u, end - p - 1u)) : 0u;
+      defer = len1 > len;  // lazy: p becomes a literal, the longer match starts at p + 1
+    }
+    if (len >= 4u && !defer) {
+      uint32_t v, nb, sym, ne, ex, ds, dne, dex;
+      match_code(len, d, v, nb);
+      len_sym(len, sym, ne, ex);
+      dist_sym(d, ds, dne, dex);
+      atomicAdd(&hll[sym], 1u);
+      atomicAdd(&hd[ds], 1u);
+      extra += ne + dne;
+      bits += nb;
+      cd[cphys(p)] = (uint16_t)len;
+      cd[cphys(p + 1u)] = (uint16_t)d;
+      p += len;
+    } else {
+      const uint32_t b = seg4(data, p + sh) & 0xFFu;
+      atomicAdd(&hll[b], 1u);
+      bits += b < 144u ? 8u : 9u;
+      cd[cphys(p)] = (uint16_t)(0x8000u | b);
+      p += 1u;
+      if (defer) {
         len = len1;
         d = d1;
         have = true;
       }
     }
-    if (len >= 4u && !defer) {
-      match_code(len, d, v, nb);
-      step = len;
-    } else {
-      lit_code(seg4(data, p + sh) & 0xFFu, v, nb);
-      step = 1u;
-    }
-    if (EMIT) {
-      const uint32_t w = o >> 5, s = o & 31u;
-      atomicOr(&img[w], v << s);
-      if (s + nb > 32u) atomicOr(&img[w + 1u], v >> (32u - s));
-      o += nb;
-    }
-    bits += nb;
-    p += step;
   }
   return bits;
+}
+
+__device__ __forceinline__ void emit_bits(uint32_t* img, uint32_t& o, uint32_t v, uint32_t nb) {
+  const uint32_t w = o >> 5, s = o & 31u;
+  atomicOr(&img[w], v << s);
+  if (s + nb > 32u) atomicOr(&img[w + 1u], v >> (32u - s));
+  o += nb;
+}
+
+// Step 3: walk thread t's tokens with the code tables (entry = reversed code
+// | length << 16); EMIT = false returns their bits, EMIT = true writes them.
+template <bool EMIT>
+__device__ __forceinline__ uint32_t walk_tokens(const uint16_t* cd, const uint32_t* llc, const uint32_t* dcc,
+                                                uint32_t* img, uint32_t n, uint32_t o) {
+  const uint32_t r0 = threadIdx.x * kSub;
+  const uint32_t end = min(r0 + kSub, n);
+  uint32_t bits = 0u;
+  for (uint32_t p = r0; p < end;) {
+    const uint32_t v = cd[cphys(p)];
+    if (v & 0x8000u) {
+      const uint32_t e = llc[v & 0xFFu];
+      if (EMIT) emit_bits(img, o, e & 0xFFFFu, e >> 16);
+      bits += e >> 16;
+      p += 1u;
+    } else {
+      const uint32_t dist = cd[cphys(p + 1u)];
+      uint32_t sym, ne, ex, ds, dne, dex;
+      len_sym(v, sym, ne, ex);
+      dist_sym(dist, ds, dne, dex);
+      const uint32_t e = llc[sym], f = dcc[ds];
+      const uint32_t nl = (e >> 16) + ne, nd = (f >> 16) + dne;
+      if (EMIT) {
+        emit_bits(img, o, (e & 0xFFFFu) | (ex << (e >> 16)), nl);
+        emit_bits(img, o, (f & 0xFFFFu) | (dex << (f >> 16)), nd);
+      }
+      bits += nl + nd;
+      p += v;
+    }
+  }
+  return bits;
+}
+
+// ---- dynamic Huffman codes (RFC 1951 §3.2.7), built by one thread ----------
+// keys[0..m): (freq << 9 | symbol), ascending.  Code lengths <= limit into
+// lens[symbol] (a length-limited code by halving the frequencies until the
+// Huffman tree is shallow enough: always a complete code).  w, par, dep:
+// scratch of 2m entries.
+__device__ void huff_lengths(const uint32_t* keys, uint32_t m, uint32_t limit, uint8_t* lens, uint32_t* w,
+                             uint16_t* par, uint8_t* dep) {
+  if (m == 1u) {
+    lens[keys[0] & 511u] = 1u;
+    return;
+  }
+  for (uint32_t shift = 0;; shift++) {
+    for (uint32_t i = 0; i < m; i++) w[i] = ((keys[i] >> 9) >> shift) | 1u;
+    uint32_t i = 0, j = m;
+    for (uint32_t k = m; k < 2u * m - 1u; k++) {
+      uint32_t a, b;
+      if (i < m && (j >= k || w[i] <= w[j])) a = i++; else a = j++;
+      if (i < m && (j >= k || w[i] <= w[j])) b = i++; else b = j++;
+      w[k] = w[a] + w[b];
+      par[a] = (uint16_t)k;
+      par[b] = (uint16_t)k;
+    }
+    dep[2u * m - 2u] = 0u;
+    uint32_t maxd = 0u;
+    for (int x = (int)(2u * m) - 3; x >= 0; x--) {
+      dep[x] = (uint8_t)(dep[par[x]] + 1u);
+      if ((uint32_t)x < m && dep[x] > maxd) maxd = dep[x];
+    }
+    if (maxd <= limit) break;
+  }
+  for (uint32_t i = 0; i < m; i++) lens[keys[i] & 511u] = dep[i];
+}
+
+// Canonical codes (RFC 1951 §3.2.2) as reversed code | length << 16.
+__device__ void canon_codes(const uint8_t* lens, uint32_t nsym, uint32_t* out, uint32_t* blc) {
+  for (uint32_t b = 0; b < 16u; b++) blc[b] = 0u;
+  for (uint32_t s = 0; s < nsym; s++) blc[lens[s]]++;
+  blc[0] = 0u;
+  uint32_t code = 0u, next[16];
+  next[0] = 0u;
+#pragma unroll
+  for (uint32_t b = 1; b < 16u; b++) {
+    code = (code + blc[b - 1u]) << 1;
+    next[b] = code;
+  }
+#pragma unroll
+  for (uint32_t b = 0; b < 16u; b++) blc[b] = next[b];
+  for (uint32_t s = 0; s < nsym; s++) {
+    const uint32_t l = lens[s];
+    out[s] = l ? (rev(blc[l]++, l) | (l << 16)) : 0u;
+  }
+}
+
+// Order of the code-length code lengths in the header (RFC 1951 §3.2.7).
+__device__ const uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+// Serial insertion sort of the nonzero frequencies of f[0..nsym) into keys.
+__device__ uint32_t sort_small(const uint32_t* f, uint32_t nsym, uint32_t* keys) {
+  uint32_t m = 0u;
+  for (uint32_t s = 0; s < nsym; s++) {
+    if (!f[s]) continue;
+    const uint32_t key = (f[s] << 9) | s;
+    uint32_t j = m++;
+    while (j > 0u && keys[j - 1u] > key) {
+      keys[j] = keys[j - 1u];
+      j--;
+    }
+    keys[j] = key;
+  }
+  return m;
 }
 
 // Inclusive prefix sum over the workgroup; `tot` = the total.
@@ -264,6 +412,8 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
   __shared__ uint16_t cd[kCdPhys];
   __shared__ uint32_t wsum[kWaves];
   __shared__ unsigned long long wadler[2 * kWaves];
+  __shared__ uint32_t hll[288], hd[32], llc[288], dcc[32], rle[320], clf[19], clc[19], zpar[8];
+  __shared__ uint8_t zl[320], cll[20];
   const uint32_t g = blockIdx.x;
   if (g >= nseg) return;
   const ZBlock bk = blocks[zblock_of(blocks, nb, g)];
@@ -274,6 +424,8 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
   uint32_t sh;
   load_segment(data, reinterpret_cast<const uint8_t*>(bk.src) + off, n, sh);
   for (uint32_t k = t; k < kTabWords; k += kThreads) tab[k] = 0u;
+  for (uint32_t k = t; k < 288u; k += kThreads) hll[k] = k == 256u ? 1u : 0u;  // EOB once
+  for (uint32_t k = t; k < 32u; k += kThreads) hd[k] = 0u;
   __syncthreads();
 
   // 1. candidates in position order + Adler partials
@@ -311,31 +463,201 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
     __syncthreads();
   }
 
-  // 2. count
-  const uint32_t bits = parse_range<false>(data, cd, nullptr, sh, n, 0u);
-  uint32_t tb;
-  const uint32_t incl = wg_incl_sum(bits, wsum, tb);
-  const uint32_t total_bits = 3u + tb + 7u + 3u;  // header, tokens, EOB, empty stored header
-  const uint32_t fixed_bytes = ((total_bits + 7u) >> 3) + 4u;
+  // 2. tokens, symbol frequencies, fixed-code size
+  uint32_t extra;
+  const uint32_t fbits = tokenize(data, cd, hll, hd, sh, n, extra);
+  uint32_t ftot, etot, ntok;
+  const uint32_t fincl = wg_incl_sum(fbits, wsum, ftot);
+  (void)wg_incl_sum(extra, wsum, etot);
+  const uint32_t fixed_bytes = ((3u + ftot + 7u + 3u + 7u) >> 3) + 4u;  // header, tokens, EOB, sync flush
   const uint32_t stored_bytes = 5u + n;
-  const bool fixed = fixed_bytes < stored_bytes;
-  uint32_t* img = tab;
-  for (uint32_t k = t; k < kImgWords; k += kThreads) img[k] = 0u;
-  __syncthreads();
-  if (fixed) {
-    // 3. emit: header bits 0..2 = BFINAL 0, BTYPE 01; EOB and the empty stored
-    // block's header are zero bits; its LEN/NLEN on the next byte boundary
-    if (t == 0) atomicOr(&img[0], 2u);
-    parse_range<true>(data, cd, img, sh, n, 3u + incl - bits);
+  // entropy estimate of a dynamic code: build one only if it can win
+  const uint32_t f_t = t < 286u ? hll[t] : (t >= 288u && t < 318u ? hd[t - 288u] : 0u);
+  (void)wg_incl_sum(t < 286u ? f_t : 0u, wsum, ntok);
+  uint32_t ndist;
+  (void)wg_incl_sum(t >= 288u ? f_t : 0u, wsum, ndist);
+  const float nn = t < 286u ? (float)ntok : (float)max(ndist, 1u);
+  const uint32_t h_t = f_t ? (uint32_t)((float)f_t * (__log2f(nn) - __log2f((float)f_t))) : 0u;
+  uint32_t htot;
+  (void)wg_incl_sum(h_t, wsum, htot);
+  const uint32_t best_other = min(fixed_bytes, stored_bytes) * 8u;
+  const bool try_dyn = htot + etot + 600u < best_other;
+  if (try_dyn) {
+    uint32_t* keys = tab;                                   // 512
+    uint32_t* keys2 = tab + 512;                            // 32
+    uint32_t* hw = tab + 576;                               // 2 x 288 weights
+    uint16_t* hpar = reinterpret_cast<uint16_t*>(tab + 1152);  // 576
+    uint8_t* hdep = reinterpret_cast<uint8_t*>(tab + 1440);    // 576
+    uint32_t* blc = tab + 1600;                             // 16
+    for (uint32_t k = t; k < 512u; k += kThreads) keys[k] = (k < 286u && hll[k]) ? (hll[k] << 9) | k : 0xFFFFFFFFu;
+    for (uint32_t k = t; k < 320u; k += kThreads) zl[k] = 0u;
+    __syncthreads();
+    if (t < 64u) {  // bitonic sort, ascending, one wave
+      for (uint32_t k = 2; k <= 512u; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0u; j >>= 1)
+          for (uint32_t i = t; i < 512u; i += 64u) {
+            const uint32_t ixj = i ^ j;
+            if (ixj > i) {
+              const uint32_t a = keys[i], b = keys[ixj];
+              if ((a > b) == ((i & k) == 0u)) {
+                keys[i] = b;
+                keys[ixj] = a;
+              }
+            }
+          }
+    }
     __syncthreads();
     if (t == 0) {
+      uint32_t m = 0u;
+      while (m < 286u && keys[m] != 0xFFFFFFFFu) m++;
+      huff_lengths(keys, m, 15u, zl, hw, hpar, hdep);
+      const uint32_t md = sort_small(hd, 30u, keys2);
+      if (md == 0u) {
+        zl[288] = 1u;
+        zl[289] = 1u;
+      } else if (md == 1u) {
+        const uint32_t x = keys2[0] & 511u;
+        zl[288 + x] = 1u;
+        zl[288 + (x ? 0u : 1u)] = 1u;
+      } else {
+        huff_lengths(keys2, md, 15u, zl + 288, hw, hpar, hdep);
+      }
+      uint32_t hlit = 257u, hdist = 1u;
+      for (uint32_t k = 257u; k < 286u; k++)
+        if (zl[k]) hlit = k + 1u;
+      for (uint32_t k = 0u; k < 30u; k++)
+        if (zl[288 + k]) hdist = k + 1u;
+      canon_codes(zl, 286u, llc, blc);
+      canon_codes(zl + 288, 30u, dcc, blc);
+      // code-length sequence, run-length coded (16/17/18)
+      for (uint32_t k = 0; k < 19u; k++) clf[k] = 0u;
+      const uint32_t nl = hlit + hdist;
+      uint32_t nr = 0u;
+      for (uint32_t i = 0; i < nl;) {
+        const uint32_t cur = i < hlit ? zl[i] : zl[288 + i - hlit];
+        uint32_t run = 1u;
+        while (i + run < nl && (i + run < hlit ? zl[i + run] : zl[288 + i + run - hlit]) == cur) run++;
+        uint32_t r = run;
+        if (cur == 0u) {
+          while (r >= 11u) {
+            const uint32_t q = min(r, 138u);
+            rle[nr++] = 18u | ((q - 11u) << 8);
+            clf[18]++;
+            r -= q;
+          }
+          if (r >= 3u) {
+            rle[nr++] = 17u | ((r - 3u) << 8);
+            clf[17]++;
+            r = 0u;
+          }
+        } else {
+          rle[nr++] = cur;
+          clf[cur]++;
+          r--;
+          while (r >= 3u) {
+            const uint32_t q = min(r, 6u);
+            rle[nr++] = 16u | ((q - 3u) << 8);
+            clf[16]++;
+            r -= q;
+          }
+        }
+        while (r > 0u) {
+          rle[nr++] = cur;
+          clf[cur]++;
+          r--;
+        }
+        i += run;
+      }
+      for (uint32_t k = 0; k < 19u; k++) cll[k] = 0u;
+      const uint32_t mc = sort_small(clf, 19u, keys2);
+      if (mc == 1u) {
+        const uint32_t x = keys2[0] & 511u;
+        cll[x] = 1u;
+        cll[x ? 0u : 1u] = 1u;
+      } else {
+        huff_lengths(keys2, mc, 7u, cll, hw, hpar, hdep);
+      }
+      canon_codes(cll, 19u, clc, blc);
+      uint32_t hclen = 4u;
+      for (uint32_t k = 0; k < 19u; k++)
+        if (cll[kClOrder[k]]) hclen = max(hclen, k + 1u);
+      uint32_t hb = 3u + 5u + 5u + 4u + 3u * hclen;
+      for (uint32_t k = 0; k < nr; k++) {
+        const uint32_t sy = rle[k] & 31u;
+        hb += (clc[sy] >> 16) + (sy == 16u ? 2u : sy == 17u ? 3u : sy == 18u ? 7u : 0u);
+      }
+      uint32_t tok = etot;
+      for (uint32_t k = 0; k < 286u; k++) tok += hll[k] * zl[k];  // EOB included (hll[256] = 1)
+      for (uint32_t k = 0; k < 30u; k++) tok += hd[k] * zl[288 + k];
+      const uint32_t dyn_bytes = ((hb + tok + 3u + 7u) >> 3) + 4u;
+      zpar[0] = dyn_bytes < min(fixed_bytes, stored_bytes) ? 2u : 0u;
+      zpar[1] = hb;
+      zpar[2] = dyn_bytes;
+      zpar[3] = hlit | (hdist << 16);
+      zpar[4] = hclen | (nr << 16);
+    }
+    __syncthreads();
+  } else if (t == 0) {
+    zpar[0] = 0u;
+  }
+  __syncthreads();
+  uint32_t mode = zpar[0];  // 2 dynamic, 1 fixed, 0 stored
+  if (mode == 0u && fixed_bytes < stored_bytes) mode = 1u;
+  if (mode == 1u) {  // fixed code tables
+    for (uint32_t k = t; k < 288u; k += kThreads)
+      llc[k] = k < 144u ? rev(0x30u + k, 8u) | (8u << 16)
+             : k < 256u ? rev(0x190u + k - 144u, 9u) | (9u << 16)
+             : k < 280u ? rev(k - 256u, 7u) | (7u << 16)
+                        : rev(0xC0u + k - 280u, 8u) | (8u << 16);
+    for (uint32_t k = t; k < 32u; k += kThreads) dcc[k] = rev(k, 5u) | (5u << 16);
+  }
+  uint32_t* img = tab;
+  __syncthreads();
+  for (uint32_t k = t; k < kImgWords; k += kThreads) img[k] = 0u;
+  __syncthreads();
+  uint32_t nbytes = stored_bytes;
+  if (mode != 0u) {
+    // 3. emit: this thread's tokens at its prefix offset after the block header
+    uint32_t mine = fbits, incl = fincl, tot = ftot;
+    if (mode == 2u) {
+      mine = walk_tokens<false>(cd, llc, dcc, nullptr, n, 0u);
+      incl = wg_incl_sum(mine, wsum, tot);
+    }
+    const uint32_t base = mode == 2u ? zpar[1] : 3u;
+    if (t == 0) {
+      uint32_t o = 0u;
+      if (mode == 1u) {
+        emit_bits(img, o, 2u, 3u);  // BFINAL 0, BTYPE 01
+      } else {
+        const uint32_t hlit = zpar[3] & 0xFFFFu, hdist = zpar[3] >> 16;
+        const uint32_t hclen = zpar[4] & 0xFFFFu, nr = zpar[4] >> 16;
+        emit_bits(img, o, 4u, 3u);  // BFINAL 0, BTYPE 10
+        emit_bits(img, o, hlit - 257u, 5u);
+        emit_bits(img, o, hdist - 1u, 5u);
+        emit_bits(img, o, hclen - 4u, 4u);
+        for (uint32_t k = 0; k < hclen; k++) emit_bits(img, o, cll[kClOrder[k]], 3u);
+        for (uint32_t k = 0; k < nr; k++) {
+          const uint32_t sy = rle[k] & 31u, e = clc[sy];
+          emit_bits(img, o, e & 0xFFFFu, e >> 16);
+          if (sy >= 16u) emit_bits(img, o, rle[k] >> 8, sy == 16u ? 2u : sy == 17u ? 3u : 7u);
+        }
+      }
+    }
+    walk_tokens<true>(cd, llc, dcc, img, n, base + incl - mine);
+    __syncthreads();
+    if (t == 0) {
+      uint32_t o = base + tot;
+      emit_bits(img, o, llc[256] & 0xFFFFu, llc[256] >> 16);  // end of block
+      const uint32_t e = (o + 3u + 7u) >> 3;                  // + the empty stored block's 3 header bits
       uint8_t* ob = reinterpret_cast<uint8_t*>(img);
-      const uint32_t e = fixed_bytes - 4u;
       ob[e] = 0x00;
       ob[e + 1] = 0x00;
       ob[e + 2] = 0xFF;
       ob[e + 3] = 0xFF;
+      zpar[5] = e + 4u;
     }
+    __syncthreads();
+    nbytes = zpar[5];
   } else {
     // stored image: 00 | LEN | ~LEN | data
     for (uint32_t k = t; k < (n + 5u + 3u) / 4u; k += kThreads) {
@@ -351,7 +673,6 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
     }
   }
   __syncthreads();
-  const uint32_t nbytes = fixed ? fixed_bytes : stored_bytes;
   uint32_t* slot = scratch + (uint64_t)g * kImgWords;
   for (uint32_t k = t; k < (nbytes + 3u) / 4u; k += kThreads) slot[k] = img[k];
 
@@ -373,7 +694,7 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
       Js += wadler[2 * k + 1];
     }
     SegInfo si;
-    si.mode = fixed ? 1u : 0u;
+    si.mode = mode;
     si.bytes = nbytes;
     si.a = (uint32_t)(As % kAdlerMod);
     si.b = (uint32_t)(((unsigned long long)n * As - Js) % kAdlerMod);

@@ -48,7 +48,7 @@ def test_random_is_stored_and_text_compresses(engine):
     assert len(zr) == len(rnd) + 5 * (len(rnd) // 32768) + 11  # all stored: +5 B per 32 KiB segment
     ref = len(OD.compress_ref(txt))
     assert len(zt) < 0.75 * len(txt), (len(zt), len(txt))
-    assert len(zt) < 1.7 * ref, (len(zt), ref)  # fixed Huffman, 32 KiB segments vs zlib -6
+    assert len(zt) < 1.4 * ref, (len(zt), ref)  # per-segment dynamic Huffman, 32 KiB windows vs zlib -6
     assert len(zz) < (1 << 20) // 16  # >= one match token per 64-byte parse range
 
 
