@@ -28,10 +28,11 @@ EXPORTS = [
     "hbx_chain_block_serialize", "hbx_chain_block_parse", "hbx_directory_block_size",
     "hbx_directory_block_serialize", "hbx_directory_block_parse", "hbx_directory_block_ids",
     "hbx_deflate_bound", "hbx_deflate_blocks_device", "hbx_deflate_blocks",
+    "hbx_deflate_file_bound", "hbx_store_paths_z",
 ]
 # Functions returning something other than an int status.
 _NON_STATUS = ("hbx_ctx_destroy", "hbx_last_error", "hbx_max_chunks", "hbx_file_entry_size",
-               "hbx_directory_block_size", "hbx_deflate_bound")
+               "hbx_directory_block_size", "hbx_deflate_bound", "hbx_deflate_file_bound")
 
 
 class FileEntry(ctypes.Structure):
@@ -118,6 +119,9 @@ def load() -> ctypes.CDLL:
     L.hbx_deflate_bound.restype = U64
     L.hbx_deflate_blocks_device.argtypes = [P, P, U64, P, P, P, P, P, P]
     L.hbx_deflate_blocks.argtypes = [P, U64, P, P, P, P, P]
+    L.hbx_deflate_file_bound.argtypes = [U64]
+    L.hbx_deflate_file_bound.restype = U64
+    L.hbx_store_paths_z.argtypes = [P, U64, P, P, P, P, P, P, P, ctypes.c_uint32, U64, P, P, P, P]
     for name in EXPORTS:
         if name not in _NON_STATUS:
             getattr(L, name).restype = I

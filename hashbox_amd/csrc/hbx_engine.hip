@@ -166,6 +166,7 @@ struct hbx_ctx {
   DevBuf d_vdesc, d_vlinks, d_vout, d_vexp, d_zeros;  // hbx_verify_blocks*
   DevBuf d_zblk, d_zinfo, d_zoff, d_zlen, d_zout, d_zimg;  // hbx_deflate_blocks*
   PinBuf h_read[2];         // hbx_store_paths: pinned landing slots for file reads
+  PinBuf h_zstage;          // hbx_store_paths_z: compressed streams of one batch
   hipEvent_t h2d_done[2] = {nullptr, nullptr};  // slot's H2D copy has completed
   std::vector<DevBuf> d_ring;  // hbx_store_paths: device arenas of the batches in flight
   double io_s[3] = {0, 0, 0};  // hbx_store_paths: reading files | waiting for an arena | waiting for a copy
@@ -686,6 +687,7 @@ void hbx_ctx_destroy(hbx_ctx* c) {
                     &c->d_zlen, &c->d_zout, &c->d_zimg})
     b->release();
   for (PinBuf& h : c->h_read) h.release();
+  c->h_zstage.release();
   for (DevBuf& d : c->d_ring) d.release();
   for (hipEvent_t e : c->h2d_done)
     if (e) (void)hipEventDestroy(e);
@@ -1046,6 +1048,82 @@ int read_files(uint64_t n, const char* const* paths, const uint64_t* lens, const
 
 }  // namespace
 
+namespace {
+int deflate_device(hbx_ctx* c, uint64_t n, const uint64_t* src, const uint64_t* lens, const uint64_t* dst,
+                   uint64_t* out_lens);
+
+// Output of hbx_store_paths_z (null members: no compression).
+struct ZOut {
+  uint8_t* zout = nullptr;
+  const uint64_t* zbase = nullptr;
+  uint64_t* zoff = nullptr;
+  uint64_t* zlen = nullptr;
+};
+// A collected batch whose device arena still holds its files.
+struct ZJob {
+  uint64_t first = 0, count = 0;
+  const uint8_t* arena = nullptr;
+  std::vector<uint64_t> offs;
+};
+
+// CompressData of every chunk of a collected batch (client.go:249-258): K7
+// on the batch's arena, one copy of the streams back, packed per file at
+// zout[zbase[f] ..].
+int deflate_batch(hbx_ctx* c, const ZJob& j, const uint64_t* cut_ends, const uint64_t* out_base,
+                  const hbx_file_summary* sums, const ZOut& z, uint32_t threads) {
+  std::vector<uint64_t> src, len, dst;
+  uint64_t d = 0;
+  for (uint64_t i = 0; i < j.count; i++) {
+    const uint64_t f = j.first + i;
+    uint64_t start = 0;
+    for (uint32_t q = 0; q < sums[f].n_chunks; q++) {
+      const uint64_t e = cut_ends[out_base[f] + q];
+      src.push_back(reinterpret_cast<uint64_t>(j.arena + j.offs[i] + start));
+      len.push_back(e - start);
+      dst.push_back(d);
+      d += (hbx_deflate_bound(e - start) + 15) & ~uint64_t(15);
+      start = e;
+    }
+  }
+  const uint64_t nc = src.size();
+  if (nc == 0) return HBX_OK;
+  HBX_TRY(c, c->d_zout.ensure(d + 64));
+  HBX_TRY(c, c->h_zstage.ensure(d + 64));
+  std::vector<uint64_t> dabs(nc), ol(nc);
+  for (uint64_t i = 0; i < nc; i++) dabs[i] = reinterpret_cast<uint64_t>(c->d_zout.as<uint8_t>() + dst[i]);
+  const int rc = deflate_device(c, nc, src.data(), len.data(), dabs.data(), ol.data());
+  if (rc) return rc;
+  HBX_TRY(c, hipMemcpy(c->h_zstage.p, c->d_zout.p, d, hipMemcpyDeviceToHost));
+  const uint8_t* h = c->h_zstage.as<uint8_t>();
+  // placement (serial, cheap), then the copies out of the pinned stage on
+  // `threads` threads (one thread copies a few GB/s)
+  std::vector<uint64_t> to(nc);
+  uint64_t k = 0;
+  for (uint64_t i = 0; i < j.count; i++) {
+    const uint64_t f = j.first + i;
+    uint64_t run = z.zbase[f];
+    for (uint32_t q = 0; q < sums[f].n_chunks; q++, k++) {
+      to[k] = run;
+      z.zoff[out_base[f] + q] = run;
+      z.zlen[out_base[f] + q] = ol[k];
+      run += ol[k];
+    }
+  }
+  const uint32_t nt = std::max<uint32_t>(1u, std::min<uint32_t>(threads, 64u));
+  std::vector<std::thread> pool;
+  for (uint32_t t = 0; t < nt; t++)
+    pool.emplace_back([&, t] {
+      for (uint64_t i = t; i < nc; i += nt) std::memcpy(z.zout + to[i], h + dst[i], ol[i]);
+    });
+  for (auto& th : pool) th.join();
+  return HBX_OK;
+}
+
+int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uint64_t* lens,
+                     uint64_t* cut_ends, uint8_t* ids, const uint64_t* out_base, const uint64_t* caps,
+                     hbx_file_summary* sums, uint32_t io_threads, uint64_t batch_bytes, const ZOut& z);
+}  // namespace
+
 int hbx_store_paths(hbx_ctx* c, uint64_t n, const char* const* paths, const uint64_t* lens,
                     uint64_t* cut_ends, uint8_t* ids, const uint64_t* out_base,
                     const uint64_t* caps, hbx_file_summary* sums, uint32_t io_threads,
@@ -1053,6 +1131,30 @@ int hbx_store_paths(hbx_ctx* c, uint64_t n, const char* const* paths, const uint
   if (!c) return HBX_ERR_ARG;
   if (n && (!paths || !lens || !out_base || !caps)) return HBX_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
+  return store_paths_impl(c, n, paths, lens, cut_ends, ids, out_base, caps, sums, io_threads, batch_bytes,
+                          ZOut{});
+}
+
+uint64_t hbx_deflate_file_bound(uint64_t len) {
+  return len + 16ull * hbx_max_chunks(len) + 5ull * (len / hbxz::kSeg);
+}
+
+int hbx_store_paths_z(hbx_ctx* c, uint64_t n, const char* const* paths, const uint64_t* lens,
+                      uint64_t* cut_ends, uint8_t* ids, const uint64_t* out_base, const uint64_t* caps,
+                      hbx_file_summary* sums, uint32_t io_threads, uint64_t batch_bytes, uint8_t* zout,
+                      const uint64_t* zbase, uint64_t* zoff, uint64_t* zlen) {
+  if (!c) return HBX_ERR_ARG;
+  if (n && (!paths || !lens || !out_base || !caps || !sums || !zout || !zbase || !zoff || !zlen))
+    return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  return store_paths_impl(c, n, paths, lens, cut_ends, ids, out_base, caps, sums, io_threads, batch_bytes,
+                          ZOut{zout, zbase, zoff, zlen});
+}
+
+namespace {
+int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uint64_t* lens,
+                     uint64_t* cut_ends, uint8_t* ids, const uint64_t* out_base, const uint64_t* caps,
+                     hbx_file_summary* sums, uint32_t io_threads, uint64_t batch_bytes, const ZOut& z) {
   if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
   HBX_TRY(c, hipSetDevice(c->device));
   if (batch_bytes < (64ull << 20)) batch_bytes = 64ull << 20;
@@ -1090,6 +1192,17 @@ int hbx_store_paths(hbx_ctx* c, uint64_t n, const char* const* paths, const uint
   std::vector<uint64_t> offs;
   uint64_t f = 0, k = 0;
   int rc = HBX_OK;
+  // with compression, each collected batch is compressed from its arena
+  // before the arena takes the next batch (FIFO, like the collection)
+  std::deque<ZJob> jobs;
+  auto collect = [&]() -> int {
+    int r = wait_oldest(c);
+    if (z.zout) {
+      if (!r && !jobs.empty()) r = deflate_batch(c, jobs.front(), cut_ends, out_base, sums, z, io_threads);
+      if (!jobs.empty()) jobs.pop_front();
+    }
+    return r;
+  };
   while (f < n && rc == HBX_OK) {
     const uint64_t first = f;
     offs.clear();
@@ -1102,7 +1215,7 @@ int hbx_store_paths(hbx_ctx* c, uint64_t n, const char* const* paths, const uint
     const int p = (int)(k & 1);
     DevBuf& arena = c->d_ring[k % depth];
     double t0 = now();
-    if (c->pending.size() >= depth && (rc = wait_oldest(c))) break;  // frees arena k % depth
+    if (c->pending.size() >= depth && (rc = collect())) break;  // frees arena k % depth
     double t1 = now();
     if (slot_used[p] && (rc = c->hip(hipEventSynchronize(c->h2d_done[p]), "h2d wait"))) break;
     double t2 = now();
@@ -1119,18 +1232,20 @@ int hbx_store_paths(hbx_ctx* c, uint64_t n, const char* const* paths, const uint
     slot_used[p] = true;
     rc = submit_batch(c, arena.p, f - first, offs.data(), lens + first, cut_ends, ids,
                       out_base + first, caps + first, sums ? sums + first : nullptr, budget);
+    if (z.zout && rc == HBX_OK) jobs.push_back(ZJob{first, f - first, static_cast<const uint8_t*>(arena.p), offs});
     k++;
   }
   // collect everything in flight (also after a failure: the caller's arrays
   // must not be written once this call has returned)
   while (!c->pending.empty()) {
     const std::string keep = c->err;
-    const int r2 = wait_oldest(c);
+    const int r2 = rc == HBX_OK ? collect() : wait_oldest(c);
     if (rc == HBX_OK) rc = r2;
     else c->err = keep;
   }
   return rc;
 }
+}  // namespace
 
 int hbx_io_times(hbx_ctx* c, double s[3], int reset) {
   if (!c || !s) return HBX_ERR_ARG;

@@ -53,6 +53,7 @@ class FileChunks:
     ids: np.ndarray  # uint8 [k, 16]: BlockID per chunk (core.Byte128)
     content_type: int  # 2 FileData, 3 FileChain (0 for an empty file)
     content_id: bytes  # entry.ContentBlockID
+    zstreams: Optional[list] = None  # zlib stream per chunk, uint8 views (store_paths(compress=True))
 
     @property
     def n_chunks(self) -> int:
@@ -327,18 +328,39 @@ class Engine:
                     "hbx_memcpy_h2d_async")
 
     def store_paths(self, paths: Sequence[Union[str, os.PathLike]], io_threads: int = 16,
-                    batch_bytes: int = 1 << 30) -> List[FileChunks]:
+                    batch_bytes: int = 1 << 30, compress: bool = False) -> List[FileChunks]:
         """storeFile for many files on disk, end to end: the library reads them
         into pinned memory on ``io_threads`` threads and overlaps reading the
-        next batch with the copy + kernels of the current one."""
+        next batch with the copy + kernels of the current one.  With
+        ``compress`` every chunk is also zlib-compressed on the device
+        (HashboxBlock.CompressData, the client's send path) and returned in
+        ``FileChunks.zstreams``."""
         enc = [os.fsencode(p) for p in paths]
         lens = np.array([os.stat(p).st_size for p in enc], np.uint64)
         arr = (ctypes.c_char_p * max(len(enc), 1))(*enc)
         caps, base, cuts, ids, sums = self._alloc_out(lens)
-        self._check(self._L.hbx_store_paths(self._ctx, len(enc), ctypes.cast(arr, ctypes.c_void_p),
-                                            _p(lens), _p(cuts), _p(ids), _p(base), _p(caps), sums,
-                                            int(io_threads), int(batch_bytes)), "hbx_store_paths")
-        return self._unpack(lens, caps, base, cuts, ids, sums)
+        if not compress:
+            self._check(self._L.hbx_store_paths(self._ctx, len(enc), ctypes.cast(arr, ctypes.c_void_p),
+                                                _p(lens), _p(cuts), _p(ids), _p(base), _p(caps), sums,
+                                                int(io_threads), int(batch_bytes)), "hbx_store_paths")
+            return self._unpack(lens, caps, base, cuts, ids, sums)
+        fb = np.array([self._L.hbx_deflate_file_bound(int(x)) for x in lens], np.uint64)
+        zbase = np.zeros(max(lens.size, 1), np.uint64)
+        if lens.size > 1:
+            zbase[1:lens.size] = np.cumsum(fb[:-1])
+        zout = np.empty(int(fb.sum()) + 16, np.uint8)
+        zoff = np.zeros(max(int(caps.sum()), 1), np.uint64)
+        zlen = np.zeros_like(zoff)
+        self._check(self._L.hbx_store_paths_z(self._ctx, len(enc), ctypes.cast(arr, ctypes.c_void_p),
+                                              _p(lens), _p(cuts), _p(ids), _p(base), _p(caps), sums,
+                                              int(io_threads), int(batch_bytes), _p(zout), _p(zbase),
+                                              _p(zoff), _p(zlen)), "hbx_store_paths_z")
+        res = self._unpack(lens, caps, base, cuts, ids, sums)
+        for f, r in enumerate(res):
+            b = int(base[f])
+            r.zstreams = [zout[int(zoff[b + i]):int(zoff[b + i] + zlen[b + i])]  # views, no copy
+                          for i in range(r.n_chunks)]
+        return res
 
     def io_times(self, reset: bool = False) -> np.ndarray:
         """store_paths host seconds: reading files, waiting for an arena,

@@ -284,6 +284,18 @@ int hbx_deflate_blocks_device(hbx_ctx *ctx, const void *d_arena, uint64_t n, con
 int hbx_deflate_blocks(hbx_ctx *ctx, uint64_t n, const uint8_t *const *datas, const uint64_t *lens,
                        uint8_t *const *outs, const uint64_t *caps, uint64_t *out_lens);
 
+/* hbx_store_paths plus CompressData of every chunk on the device (the
+ * client's send path: StoreData -> workers compress -> socket,
+ * client.go:249-258).  sums is required.  Chunk i of file f (index
+ * out_base[f] + i, like cut_ends) gets its zlib stream at zout[zoff[..]] with
+ * length zlen[..]; file f's streams are packed from zout[zbase[f]], which
+ * needs hbx_deflate_file_bound(lens[f]) bytes. */
+uint64_t hbx_deflate_file_bound(uint64_t len);
+int hbx_store_paths_z(hbx_ctx *ctx, uint64_t n_files, const char *const *paths, const uint64_t *lens,
+                      uint64_t *cut_ends, uint8_t *ids, const uint64_t *out_base, const uint64_t *caps,
+                      hbx_file_summary *summaries, uint32_t io_threads, uint64_t batch_bytes,
+                      uint8_t *zout, const uint64_t *zbase, uint64_t *zoff, uint64_t *zlen);
+
 /* Device arena helpers (allocations include HBX_ARENA_SLACK). */
 int hbx_arena_alloc(hbx_ctx *ctx, uint64_t bytes, void **d_ptr);
 int hbx_arena_free(hbx_ctx *ctx, void *d_ptr);

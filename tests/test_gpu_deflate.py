@@ -107,3 +107,27 @@ def test_capacity_refused(engine):
     dst = torch.zeros(1024, dtype=torch.uint8, device="cuda:0")
     with pytest.raises(HbxError):
         engine.deflate_blocks_device(src.data_ptr(), [0], [900], dst.data_ptr(), [0], [900])
+
+
+def test_store_paths_compressed(engine, tmp_path):
+    # the client's send path end to end: files on disk -> chunks + ids + one zlib stream per chunk
+    rng = np.random.default_rng(12)
+    paths, datas = [], []
+    for i in range(44):  # > 64 MiB in total: several pipelined batches
+        kind = i % 4
+        n = int(rng.integers(1, 3 << 20)) if i % 11 else [0, 100, 131_073, 9 << 20][i // 11]
+        d = (rng.integers(0, 256, n, dtype=np.uint8).tobytes() if kind == 0 else _text(n, i) if kind == 1
+             else bytes(n) if kind == 2 else (rng.integers(0, 256, 5000, dtype=np.uint8).tobytes() * (n // 5000 + 1))[:n])
+        p = tmp_path / f"f{i:02d}"
+        p.write_bytes(d)
+        paths.append(p)
+        datas.append(d)
+    plain = engine.store_paths(paths, io_threads=4)
+    comp = engine.store_paths(paths, io_threads=4, compress=True)
+    for d, a, b in zip(datas, plain, comp):
+        assert np.array_equal(a.cut_ends, b.cut_ends) and np.array_equal(a.ids, b.ids)
+        assert a.content_id == b.content_id
+        assert len(b.zstreams) == b.n_chunks
+        starts, ends = b.chunk_bounds()
+        for s, e, z in zip(starts, ends, b.zstreams):
+            assert OD.inflate_strict(z) == d[int(s):int(e)]

@@ -37,6 +37,12 @@ def make_files(d, n, seed):
     return paths, sizes
 
 
+def r_bounds(r):
+    ends = r.cut_ends
+    starts = np.concatenate([[0], ends[:-1]]).astype(np.uint64)
+    return starts, ends
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--files", type=int, default=100_000)
@@ -45,6 +51,8 @@ def main():
     ap.add_argument("--batch-mib", type=int, default=1024)
     ap.add_argument("--cpu-sample", type=int, default=10_000)
     ap.add_argument("--keep", action="store_true")
+    ap.add_argument("--compress", action="store_true",
+                    help="also time store_paths(compress=True): every chunk zlib-compressed on the device")
     a = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime per process: see hashbox_amd/_lib.py)
     from hashbox_amd import Engine
@@ -74,6 +82,36 @@ def main():
                   if not (np.array_equal(res[i].cut_ends, r.cut_ends)
                           and np.array_equal(res[i].ids, r.ids)))
         n_chunks = sum(r.n_chunks for r in res)
+        zrep = None
+        if a.compress:
+            import zlib
+            from oracle import deflate as OD
+            del res
+            eng.io_times(reset=True)
+            t0 = time.time()
+            zres = eng.store_paths(paths, a.io_threads, a.batch_mib << 20, compress=True)
+            t_z = time.time() - t0
+            zio = eng.io_times()
+            zbytes = sum(int(z.size) for r in zres for z in r.zstreams)
+            zbad = 0
+            for i in pick[:500]:
+                d = datas[int(np.searchsorted(pick, i))]
+                st, en = zres[i].chunk_bounds()
+                zbad += sum(OD.inflate_strict(z) != d[int(s0):int(e0)].tobytes()
+                            for s0, e0, z in zip(st, en, zres[i].zstreams))
+            # the reference client's per-chunk work on the CPU: MD5 id (oracle) + zlib -6, 16 threads
+            chunks = [d[int(s0):int(e0)].tobytes() for r, d in zip(ref, datas) for s0, e0 in zip(*r_bounds(r))]
+            t0 = time.time()
+            OD.compress_ref_mt(chunks, a.io_threads)
+            t_cz = time.time() - t0
+            zrep = {"e2e_seconds": round(t_z, 3), "e2e_gibs": round(total / t_z / (1 << 30), 3),
+                    "compressed_bytes": zbytes, "ratio": round(zbytes / total, 4),
+                    "host_seconds": {"read_files": round(float(zio[0]), 3), "wait_arena": round(float(zio[1]), 3),
+                                     "wait_h2d": round(float(zio[2]), 3)},
+                    "roundtrip_checked_files": int(min(500, len(pick))), "roundtrip_mismatches": int(zbad),
+                    "cpu_zlib6_sample": {"threads": a.io_threads, "bytes": sample_bytes,
+                                         "seconds_zlib_only": round(t_cz, 3),
+                                         "gibs_hash_plus_zlib": round(sample_bytes / (t_cpu + t_cz) / (1 << 30), 3)}}
         print(json.dumps({
             "config": "BASELINE configs[4]: 100k mixed small files end to end",
             "files": a.files, "bytes": total, "chunks": n_chunks,
@@ -87,7 +125,8 @@ def main():
                            "seconds": round(t_cpu, 3),
                            "gibs": round(sample_bytes / t_cpu / (1 << 30), 3),
                            "includes": "file reads + literal storeFile loop + MD5"},
-            "sample_mismatches": bad, "make_seconds": round(t_make, 1)}), flush=True)
+            "sample_mismatches": bad, "make_seconds": round(t_make, 1),
+            "compressed": zrep}), flush=True)
     finally:
         eng.close()
         if not a.keep:
