@@ -29,6 +29,7 @@ EXPORTS = [
     "hbx_directory_block_serialize", "hbx_directory_block_parse", "hbx_directory_block_ids",
     "hbx_deflate_bound", "hbx_deflate_blocks_device", "hbx_deflate_blocks",
     "hbx_deflate_file_bound", "hbx_store_paths_z",
+    "hbx_wire_encode_id", "hbx_wire_encode_block_header", "hbx_wire_parse",
 ]
 # Functions returning something other than an int status.
 _NON_STATUS = ("hbx_ctx_destroy", "hbx_last_error", "hbx_max_chunks", "hbx_file_entry_size",
@@ -42,6 +43,14 @@ class FileEntry(ctypes.Structure):
                 ("reference_id", ctypes.c_uint8 * 16), ("content_id", ctypes.c_uint8 * 16),
                 ("decrypt_key", ctypes.c_uint8 * 16), ("link", ctypes.c_void_p), ("link_len", ctypes.c_uint32),
                 ("content_type", ctypes.c_uint8), ("pad", ctypes.c_uint8 * 3)]
+
+
+class WireMsg(ctypes.Structure):
+    """hbx_wire_msg: one parsed protocol message (pkg/core/protocol.go)."""
+    _fields_ = [("num", ctypes.c_uint16), ("type", ctypes.c_uint32), ("id", ctypes.c_uint8 * 16),
+                ("n_links", ctypes.c_uint32), ("links", ctypes.c_void_p), ("data_type", ctypes.c_uint8),
+                ("data_len", ctypes.c_uint32), ("data", ctypes.c_void_p), ("header_len", ctypes.c_uint64),
+                ("total_len", ctypes.c_uint64)]
 
 
 class FileSummary(ctypes.Structure):
@@ -121,6 +130,10 @@ def load() -> ctypes.CDLL:
     L.hbx_deflate_blocks.argtypes = [P, U64, P, P, P, P, P]
     L.hbx_deflate_file_bound.argtypes = [U64]
     L.hbx_deflate_file_bound.restype = U64
+    L.hbx_wire_encode_id.argtypes = [ctypes.c_uint16, ctypes.c_uint32, P, P]
+    L.hbx_wire_encode_block_header.argtypes = [ctypes.c_uint16, ctypes.c_uint32, P, P, ctypes.c_uint32,
+                                               ctypes.c_uint8, ctypes.c_uint32, P, U64, PU64]
+    L.hbx_wire_parse.argtypes = [P, U64, P]
     L.hbx_store_paths_z.argtypes = [P, U64, P, P, P, P, P, P, P, ctypes.c_uint32, U64, P, P, P, P]
     for name in EXPORTS:
         if name not in _NON_STATUS:

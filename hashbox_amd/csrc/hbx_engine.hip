@@ -31,6 +31,7 @@
 #include "hbx_kernels.hip"
 #include "hbx_deflate.hip"
 #include "hbx_formats.h"
+#include "hbx_wire.h"
 
 namespace {
 
@@ -1488,6 +1489,40 @@ int hbx_deflate_blocks(hbx_ctx* c, uint64_t n, const uint8_t* const* datas, cons
   HBX_TRY(c, hipMemcpy(host.data(), zo, sout, hipMemcpyDeviceToHost));
   for (uint64_t i = 0; i < n; i++) std::memcpy(outs[i], host.data() + doff[i], out_lens[i]);
   return HBX_OK;
+}
+
+// ---- wire protocol framing (hbx_wire.h) -----------------------
+int hbx_wire_encode_id(uint16_t num, uint32_t type, const uint8_t id[16], uint8_t out[22]) {
+  if (!id || !out || !hbxwire::is_id_msg(type)) return HBX_ERR_ARG;
+  hbxfmt::Writer w{out, 22};
+  const uint8_t nb[2] = {(uint8_t)(num >> 8), (uint8_t)num};
+  w.bytes(nb, 2);
+  w.u32(type);
+  w.bytes(id, 16);
+  return w.ok ? HBX_OK : HBX_ERR_CAPACITY;
+}
+
+int hbx_wire_encode_block_header(uint16_t num, uint32_t type, const uint8_t id[16], const uint8_t* links,
+                                 uint32_t n_links, uint8_t data_type, uint32_t data_len, uint8_t* out,
+                                 uint64_t cap, uint64_t* n) {
+  if (!id || (n_links && !links) || (cap && !out) || !hbxwire::is_block_msg(type)) return HBX_ERR_ARG;
+  hbxfmt::Writer w{out, cap};
+  const uint8_t nb[2] = {(uint8_t)(num >> 8), (uint8_t)num};
+  w.bytes(nb, 2);
+  w.u32(type);
+  w.bytes(id, 16);  // HashboxBlock.Serialize, block.go:56-69
+  w.u32(n_links);
+  w.bytes(links, 16ull * n_links);
+  w.u8(data_type);
+  w.u32(data_len);
+  if (!w.ok) return HBX_ERR_CAPACITY;
+  if (n) *n = w.n;
+  return HBX_OK;
+}
+
+int hbx_wire_parse(const uint8_t* in, uint64_t len, hbx_wire_msg* msg) {
+  if (!msg || (len && !in)) return HBX_ERR_ARG;
+  return hbxwire::parse(in, len, msg);
 }
 
 }  // extern "C"

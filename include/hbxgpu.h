@@ -25,6 +25,7 @@
  *   hbx_chain_block_*,    Serialize + Unserialize (hashback/hashback.go:80-214)
  *   hbx_directory_block_* and storeDir's block id (store.go:201-234)
  *   hbx_deflate_blocks    HashboxBlock.CompressData, zlib (block.go:133-184)
+ *   hbx_wire_*            allo/READ/writ/ACKN framing (pkg/core/protocol.go)
  *
  * Conventions
  *   - Every function returns an int status: 0 = OK, negative = error
@@ -295,6 +296,53 @@ int hbx_store_paths_z(hbx_ctx *ctx, uint64_t n_files, const char *const *paths, 
                       uint64_t *cut_ends, uint8_t *ids, const uint64_t *out_base, const uint64_t *caps,
                       hbx_file_summary *summaries, uint32_t io_threads, uint64_t batch_bytes,
                       uint8_t *zout, const uint64_t *zbase, uint64_t *zoff, uint64_t *zlen);
+
+/* ---- wire protocol, block-store subset ----------------------
+ * pkg/core/protocol.go: a message is u16 Num | u32 Type | its fields, big
+ * endian (ProtocolMessage.Serialize, protocol.go:184-203).  Client types are
+ * the lowercase constants; the server replies with Type & 0xDFDFDFDF
+ * ("READ", "ACKN", "WRIT", "ERRS").  The StoreBlock exchange
+ * (client.go:563-584, server.go:160-202): allo(id) -> READ(id) -> writ(block)
+ * -> ACKN(id), or allo(id) -> ACKN(id) when the server has the block.  Pure
+ * host code, no context. */
+#define HBX_MSG_GREETING 0x68616C6Fu    /* "halo" */
+#define HBX_MSG_GOODBYE 0x71756974u     /* "quit" */
+#define HBX_MSG_ALLOCATE 0x616C6C6Fu    /* "allo" */
+#define HBX_MSG_READ 0x72656164u        /* "read" */
+#define HBX_MSG_WRITE 0x77726974u       /* "writ" */
+#define HBX_MSG_ACKNOWLEDGE 0x61636B6Eu /* "ackn" */
+#define HBX_MSG_ERROR 0x65727273u       /* "errs" (sent as "ERRS") */
+#define HBX_SERVER_MASK 0xDFDFDFDFu
+#define HBX_BLOCK_DATA_RAW 0xFFu  /* BlockDataTypeRaw,  block.go:21 */
+#define HBX_BLOCK_DATA_ZLIB 0x01u /* BlockDataTypeZlib, block.go:22 */
+
+typedef struct {
+  uint16_t num;
+  uint32_t type;
+  uint8_t id[16];         /* allo/ACKN/read/READ/writ/WRIT: BlockID; HALO: nonce */
+  uint32_t n_links;       /* writ/WRIT */
+  const uint8_t *links;   /* writ/WRIT: into the input */
+  uint8_t data_type;      /* writ/WRIT */
+  uint32_t data_len;      /* writ/WRIT data; ERRS text; halo: version */
+  const uint8_t *data;    /* writ/WRIT data, ERRS text: into the input */
+  uint64_t header_len;    /* bytes before the data */
+  uint64_t total_len;     /* bytes of the whole message */
+} hbx_wire_msg;
+
+/* allo / read (client) or ACKN / READ (server, pass type & HBX_SERVER_MASK):
+ * 22 bytes. */
+int hbx_wire_encode_id(uint16_t num, uint32_t type, const uint8_t id[16], uint8_t out[22]);
+/* writ / WRIT up to (not including) the data: 31 + 16*n_links bytes; the
+ * data_len bytes of block data follow on the wire as they are (for
+ * BlockDataTypeZlib: the zlib stream, block.go:56-69). */
+int hbx_wire_encode_block_header(uint16_t num, uint32_t type, const uint8_t id[16], const uint8_t *links,
+                                 uint32_t n_links, uint8_t data_type, uint32_t data_len, uint8_t *out,
+                                 uint64_t cap, uint64_t *n);
+/* Parse one message at in[0..len) (ProtocolMessage.Unserialize,
+ * protocol.go:204-264): HBX_OK, HBX_ERR_CAPACITY if the message is not
+ * complete yet (msg->total_len is set once its header is), HBX_ERR_FORMAT for
+ * an unknown type. */
+int hbx_wire_parse(const uint8_t *in, uint64_t len, hbx_wire_msg *msg);
 
 /* Device arena helpers (allocations include HBX_ARENA_SLACK). */
 int hbx_arena_alloc(hbx_ctx *ctx, uint64_t bytes, void **d_ptr);
