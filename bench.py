@@ -43,7 +43,7 @@ GIB = 1 << 30
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--steps", type=int, default=600)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--files", type=int, default=64)
     ap.add_argument("--file-mib", type=int, default=128)

@@ -1045,6 +1045,9 @@ __device__ __forceinline__ void coop_load(u32x4 (&G)[16], const uint64_t (&Q)[16
 #ifndef HBX_COOP_BYTE
 #define HBX_COOP_BYTE 1
 #endif
+#ifndef HBX_COOP_SETS
+#define HBX_COOP_SETS 2  // register sets of cooperative loads in flight (2 or 3; 3 needs HBX_COOP_BYTE)
+#endif
 
 __device__ void md5_coop(uint8_t* wl, const uint8_t* c, uint32_t (&h)[4], uint32_t b1, uint32_t R) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -1111,10 +1114,44 @@ __device__ void md5_coop(uint8_t* wl, const uint8_t* c, uint32_t (&h)[4], uint32
 #endif
     }
   };
+#if HBX_COOP_SETS == 3
+  // Three register sets in flight (stages s+1..s+3 while stage s is hashed):
+  // the sets rotate statically (unrolled by 3), the LDS half alternates at
+  // run time.
+  (void)stage_pair;
+  u32x4 GC[16];
+  coop_load(GC, Q, 3u, t, ngr);  // GA holds stage 2, GB stage 1, stage 0 is in half 0
+  auto stage_rt = [&](uint32_t s, u32x4(&Gn)[16]) {
+    const uint32_t half = s & 1u;
+    // stage s+1 (in Gn) into the other half, then Gn takes the loads of s+4
+#pragma unroll
+    for (int q = 0; q < 16; q++)
+      *reinterpret_cast<u32x4*>(wl + wr + (half ^ 1u) * kCoopHalf + 1088u * (uint32_t)q) = Gn[q];
+    coop_load(Gn, Q, min(s + 4u, nst - 1u), t, ngr);
+    const uint8_t* hb = wl + rd + half * kCoopHalf;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t blk = 4u * s + (uint32_t)u;
+      if (blk >= R) break;  // wave-uniform
+      u32x4 W[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) W[i] = *reinterpret_cast<const u32x4*>(hb + 16u * (4u * u + (uint32_t)i));
+      const uint32_t m[16] = {W[0].x, W[0].y, W[0].z, W[0].w, W[1].x, W[1].y, W[1].z, W[1].w,
+                              W[2].x, W[2].y, W[2].z, W[2].w, W[3].x, W[3].y, W[3].z, W[3].w};
+      md5_compress(h, m);
+    }
+  };
+  for (uint32_t s = 0; 4u * s < R; s += 3u) {
+    stage_rt(s, GB);       // GB: stage s+1
+    stage_rt(s + 1u, GA);  // GA: stage s+2
+    stage_rt(s + 2u, GC);  // GC: stage s+3 (hashes nothing past block R)
+  }
+#else
   for (uint32_t s = 0; 4u * s < R; s += 2u) {
     stage_pair(std::integral_constant<int, 0>{}, s, GB);
     stage_pair(std::integral_constant<int, 1>{}, s + 1u, GA);  // hashes nothing past block R
   }
+#endif
 }
 
 }  // namespace
