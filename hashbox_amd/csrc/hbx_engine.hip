@@ -112,6 +112,12 @@ struct Batch {
   std::vector<uint64_t> out_base, capv;
   uint32_t need = 1, done = 0;  // K3 launches its chains need / have had
   bool finalized = false;
+  // a VerifyBlock batch (hbx_verify_submit_device) instead of files
+  bool verify = false;
+  uint8_t* v_ids = nullptr;
+  const uint8_t* v_expect = nullptr;
+  uint8_t* v_ok = nullptr;
+  uint64_t* v_nbad = nullptr;
   hipEvent_t ev[5] = {};  // K1 start | K1 end | K2 end | plan+K3 end (first) | results ready
   void release() {
     for (DevBuf* d : {&d_meta, &d_cuts, &d_count, &d_ids, &d_cid, &d_ctype, &d_run, &d_fresh, &d_fcnt}) d->release();
@@ -303,6 +309,11 @@ Batch* acquire_batch(hbx_ctx* c) {
   b->cut_ends = nullptr;
   b->ids = nullptr;
   b->sums = nullptr;
+  b->verify = false;
+  b->v_ids = nullptr;
+  b->v_expect = nullptr;
+  b->v_ok = nullptr;
+  b->v_nbad = nullptr;
   return b;
 }
 
@@ -312,6 +323,11 @@ Batch* acquire_batch(hbx_ctx* c) {
 int finalize_batch(hbx_ctx* c, Batch* b) {
   hipStream_t s = c->rstream;
   b->finalized = true;
+  if (b->verify) {
+    if (b->n) HBX_TRY(c, hipMemcpyAsync(b->h_res.p, b->d_ids.p, b->n * 16, hipMemcpyDeviceToHost, s));
+    HBX_TRY(c, hipEventRecord(b->ev[4], s));
+    return HBX_OK;
+  }
   if (b->n) {
     const uint64_t n = b->n;
     const uint64_t* d_cb = b->d_meta.as<uint64_t>() + 3 * n;
@@ -542,9 +558,90 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
   return md5_launch(c, b, budget);
 }
 
+// Plan + enqueue a VerifyBlock batch: K6p hashes each block's prefix blocks
+// and turns the rest into K3 chains, which then share the time-sliced MD5
+// pipeline (and the FIFO of hbx_wait) with the chunking batches.
+int submit_verify(hbx_ctx* c, const uint8_t* arena, uint64_t n, const uint64_t* offs, const uint64_t* lens,
+                  const uint8_t* links, const uint64_t* link_base, const uint32_t* n_links, uint8_t* ids,
+                  const uint8_t* expect, uint8_t* ok, uint64_t* n_bad, uint32_t budget) {
+  if (n > 0xFFFFFFFFull) return c->fail(HBX_ERR_ARG, "too many blocks");
+  uint64_t nlinks_total = 0, longest = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    const uint32_t nl = n_links ? n_links[i] : 0u;
+    if (nl && (!links || !link_base)) return c->fail(HBX_ERR_ARG, "links missing");
+    if (lens[i] + 8ull + 16ull * nl + 128ull > 0xFFFFFFFFull) return c->fail(HBX_ERR_ARG, "block too large");
+    if (nl) nlinks_total = std::max(nlinks_total, link_base[i] + nl);
+    longest = std::max<uint64_t>(longest, (lens[i] + 8ull + 16ull * nl) >> 6);
+  }
+  Batch* b = acquire_batch(c);
+  if (!b) return c->fail(HBX_ERR_HIP, "cannot create batch events");
+  b->verify = true;
+  b->n = n;
+  b->caps = n;
+  b->v_ids = ids;
+  b->v_expect = expect;
+  b->v_ok = ok;
+  b->v_nbad = n_bad;
+  b->need = budget == kBudgetAll ? 1u : (uint32_t)std::max<uint64_t>(1, (longest + budget - 1) / budget);
+  c->pending.push_back(b);
+  hipStream_t s = c->stream;
+  if (n == 0) {
+    for (int i = 0; i < 4; i++) HBX_TRY(c, hipEventRecord(b->ev[i], s));
+    b->finalized = true;
+    HBX_TRY(c, hipEventRecord(b->ev[4], s));
+    return HBX_OK;
+  }
+  // meta block: descriptors | links
+  const size_t meta_bytes = n * sizeof(VerifyDesc) + 16 * nlinks_total;
+  HBX_TRY(c, b->h_meta.ensure(meta_bytes));
+  HBX_TRY(c, b->d_meta.ensure(meta_bytes));
+  HBX_TRY(c, b->d_ids.ensure(n * 16));
+  HBX_TRY(c, b->d_run.ensure(n * sizeof(Chain)));
+  HBX_TRY(c, b->d_fresh.ensure(n * sizeof(OrderEntry)));
+  HBX_TRY(c, b->d_fcnt.ensure(256));
+  HBX_TRY(c, b->h_res.ensure(n * 16));
+  VerifyDesc* hd = b->h_meta.as<VerifyDesc>();
+  uint8_t* dl = b->d_meta.as<uint8_t>() + n * sizeof(VerifyDesc);
+  for (uint64_t i = 0; i < n; i++) {
+    const uint32_t nl = n_links ? n_links[i] : 0u;
+    hd[i].src = reinterpret_cast<uint64_t>(arena + offs[i]);
+    hd[i].links = reinterpret_cast<uint64_t>(dl + (nl ? 16 * link_base[i] : 0));
+    hd[i].len = (uint32_t)lens[i];
+    hd[i].n_links = nl;
+    hd[i].pad = 0;
+  }
+  if (nlinks_total) std::memcpy(b->h_meta.as<uint8_t>() + n * sizeof(VerifyDesc), links, 16 * nlinks_total);
+  HBX_TRY(c, hipEventRecord(b->ev[0], s));
+  HBX_TRY(c, hipMemcpyAsync(b->d_meta.p, b->h_meta.p, meta_bytes, hipMemcpyHostToDevice, s));
+  HBX_TRY(c, hipMemsetAsync(b->d_fcnt.p, 0, 4, s));
+  HBX_TRY(c, hipEventRecord(b->ev[1], s));
+  hipLaunchKernelGGL(hbx_k6p_verify_chains, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
+                     b->d_meta.as<VerifyDesc>(), (uint32_t)n, b->d_ids.as<uint32_t>(), b->d_run.as<Chain>(),
+                     b->d_fresh.as<OrderEntry>(), b->d_fcnt.as<uint32_t>());
+  HBX_TRY(c, hipGetLastError());
+  HBX_TRY(c, hipEventRecord(b->ev[2], s));
+  int rc = plan_launch(c, b, budget);
+  if (rc) return rc;
+  return md5_launch(c, b, budget);
+}
+
 // Scatter a collected batch's pinned results into the caller's arrays.
 int collect_batch(hbx_ctx* c, Batch* b) {
   const uint64_t n = b->n;
+  if (b->verify) {  // VerifyBlock: ids, and the comparison with the expected ids
+    const uint8_t* hid = b->h_res.as<uint8_t>();
+    if (b->v_ids && n) std::memcpy(b->v_ids, hid, n * 16);
+    uint64_t bad = 0;
+    if (b->v_expect) {
+      for (uint64_t i = 0; i < n; i++) {
+        const uint8_t good = std::memcmp(hid + 16 * i, b->v_expect + 16 * i, 16) == 0;
+        if (b->v_ok) b->v_ok[i] = good;
+        bad += good ? 0 : 1;
+      }
+    }
+    if (b->v_nbad) *b->v_nbad = bad;
+    return HBX_OK;
+  }
   const ResLayout rl = res_layout(n, b->caps);
   const uint8_t* hr = b->h_res.as<uint8_t>();
   const uint32_t* counts = reinterpret_cast<const uint32_t*>(hr + rl.counts);
@@ -1523,6 +1620,18 @@ int hbx_wire_encode_block_header(uint16_t num, uint32_t type, const uint8_t id[1
 int hbx_wire_parse(const uint8_t* in, uint64_t len, hbx_wire_msg* msg) {
   if (!msg || (len && !in)) return HBX_ERR_ARG;
   return hbxwire::parse(in, len, msg);
+}
+
+int hbx_verify_submit_device(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* offs,
+                             const uint64_t* lens, const uint8_t* links, const uint64_t* link_base,
+                             const uint32_t* n_links, uint8_t* ids, const uint8_t* expect, uint8_t* ok,
+                             uint64_t* n_bad) {
+  if (!c || (n && (!d_arena || !offs || !lens))) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  HBX_TRY(c, hipSetDevice(c->device));
+  if (n_bad) *n_bad = 0;
+  return submit_verify(c, static_cast<const uint8_t*>(d_arena), n, offs, lens, links, link_base, n_links, ids,
+                       expect, ok, n_bad, c->md5_slice ? c->md5_slice : kBudgetAll);
 }
 
 }  // extern "C"

@@ -1580,3 +1580,78 @@ extern "C" __global__ __launch_bounds__(64, 1) void hbx_k6_hash_blocks(
                         h[3] == expect[4u * i + 3u]);
   }
 }
+
+// Pipelined VerifyBlock (hbx_verify_submit_device): thread per block.  A
+// block's message is BE32(n) || links || BE32(len) || data; K3's chains hash
+// BE32(0) || BE32(len') || chunk'.  With chunk' = data - 16n and
+// len' = len + 16n the two agree from the first message block that holds no
+// prefix byte on, so this kernel hashes the prefix blocks byte by byte (as
+// K6) and hands the rest to the time-sliced K3 pipeline as an ordinary chain
+// starting at that block.  A block whose last partial message block still
+// holds prefix bytes is finished here.  Blocks without links are plain K3
+// chains from block 0.
+extern "C" __global__ __launch_bounds__(256) void hbx_k6p_verify_chains(
+    const VerifyDesc* __restrict__ desc, uint32_t n, uint32_t* __restrict__ ids, Chain* __restrict__ run,
+    OrderEntry* __restrict__ fresh, uint32_t* __restrict__ cnt) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  const VerifyDesc v = desc[i];
+  const uint32_t len = v.len, nl = v.n_links;
+  Chain ch;
+  ch.out = reinterpret_cast<uint64_t>(ids + 4u * i);
+  ch.pad = 0ull;
+  uint32_t rem;
+  if (nl == 0u) {
+    ch.src = v.src;
+    ch.len = len;
+    ch.next = 0u;
+    md5_init(ch.h);
+    rem = ((len + 8u) >> 6) + 1u;
+  } else {
+    const uint32_t p = 8u + 16u * nl;
+    const uint64_t T = (uint64_t)len + p;
+    const uint32_t nfull = (uint32_t)(T >> 6);
+    const uint32_t hb = (p + 63u) >> 6;
+    const bool fast = nfull >= hb;
+    const uint32_t nslow = fast ? hb : (uint32_t)((T + 8u) >> 6) + 1u;
+    const uint8_t* data = reinterpret_cast<const uint8_t*>(v.src);
+    const uint8_t* links = reinterpret_cast<const uint8_t*>(v.links);
+    uint32_t h[4];
+    md5_init(h);
+    for (uint32_t b = 0; b < nslow; b++) {
+      uint32_t m[16];
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const uint64_t o = 64ull * b + 4u * (uint32_t)j;
+        m[j] = k6_byte(o, nl, len, p, T, links, data) | (k6_byte(o + 1u, nl, len, p, T, links, data) << 8) |
+               (k6_byte(o + 2u, nl, len, p, T, links, data) << 16) |
+               (k6_byte(o + 3u, nl, len, p, T, links, data) << 24);
+      }
+      if (!fast && b + 1u == nslow) {
+        const uint64_t bits = T * 8ull;
+        m[14] = (uint32_t)bits;
+        m[15] = (uint32_t)(bits >> 32);
+      }
+      md5_compress(h, m);
+    }
+    if (!fast) {  // finished here
+      *reinterpret_cast<uint4*>(ids + 4u * i) = make_uint4(h[0], h[1], h[2], h[3]);
+      return;
+    }
+    ch.src = v.src - (p - 8u);
+    ch.len = len + p - 8u;
+    ch.next = hb;
+    ch.h[0] = h[0];
+    ch.h[1] = h[1];
+    ch.h[2] = h[2];
+    ch.h[3] = h[3];
+    rem = nfull - hb + 1u;
+  }
+  const uint32_t slot = atomicAdd(cnt, 1u);
+  run[slot] = ch;
+  OrderEntry o;
+  o.chain = reinterpret_cast<uint64_t>(run + slot);
+  o.rem = rem;
+  o.pad = 0u;
+  fresh[slot] = o;
+}

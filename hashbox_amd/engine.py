@@ -190,13 +190,46 @@ class Engine:
                                               _p(caps), sums), "hbx_submit_device")
         self._pending.append((offs, lens, caps, base, cuts, ids, sums))
 
-    def wait(self) -> List[FileChunks]:
-        """Results of the oldest submitted batch ([] if none is pending)."""
+    def wait(self):
+        """Results of the oldest submitted batch ([] if none is pending): a
+        list of FileChunks for a chunking batch, (ids, ok, n_bad) for a
+        verify batch."""
         if not self._pending:
             return []
-        offs, lens, caps, base, cuts, ids, sums = self._pending.popleft()
+        item = self._pending.popleft()
         self._check(self._L.hbx_wait(self._ctx), "hbx_wait")
+        if isinstance(item[0], str):  # ("verify", ...)
+            _, n, ids, ok, bad, keep = item
+            return ids[:n], (ok[:n].astype(bool) if keep[1] is not None else None), int(bad.value)
+        offs, lens, caps, base, cuts, ids, sums = item
         return self._unpack(lens, caps, base, cuts, ids, sums)
+
+    def verify_submit_device(self, d_arena: int, offs: Sequence[int], lens: Sequence[int],
+                             links: Optional[Sequence[Sequence[bytes]]] = None,
+                             expect: Optional[Sequence[bytes]] = None):
+        """Pipelined VerifyBlock of device-resident blocks (hbx_verify_submit_device):
+        returns at once; :meth:`wait` (FIFO with chunking batches) returns
+        (ids, ok, n_bad)."""
+        _sync_producer()
+        offs = np.ascontiguousarray(offs, np.uint64)
+        lens = np.ascontiguousarray(lens, np.uint64)
+        n = int(lens.size)
+        links_a, base, counts = self._links_arrays(links, n)
+        ids = np.zeros((max(n, 1), 16), np.uint8)
+        exp = None
+        if expect is not None:
+            exp = np.ascontiguousarray(np.frombuffer(b"".join(bytes(e) for e in expect), np.uint8))
+            if exp.size != 16 * n:
+                raise ValueError("expect must hold one 16-byte ID per block")
+        ok = np.zeros(max(n, 1), np.uint8)
+        bad = ctypes.c_uint64(0)
+        self._check(self._L.hbx_verify_submit_device(
+            self._ctx, ctypes.c_void_p(int(d_arena)), n, _p(offs), _p(lens),
+            _p(links_a) if links_a is not None else None, _p(base) if base is not None else None,
+            _p(counts) if counts is not None else None, _p(ids), _p(exp) if exp is not None else None,
+            _p(ok), ctypes.byref(bad)), "hbx_verify_submit_device")
+        # everything the library writes or reads until the wait stays alive here
+        self._pending.append(("verify", n, ids, ok, bad, (offs, exp, lens)))
 
     def pending(self) -> int:
         n = self._L.hbx_pending(self._ctx)

@@ -344,6 +344,19 @@ int hbx_wire_encode_block_header(uint16_t num, uint32_t type, const uint8_t id[1
  * an unknown type. */
 int hbx_wire_parse(const uint8_t *in, uint64_t len, hbx_wire_msg *msg);
 
+/* Pipelined VerifyBlock: the same inputs and outputs as
+ * hbx_verify_blocks_device, enqueued like hbx_submit_device and completed by
+ * hbx_wait in FIFO order with the chunking batches.  Each block's link prefix
+ * is hashed first; the rest of its message joins the time-sliced MD5 chains
+ * (hbx_set_md5_slice), so a bulk verification streams like the chunking path
+ * instead of waiting on one launch's longest block.  ids, expect, ok and
+ * n_bad must stay valid until the hbx_wait that completes the batch; links
+ * are copied at submit. */
+int hbx_verify_submit_device(hbx_ctx *ctx, const void *d_arena, uint64_t n, const uint64_t *offs,
+                             const uint64_t *lens, const uint8_t *links, const uint64_t *link_base,
+                             const uint32_t *n_links, uint8_t *ids, const uint8_t *expect,
+                             uint8_t *ok, uint64_t *n_bad);
+
 /* Device arena helpers (allocations include HBX_ARENA_SLACK). */
 int hbx_arena_alloc(hbx_ctx *ctx, uint64_t bytes, void **d_ptr);
 int hbx_arena_free(hbx_ctx *ctx, void *d_ptr);

@@ -77,3 +77,58 @@ def test_device_resident(engine, oracle):
     ids, ok, bad = engine.verify_blocks_device(dev.data_ptr(), offs, sizes, links, expect)
     assert bad == 0 and ok.all()
     assert [i.tobytes() for i in ids] == expect
+
+
+@pytest.mark.parametrize("md5_slice", [0, 3, 256])
+def test_pipelined_verify_with_chunking(oracle, md5_slice):
+    """hbx_verify_submit_device: verify batches share the time-sliced K3
+    pipeline and the wait FIFO with chunking batches; every edge length for
+    0-9 links, blocks past 8 MiB, expected-id mismatches."""
+    import torch
+    from hashbox_amd import Engine
+    rng = np.random.default_rng(77 + md5_slice)
+    lens = LENS + [(8 << 20) + 12345, 3 << 20]
+    specs = [(n, k) for k in (0, 1, 2, 3, 5, 9) for n in lens]
+    datas = [oracle.random_bytes(n, 31 * n + k + 1) for n, k in specs]
+    links = [_rand_links(rng, k) for _, k in specs]
+    want = [oracle.block_id(d, l) for d, l in zip(datas, links)]
+    expect = list(want)
+    for j in range(0, len(expect), 7):  # tampered expectations
+        expect[j] = bytes(16) if expect[j] != bytes(16) else b"\x01" * 16
+    offs, pos = [], 0
+    for d in datas:
+        offs.append(pos)
+        pos += (d.size + 255) // 256 * 256 + 256
+    host = np.zeros(pos + 65536, np.uint8)
+    for o, d in zip(offs, datas):
+        host[o:o + d.size] = d
+    arena = torch.from_numpy(host).to("cuda:0")
+    files = [oracle.random_bytes(3 << 20, 5), oracle.random_bytes(300_000, 6)]
+    fhost = np.zeros((4 << 20) + 300_000 + 65536, np.uint8)
+    fhost[:files[0].size] = files[0]
+    fhost[4 << 20:(4 << 20) + files[1].size] = files[1]
+    farena = torch.from_numpy(fhost).to("cuda:0")
+    torch.cuda.synchronize()
+    third = len(specs) // 3
+    with Engine(0, md5_slice=md5_slice) as eng:
+        eng.verify_submit_device(arena.data_ptr(), offs[:third], [d.size for d in datas[:third]],
+                                 links[:third], expect[:third])
+        eng.submit_device(farena.data_ptr(), [0, 4 << 20], [f.size for f in files])
+        eng.verify_submit_device(arena.data_ptr(), offs[third:], [d.size for d in datas[third:]],
+                                 links[third:], expect[third:])
+        eng.verify_submit_device(arena.data_ptr(), offs[:5], [d.size for d in datas[:5]])  # ids only
+        r1 = eng.wait()
+        rf = eng.wait()
+        r2 = eng.wait()
+        r3 = eng.wait()
+        assert eng.pending() == 0
+    ids = np.concatenate([r1[0], r2[0]])
+    ok = np.concatenate([r1[1], r2[1]])
+    for i in range(len(specs)):
+        assert ids[i].tobytes() == want[i], (i, specs[i])
+        assert bool(ok[i]) == (expect[i] == want[i])
+    assert r1[2] + r2[2] == sum(e != w for e, w in zip(expect, want))
+    assert r3[1] is None and all(r3[0][i].tobytes() == want[i] for i in range(5))
+    for f, r in zip(files, rf):
+        ref = oracle.store_file(f, fast=True)
+        assert np.array_equal(r.cut_ends, ref.cut_ends) and np.array_equal(r.ids, ref.ids)
