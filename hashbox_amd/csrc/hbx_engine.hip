@@ -30,6 +30,7 @@
 #include "../../include/hbxgpu.h"
 #include "hbx_kernels.hip"
 #include "hbx_deflate.hip"
+#include "hbx_inflate.hip"
 #include "hbx_formats.h"
 #include "hbx_wire.h"
 
@@ -172,6 +173,7 @@ struct hbx_ctx {
   DevBuf d_plan;            // chain planner: global bin counts + cursors
   DevBuf d_vdesc, d_vlinks, d_vout, d_vexp, d_zeros;  // hbx_verify_blocks*
   DevBuf d_zblk, d_zinfo, d_zoff, d_zlen, d_zout, d_zimg;  // hbx_deflate_blocks*
+  DevBuf d_idesc, d_ires;                                  // hbx_inflate_blocks_device
   PinBuf h_read[2];         // hbx_store_paths: pinned landing slots for file reads
   PinBuf h_zstage;          // hbx_store_paths_z: compressed streams of one batch
   hipEvent_t h2d_done[2] = {nullptr, nullptr};  // slot's H2D copy has completed
@@ -782,7 +784,7 @@ void hbx_ctx_destroy(hbx_ctx* c) {
                     &c->d_octl[0], &c->d_octl[1], &c->d_octl[2],
                     &c->d_stage, &c->d_msg, &c->d_plan, &c->d_vdesc, &c->d_vlinks,
                     &c->d_vout, &c->d_vexp, &c->d_zeros, &c->d_zblk, &c->d_zinfo, &c->d_zoff,
-                    &c->d_zlen, &c->d_zout, &c->d_zimg})
+                    &c->d_zlen, &c->d_zout, &c->d_zimg, &c->d_idesc, &c->d_ires})
     b->release();
   for (PinBuf& h : c->h_read) h.release();
   c->h_zstage.release();
@@ -1632,6 +1634,50 @@ int hbx_verify_submit_device(hbx_ctx* c, const void* d_arena, uint64_t n, const 
   if (n_bad) *n_bad = 0;
   return submit_verify(c, static_cast<const uint8_t*>(d_arena), n, offs, lens, links, link_base, n_links, ids,
                        expect, ok, n_bad, c->md5_slice ? c->md5_slice : kBudgetAll);
+}
+
+// ---- zlib inflate (hbx_inflate.hip) -----------------------------------------
+int hbx_inflate_blocks_device(hbx_ctx* c, const void* d_in, uint64_t n, const uint64_t* in_offs,
+                              const uint64_t* in_lens, void* d_out, const uint64_t* out_offs,
+                              const uint64_t* out_caps, uint64_t* out_lens, uint32_t* status) {
+  if (!c || (n && (!d_in || !in_offs || !in_lens || !d_out || !out_offs || !out_caps || !out_lens || !status)))
+    return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
+  if (n == 0) return HBX_OK;
+  if (n > 0xFFFFFFFFull) return c->fail(HBX_ERR_ARG, "too many streams");
+  HBX_TRY(c, hipSetDevice(c->device));
+  // longest stream first: a wave's 64 lanes then decode about equally long streams
+  std::vector<uint32_t> perm(n);
+  for (uint64_t i = 0; i < n; i++) {
+    if (in_lens[i] > 0xFFFFFFFFull || out_caps[i] > 0xFFFFFFFFull) return c->fail(HBX_ERR_ARG, "stream too large");
+    perm[i] = (uint32_t)i;
+  }
+  std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) { return in_lens[a] > in_lens[b]; });
+  std::vector<InflateDesc> desc(n);
+  for (uint64_t k = 0; k < n; k++) {
+    const uint32_t i = perm[k];
+    desc[k].src = reinterpret_cast<uint64_t>(d_in) + in_offs[i];
+    desc[k].dst = reinterpret_cast<uint64_t>(d_out) + out_offs[i];
+    desc[k].len = (uint32_t)in_lens[i];
+    desc[k].cap = (uint32_t)out_caps[i];
+  }
+  hipStream_t s = c->stream;
+  HBX_TRY(c, c->d_idesc.ensure(n * sizeof(InflateDesc)));
+  HBX_TRY(c, c->d_ires.ensure(n * 8));
+  HBX_TRY(c, hipMemcpyAsync(c->d_idesc.p, desc.data(), n * sizeof(InflateDesc), hipMemcpyHostToDevice, s));
+  uint32_t* dres = c->d_ires.as<uint32_t>();
+  hipLaunchKernelGGL(hbx_k8_inflate, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, s, c->d_idesc.as<InflateDesc>(),
+                     (uint32_t)n, dres, dres + n);
+  HBX_TRY(c, hipGetLastError());
+  std::vector<uint32_t> res(2 * n);
+  HBX_TRY(c, hipMemcpyAsync(res.data(), dres, n * 8, hipMemcpyDeviceToHost, s));
+  HBX_TRY(c, hipStreamSynchronize(s));
+  for (uint64_t k = 0; k < n; k++) {
+    out_lens[perm[k]] = res[k];
+    status[perm[k]] = res[n + k];
+  }
+  return HBX_OK;
 }
 
 }  // extern "C"

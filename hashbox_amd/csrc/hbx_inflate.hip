@@ -1,0 +1,329 @@
+// hbx_inflate.hip — zlib inflate on gfx950, one lane per stream (the read
+// side of SURVEY §8f2/§8f4).
+//
+// Reference: HashboxBlock.UncompressData / zlibUncompress (pkg/core/
+// block.go:113-131, 186-201) before VerifyBlock hashes a stored block
+// (block.go:152-174): restore (hashback/restore.go:52, 256), the server's
+// write check (server/server.go:182), verify -content (pkg/storagedb/
+// integrity.go:117, 282).  The streams come from Go's compress/zlib (or from
+// K7), so this is a general RFC 1950/1951 decoder: stored, fixed and dynamic
+// blocks, any window distance.
+//
+// A stream is serial, so a lane decodes one stream (64 per wave; the host
+// sorts streams longest first).  Huffman decoding is canonical: per code
+// length l, `cnt[l]` codes follow the first code of that length, and the
+// symbols of each table are listed in code order (RFC 1951 §3.2.2), as in
+// zlib's contrib/puff; the tables live in LDS per lane.  Every read and write
+// is bounds-checked: a corrupt stream sets its status and stops, it never
+// touches memory outside its input and output.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace hbxi {
+
+constexpr uint32_t kLanes = 64;
+constexpr uint32_t kLenSyms = 288, kDistSyms = 32;
+
+// status codes (out_status)
+constexpr uint32_t kOk = 0, kErrHeader = 1, kErrInput = 2, kErrOutput = 3, kErrCode = 4, kErrDist = 5,
+                   kErrStored = 6;
+
+struct LaneTables {
+  uint16_t lcnt[16], dcnt[16], offs[16];
+  uint16_t lsym[kLenSyms];
+  uint16_t dsym[kDistSyms];
+  uint8_t lens[320];  // code lengths while a dynamic table is built
+  uint8_t dlens[32];
+};
+
+__device__ const uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
+                                          31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+__device__ const uint8_t kOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+struct Bits {
+  const uint8_t* start;
+  const uint8_t* p;  // next byte to load (may run past `end`: zeros are loaded)
+  const uint8_t* end;
+  uint64_t buf;
+  uint32_t n;  // bits in buf
+  __device__ __forceinline__ void fill() {
+    while (n <= 56u) {
+      const uint32_t b = p < end ? (uint32_t)*p : 0u;
+      p++;
+      buf |= (uint64_t)b << n;
+      n += 8u;
+    }
+  }
+  // more bits consumed than the input holds (the look-ahead alone is fine)
+  __device__ __forceinline__ bool overrun() const {
+    return 8ull * (uint64_t)(p - start) - n > 8ull * (uint64_t)(end - start);
+  }
+  __device__ __forceinline__ uint32_t get(uint32_t k) {  // k <= 32
+    if (n < k) fill();
+    const uint32_t v = (uint32_t)(buf & ((1ull << k) - 1ull));
+    buf >>= k;
+    n -= k;
+    return v;
+  }
+  __device__ __forceinline__ void align_byte() {
+    const uint32_t k = n & 7u;
+    buf >>= k;
+    n -= k;
+  }
+};
+
+// Canonical decode: codes are read MSB-first, one bit at a time (puff's
+// `decode`).  Returns the symbol, or -1 for an invalid code.
+__device__ __forceinline__ int decode(Bits& br, const uint16_t* cnt, const uint16_t* sym) {
+  int code = 0, first = 0, index = 0;
+  if (br.n < 16u) br.fill();
+  for (int len = 1; len <= 15; len++) {
+    code |= (int)(br.buf & 1u);
+    br.buf >>= 1;
+    br.n--;
+    const int count = cnt[len];
+    if (code - count < first) return sym[index + (code - first)];
+    index += count;
+    first += count;
+    first <<= 1;
+    code <<= 1;
+  }
+  return -1;
+}
+
+// Tables from code lengths (puff's `construct`); returns false for an
+// over-subscribed set.  Incomplete sets are allowed (the decoder then meets an
+// invalid code only on corrupt input).
+__device__ __forceinline__ bool construct(uint16_t* cnt, uint16_t* sym, uint16_t* offs, const uint8_t* lens,
+                                          int n) {
+  for (int l = 0; l < 16; l++) cnt[l] = 0;
+  for (int s = 0; s < n; s++) cnt[lens[s]]++;
+  if (cnt[0] == n) return true;
+  int left = 1;
+  for (int l = 1; l < 16; l++) {
+    left <<= 1;
+    left -= cnt[l];
+    if (left < 0) return false;
+  }
+  offs[1] = 0;
+  for (int l = 1; l < 15; l++) offs[l + 1] = (uint16_t)(offs[l] + cnt[l]);
+  for (int s = 0; s < n; s++)
+    if (lens[s]) sym[offs[lens[s]]++] = (uint16_t)s;
+  return true;
+}
+
+__device__ __forceinline__ uint32_t len_base(uint32_t s) { return kLenBase[s]; }  // s = symbol - 257, 0..28
+__device__ __forceinline__ uint32_t len_extra(uint32_t s) {
+  return s < 8u ? 0u : s == 28u ? 0u : (s - 4u) >> 2;
+}
+__device__ __forceinline__ uint32_t dist_base(uint32_t s) {  // 0..29
+  return s < 4u ? s + 1u : ((2u + (s & 1u)) << ((s >> 1) - 1u)) + 1u;
+}
+__device__ __forceinline__ uint32_t dist_extra(uint32_t s) { return s < 4u ? 0u : (s >> 1) - 1u; }
+
+}  // namespace hbxi
+
+struct InflateDesc {
+  uint64_t src;   // device address of the zlib stream
+  uint64_t dst;   // device address of the output
+  uint32_t len;   // stream bytes
+  uint32_t cap;   // output capacity
+};
+
+// One lane per stream.  out_len[i] = inflated bytes, status[i] = 0 or an
+// hbxi::kErr* code.
+extern "C" __global__ __launch_bounds__(64) void hbx_k8_inflate(const InflateDesc* __restrict__ desc, uint32_t n,
+                                                                 uint32_t* __restrict__ out_len,
+                                                                 uint32_t* __restrict__ status) {
+  using namespace hbxi;
+  __shared__ LaneTables tabs[kLanes];
+  const uint32_t i = blockIdx.x * 64u + threadIdx.x;
+  if (i >= n) return;
+  LaneTables& T = tabs[threadIdx.x];
+  const InflateDesc d = desc[i];
+  const uint8_t* in = reinterpret_cast<const uint8_t*>(d.src);
+  uint8_t* out = reinterpret_cast<uint8_t*>(d.dst);
+  Bits br{in, in, in + d.len, 0ull, 0u};
+  uint32_t o = 0u, st = kOk;
+  // zlib header (RFC 1950 §2.2): deflate, 32 KiB window at most, check bits, no dictionary
+  const uint32_t cmf = br.get(8), flg = br.get(8);
+  if ((cmf & 15u) != 8u || (cmf >> 4) > 7u || ((cmf << 8) | flg) % 31u != 0u || (flg & 0x20u)) st = kErrHeader;
+  bool last = st != kOk;
+  while (!last) {
+    last = br.get(1) != 0u;
+    const uint32_t type = br.get(2);
+    if (type == 0u) {  // stored
+      br.align_byte();
+      const uint32_t L = br.get(16), NL = br.get(16);
+      if ((L ^ 0xFFFFu) != NL) {
+        st = kErrStored;
+        break;
+      }
+      // the bit buffer holds whole bytes now: drain it first, then copy
+      uint32_t k = 0;
+      for (; k < L && br.n >= 8u; k++) {
+        if (o >= d.cap) break;
+        out[o++] = (uint8_t)br.get(8);
+      }
+      if (k < L) {
+        if (o + (L - k) > d.cap) {
+          st = kErrOutput;
+          break;
+        }
+        if (br.p + (L - k) > br.end) {
+          st = kErrInput;
+          break;
+        }
+        for (uint32_t j = 0; j < L - k; j++) out[o + j] = br.p[j];
+        o += L - k;
+        br.p += L - k;
+      }
+      if (br.overrun()) {
+        st = kErrInput;
+        break;
+      }
+      continue;
+    }
+    if (type == 3u) {
+      st = kErrCode;
+      break;
+    }
+    if (type == 1u) {  // fixed codes (RFC 1951 §3.2.6)
+      for (int s = 0; s < 144; s++) T.lens[s] = 8;
+      for (int s = 144; s < 256; s++) T.lens[s] = 9;
+      for (int s = 256; s < 280; s++) T.lens[s] = 7;
+      for (int s = 280; s < 288; s++) T.lens[s] = 8;
+      construct(T.lcnt, T.lsym, T.offs, T.lens, 288);
+      for (int s = 0; s < 30; s++) T.lens[s] = 5;
+      construct(T.dcnt, T.dsym, T.offs, T.lens, 30);
+    } else {  // dynamic (RFC 1951 §3.2.7)
+      const uint32_t nlen = br.get(5) + 257u, ndist = br.get(5) + 1u, ncode = br.get(4) + 4u;
+      if (nlen > 286u || ndist > 30u) {
+        st = kErrCode;
+        break;
+      }
+      for (int s = 0; s < 19; s++) T.lens[s] = 0;
+      for (uint32_t s = 0; s < ncode; s++) T.lens[kOrder[s]] = (uint8_t)br.get(3);
+      if (!construct(T.lcnt, T.lsym, T.offs, T.lens, 19)) {
+        st = kErrCode;
+        break;
+      }
+      uint32_t idx = 0;
+      bool bad = false;
+      while (idx < nlen + ndist) {
+        int sym = decode(br, T.lcnt, T.lsym);
+        if (sym < 0) {
+          bad = true;
+          break;
+        }
+        if (sym < 16) {
+          T.lens[idx++] = (uint8_t)sym;
+        } else {
+          uint32_t rep, v = 0u;
+          if (sym == 16) {
+            if (idx == 0u) {
+              bad = true;
+              break;
+            }
+            v = T.lens[idx - 1u];
+            rep = 3u + br.get(2);
+          } else if (sym == 17) {
+            rep = 3u + br.get(3);
+          } else {
+            rep = 11u + br.get(7);
+          }
+          if (idx + rep > nlen + ndist) {
+            bad = true;
+            break;
+          }
+          while (rep--) T.lens[idx++] = (uint8_t)v;
+        }
+      }
+      if (bad || T.lens[256] == 0u) {
+        st = kErrCode;
+        break;
+      }
+      // distance lengths first (they sit after the literal/length ones in lens)
+      for (uint32_t s = 0; s < 30u; s++) T.dlens[s] = s < ndist ? T.lens[nlen + s] : 0u;
+      for (uint32_t s = nlen; s < 288u; s++) T.lens[s] = 0u;
+      if (!construct(T.lcnt, T.lsym, T.offs, T.lens, 288)) {
+        st = kErrCode;
+        break;
+      }
+      if (!construct(T.dcnt, T.dsym, T.offs, T.dlens, 30)) {
+        st = kErrCode;
+        break;
+      }
+    }
+    // the block's symbols
+    for (;;) {
+      const int sym = decode(br, T.lcnt, T.lsym);
+      if (sym < 0) {
+        st = kErrCode;
+        break;
+      }
+      if (sym < 256) {
+        if (o >= d.cap) {
+          st = kErrOutput;
+          break;
+        }
+        out[o++] = (uint8_t)sym;
+      } else if (sym == 256) {
+        break;
+      } else {
+        const uint32_t ls = (uint32_t)sym - 257u;
+        if (ls >= 29u) {
+          st = kErrCode;
+          break;
+        }
+        const uint32_t len = len_base(ls) + br.get(len_extra(ls));
+        const int ds = decode(br, T.dcnt, T.dsym);
+        if (ds < 0 || ds >= 30) {
+          st = kErrCode;
+          break;
+        }
+        const uint32_t dist = dist_base((uint32_t)ds) + br.get(dist_extra((uint32_t)ds));
+        if (dist > o) {
+          st = kErrDist;
+          break;
+        }
+        if (o + len > d.cap) {
+          st = kErrOutput;
+          break;
+        }
+        for (uint32_t j = 0; j < len; j++) out[o + j] = out[o + j - dist];
+        o += len;
+      }
+    }
+    if (st != kOk) break;
+    if (br.overrun()) {
+      st = kErrInput;
+      break;
+    }
+  }
+  if (st == kOk) {  // Adler-32 trailer (RFC 1950 §2.2), checked against the output
+    br.align_byte();
+    const uint32_t a1 = br.get(8), a2 = br.get(8), a3 = br.get(8), a4 = br.get(8);
+    const uint32_t want = (a1 << 24) | (a2 << 16) | (a3 << 8) | a4;
+    if (br.overrun()) {
+      st = kErrInput;
+    } else {
+      uint32_t a = 1u, b = 0u;
+      for (uint32_t j = 0; j < o;) {
+        const uint32_t stop = min(o, j + 5552u);  // zlib's NMAX: no overflow before the modulo
+        for (; j < stop; j++) {
+          a += out[j];
+          b += a;
+        }
+        a %= 65521u;
+        b %= 65521u;
+      }
+      if (((b << 16) | a) != want) st = kErrHeader;
+    }
+  }
+  out_len[i] = o;
+  status[i] = st;
+}

@@ -354,6 +354,49 @@ class Engine:
                                                       _p(oc), _p(olen)), "hbx_deflate_blocks_device")
         return olen[:lens.size]
 
+    def inflate_blocks_device(self, d_in: int, in_offs: Sequence[int], in_lens: Sequence[int], d_out: int,
+                              out_offs: Sequence[int], out_caps: Sequence[int]):
+        """HashboxBlock.UncompressData (block.go:113-131) of many zlib streams on
+        the device: returns (out_lens, status) (status 0 = ok)."""
+        _sync_producer()
+        io = np.ascontiguousarray(in_offs, np.uint64)
+        il = np.ascontiguousarray(in_lens, np.uint64)
+        oo = np.ascontiguousarray(out_offs, np.uint64)
+        oc = np.ascontiguousarray(out_caps, np.uint64)
+        n = int(il.size)
+        ol = np.zeros(max(n, 1), np.uint64)
+        st = np.zeros(max(n, 1), np.uint32)
+        self._check(self._L.hbx_inflate_blocks_device(self._ctx, ctypes.c_void_p(int(d_in)), n, _p(io), _p(il),
+                                                      ctypes.c_void_p(int(d_out)), _p(oo), _p(oc), _p(ol),
+                                                      _p(st)), "hbx_inflate_blocks_device")
+        return ol[:n], st[:n]
+
+    def inflate_blocks(self, streams: Sequence[BytesLike], caps: Sequence[int]):
+        """Host convenience: inflate zlib streams on the device; returns
+        (list of bytes or None per stream, status array)."""
+        import torch
+        arrs = [_u8(z) for z in streams]
+        n = len(arrs)
+        if n == 0:
+            return [], np.zeros(0, np.uint32)
+        io = np.zeros(n, np.uint64)
+        pos = 0
+        for i, a in enumerate(arrs):
+            io[i] = pos
+            pos += (a.size + 255) // 256 * 256
+        host = np.zeros(pos + 64, np.uint8)
+        for i, a in enumerate(arrs):
+            host[int(io[i]):int(io[i]) + a.size] = a
+        oc = np.ascontiguousarray(caps, np.uint64)
+        oo = np.zeros(n, np.uint64)
+        oo[1:] = np.cumsum((oc[:-1] + 255) // 256 * 256)
+        d_in = torch.from_numpy(host).to("cuda:0")
+        d_out = torch.zeros(int(oo[-1] + oc[-1]) + 64, dtype=torch.uint8, device="cuda:0")
+        torch.cuda.synchronize()
+        ol, st = self.inflate_blocks_device(d_in.data_ptr(), io, [a.size for a in arrs], d_out.data_ptr(), oo, oc)
+        out = d_out.cpu().numpy()
+        return [out[int(oo[i]):int(oo[i] + ol[i])].tobytes() if st[i] == 0 else None for i in range(n)], st
+
     def memcpy_h2d_async(self, d_dst: int, h_src: int, nbytes: int):
         """Enqueue an H2D copy on this engine's stream (pinned source)."""
         self._check(self._L.hbx_memcpy_h2d_async(self._ctx, ctypes.c_void_p(int(d_dst)),

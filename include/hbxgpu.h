@@ -25,6 +25,7 @@
  *   hbx_chain_block_*,    Serialize + Unserialize (hashback/hashback.go:80-214)
  *   hbx_directory_block_* and storeDir's block id (store.go:201-234)
  *   hbx_deflate_blocks    HashboxBlock.CompressData, zlib (block.go:133-184)
+ *   hbx_inflate_blocks_device  UncompressData (block.go:113-131), on the device
  *   hbx_wire_*            allo/READ/writ/ACKN framing (pkg/core/protocol.go)
  *
  * Conventions
@@ -356,6 +357,20 @@ int hbx_verify_submit_device(hbx_ctx *ctx, const void *d_arena, uint64_t n, cons
                              const uint64_t *lens, const uint8_t *links, const uint64_t *link_base,
                              const uint32_t *n_links, uint8_t *ids, const uint8_t *expect,
                              uint8_t *ok, uint64_t *n_bad);
+
+/* HashboxBlock.UncompressData for zlib blocks (pkg/core/block.go:113-131,
+ * 186-201), many streams at once on the device: stream i =
+ * d_in[in_offs[i] .. +in_lens[i]) inflates into d_out[out_offs[i] ..] (at most
+ * out_caps[i] bytes); out_lens[i] (host) = inflated bytes, status[i] (host) =
+ * 0, or 1 bad header / Adler-32, 2 truncated input, 3 output capacity,
+ * 4 invalid code, 5 distance too far back, 6 bad stored length.  Any RFC
+ * 1950 stream (Go's compress/zlib, K7's).  A corrupt stream only sets its
+ * status.  Then hbx_verify_blocks_device / hbx_verify_submit_device on the
+ * output is VerifyBlock of compressed blocks (block.go:152-166).
+ * Synchronous; refused (HBX_ERR_STATE) while batches are pending. */
+int hbx_inflate_blocks_device(hbx_ctx *ctx, const void *d_in, uint64_t n, const uint64_t *in_offs,
+                              const uint64_t *in_lens, void *d_out, const uint64_t *out_offs,
+                              const uint64_t *out_caps, uint64_t *out_lens, uint32_t *status);
 
 /* Device arena helpers (allocations include HBX_ARENA_SLACK). */
 int hbx_arena_alloc(hbx_ctx *ctx, uint64_t bytes, void **d_ptr);
