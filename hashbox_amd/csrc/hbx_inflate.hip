@@ -124,6 +124,37 @@ __device__ __forceinline__ uint32_t dist_base(uint32_t s) {  // 0..29
 }
 __device__ __forceinline__ uint32_t dist_extra(uint32_t s) { return s < 4u ? 0u : (s >> 1) - 1u; }
 
+// Non-overlapping copy, 16 independent byte loads in flight per step (the
+// byte-at-a-time loop serialised on the possible aliasing of in and out).
+__device__ __forceinline__ void copy_bytes(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t n) {
+  uint32_t j = 0;
+  for (; j + 16u <= n; j += 16u) {
+    uint8_t t[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) t[q] = src[j + q];
+#pragma unroll
+    for (int q = 0; q < 16; q++) dst[j + q] = t[q];
+  }
+  for (; j < n; j++) dst[j] = src[j];
+}
+
+// LZ77 copy of len bytes from dist back (dist <= bytes already written; the
+// source may overlap the destination: then byte by byte)
+__device__ __forceinline__ void copy_match(uint8_t* out, uint32_t dist, uint32_t len) {
+  const uint8_t* src = out - dist;  // pointer arithmetic: never an unsigned wrap
+  uint32_t j = 0;
+  if (dist >= 16u) {
+    for (; j + 16u <= len; j += 16u) {
+      uint8_t t[16];
+#pragma unroll
+      for (int q = 0; q < 16; q++) t[q] = src[j + q];
+#pragma unroll
+      for (int q = 0; q < 16; q++) out[j + q] = t[q];
+    }
+  }
+  for (; j < len; j++) out[j] = src[j];
+}
+
 }  // namespace hbxi
 
 struct InflateDesc {
@@ -177,7 +208,7 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k8_inflate(const InflateDes
           st = kErrInput;
           break;
         }
-        for (uint32_t j = 0; j < L - k; j++) out[o + j] = br.p[j];
+        copy_bytes(out + o, br.p, L - k);
         o += L - k;
         br.p += L - k;
       }
@@ -294,7 +325,7 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k8_inflate(const InflateDes
           st = kErrOutput;
           break;
         }
-        for (uint32_t j = 0; j < len; j++) out[o + j] = out[o + j - dist];
+        copy_match(out + o, dist, len);
         o += len;
       }
     }

@@ -42,3 +42,8 @@ def compress_ref_mt(blocks: Sequence[bytes], threads: int, level: int = LEVEL_DE
     """zlib releases the GIL while compressing, so threads scale."""
     with ThreadPoolExecutor(threads) as ex:
         return list(ex.map(lambda b: zlib.compress(b, level), blocks))
+
+
+def inflate_mt(streams: Sequence[bytes], threads: int) -> List[bytes]:
+    with ThreadPoolExecutor(threads) as ex:
+        return list(ex.map(zlib.decompress, streams))

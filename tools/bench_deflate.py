@@ -81,7 +81,25 @@ def run_corpus(eng, torch, name, host_or_dev, file_bytes, nfiles, sample, thread
     t_cpu = time.perf_counter() - t0
     s_in = sum(len(b) for b in blocks)
     s_gpu = sum(int(lens[i]) for i in pick)
+    # device inflate of the device's own streams (every chunk), checked on the sample
+    icap = c_len.copy()
+    i_off = np.zeros_like(icap)
+    i_off[1:] = np.cumsum(icap[:-1])
+    back = torch.empty(int(icap.sum()) + 64, dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ilen, ist = eng.inflate_blocks_device(out.data_ptr(), o_off, lens, back.data_ptr(), i_off, icap)
+    t_inf = time.perf_counter() - t0
+    ib = back.cpu().numpy()
+    ibad = int((ist != 0).sum()) + sum(ib[int(i_off[i]):int(i_off[i] + ilen[i])].tobytes() != b
+                                       for i, b in zip(pick, blocks))
+    t0 = time.perf_counter()
+    OD.inflate_mt([host_out[int(o_off[i]): int(o_off[i] + lens[i])].tobytes() for i in pick], threads)
+    t_cinf = time.perf_counter() - t0
     return {
+        "inflate_device": {"seconds": round(t_inf, 4), "gbs_out": round(total_in / t_inf / 1e9, 2),
+                           "streams": int(c_off.size), "failures_or_mismatches": ibad,
+                           "cpu_zlib_inflate_gbs_out": round(s_in / t_cinf / 1e9, 3), "cpu_threads": threads},
         "chunks": int(c_off.size), "bytes_in": total_in, "bytes_out": total_out,
         "ratio": round(total_out / total_in, 4), "seconds": round(t, 4),
         "gbs": round(total_in / t / 1e9, 2), "gibs": round(total_in / t / 2**30, 2),
