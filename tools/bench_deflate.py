@@ -132,9 +132,45 @@ def main():
         torch.cuda.empty_cache()
         txt = text_corpus(8 * fb, 5)
         out["text"] = run_corpus(eng, torch, "text", txt, fb, 8, a.sample, a.threads)
+        out["inflate_many_small"] = inflate_many(eng, torch, txt, a.threads)
     finally:
         eng.close()
     print(json.dumps(out), flush=True)
+
+
+def inflate_many(eng, torch, txt, threads, n=65536, size=16384):
+    """Many small zlib -6 streams (the stand-in for Go-compressed stored
+    blocks): K8 with one lane per stream vs CPython zlib on `threads`."""
+    import zlib
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import deflate as OD
+    rng = np.random.default_rng(9)
+    starts = rng.integers(0, txt.size - size, n)
+    raw = [txt[int(s0):int(s0) + size].tobytes() for s0 in starts]
+    with ThreadPoolExecutor(threads) as ex:
+        zs = list(ex.map(lambda b: zlib.compress(b, 6), raw))
+    io = np.zeros(n, np.uint64)
+    io[1:] = np.cumsum([(len(z) + 15) // 16 * 16 for z in zs[:-1]])
+    host = np.zeros(int(io[-1]) + len(zs[-1]) + 64, np.uint8)
+    for o, z in zip(io, zs):
+        host[int(o):int(o) + len(z)] = np.frombuffer(z, np.uint8)
+    d_in = torch.from_numpy(host).to("cuda:0")
+    oo = np.arange(n, dtype=np.uint64) * np.uint64(size)
+    d_out = torch.empty(n * size + 64, dtype=torch.uint8, device="cuda:0")
+    caps = np.full(n, size, np.uint64)
+    torch.cuda.synchronize()
+    eng.inflate_blocks_device(d_in.data_ptr(), io[:64], [len(z) for z in zs[:64]], d_out.data_ptr(), oo[:64], caps[:64])
+    t0 = time.perf_counter()
+    ol, st = eng.inflate_blocks_device(d_in.data_ptr(), io, [len(z) for z in zs], d_out.data_ptr(), oo, caps)
+    t = time.perf_counter() - t0
+    back = d_out.cpu().numpy()
+    bad = int((st != 0).sum()) + sum(back[i * size:(i + 1) * size].tobytes() != raw[i] for i in range(0, n, 97))
+    t0 = time.perf_counter()
+    OD.inflate_mt(zs, threads)
+    t_cpu = time.perf_counter() - t0
+    return {"streams": n, "stream_bytes": size, "compressed_bytes": int(sum(map(len, zs))),
+            "seconds": round(t, 4), "gbs_out": round(n * size / t / 1e9, 2), "failures_or_mismatches": bad,
+            "cpu_zlib_inflate": {"threads": threads, "gbs_out": round(n * size / t_cpu / 1e9, 3)}}
 
 
 if __name__ == "__main__":
