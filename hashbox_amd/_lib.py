@@ -30,7 +30,7 @@ EXPORTS = [
     "hbx_deflate_bound", "hbx_deflate_blocks_device", "hbx_deflate_blocks",
     "hbx_deflate_file_bound", "hbx_store_paths_z",
     "hbx_wire_encode_id", "hbx_wire_encode_block_header", "hbx_wire_parse",
-    "hbx_verify_submit_device", "hbx_inflate_blocks_device",
+    "hbx_verify_submit_device", "hbx_inflate_blocks_device", "hbx_store_paths_zcb",
 ]
 # Functions returning something other than an int status.
 _NON_STATUS = ("hbx_ctx_destroy", "hbx_last_error", "hbx_max_chunks", "hbx_file_entry_size",
@@ -135,6 +135,7 @@ def load() -> ctypes.CDLL:
     L.hbx_wire_encode_block_header.argtypes = [ctypes.c_uint16, ctypes.c_uint32, P, P, ctypes.c_uint32,
                                                ctypes.c_uint8, ctypes.c_uint32, P, U64, PU64]
     L.hbx_wire_parse.argtypes = [P, U64, P]
+    L.hbx_store_paths_zcb.argtypes = [P, U64, P, P, P, P, P, P, P, ctypes.c_uint32, U64, P, P, P, P, P, P]
     L.hbx_inflate_blocks_device.argtypes = [P, P, U64, P, P, P, P, P, P, P]
     L.hbx_verify_submit_device.argtypes = [P, P, U64, P, P, P, P, P, P, P, P, PU64]
     L.hbx_store_paths_z.argtypes = [P, U64, P, P, P, P, P, P, P, ctypes.c_uint32, U64, P, P, P, P]

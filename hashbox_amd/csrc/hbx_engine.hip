@@ -1158,6 +1158,8 @@ struct ZOut {
   const uint64_t* zbase = nullptr;
   uint64_t* zoff = nullptr;
   uint64_t* zlen = nullptr;
+  hbx_batch_ready_fn ready = nullptr;  // called once a batch's results are all written
+  void* user = nullptr;
 };
 // A collected batch whose device arena still holds its files.
 struct ZJob {
@@ -1248,7 +1250,20 @@ int hbx_store_paths_z(hbx_ctx* c, uint64_t n, const char* const* paths, const ui
     return HBX_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   return store_paths_impl(c, n, paths, lens, cut_ends, ids, out_base, caps, sums, io_threads, batch_bytes,
-                          ZOut{zout, zbase, zoff, zlen});
+                          ZOut{zout, zbase, zoff, zlen, nullptr, nullptr});
+}
+
+int hbx_store_paths_zcb(hbx_ctx* c, uint64_t n, const char* const* paths, const uint64_t* lens,
+                        uint64_t* cut_ends, uint8_t* ids, const uint64_t* out_base, const uint64_t* caps,
+                        hbx_file_summary* sums, uint32_t io_threads, uint64_t batch_bytes, uint8_t* zout,
+                        const uint64_t* zbase, uint64_t* zoff, uint64_t* zlen, hbx_batch_ready_fn ready,
+                        void* user) {
+  if (!c) return HBX_ERR_ARG;
+  if (n && (!paths || !lens || !out_base || !caps || !sums || !zout || !zbase || !zoff || !zlen))
+    return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  return store_paths_impl(c, n, paths, lens, cut_ends, ids, out_base, caps, sums, io_threads, batch_bytes,
+                          ZOut{zout, zbase, zoff, zlen, ready, user});
 }
 
 namespace {
@@ -1299,6 +1314,7 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
     int r = wait_oldest(c);
     if (z.zout) {
       if (!r && !jobs.empty()) r = deflate_batch(c, jobs.front(), cut_ends, out_base, sums, z, io_threads);
+      if (!r && !jobs.empty() && z.ready) z.ready(z.user, jobs.front().first, jobs.front().count);
       if (!jobs.empty()) jobs.pop_front();
     }
     return r;

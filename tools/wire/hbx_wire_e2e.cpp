@@ -1,6 +1,7 @@
 // hbx_wire_e2e — the client's whole send path over a real socket (SURVEY
-// §8f3): files on disk -> hbx_store_paths_z (rollsum split, block ids and a
-// zlib stream per chunk on the GPU) -> the StoreBlock exchange of
+// §8d config 5, §8f3): files on disk -> hbx_store_paths_zcb (rollsum split,
+// block ids and a zlib stream per chunk on the GPU; a callback per collected
+// batch) -> the StoreBlock exchange of
 // pkg/core/client.go:563-584 over loopback TCP to an in-process sink that
 // answers like the server (server/server.go:160-202):
 //
@@ -193,28 +194,9 @@ int main(int argc, char** argv) {
   hbx_store_paths_z(ctx, std::min<uint64_t>(n, 64), paths.data(), lens.data(), cuts.data(), ids.data(),
                     base.data(), caps.data(), sums.data(), io_threads, 1ull << 30, zout.data(), zbase.data(),
                     zoff.data(), zlen.data());
-  const double t0 = now();
-  int rc = hbx_store_paths_z(ctx, n, paths.data(), lens.data(), cuts.data(), ids.data(), base.data(),
-                             caps.data(), sums.data(), io_threads, 1ull << 30, zout.data(), zbase.data(),
-                             zoff.data(), zlen.data());
-  const double t1 = now();
-  if (rc != HBX_OK) {
-    std::fprintf(stderr, "hbx_store_paths_z: %s\n", hbx_last_error(ctx));
-    return 1;
-  }
-  std::vector<Block> blocks;
-  uint64_t zbytes = 0;
-  for (uint64_t f = 0; f < n; f++) {
-    uint64_t start = 0;
-    for (uint32_t q = 0; q < sums[f].n_chunks; q++) {
-      const uint64_t k = base[f] + q, e = cuts[k];
-      blocks.push_back(Block{&ids[16 * k], zout.data() + zoff[k], zlen[k], e - start});
-      zbytes += zlen[k];
-      start = e;
-    }
-  }
-
-  // loopback TCP: listener, sink thread, client (sender + receiver)
+  // loopback TCP: listener, sink thread, client (sender + receiver); the
+  // sender starts on a batch's blocks as soon as hbx_store_paths_zcb reports
+  // the batch collected, so the wire overlaps the reading and hashing
   const int ls = ::socket(AF_INET, SOCK_STREAM, 0);
   sockaddr_in a{};
   a.sin_family = AF_INET;
@@ -241,80 +223,135 @@ int main(int argc, char** argv) {
   const int one = 1;
   ::setsockopt(cs, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
 
-  std::mutex mu;
-  std::condition_variable cv;
-  std::deque<uint32_t> to_write;  // blocks the server asked for (READ)
-  uint64_t outstanding = 0, acked = 0, dedup = 0, written = 0;
-  bool failed = false;
-  const uint64_t nb = blocks.size();
-  const double t2 = now();
-  std::thread rx([&] {  // the client's receive side: READ -> queue the writ, ACKN -> done
+  struct Shared {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<Block> blocks;       // grows as batches are collected (reserved: never moves)
+    std::deque<uint32_t> to_write;   // message numbers the server asked for (READ)
+    uint64_t outstanding = 0, acked = 0, written = 0, zbytes = 0;
+    bool store_done = false, failed = false;
+    const uint8_t* ids;
+    const uint64_t* cuts;
+    const uint64_t* base;
+    const uint64_t* zoff;
+    const uint64_t* zlen;
+    const hbx_file_summary* sums;
+    const uint8_t* zout;
+  } S;
+  S.blocks.reserve(ncap);
+  S.ids = ids.data();
+  S.cuts = cuts.data();
+  S.base = base.data();
+  S.zoff = zoff.data();
+  S.zlen = zlen.data();
+  S.sums = sums.data();
+  S.zout = zout.data();
+  auto ready = [](void* user, uint64_t first, uint64_t count) {
+    Shared& S = *static_cast<Shared*>(user);
+    std::lock_guard<std::mutex> g(S.mu);
+    for (uint64_t f = first; f < first + count; f++) {
+      uint64_t start = 0;
+      for (uint32_t q = 0; q < S.sums[f].n_chunks; q++) {
+        const uint64_t k = S.base[f] + q, e = S.cuts[k];
+        S.blocks.push_back(Block{S.ids + 16 * k, S.zout + S.zoff[k], S.zlen[k], e - start});
+        S.zbytes += S.zlen[k];
+        start = e;
+      }
+    }
+    S.cv.notify_all();
+  };
+  std::thread rx([&] {  // READ -> queue the writ; ACKN -> done
     Reader r{cs};
     hbx_wire_msg m;
     while (r.next(m)) {
-      std::lock_guard<std::mutex> g(mu);
+      std::lock_guard<std::mutex> g(S.mu);
       if (m.type == (HBX_MSG_READ & HBX_SERVER_MASK)) {
-        to_write.push_back(m.num);  // the server wants this block's data
+        S.to_write.push_back(m.num);
       } else if (m.type == (HBX_MSG_ACKNOWLEDGE & HBX_SERVER_MASK)) {
-        acked++;
-        outstanding--;
+        S.acked++;
+        S.outstanding--;
       } else {
-        failed = true;
+        S.failed = true;
       }
-      cv.notify_all();
-      if (acked == nb) break;
+      S.cv.notify_all();
+      if (S.store_done && S.acked == S.blocks.size()) break;
     }
   });
-  // sender: allo for every block (at most `window` unacknowledged), writ on demand
-  uint64_t next = 0;
-  std::vector<uint8_t> hdr(64);
-  for (;;) {
-    std::unique_lock<std::mutex> g(mu);
-    cv.wait(g, [&] { return failed || !to_write.empty() || (next < nb && outstanding < window) || acked == nb; });
-    if (failed || acked == nb) break;
-    if (!to_write.empty()) {
-      const uint32_t num = to_write.front();
-      to_write.pop_front();
-      g.unlock();
-      // message numbers are block indices mod 2^16; with window < 65536 the
-      // unacknowledged block with this number is unique
-      uint64_t idx = (next - 1) - ((uint16_t)((uint16_t)(next - 1) - num));
-      const Block& b = blocks[idx];
-      uint64_t hn = 0;
-      hbx_wire_encode_block_header((uint16_t)idx, HBX_MSG_WRITE, b.id, nullptr, 0, HBX_BLOCK_DATA_ZLIB,
-                                   (uint32_t)b.zlen, hdr.data(), hdr.size(), &hn);
-      iovec v[2] = {{hdr.data(), hn}, {const_cast<uint8_t*>(b.z), b.zlen}};
-      if (!sendv_all(cs, v, 2)) break;
-      written++;
-    } else if (next < nb && outstanding < window) {
-      outstanding++;
-      const uint64_t idx = next++;
-      g.unlock();
-      uint8_t out[22];
-      hbx_wire_encode_id((uint16_t)idx, HBX_MSG_ALLOCATE, blocks[idx].id, out);
-      if (!send_all(cs, out, 22)) break;
+  std::thread tx([&] {  // allo for every block (at most `window` open), writ on demand
+    uint64_t next = 0;
+    std::vector<uint8_t> hdr(64);
+    for (;;) {
+      std::unique_lock<std::mutex> g(S.mu);
+      S.cv.wait(g, [&] {
+        return S.failed || !S.to_write.empty() || (next < S.blocks.size() && S.outstanding < window) ||
+               (S.store_done && S.acked == S.blocks.size());
+      });
+      if (S.failed || (S.store_done && S.acked == S.blocks.size() && S.to_write.empty())) break;
+      if (!S.to_write.empty()) {
+        const uint32_t num = S.to_write.front();
+        S.to_write.pop_front();
+        // message numbers are block indices mod 2^16; fewer than 2^16 are open
+        const uint64_t idx = (next - 1) - ((uint16_t)((uint16_t)(next - 1) - num));
+        const Block b = S.blocks[idx];
+        g.unlock();
+        uint64_t hn = 0;
+        hbx_wire_encode_block_header((uint16_t)idx, HBX_MSG_WRITE, b.id, nullptr, 0, HBX_BLOCK_DATA_ZLIB,
+                                     (uint32_t)b.zlen, hdr.data(), hdr.size(), &hn);
+        iovec v[2] = {{hdr.data(), hn}, {const_cast<uint8_t*>(b.z), b.zlen}};
+        if (!sendv_all(cs, v, 2)) break;
+        std::lock_guard<std::mutex> g2(S.mu);
+        S.written++;
+      } else if (next < S.blocks.size() && S.outstanding < window) {
+        S.outstanding++;
+        const uint64_t idx = next++;
+        const uint8_t* id = S.blocks[idx].id;
+        g.unlock();
+        uint8_t out[22];
+        hbx_wire_encode_id((uint16_t)idx, HBX_MSG_ALLOCATE, id, out);
+        if (!send_all(cs, out, 22)) break;
+      }
     }
+  });
+  const double t0 = now();
+  int rc = hbx_store_paths_zcb(ctx, n, paths.data(), lens.data(), cuts.data(), ids.data(), base.data(),
+                               caps.data(), sums.data(), io_threads, 1ull << 30, zout.data(), zbase.data(),
+                               zoff.data(), zlen.data(), ready, &S);
+  const double t1 = now();
+  {
+    std::lock_guard<std::mutex> g(S.mu);
+    S.store_done = true;
+    if (rc != HBX_OK) S.failed = true;
+    S.cv.notify_all();
   }
-  rx.join();
+  if (rc != HBX_OK) std::fprintf(stderr, "hbx_store_paths_zcb: %s\n", hbx_last_error(ctx));
+  tx.join();
   const double t3 = now();
+  // goodbye: the sink leaves its loop and closes, which ends the receiver
   uint8_t bye[6] = {0, 0, (uint8_t)(HBX_MSG_GOODBYE >> 24), (uint8_t)(HBX_MSG_GOODBYE >> 16),
                     (uint8_t)(HBX_MSG_GOODBYE >> 8), (uint8_t)HBX_MSG_GOODBYE};
   send_all(cs, bye, 6);
+  if (S.failed) ::shutdown(cs, SHUT_RDWR);
+  rx.join();
+  const uint64_t nb = S.blocks.size(), zbytes = S.zbytes, acked = S.acked, written = S.written;
+  const bool failed = S.failed;
+  uint64_t dedup = 0;
   srv.join();
   ::close(cs);
   ::close(ls);
   hbx_ctx_destroy(ctx);
   dedup = st.acks_dedup;
   std::printf(
-      "{\"workload\": \"send path over loopback TCP: hbx_store_paths_z then allo/READ/writ/ACKN per chunk\", "
+      "{\"workload\": \"send path over loopback TCP, overlapped: hbx_store_paths_zcb (per-batch callback) feeding "
+      "allo/READ/writ/ACKN per chunk\", "
       "\"files\": %llu, \"bytes\": %llu, \"chunks\": %llu, \"compressed_bytes\": %llu, "
-      "\"gpu_seconds\": %.3f, \"gpu_gibs\": %.3f, \"wire_seconds\": %.3f, \"wire_gbs_compressed\": %.3f, "
-      "\"end_to_end_gibs\": %.3f, \"window\": %u, \"sink\": {\"allocs\": %llu, \"reads\": %llu, "
-      "\"dedup_acks\": %llu, \"writes\": %llu, \"verified\": %llu, \"verify_failures\": %llu}, "
-      "\"client_writes\": %llu, \"acked\": %llu, \"failed\": %s}\n",
+      "\"store_seconds\": %.3f, \"store_gibs\": %.3f, \"end_to_end_seconds\": %.3f, "
+      "\"wire_tail_after_store_seconds\": %.3f, \"end_to_end_gibs\": %.3f, \"window\": %u, "
+      "\"sink\": {\"allocs\": %llu, \"reads\": %llu, \"dedup_acks\": %llu, \"writes\": %llu, "
+      "\"verified\": %llu, \"verify_failures\": %llu}, \"client_writes\": %llu, \"acked\": %llu, "
+      "\"failed\": %s}\n",
       (unsigned long long)n, (unsigned long long)total, (unsigned long long)nb, (unsigned long long)zbytes,
-      t1 - t0, total / (t1 - t0) / (1 << 30), t3 - t2, zbytes / (t3 - t2) / 1e9, total / (t3 - t0) / (1 << 30),
-      window, (unsigned long long)st.allocs, (unsigned long long)st.reads, (unsigned long long)dedup,
+      t1 - t0, total / (t1 - t0) / (1 << 30), t3 - t0, t3 - t1, total / (t3 - t0) / (1 << 30), window,
+      (unsigned long long)st.allocs, (unsigned long long)st.reads, (unsigned long long)dedup,
       (unsigned long long)st.writes, (unsigned long long)st.verified, (unsigned long long)st.bad,
       (unsigned long long)written, (unsigned long long)acked, failed ? "true" : "false");
   return (failed || st.bad || acked != nb) ? 1 : 0;
