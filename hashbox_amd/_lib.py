@@ -59,6 +59,9 @@ class FileSummary(ctypes.Structure):
                 ("n_chunks", ctypes.c_uint32)]
 
 
+# hbx_batch_ready_fn (include/hbxgpu.h)
+BATCH_READY = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64)
+
 _lib = None
 
 

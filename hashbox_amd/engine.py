@@ -22,7 +22,7 @@ import os
 import sys
 from collections import deque
 from dataclasses import dataclass
-from typing import List, Optional, Sequence, Union
+from typing import Callable, List, Optional, Sequence, Union
 
 import numpy as np
 
@@ -404,13 +404,19 @@ class Engine:
                     "hbx_memcpy_h2d_async")
 
     def store_paths(self, paths: Sequence[Union[str, os.PathLike]], io_threads: int = 16,
-                    batch_bytes: int = 1 << 30, compress: bool = False) -> List[FileChunks]:
+                    batch_bytes: int = 1 << 30, compress: bool = False,
+                    on_batch: Optional[Callable[[int, int], None]] = None) -> List[FileChunks]:
         """storeFile for many files on disk, end to end: the library reads them
         into pinned memory on ``io_threads`` threads and overlaps reading the
         next batch with the copy + kernels of the current one.  With
         ``compress`` every chunk is also zlib-compressed on the device
         (HashboxBlock.CompressData, the client's send path) and returned in
-        ``FileChunks.zstreams``."""
+        ``FileChunks.zstreams``.  ``on_batch(first, count)`` (compress only)
+        runs on this thread as soon as files [first, first+count) have their
+        ids, summaries and zlib streams written (hbx_store_paths_zcb), so a
+        sender can ship them while later batches are still read and hashed."""
+        if on_batch is not None and not compress:
+            raise ValueError("on_batch needs compress=True (hbx_store_paths_zcb)")
         enc = [os.fsencode(p) for p in paths]
         lens = np.array([os.stat(p).st_size for p in enc], np.uint64)
         arr = (ctypes.c_char_p * max(len(enc), 1))(*enc)
@@ -427,10 +433,26 @@ class Engine:
         zout = np.empty(int(fb.sum()) + 16, np.uint8)
         zoff = np.zeros(max(int(caps.sum()), 1), np.uint64)
         zlen = np.zeros_like(zoff)
-        self._check(self._L.hbx_store_paths_z(self._ctx, len(enc), ctypes.cast(arr, ctypes.c_void_p),
-                                              _p(lens), _p(cuts), _p(ids), _p(base), _p(caps), sums,
-                                              int(io_threads), int(batch_bytes), _p(zout), _p(zbase),
-                                              _p(zoff), _p(zlen)), "hbx_store_paths_z")
+        zargs = (self._ctx, len(enc), ctypes.cast(arr, ctypes.c_void_p), _p(lens), _p(cuts), _p(ids),
+                 _p(base), _p(caps), sums, int(io_threads), int(batch_bytes), _p(zout), _p(zbase),
+                 _p(zoff), _p(zlen))
+        if on_batch is None:
+            self._check(self._L.hbx_store_paths_z(*zargs), "hbx_store_paths_z")
+        else:
+            raised = []
+
+            def ready(_user, first, count):
+                if raised:
+                    return
+                try:
+                    on_batch(int(first), int(count))
+                except BaseException as e:  # never unwind through C
+                    raised.append(e)
+            cb = _lib.BATCH_READY(ready)
+            self._check(self._L.hbx_store_paths_zcb(*zargs, ctypes.cast(cb, ctypes.c_void_p), None),
+                        "hbx_store_paths_zcb")
+            if raised:
+                raise raised[0]
         res = self._unpack(lens, caps, base, cuts, ids, sums)
         for f, r in enumerate(res):
             b = int(base[f])

@@ -131,3 +131,34 @@ def test_store_paths_compressed(engine, tmp_path):
         starts, ends = b.chunk_bounds()
         for s, e, z in zip(starts, ends, b.zstreams):
             assert OD.inflate_strict(z) == d[int(s):int(e)]
+
+
+def test_store_paths_on_batch_covers_every_file_once(engine, tmp_path):
+    """store_paths(compress=True, on_batch=...) -> hbx_store_paths_zcb: the
+    per-batch callback reports every file exactly once, in order, and the
+    streams it announced are the ones returned (SURVEY §8f3 send path)."""
+    rng = np.random.default_rng(21)
+    paths = []
+    for i in range(48):  # ~96 MiB: several 64 MiB (the minimum) batches
+        p = tmp_path / f"g{i:02d}"
+        p.write_bytes(rng.integers(0, 256, int(rng.integers(1, 4 << 20)), dtype=np.uint8).tobytes())
+        paths.append(p)
+    seen = []
+    res = engine.store_paths(paths, io_threads=4, batch_bytes=64 << 20, compress=True,
+                             on_batch=lambda first, count: seen.append((first, count)))
+    assert len(seen) >= 2
+    assert [f for a, c in seen for f in range(a, a + c)] == list(range(len(paths)))
+    for p, r in zip(paths, res):
+        ref = engine.chunk_hash(np.fromfile(p, np.uint8))
+        assert np.array_equal(r.ids, ref.ids)
+        data = p.read_bytes()
+        starts, ends = r.chunk_bounds()
+        for z, a, b in list(zip(r.zstreams, starts, ends))[:2]:
+            assert OD.inflate_strict(bytes(z)) == data[int(a):int(b)]
+
+
+def test_store_paths_on_batch_needs_compress(engine, tmp_path):
+    p = tmp_path / "x"
+    p.write_bytes(b"abc")
+    with pytest.raises(ValueError):
+        engine.store_paths([p], on_batch=lambda a, c: None)
