@@ -331,6 +331,65 @@ __device__ void huff_lengths(const uint32_t* keys, uint32_t m, uint32_t limit, u
   for (uint32_t i = 0; i < m; i++) lens[keys[i] & 511u] = dep[i];
 }
 
+// The two-queue merge of huff_lengths alone, for the parallel depth pass:
+// leaves 0..m) in key order, internal nodes m..2m-1); par[node] = pbase +
+// its parent.  Same tie rule as huff_lengths (leaf first).
+__device__ void huff_merge(const uint32_t* keys, uint32_t m, uint32_t shift, uint32_t* w, uint32_t* par,
+                           uint32_t pbase) {
+  constexpr uint32_t kInf = 0xFFFFFFFFu;
+  auto leaf = [&](uint32_t i) { return i < m ? ((keys[i] >> 9) >> shift) | 1u : kInf; };
+  uint32_t i = 0u, j = m, wi = leaf(0u), wj = kInf;
+  for (uint32_t k = m; k < 2u * m - 1u; k++) {
+    uint32_t a, b, wa, wb;
+    if (wi <= wj) { a = i++; wa = wi; wi = leaf(i); } else { a = j++; wa = wj; wj = j < k ? w[j] : kInf; }
+    if (wi <= wj) { b = i++; wb = wi; wi = leaf(i); } else { b = j++; wb = wj; wj = j < k ? w[j] : kInf; }
+    const uint32_t s = wa + wb;
+    w[k] = s;
+    if (j == k) wj = s;  // the internal queue was empty: the new node heads it
+    par[a] = pbase + k;
+    par[b] = pbase + k;
+  }
+}
+
+// The run-length code of one run of `run` equal code lengths `cur`, as
+// huff header symbols (16 repeat 3-6, 17 zeros 3-10, 18 zeros 11-138), in
+// zlib's order.  With EMIT they go to out[] and their counts into f[].
+template <bool EMIT>
+__device__ __forceinline__ uint32_t rle_runs(uint32_t cur, uint32_t r, uint32_t* out, uint32_t* f) {
+  uint32_t nr = 0u;
+  auto put = [&](uint32_t sym) {
+    if (EMIT) {
+      out[nr] = sym;
+      atomicAdd(&f[sym & 31u], 1u);
+    }
+    nr++;
+  };
+  if (cur == 0u) {
+    while (r >= 11u) {
+      const uint32_t q = min(r, 138u);
+      put(18u | ((q - 11u) << 8));
+      r -= q;
+    }
+    if (r >= 3u) {
+      put(17u | ((r - 3u) << 8));
+      r = 0u;
+    }
+  } else {
+    put(cur);
+    r--;
+    while (r >= 3u) {
+      const uint32_t q = min(r, 6u);
+      put(16u | ((q - 3u) << 8));
+      r -= q;
+    }
+  }
+  while (r > 0u) {
+    put(cur);
+    r--;
+  }
+  return nr;
+}
+
 // Canonical codes (RFC 1951 §3.2.2) as reversed code | length << 16.
 __device__ void canon_codes(const uint8_t* lens, uint32_t nsym, uint32_t* out, uint32_t* blc) {
   for (uint32_t b = 0; b < 16u; b++) blc[b] = 0u;
@@ -412,8 +471,9 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
   __shared__ uint16_t cd[kCdPhys];
   __shared__ uint32_t wsum[kWaves];
   __shared__ unsigned long long wadler[2 * kWaves];
-  __shared__ uint32_t hll[288], hd[32], llc[288], dcc[32], rle[320], clf[19], clc[19], zpar[8];
-  __shared__ uint8_t zl[320], cll[20];
+  __shared__ uint32_t hll[288], hd[32], llc[288], dcc[32], rle[320], clf[19], clc[19], zpar[8], zctl[8];
+  __shared__ __attribute__((aligned(4))) uint8_t zl[320];
+  __shared__ uint8_t cll[20];
   const uint32_t g = blockIdx.x;
   if (g >= nseg) return;
   const ZBlock bk = blocks[zblock_of(blocks, nb, g)];
@@ -483,16 +543,25 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
   const uint32_t best_other = min(fixed_bytes, stored_bytes) * 8u;
   const bool try_dyn = htot + etot + 600u < best_other;
   if (try_dyn) {
-    uint32_t* keys = tab;                                   // 512
-    uint32_t* keys2 = tab + 512;                            // 32
-    uint32_t* hw = tab + 576;                               // 2 x 288 weights
-    uint16_t* hpar = reinterpret_cast<uint16_t*>(tab + 1152);  // 576
-    uint8_t* hdep = reinterpret_cast<uint8_t*>(tab + 1440);    // 576
-    uint32_t* blc = tab + 1600;                             // 16
+    // scratch in the (idle) hash table
+    uint32_t* keys = tab;                                      // 512 litlen keys, sorted
+    uint32_t* keysd = tab + 512;                               // 32 distance keys, sorted
+    uint32_t* keys2 = tab + 544;                               // 32 code-length keys
+    uint32_t* hw = tab + 576;                                  // weights: litlen 572, distance 60 at +576
+    uint32_t* npar = tab + 1792;                               // tree parents, distance nodes at +576
+    uint32_t* nanc = tab + 2816;                               // pointer-jumping ancestors
+    uint32_t* ndep = tab + 3840;                               // depths
+    uint32_t* blc = tab + 4864;                                // 2 x 16 length counts
+    uint32_t* cw = tab + 4896;                                 // code-length code: weights (38)
+    uint16_t* cpar = reinterpret_cast<uint16_t*>(tab + 4960);  // 38
+    uint8_t* cdep = reinterpret_cast<uint8_t*>(tab + 4992);    // 38
     for (uint32_t k = t; k < 512u; k += kThreads) keys[k] = (k < 286u && hll[k]) ? (hll[k] << 9) | k : 0xFFFFFFFFu;
     for (uint32_t k = t; k < 320u; k += kThreads) zl[k] = 0u;
+    if (t < 32u) blc[t] = 0u;
+    if (t < 19u) clf[t] = 0u;
+    if (t < 8u) zctl[t] = 0u;
     __syncthreads();
-    if (t < 64u) {  // bitonic sort, ascending, one wave
+    if (t < 64u) {  // bitonic sort of the litlen keys, ascending, one wave
       for (uint32_t k = 2; k <= 512u; k <<= 1)
         for (uint32_t j = k >> 1; j > 0u; j >>= 1)
           for (uint32_t i = t; i < 512u; i += 64u) {
@@ -505,69 +574,115 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
               }
             }
           }
+    } else if (t < 96u) {  // rank sort of the distance keys, a second wave
+      const uint32_t k = t - 64u;
+      const uint32_t key = (k < 30u && hd[k]) ? (hd[k] << 9) | k : 0xFFFFFFFFu;
+      if (key != 0xFFFFFFFFu) {
+        uint32_t r = 0u;
+        for (uint32_t q = 0; q < 30u; q++) r += hd[q] && ((hd[q] << 9) | q) < key;
+        keysd[r] = key;
+      }
+    }
+    const uint32_t ml = (uint32_t)__syncthreads_count(t < 286u && hll[t] != 0u);  // >= 1 (EOB)
+    const uint32_t md = (uint32_t)__syncthreads_count(t < 30u && hd[t] != 0u);
+    // Huffman trees of both codes at once: the serial merges on two waves,
+    // then depths by pointer jumping over every node; halve and rebuild a
+    // code whose longest length exceeds 15.
+    bool need_l = ml >= 2u, need_d = md >= 2u;
+    for (uint32_t shift = 0; need_l || need_d; shift++) {
+      if (t == 0u && need_l) huff_merge(keys, ml, shift, hw, npar, 0u);
+      if (t == 64u && need_d) huff_merge(keysd, md, shift, hw + 576, npar + 576, 576u);
+      if (t < 2u) zctl[t] = 0u;
+      __syncthreads();
+      uint32_t x0 = t, x1 = t + kThreads, a0, a1, d0, d1;
+      auto init = [&](uint32_t x, uint32_t& a, uint32_t& d) {
+        const bool dist = x >= 576u;
+        const uint32_t m = dist ? md : ml, root = (dist ? 576u : 0u) + 2u * m - 2u;
+        const bool live = m >= 2u && x <= root && x >= (dist ? 576u : 0u);
+        a = live && x != root ? npar[x] : x;
+        d = live && x != root ? 1u : 0u;
+      };
+      init(x0, a0, d0);
+      init(x1, a1, d1);
+      nanc[x0] = a0;
+      nanc[x1] = a1;
+      ndep[x0] = d0;
+      ndep[x1] = d1;
+      __syncthreads();
+      for (int r = 0; r < 10; r++) {  // depth <= 571 < 2^10
+        const uint32_t e0 = ndep[a0], e1 = ndep[a1], b0 = nanc[a0], b1 = nanc[a1];
+        __syncthreads();
+        d0 += e0;
+        d1 += e1;
+        a0 = b0;
+        a1 = b1;
+        ndep[x0] = d0;
+        ndep[x1] = d1;
+        nanc[x0] = a0;
+        nanc[x1] = a1;
+        __syncthreads();
+      }
+      if (x0 < ml) atomicMax(&zctl[0], d0);
+      if (x0 >= 576u && x0 < 576u + md) atomicMax(&zctl[1], d0);
+      if (x1 >= 576u && x1 < 576u + md) atomicMax(&zctl[1], d1);
+      __syncthreads();
+      need_l = need_l && zctl[0] > 15u;
+      need_d = need_d && zctl[1] > 15u;
+      __syncthreads();
+    }
+    // code lengths (one distance symbol gets a second: RFC 1951 §3.2.7)
+    if (t < ml) zl[keys[t] & 511u] = ml >= 2u ? (uint8_t)ndep[t] : 1u;
+    if (md >= 2u && t < md) zl[288u + (keysd[t] & 511u)] = (uint8_t)ndep[576u + t];
+    if (md == 0u && t < 2u) zl[288u + t] = 1u;
+    if (md == 1u && t < 2u) {
+      const uint32_t x = keysd[0] & 511u;
+      zl[288u + (t ? (x ? 0u : 1u) : x)] = 1u;
     }
     __syncthreads();
-    if (t == 0) {
-      uint32_t m = 0u;
-      while (m < 286u && keys[m] != 0xFFFFFFFFu) m++;
-      huff_lengths(keys, m, 15u, zl, hw, hpar, hdep);
-      const uint32_t md = sort_small(hd, 30u, keys2);
-      if (md == 0u) {
-        zl[288] = 1u;
-        zl[289] = 1u;
-      } else if (md == 1u) {
-        const uint32_t x = keys2[0] & 511u;
-        zl[288 + x] = 1u;
-        zl[288 + (x ? 0u : 1u)] = 1u;
-      } else {
-        huff_lengths(keys2, md, 15u, zl + 288, hw, hpar, hdep);
+    // HLIT, HDIST, per-length counts
+    const uint32_t zt = t < 286u ? zl[t] : (t >= 288u && t < 318u ? zl[t] : 0u);
+    if (zt) atomicAdd(&blc[(t >= 288u ? 16u : 0u) + zt], 1u);
+    if (zt && t >= 257u && t < 286u) atomicMax(&zctl[2], t + 1u);
+    if (zt && t >= 288u) atomicMax(&zctl[3], t - 288u + 1u);
+    __syncthreads();
+    const uint32_t hlit = max(zctl[2], 257u), hdist = max(zctl[3], 1u);
+    // canonical codes (RFC 1951 §3.2.2): first code of the length + the rank
+    // among the symbols of that length before this one
+    if (zt) {
+      const uint32_t cb = t >= 288u ? 16u : 0u, s0 = t >= 288u ? 288u : 0u;
+      uint32_t code = 0u;
+      for (uint32_t b = 1; b <= zt; b++) code = (code + (b > 1u ? blc[cb + b - 1u] : 0u)) << 1;
+      const uint32_t* zw = reinterpret_cast<const uint32_t*>(zl);
+      const uint32_t pat = zt * 0x01010101u;
+      uint32_t rank = 0u;
+      for (uint32_t q = s0; q < t; q += 4u) {
+        uint32_t v = zw[q >> 2] ^ pat;
+        if (t - q < 4u) v |= 0xFFFFFFFFu << (8u * (t - q));  // bytes at or past t never count
+        const uint32_t y = ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v | 0x7F7F7F7Fu);
+        rank += __builtin_popcount(y);
       }
-      uint32_t hlit = 257u, hdist = 1u;
-      for (uint32_t k = 257u; k < 286u; k++)
-        if (zl[k]) hlit = k + 1u;
-      for (uint32_t k = 0u; k < 30u; k++)
-        if (zl[288 + k]) hdist = k + 1u;
-      canon_codes(zl, 286u, llc, blc);
-      canon_codes(zl + 288, 30u, dcc, blc);
-      // code-length sequence, run-length coded (16/17/18)
-      for (uint32_t k = 0; k < 19u; k++) clf[k] = 0u;
-      const uint32_t nl = hlit + hdist;
-      uint32_t nr = 0u;
-      for (uint32_t i = 0; i < nl;) {
-        const uint32_t cur = i < hlit ? zl[i] : zl[288 + i - hlit];
-        uint32_t run = 1u;
-        while (i + run < nl && (i + run < hlit ? zl[i + run] : zl[288 + i + run - hlit]) == cur) run++;
-        uint32_t r = run;
-        if (cur == 0u) {
-          while (r >= 11u) {
-            const uint32_t q = min(r, 138u);
-            rle[nr++] = 18u | ((q - 11u) << 8);
-            clf[18]++;
-            r -= q;
-          }
-          if (r >= 3u) {
-            rle[nr++] = 17u | ((r - 3u) << 8);
-            clf[17]++;
-            r = 0u;
-          }
-        } else {
-          rle[nr++] = cur;
-          clf[cur]++;
-          r--;
-          while (r >= 3u) {
-            const uint32_t q = min(r, 6u);
-            rle[nr++] = 16u | ((q - 3u) << 8);
-            clf[16]++;
-            r -= q;
-          }
-        }
-        while (r > 0u) {
-          rle[nr++] = cur;
-          clf[cur]++;
-          r--;
-        }
-        i += run;
-      }
+      const uint32_t c = rev(code + rank, zt) | (zt << 16);
+      if (t >= 288u) dcc[t - 288u] = c; else llc[t] = c;
+    } else if (t < 286u) {
+      llc[t] = 0u;
+    } else if (t >= 288u && t < 318u) {
+      dcc[t - 288u] = 0u;
+    }
+    // code-length sequence, run-length coded (16/17/18): one thread per run
+    const uint32_t nl = hlit + hdist;
+    auto zv = [&](uint32_t i) -> uint32_t { return i < hlit ? zl[i] : zl[288u + i - hlit]; };
+    uint32_t cur = 0u, run = 0u, cnt = 0u;
+    if (t < nl && (t == 0u || zv(t - 1u) != zv(t))) {
+      cur = zv(t);
+      run = 1u;
+      while (t + run < nl && zv(t + run) == cur) run++;
+      cnt = rle_runs<false>(cur, run, nullptr, nullptr);
+    }
+    uint32_t nr;
+    const uint32_t at = wg_incl_sum(cnt, wsum, nr) - cnt;
+    if (cnt) rle_runs<true>(cur, run, rle + at, clf);
+    __syncthreads();
+    if (t == 0) {  // the code-length code: <= 19 symbols, serial
       for (uint32_t k = 0; k < 19u; k++) cll[k] = 0u;
       const uint32_t mc = sort_small(clf, 19u, keys2);
       if (mc == 1u) {
@@ -575,21 +690,28 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
         cll[x] = 1u;
         cll[x ? 0u : 1u] = 1u;
       } else {
-        huff_lengths(keys2, mc, 7u, cll, hw, hpar, hdep);
+        huff_lengths(keys2, mc, 7u, cll, cw, cpar, cdep);
       }
       canon_codes(cll, 19u, clc, blc);
       uint32_t hclen = 4u;
       for (uint32_t k = 0; k < 19u; k++)
         if (cll[kClOrder[k]]) hclen = max(hclen, k + 1u);
-      uint32_t hb = 3u + 5u + 5u + 4u + 3u * hclen;
-      for (uint32_t k = 0; k < nr; k++) {
-        const uint32_t sy = rle[k] & 31u;
-        hb += (clc[sy] >> 16) + (sy == 16u ? 2u : sy == 17u ? 3u : sy == 18u ? 7u : 0u);
-      }
-      uint32_t tok = etot;
-      for (uint32_t k = 0; k < 286u; k++) tok += hll[k] * zl[k];  // EOB included (hll[256] = 1)
-      for (uint32_t k = 0; k < 30u; k++) tok += hd[k] * zl[288 + k];
-      const uint32_t dyn_bytes = ((hb + tok + 3u + 7u) >> 3) + 4u;
+      zctl[4] = hclen;
+    }
+    __syncthreads();
+    const uint32_t hclen = zctl[4];
+    uint32_t hcost = 0u, tcost = 0u, hb_body, tok_body;
+    if (t < nr) {
+      const uint32_t sy = rle[t] & 31u;
+      hcost = (clc[sy] >> 16) + (sy == 16u ? 2u : sy == 17u ? 3u : sy == 18u ? 7u : 0u);
+    }
+    if (t < 286u) tcost = hll[t] * zl[t];  // EOB included (hll[256] = 1)
+    else if (t >= 288u && t < 318u) tcost = hd[t - 288u] * zl[t];
+    (void)wg_incl_sum(hcost, wsum, hb_body);
+    (void)wg_incl_sum(tcost, wsum, tok_body);
+    if (t == 0) {
+      const uint32_t hb = 3u + 5u + 5u + 4u + 3u * hclen + hb_body;
+      const uint32_t dyn_bytes = ((hb + etot + tok_body + 3u + 7u) >> 3) + 4u;
       zpar[0] = dyn_bytes < min(fixed_bytes, stored_bytes) ? 2u : 0u;
       zpar[1] = hb;
       zpar[2] = dyn_bytes;
