@@ -719,6 +719,25 @@ int hbx_device_count(int* n) {
 
 uint64_t hbx_max_chunks(uint64_t len) { return max_chunks(len); }
 
+// HBX_SCAN_CUS / HBX_HASH_CUS / HBX_RES_CUS = "first:count[:stride]" restrict a
+// stream's dispatches to those CU indices (hipExtStreamCreateWithCUMask);
+// "off" or unset = an ordinary stream.  The scan stream defaults to a full
+// mask: a CU-masked stream gets a hardware queue of its own, and K1/K2 on it
+// beside K3 run 2.6 % faster end to end (2,100 vs 2,046 GiB/s, 3 A/B pairs,
+// tools/gpu_ab_cumask3.sh).  Masking the hash or result stream, even with
+// all CUs, serializes K1 and K3 (1,510-1,540 GiB/s): leave them unmasked.
+static hipError_t make_stream(hipStream_t* s, const char* env, int ncu, const char* dflt = nullptr) {
+  const char* v = std::getenv(env);
+  if (!v) v = dflt;
+  int first = 0, count = 0, stride = 1;
+  if (!v || std::sscanf(v, "%d:%d:%d", &first, &count, &stride) < 2 || count <= 0 || ncu <= 0)
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+  for (int i = 0, cu = first; i < count && cu < ncu; i++, cu += std::max(1, stride))
+    mask[(size_t)cu / 32] |= 1u << (cu % 32);
+  return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
+}
+
 int hbx_ctx_create(int device, hbx_ctx** out) {
   if (!out) return HBX_ERR_ARG;
   *out = nullptr;
@@ -728,16 +747,16 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   hbx_ctx* c = new hbx_ctx();
   c->device = device;
   hipDeviceProp_t prop;
+  int ncu = 0;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
-    c->md5_wgs = (uint32_t)prop.multiProcessorCount;
+    c->md5_wgs = (uint32_t)(ncu = prop.multiProcessorCount);
   if (const char* v = std::getenv("HBX_K1_DMA")) c->k1_mode = std::atoi(v) ? 1u : 0u;
   if (const char* v = std::getenv("HBX_K1_MODE")) c->k1_mode = (uint32_t)std::min(2, std::max(0, std::atoi(v)));
   if (const char* v = std::getenv("HBX_MD5_WGS")) c->md5_wgs = (uint32_t)std::max(1, std::atoi(v));
   if (const char* v = std::getenv("HBX_K3_DENSE")) c->k3_dense = std::atoi(v) ? 1u : 0u;
   if (const char* v = std::getenv("HBX_TILE_ITERS")) c->tile_iters = (uint32_t)std::min(1024, std::max(1, std::atoi(v)));
   if (const char* v = std::getenv("HBX_MD5_SLICE")) c->md5_slice = (uint32_t)std::max(0, std::atoi(v));
-  if (hipSetDevice(device) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(device) != hipSuccess || make_stream(&c->stream, "HBX_SCAN_CUS", ncu, "0:4096") != hipSuccess) {
     delete c;
     return HBX_ERR_HIP;
   }
@@ -750,8 +769,8 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
     c->cstream = c->hstream = c->rstream = c->stream;
   } else if ((own_k2 ? hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking)
                      : (c->cstream = c->stream, hipSuccess)) != hipSuccess ||
-             hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking) != hipSuccess ||
-             hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking) != hipSuccess) {
+             make_stream(&c->hstream, "HBX_HASH_CUS", ncu) != hipSuccess ||
+             make_stream(&c->rstream, "HBX_RES_CUS", ncu) != hipSuccess) {
     hbx_ctx_destroy(c);
     return HBX_ERR_HIP;
   }
