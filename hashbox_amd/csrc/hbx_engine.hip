@@ -2,7 +2,7 @@
 //
 // One context = one GPU + one HIP stream + a grown-on-demand workspace.  A
 // batch of files runs as five launches on the stream:
-//   K1  window-digest scan  grid = tiles (2 MiB of one file each), 1024 thr
+//   K1  window-digest scan  grid = tiles (16 MiB of one file each), 1024 thr
 //   K2  cut chain           grid = files, 1 wave each (sequential store.go loop)
 //   K2c plan                1 workgroup: chunks bucketed by length, longest first
 //   K3  block MD5           one 512-thread workgroup per CU, lane per chunk
@@ -140,7 +140,10 @@ struct hbx_ctx {
   hipEvent_t k3_done = nullptr;   // recorded on the hash stream after a K3 launch that completes batches
   std::mutex mu;
   std::string err;
-  uint32_t tile_iters = 64;   // K1 tile = 64 x 64 KiB (measured best: fewer halo primes)
+  // K1 tile = 256 x 64 KiB: fewer halo primes, and beside K3 fewer, longer
+  // K1 workgroups (2,139-2,146 vs 2,088-2,108 GiB/s for 64, 3 A/B pairs,
+  // tools/gpu_ab_tile.sh; 8-32 are slower)
+  uint32_t tile_iters = 256;
   uint32_t k1_mode = 1;       // K1: 0 register prefetch, 1 LDS-DMA landing, 2 K1-lite (co-resides with K3)
   uint32_t md5_wgs = 256;     // K3 grid: one 256-thread workgroup per CU (set from the device)
   // K3 wave placement: 1 packs the busy waves into the fewest CUs (4 per CU,
@@ -730,8 +733,14 @@ static hipError_t make_stream(hipStream_t* s, const char* env, int ncu, const ch
   const char* v = std::getenv(env);
   if (!v) v = dflt;
   int first = 0, count = 0, stride = 1;
-  if (!v || std::sscanf(v, "%d:%d:%d", &first, &count, &stride) < 2 || count <= 0 || ncu <= 0)
+  if (!v || std::sscanf(v, "%d:%d:%d", &first, &count, &stride) < 2 || count <= 0 || ncu <= 0) {
+    // A/B only: "prio:hi" / "prio:lo" = an unmasked stream at the device's
+    // greatest / least priority
+    int lo = 0, hi = 0;
+    if (v && std::strncmp(v, "prio:", 5) == 0 && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
+      return hipStreamCreateWithPriority(s, hipStreamNonBlocking, std::strcmp(v + 5, "hi") == 0 ? hi : lo);
     return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  }
   std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
   for (int i = 0, cu = first; i < count && cu < ncu; i++, cu += std::max(1, stride))
     mask[(size_t)cu / 32] |= 1u << (cu % 32);

@@ -74,11 +74,13 @@ def test_batch_mixed(engine, oracle):
         _check(r, oracle.store_file(f, fast=True))
 
 
-@pytest.mark.parametrize("tile_iters", [1, 3, 32])
+@pytest.mark.parametrize("tile_iters", [1, 3, 32, 64, 256, 1024])
 def test_tile_sizes(oracle, tile_iters):
     from hashbox_amd import Engine
+    # several tiles per file up to 256 iterations (16 MiB tiles); 1024 = one tile
+    n = 37 * MIN + 999 if tile_iters < 64 else (5 * tile_iters * MIN) // 2 + 999 if tile_iters <= 256 else 20 * MAXB + 5
     with Engine(0, tile_iters=tile_iters) as e:
-        x = oracle.random_bytes(37 * MIN + 999, 77)
+        x = oracle.random_bytes(n, 77)
         _check(e.chunk_hash(x), oracle.store_file(x, fast=True))
 
 
