@@ -190,9 +190,9 @@ def main():
     # a batch holds its arena from its K1 until its last K3 launch; with
     # `lead` more arenas than launches per batch, the scan stream runs `lead`
     # steps ahead of the hash stream and never waits for a collect
+    free, _ = torch.cuda.mem_get_info(dev)
+    r_fit = max(a.lead + 1, int(free * a.hbm_frac) // (total + (64 << 20)))
     if a.md5_slice < 0:
-        free, _ = torch.cuda.mem_get_info(dev)
-        r_fit = max(a.lead + 1, int(free * a.hbm_frac) // (total + (64 << 20)))
         R = a.arenas if a.arenas > 0 else r_fit
         B = -(-nfull // max(1, R - a.lead))
     else:
@@ -201,7 +201,9 @@ def main():
     if a.arenas > 0:
         R = a.arenas
     elif a.md5_slice >= 0:
-        R = need + a.lead
+        # a short slice needs more launches per batch than HBM holds batches:
+        # cap the residency (collects then wait for the hash stream)
+        R = min(need + a.lead, r_fit)
     # synthetic uniform random bytes, generated on the device (per-rank seed);
     # R distinct resident batches, batch j reads arena j % R
     g = torch.Generator(device=dev)
