@@ -320,6 +320,13 @@ __device__ __forceinline__ s32x4 make_srd(const void* base, uint32_t nbytes) {
 }
 
 // 64 lanes x 16 B from srd[voff + soff] into LDS [lds, lds + 1 KiB).
+// HBX_K1_CPOL: cache-policy bits for K1's stream.  Nontemporal by default: K1
+// reads each byte once (plus a 64-B halo), and marking its 8.6 GB per launch
+// as streaming leaves L2 to K3 beside it (K3 3.61 -> 3.57 ms, default bench
+// 2,156/2,165 -> 2,190/2,186 GiB/s; sc1, sc0 sc1: no gain; tools/gpu_ab_lib.sh)
+#ifndef HBX_K1_CPOL
+#define HBX_K1_CPOL " nt"
+#endif
 __device__ __forceinline__ void dma16(s32x4 srd, uint32_t voff, uint32_t soff, uint32_t lds) {
   uint32_t keep;
   asm volatile(
@@ -327,7 +334,7 @@ __device__ __forceinline__ void dma16(s32x4 srd, uint32_t voff, uint32_t soff, u
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %3\n\t"
       "s_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen" HBX_K1_CPOL " lds\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(voff), "s"(srd), "s"(lds), "s"(soff)
