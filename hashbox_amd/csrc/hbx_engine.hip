@@ -744,7 +744,11 @@ static hipError_t make_stream(hipStream_t* s, const char* env, int ncu, const ch
   std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
   for (int i = 0, cu = first; i < count && cu < ncu; i++, cu += std::max(1, stride))
     mask[(size_t)cu / 32] |= 1u << (cu % 32);
-  return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
+  // the mask is a scheduling choice, not a requirement: a runtime that
+  // refuses it gets an ordinary stream
+  if (hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data()) == hipSuccess) return hipSuccess;
+  (void)hipGetLastError();
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
 }
 
 int hbx_ctx_create(int device, hbx_ctx** out) {

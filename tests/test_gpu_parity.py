@@ -257,3 +257,25 @@ def test_reserved_pipeline_placements(oracle, monkeypatch, dense):
     for i, g in zip(order + [0], got + [got_last]):
         for a, r in zip(g, batches[i][3]):
             _check(a, r)
+
+
+@pytest.mark.parametrize("scan,hash_", [("off", ""), ("0:64:2", ""), ("0:4096", "0:128"), ("prio:lo", "prio:hi")])
+def test_stream_cu_sets(oracle, monkeypatch, scan, hash_):
+    """Streams created on CU subsets or priorities (HBX_SCAN_CUS / HBX_HASH_CUS,
+    A/B switches; the scan stream is masked to every CU by default) change
+    only the schedule: the pipeline stays bit-exact."""
+    from hashbox_amd import Engine
+    monkeypatch.setenv("HBX_SCAN_CUS", scan)
+    if hash_:
+        monkeypatch.setenv("HBX_HASH_CUS", hash_)
+    batches = _device_batches(oracle, 2, 47)
+    got, order = [], [0, 1, 0, 1]
+    with Engine(0, md5_slice=1024) as e:
+        for i in order:
+            dev, offs, sizes, _ = batches[i]
+            e.submit_device(dev.data_ptr(), offs, sizes)
+        while e.pending():
+            got.append(e.wait())
+    for i, g in zip(order, got):
+        for a, r in zip(g, batches[i][3]):
+            _check(a, r)
