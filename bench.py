@@ -1,19 +1,29 @@
 #!/usr/bin/env python3
 """Benchmark: device-resident rollsum split + block-ID hashing on MI355X.
 
-Workload (BASELINE.json configs[1]): batches of 64 x 128 MiB uniform random
-buffers per GPU, resident in HBM before the timed region.  One step = one
-batch through the whole hot path: K1 window-digest scan -> K2 cut chain ->
-K3 block MD5 -> K4 content ids -> D2H of cut lists + block IDs.  Steps
-pipeline on one engine context: K3 is time-sliced (--md5-slice blocks per
-chain per launch), so each step's chunks join the MD5 chains still in flight
-and no batch waits behind another's longest chunk.  The timed region runs K
-steps from an empty pipeline to a fully drained one (every batch's results
-collected); `value` = K batches / that time.  --md5-slice 0 runs every batch
-alone (one K3 launch per batch: the single-batch latency path).  Files shard
-by GPU (weak scaling: each rank owns its own batches, no collective on the
-data path; the only collectives are the start/end barrier and the max-time
-reduction).
+Workload (BASELINE.json configs[1]): a step is one batch of 64 x 128 MiB
+uniform random buffers (8 GiB) through the whole hot path: K1 window-digest
+scan -> K2 cut chain -> K3 block MD5 -> K4 content ids -> D2H of cut lists +
+block IDs (hashback/store.go:111-196, pkg/core/block.go:96-111).  Inputs are
+resident in HBM before timing.
+
+Steady state.  Steps pipeline on one engine context: K3 is time-sliced
+(--md5-slice blocks per chain per launch), so each batch's chunks join the
+MD5 chains still in flight.  Before the timer the pipeline is filled to its
+operating depth (R batches submitted, none collected) and run W warm-up
+steps.  The timed region is exactly K steps; a step collects the oldest
+batch (already complete: every chain hashed, results in host memory) and
+submits one new batch, i.e. one K1 and one K3 launch per step (asserted from
+the engine's own launch counts).  The drain that empties the pipeline runs
+after the timer and is reported beside `value` (`drain_ms`,
+`fill_drain_gibs` = the whole run from an empty pipeline to a drained one).
+
+Multi-GPU (--scaling strong, the default; BASELINE configs[2]): every step's
+64 files are split across the ranks by LPT on bytes (hashbox_amd.shard), each
+rank pipelines its shard on its own GPU and streams; value = 8 GiB x K / the
+slowest rank's time.  --scaling weak: every rank takes a whole 8 GiB batch
+per step.  No collective touches the data: torch.distributed carries only
+the barriers, the max-time reduction and the check flags.
 
 Prints ONE JSON line on rank 0.  Multi-GPU:
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -26,6 +36,7 @@ import json
 import os
 import sys
 import time
+from collections import deque
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -38,61 +49,82 @@ K3_VALU_PER_BLOCK = 325
 VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md), GB/s
 GIB = 1 << 30
+KNAMES = ["k1_digest_scan", "k2_cut_chain", "k2c_chain_plan", "k3_block_md5", "k4_content_id"]
+KERNEL_OF = {"k1_digest_scan": "hbx_k1_digest_scan_dma", "k2_cut_chain": "hbx_k2_cut_chain",
+             "k2c_chain_plan": "hbx_k2c_plan", "k3_block_md5": "hbx_k3_block_md5",
+             "k4_content_id": "hbx_k4_content_id"}
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=600)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--files", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--files", type=int, default=64, help="files per step (whole job)")
     ap.add_argument("--file-mib", type=int, default=128)
     ap.add_argument("--seed", type=int, default=1000)
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="strong: each step's files are split across the ranks (configs[2]); "
+                         "weak: every rank takes a whole batch per step")
+    ap.add_argument("--workload", choices=["both", "random", "zipf"], default="both",
+                    help="both: the random headline plus a Zipf-duplicate line under key 'zipf'")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-files", type=int, default=32,
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use")
+    ap.add_argument("--cpu-files", type=int, default=64,
                     help="files of the batch timed on the CPU oracle (bounded sample)")
     ap.add_argument("--md5-slice", type=int, default=-1,
-                    help="K3 time slice in 64-B MD5 blocks per chain per launch (0 = each batch "
-                         "hashed alone in one launch; -1 = sized from HBM, see --hbm-frac)")
+                    help="K3 time slice in 64-B MD5 blocks per chain per launch (-1 = sized from "
+                         "the residency: ceil(blocks of an 8 MiB chunk / (R - lead)))")
     ap.add_argument("--arenas", type=int, default=0,
-                    help="distinct resident batches (default: the pipeline depth the slice "
-                         "schedule needs, so no step forces a drain)")
+                    help="distinct resident batches R (default: as many as --hbm-frac of free HBM holds)")
     ap.add_argument("--hbm-frac", type=float, default=0.95,
-                    help="with --md5-slice -1: fraction of free HBM given to resident batches; "
-                         "throughput ~ resident bytes / batch latency (the longest chunk's "
-                         "serial MD5), so the pipeline is made as deep as this allows")
+                    help="fraction of free HBM given to resident batches; throughput ~ resident bytes "
+                         "/ batch lifetime (the longest chunk's serial MD5)")
     ap.add_argument("--lead", type=int, default=2,
-                    help="steps the scan stream (K1/K2 of a new batch) may run ahead of the hash "
-                         "stream: the pipeline holds launches-per-batch + lead batches")
+                    help="launches between a batch's completion and its collection (the scan stream's "
+                         "slack): R = launches per batch + lead")
     ap.add_argument("--e2e", action="store_true",
-                    help="host-inclusive mode: files in pinned host memory, H2D of batch i+1 "
-                         "overlapped with the kernels of batch i (two contexts)")
-    ap.add_argument("--check", action="store_true",
-                    help="verify the first file of the batch against the oracle")
+                    help="host-inclusive mode: each step's batch is copied from pinned host memory "
+                         "(H2D on the engine's scan stream, overlapped with the pipeline)")
+    ap.add_argument("--no-check", action="store_true",
+                    help="skip the oracle check of the last collected and the last drained batch")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPUs; gloo for tests")
     return ap.parse_args()
 
 
-def measured_traffic(kernel, nf, fbytes):
-    """HBM bytes per launch of `kernel` from the newest committed PMC pass of
-    this same workload (profiles/*_traffic.json, written by
-    tools/pmc_traffic.py from a separate rocprofv3 --pmc FETCH_SIZE run: PMC
-    counters cannot be read inside this timed run)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
-    if not files or (nf, fbytes) != (64, 128 << 20):  # measured on the default workload only
-        return None, None
-    d = json.load(open(files[-1]))
-    k = d.get("kernels", {}).get(kernel)
-    if not k:
-        return None, None
-    return int(k["hbm_bytes"]), (os.path.relpath(files[-1], ROOT) +
-                                 ("" if k.get("calibrated") else " (uncalibrated access width)"))
+# ------------------------------------------------------------------ host --
+def cpu_info():
+    """Cores this process may use (affinity and cgroup quota) and the model."""
+    n_os = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = n_os
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = min(aff, quota) if quota else aff
+    return {"os_cpu_count": n_os, "affinity": aff, "cgroup_quota_cpus": quota, "usable": usable,
+            "model": model}
 
 
-def cpu_baseline(host_files, threads):
-    """Oracle ('port': the literal store.go:111-185 loop + RFC 1321 MD5) on the
-    host cores, on a bounded sample of the same batch."""
+def cpu_baseline(host_files, threads, info):
+    """Oracle ('port': oracle/hbx_oracle.c, the C restatement of the literal
+    storeFile loop store.go:111-185 + MD5 framing block.go:96-111, standing
+    in for the Go reference: the image has no Go toolchain) on the host
+    cores, on a bounded sample of the same batch."""
     from oracle import oracle as O
     O.lib()
     nbytes = sum(int(f.size) for f in host_files)
@@ -104,244 +136,340 @@ def cpu_baseline(host_files, threads):
     t_1 = time.perf_counter() - t0
     return {
         "value": round(nbytes / t_mt / GIB, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
-        "sample": f"{len(host_files)} of the batch's 128 MiB files ({nbytes / GIB:.1f} GiB), "
-                  f"one file per thread, literal storeFile loop + MD5 (oracle/hbx_oracle.c)",
+        "sample": f"{len(host_files)} of the batch's {host_files[0].size >> 20} MiB files "
+                  f"({nbytes / GIB:.1f} GiB), files spread over {threads} threads",
+        "what": "oracle/hbx_oracle.c: C restatement of store.go:111-185 + block.go:96-111 "
+                "(stands in for the Go reference, which cannot be built here)",
         "single_core_gibs": round(host_files[0].size / t_1 / GIB, 4),
-        "seconds": round(t_mt, 2),
+        "seconds": round(t_mt, 2), "cpu": info,
     }
 
 
-def run_e2e(a, local):
-    """PCIe-inclusive rate: the batch starts in pinned host memory and its
-    results end in host memory.  Two engine contexts alternate so the H2D
-    copy of batch i+1 (DMA engine) overlaps the kernels of batch i."""
-    import ctypes
-    from hashbox_amd import Engine, pack_arena_layout
-    nf, fbytes = a.files, a.file_mib << 20
-    lens = [fbytes] * nf
-    offs, total = pack_arena_layout(lens)
-    engs = [Engine(local, md5_slice=0), Engine(local, md5_slice=0)]
-    arenas = [torch.empty(total, dtype=torch.uint8, device=f"cuda:{local}") for _ in range(2)]
-    hp = ctypes.c_void_p()
-    assert engs[0]._L.hbx_alloc_pinned(total, ctypes.byref(hp)) == 0
-    host = np.ctypeslib.as_array((ctypes.c_uint8 * total).from_address(hp.value))
-    g = torch.Generator(device=f"cuda:{local}")
-    g.manual_seed(a.seed)
-    arenas[0].random_(0, 256, generator=g)
-    host[:] = arenas[0].cpu().numpy()
+def oracle_check(arena, offs, lens, res, threads):
+    """Every file of one collected batch against the oracle (outside the timer)."""
+    from oracle import oracle as O
+    used = int(offs[-1]) + int(lens[-1])
+    host = arena[:used].cpu().numpy()
+    files = [host[int(o):int(o) + int(n)] for o, n in zip(offs, lens)]
+    refs = O.store_batch_mt(files, threads)
+    ok = len(refs) == len(res)
+    for r, g in zip(refs, res):
+        ok = ok and np.array_equal(r.cut_ends, g.cut_ends) and np.array_equal(r.ids, g.ids)
+    return bool(ok)
 
-    def one(i):
-        e, d = engs[i % 2], arenas[i % 2]
-        e.memcpy_h2d_async(d.data_ptr(), hp.value, total)
-        e.submit_device(d.data_ptr(), offs, lens)
 
-    res = None
-    for i in range(a.warmup):  # untimed, each batch completed
-        one(i)
-        res = engs[i % 2].wait()
-    torch.cuda.synchronize()
+def measured_traffic(kernel, per_launch_bytes, batch_bytes):
+    """HBM bytes per launch of `kernel` from the newest committed PMC pass of
+    the default workload (profiles/*_traffic.json, tools/pmc_traffic.py from a
+    separate rocprofv3 --pmc FETCH_SIZE run: PMC counters cannot be read
+    inside this timed run), scaled to this launch's bytes."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
+    if not files or batch_bytes != 64 * (128 << 20):
+        return None, None
+    d = json.load(open(files[-1]))
+    k = d.get("kernels", {}).get(kernel)
+    if not k:
+        return None, None
+    return int(k["hbm_bytes"]), os.path.relpath(files[-1], ROOT)
+
+
+# -------------------------------------------------------------- pipeline --
+def lane_occupancy(arena_res, R, B, need, lanes):
+    """Chains in flight per steady-state K3 launch, from the collected cut
+    lists: batch x is in its t-th launch (t < need) in launch x + t, and a
+    chunk of `nfull` full message blocks is still in the order list then iff
+    t == 0 or nfull > t * B (K2c drops it after the launch that finishes it).
+    Launch m holds batches m, m-1, .., m-need+1 (arena (m - t) % R)."""
+    per_arena = []
+    for i in range(R):
+        res = arena_res.get(i)
+        if res is None:
+            return None
+        nf = np.concatenate([((np.diff(np.concatenate([[0], r.cut_ends.astype(np.int64)])) + 8) >> 6)
+                             for r in res if r.n_chunks] or [np.zeros(0, np.int64)])
+        per_arena.append([int(nf.size) if t == 0 else int(np.count_nonzero(nf > t * B))
+                          for t in range(need)])
+    active = [sum(per_arena[(m - t) % R][t] for t in range(need)) for m in range(R)]
+    return {"active_chains_mean": round(float(np.mean(active)), 1), "active_chains_max": int(max(active)),
+            "lanes": lanes, "occupancy_mean": round(float(np.mean(active)) / lanes, 4),
+            "occupancy_max": round(max(active) / lanes, 4)}
+
+
+def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=None):
+    """Fill to R in flight, W warm-up steps, K timed steps (collect the oldest
+    + submit one), then the drain.  Returns timings, the window's launch
+    counts and results."""
+    order = deque()  # arena index of every pending batch, oldest first
+    state = {"j": 0}
+    arena_res = {}
+
+    def submit():
+        i = state["j"] % R
+        if before_submit:
+            before_submit(i)
+        eng.submit_device(arenas[i].data_ptr(), offs, lens)
+        order.append(i)
+        state["j"] += 1
+
+    def collect():
+        i = order.popleft()
+        res = eng.wait()
+        arena_res[i] = res
+        return i, res
+
+    torch.cuda.synchronize(dev)
+    t_fill = time.perf_counter()
+    for _ in range(R):
+        submit()
+    for _ in range(warmup):
+        collect()
+        submit()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    eng.stage_totals(reset=True)  # everything before the window is complete and harvested
     t0 = time.perf_counter()
-    for j in range(a.steps):  # batch j's copy+kernels overlap batch j-1's
-        one(j)
-        if j > 0:
-            res = engs[(j - 1) % 2].wait()
-    res = engs[(a.steps - 1) % 2].wait()
-    el = time.perf_counter() - t0
-    gib = a.steps * nf * fbytes / el / GIB
-    out = {"metric": "end-to-end GiB/s, pinned host memory -> HBM -> chunk lists + block IDs in "
-                     "host memory (H2D overlapped with kernels)",
-           "value": round(gib, 3), "unit": "GiB/s", "n_gpus": 1, "steps": a.steps,
-           "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3),
-           "config": {"workload": f"{nf} x {a.file_mib} MiB random buffers", "contexts": 2},
-           "chunks_per_step": sum(r.n_chunks for r in res)}
-    print(json.dumps(out), flush=True)
-    for e in engs:
-        e.close()
-    engs[0]._L.hbx_free_pinned(hp)
+    last = None
+    for _ in range(steps):
+        last = collect()
+        submit()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    tot_ms, tot_n = eng.stage_totals()
+    t_d = time.perf_counter()
+    drained = None
+    while order:
+        drained = collect()
+    torch.cuda.synchronize(dev)
+    t2 = time.perf_counter()
+    return {"el": t1 - t0, "drain": t2 - t_d, "fill_to_drained": t2 - t_fill,
+            "batches_total": state["j"], "tot_ms": tot_ms, "tot_n": tot_n,
+            "last": last, "drained": drained, "arena_res": arena_res}
+
+
+def max_over_ranks(x, dist, dev, op="max"):
+    if not dist:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.MIN)
+    return float(t.item())
+
+
+def run_workload(a, name, eng, arenas, offs, lens, R, B, need, lanes, dist, dev, world, rank,
+                 job_batch_bytes, check_threads, before_submit=None):
+    """One steady-state measurement; returns the JSON fields of its line."""
+    r = steady(eng, arenas, offs, lens, R, a.steps, a.warmup, dist, dev, before_submit)
+    el = max_over_ranks(r["el"], dist, dev)
+    tot_ms, tot_n = r["tot_ms"], r["tot_n"]
+    k1_n, k3_n = int(tot_n[0]), int(tot_n[3])
+    window_exact = k1_n == a.steps and k3_n == a.steps
+    if not window_exact:
+        raise RuntimeError(f"{name}: timed window holds {k1_n} K1 and {k3_n} K3 launches, expected "
+                           f"{a.steps} each (a forced drain or an empty batch inside the window)")
+    rank_batch = int(sum(int(n) for n in lens))
+    avg_ms = tot_ms / np.maximum(tot_n, 1)
+    # dominant kernel: K3.  Algorithmic bytes per launch = the rank's batch
+    # bytes (one K3 launch per step advances every chain in flight; in steady
+    # state the chains hashed per launch add up to one batch), over the K3
+    # launches of the window only.
+    per_launch = a.steps * rank_batch / k3_n
+    achieved = per_launch / (avg_ms[3] * 1e-3) / 1e9
+    traffic, traffic_src = measured_traffic(KERNEL_OF["k3_block_md5"], per_launch, rank_batch)
+    k1_gbs = (a.steps * rank_batch / k1_n) / (avg_ms[0] * 1e-3) / 1e9 if tot_ms[0] > 0 else 0.0
+    k3_bps = a.steps * rank_batch / (tot_ms[3] * 1e-3) if tot_ms[3] > 0 else 0.0
+    res = r["last"][1]
+    n_chunks = sum(x.n_chunks for x in res)
+    longest = max((int(np.max(np.diff(np.concatenate([[0], x.cut_ends]).astype(np.int64))))
+                   for x in res if x.n_chunks), default=0)
+    check = None
+    if not a.no_check:  # outside the timer: the last batch collected in the window, and the
+        # last one drained (completed by the forced drain launch)
+        ok = oracle_check(arenas[r["last"][0]], offs, lens, res, check_threads)
+        if r["drained"] is not None:
+            ok = ok and oracle_check(arenas[r["drained"][0]], offs, lens, r["drained"][1], check_threads)
+        check = bool(max_over_ranks(1.0 if ok else 0.0, dist, dev, op="min") == 1.0)
+    value = a.steps * job_batch_bytes / el / GIB
+    drain = max_over_ranks(r["drain"], dist, dev)
+    fill = max_over_ranks(r["fill_to_drained"], dist, dev)
+    out = {
+        "value": round(value, 3), "ms_per_step": round(el / a.steps * 1e3, 4),
+        "drain_ms": round(drain * 1e3, 2),
+        "fill_drain_gibs": round(r["batches_total"] * job_batch_bytes / fill / GIB, 3),
+        "chunks_per_gpu_step": n_chunks,
+        "longest_chunk_bytes": longest,
+        "roofline": {"kernel": "k3_block_md5", "bound": "hbm", "achieved": round(achieved, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                     "traffic": traffic, "traffic_source": traffic_src, "launches": k3_n,
+                     "avg_launch_ms": round(float(avg_ms[3]), 4),
+                     "algorithmic_bytes_per_launch": int(per_launch), "window_only": True},
+        "k1_roofline": {"achieved": round(k1_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(k1_gbs / HBM_PEAK_GBS, 4), "avg_launch_ms": round(float(avg_ms[0]), 4)},
+        # K3 is VALU-issue work: ~325 VALU per 64-B block on the cooperative
+        # path (5 per MD5 step); chip peak 256 CU x 4 SIMD-32 x 32 lanes x
+        # 2.4 GHz; one wave issues at most one VALU per 4 cycles.
+        "k3_valu": {"valu_per_block": K3_VALU_PER_BLOCK,
+                    "achieved_tops": round(k3_bps * K3_VALU_PER_BLOCK / 64 / 1e12, 3),
+                    "peak_tops": round(VALU_PEAK_LANE_OPS / 1e12, 2),
+                    "frac": round(k3_bps * K3_VALU_PER_BLOCK / 64 / VALU_PEAK_LANE_OPS, 4)},
+        "k3_lanes": lane_occupancy(r["arena_res"], R, B, need, lanes),
+        "kernel_ms_per_step": {n: round(float(v) / a.steps, 4) for n, v in zip(KNAMES, tot_ms)},
+        "window_launches": {n: int(v) for n, v in zip(KNAMES, tot_n)},
+    }
+    if check is not None:
+        out["check_vs_oracle"] = check
+    return out
 
 
 def main():
     a = parse()
-    if a.e2e:
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-        return run_e2e(a, int(os.environ.get("LOCAL_RANK", "0")))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        if rank == 0:
-            print(f"note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE",
-                  file=sys.stderr)
-    torch.cuda.set_device(local)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if world != a.gpus and rank == 0:
+        print(f"note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    ndev = torch.cuda.device_count()
+    dev_idx = local % max(ndev, 1)
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(a.dist_backend)
+    red_dev = dev if (dist and a.dist_backend == "nccl") else torch.device("cpu")
 
-    from hashbox_amd import Engine, pack_arena_layout
+    from hashbox_amd import Engine, _lib
+    from hashbox_amd.shard import lpt_assign
+    import workloads as W
 
-    dev = torch.device("cuda", local)
-    nf, fbytes = a.files, a.file_mib << 20
-    lens = [fbytes] * nf
-    offs, total = pack_arena_layout(lens)
-    # launches a batch needs before its chains are all hashed; a batch can be
-    # collected without a forced drain once `need` newer steps have launched
+    fbytes = a.file_mib << 20
+    job_lens = [fbytes] * a.files
+    mine = lpt_assign(job_lens, world)[rank] if a.scaling == "strong" else list(range(a.files))
+    lens = [job_lens[i] for i in mine]
+    if not lens:
+        raise SystemExit(f"rank {rank} has no files: --files {a.files} < world {world}")
+    nf = len(lens)
+    offs, total = W.pack_layout(lens)
+    job_batch = (sum(job_lens) if a.scaling == "strong" else sum(job_lens) * world)
+    # launches a batch needs before its chains are all hashed
     nfull = (min(fbytes, 8 << 20) + 8) >> 6
-    # a batch holds its arena from its K1 until its last K3 launch; with
-    # `lead` more arenas than launches per batch, the scan stream runs `lead`
-    # steps ahead of the hash stream and never waits for a collect
+    # ranks sharing one device (tests) share its HBM
+    share = max(1, -(-local_world // max(ndev, 1)))
     free, _ = torch.cuda.mem_get_info(dev)
-    r_fit = max(a.lead + 1, int(free * a.hbm_frac) // (total + (64 << 20)))
+    r_fit = max(a.lead + 1, int(free * a.hbm_frac / share) // (total + (64 << 20)))
+    if a.e2e:
+        r_fit = min(r_fit, a.lead + 2)  # PCIe-bound: a shallow pipeline suffices
     if a.md5_slice < 0:
         R = a.arenas if a.arenas > 0 else r_fit
         B = -(-nfull // max(1, R - a.lead))
     else:
         B = a.md5_slice
+        R = a.arenas if a.arenas > 0 else min((1 if B == 0 else -(-nfull // B)) + a.lead, r_fit)
     need = 1 if B == 0 else -(-nfull // B)
-    if a.arenas > 0:
-        R = a.arenas
-    elif a.md5_slice >= 0:
-        # a short slice needs more launches per batch than HBM holds batches:
-        # cap the residency (collects then wait for the hash stream)
-        R = min(need + a.lead, r_fit)
-    # synthetic uniform random bytes, generated on the device (per-rank seed);
-    # R distinct resident batches, batch j reads arena j % R
-    g = torch.Generator(device=dev)
-    g.manual_seed(a.seed + 7919 * rank)
-    arenas = []
-    for _ in range(R):
-        t = torch.empty(total, dtype=torch.uint8, device=dev)
-        t.random_(0, 256, generator=g)
-        arenas.append(t)
-    arena = arenas[0]
-    torch.cuda.synchronize()
+    if need + 1 > R:
+        raise SystemExit(f"pipeline depth {R} < launches per batch {need} + 1: raise --arenas or the slice")
+    cores = cpu_info()
+    threads = a.cpu_threads or cores["usable"]
+    if dist:  # ranks share the host's cores for the oracle check
+        threads = max(1, threads // local_world)
+    arenas = W.random_arenas(R, total, a.seed + 7919 * rank, dev)
+    torch.cuda.synchronize(dev)
 
-    eng = Engine(local, md5_slice=B)
+    eng = Engine(dev_idx, md5_slice=B)
     # every batch slot, chain table and summary buffer of the pipeline is
-    # allocated now: an allocation inside the timed region would drain both
-    # streams
-    eng.reserve(R + 1, nf, nf * fbytes)
-    # single-batch latency (one batch alone, synchronous call), untimed
-    for _ in range(2):
-        eng.chunk_hash_device(arena.data_ptr(), offs, lens)
+    # allocated now: an allocation inside the timed region would drain the streams
+    eng.reserve(R + 1, nf, sum(lens))
+    for _ in range(2):  # single-batch latency (one batch alone, synchronous call), untimed
+        eng.chunk_hash_device(arenas[0].data_ptr(), offs, lens)
     latency = eng.stage_times()
+    lanes = torch.cuda.get_device_properties(dev).multi_processor_count * 4 * 64
 
-    def run(steps):
-        """steps batches through the pipeline, fully drained; last result."""
-        last = None
-        for j in range(steps):
-            if eng.pending() >= R:  # arena j % R is free once its batch is collected
-                last = eng.wait()
-            eng.submit_device(arenas[j % R].data_ptr(), offs, lens)
-        while eng.pending():
-            last = eng.wait()
-        return last
+    before = None
+    host_pin = None
+    if a.e2e:  # the batch starts in pinned host memory; each step copies it into its arena
+        import ctypes
+        used = int(offs[-1]) + lens[-1]
+        hp = ctypes.c_void_p()
+        if eng._L.hbx_alloc_pinned(used, ctypes.byref(hp)) != 0:
+            raise RuntimeError("hbx_alloc_pinned failed")
+        host_pin = hp
+        np.ctypeslib.as_array((ctypes.c_uint8 * used).from_address(hp.value))[:] = \
+            arenas[0][:used].cpu().numpy()
 
-    run(a.warmup)
-    eng.stage_totals(reset=True)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    res = run(a.steps)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if dist:
-        dist.barrier()
-    el = t1 - t0
-    if dist:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    tot_ms, tot_n = eng.stage_totals()
-    n_chunks = sum(r.n_chunks for r in res)
-    longest = max(int(np.max(np.diff(np.concatenate([[0], r.cut_ends]).astype(np.int64))))
-                  for r in res if r.n_chunks)
+        def before(i):
+            eng.memcpy_h2d_async(arenas[i].data_ptr(), host_pin.value, used)
 
-    check = None
-    if a.check and rank == 0:  # every file of the last timed batch vs the oracle
-        from oracle import oracle as O
-        last = arenas[(a.steps - 1) % R]
-        host = [last[int(o):int(o) + fbytes].cpu().numpy() for o in offs]
-        refs = O.store_batch_mt(host, a.cpu_threads)
-        check = all(np.array_equal(r.cut_ends, g.cut_ends) and np.array_equal(r.ids, g.ids)
-                    for r, g in zip(refs, res)) and len(res) == len(refs)
-        del host
+    lines = {}
+    workloads = ["random", "zipf"] if a.workload == "both" else [a.workload]
+    if a.e2e:  # each step copies the random batch in: one line
+        workloads = ["random"]
+    zipf_repeat = None
+    for wl in workloads:
+        if wl == "zipf":
+            zipf_repeat = W.zipf_fill(arenas, int(offs[-1]) + lens[-1], a.seed + 4 + 7919 * rank)
+        lines[wl] = run_workload(a, wl, eng, arenas, offs, lens, R, B, need, lanes, dist, red_dev,
+                                 world, rank, job_batch, threads, before)
+        if zipf_repeat is not None and wl == "zipf":
+            lines[wl]["repeat_fraction"] = round(zipf_repeat, 4)
 
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.e2e:
+        # rebuild the random batch 0 (the arenas may hold the Zipf corpus now)
+        g = torch.Generator(device=dev)
+        g.manual_seed(a.seed)
+        arenas[0].random_(0, 256, generator=g)
         k = min(a.cpu_files, nf)
-        host = [arena[int(offs[i]):int(offs[i]) + fbytes].cpu().numpy() for i in range(k)]
-        cpu = cpu_baseline(host, a.cpu_threads)
+        host = arenas[0][:int(offs[k - 1]) + lens[k - 1]].cpu().numpy()
+        cpu = cpu_baseline([host[int(offs[i]):int(offs[i]) + lens[i]] for i in range(k)], threads, cores)
         del host
 
-    batch_bytes = nf * fbytes
-    total_bytes = batch_bytes * world * a.steps
-    value = total_bytes / el / GIB
-    names = ["k1_digest_scan", "k2_cut_chain", "k2c_chain_plan", "k3_block_md5", "k4_content_id"]
-    kernel_of = {"k1_digest_scan": "hbx_k1_digest_scan_dma", "k2_cut_chain": "hbx_k2_cut_chain",
-                 "k2c_chain_plan": "hbx_k2c_plan", "k3_block_md5": "hbx_k3_block_md5",
-                 "k4_content_id": "hbx_k4_content_id"}
-    avg_ms = tot_ms / np.maximum(tot_n, 1)
-    dom = int(np.argmax(tot_ms))
-    # algorithmic bytes per launch: every input byte is scanned once by K1 and
-    # MD5-hashed once by K3, so a kernel's average launch covers
-    # (bytes of the K batches) / (its launches); K2/K2c/K4 are priced the same
-    per_launch = a.steps * batch_bytes / max(int(tot_n[dom]), 1)
-    achieved = per_launch / (avg_ms[dom] * 1e-3) / 1e9
-    traffic, traffic_src = measured_traffic(kernel_of[names[dom]], nf, fbytes)
-    k1_gbs = (a.steps * batch_bytes / max(int(tot_n[0]), 1)) / (avg_ms[0] * 1e-3) / 1e9 \
-        if tot_ms[0] > 0 else 0.0
-    k3_bps = a.steps * batch_bytes / (tot_ms[3] * 1e-3) if tot_ms[3] > 0 else 0.0
+    head = lines[workloads[0]]
+    if a.e2e:
+        metric = ("end-to-end GiB/s, pinned host memory -> HBM (H2D on the scan stream) -> chunk lists + "
+                  "block IDs in host memory, pipelined MD5")
+    else:
+        metric = METRIC
     out = {
-        "metric": METRIC,
-        "value": round(value, 3),
+        "metric": metric,
+        "value": head["value"],
         "unit": "GiB/s",
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": round(el / a.steps * 1e3, 3),
+        "ms_per_step": head["ms_per_step"],
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": a.scaling,
         "vs_baseline": None,
         "dtype": "u8",
-        "data": f"synthetic: uniform random bytes generated on the device (torch Generator), "
-                f"{R} distinct resident batches, resident in HBM before timing",
-        "config": {"workload": f"{nf} x {a.file_mib} MiB random buffers per GPU per step, rollsum "
-                               "split + MD5 block IDs + file content ids, device-resident "
-                               "(configs[1])",
-                   "files_per_step": nf, "file_bytes": fbytes, "chunks_per_step": n_chunks,
-                   "longest_chunk_bytes": longest, "md5_slice_blocks": B,
-                   "pipeline_depth": R, "launches_per_batch": need, "scan_lead": a.lead,
-                   "k1_kernel": os.environ.get("HBX_K1_MODE", "default"),
-                   "parallelism": f"file-sharded x{world} (independent HIP streams, no data-path "
-                                  "collective)"},
-        "roofline": {"kernel": names[dom], "bound": "hbm", "achieved": round(achieved, 2),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                     "traffic": traffic, "traffic_source": traffic_src,
-                     "launches": int(tot_n[dom]), "avg_launch_ms": round(float(avg_ms[dom]), 4),
-                     "algorithmic_bytes_per_launch": int(per_launch)},
-        # K3 is VALU-issue work: ~325 VALU per 64-B block on the cooperative path
-        # (5 per MD5 step).  Chip peak = 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz;
-        # one wave alone issues at most one VALU per 4 cycles (MI355X_MICROARCH.md),
-        # so one serial chain is floored at 325 x 4 cycles per block.
-        "k3_valu": {"valu_per_block": K3_VALU_PER_BLOCK,
-                    "achieved_tops": round(k3_bps * K3_VALU_PER_BLOCK / 64 / 1e12, 3),
-                    "peak_tops": round(VALU_PEAK_LANE_OPS / 1e12, 2),
-                    "frac": round(k3_bps * K3_VALU_PER_BLOCK / 64 / VALU_PEAK_LANE_OPS, 4)},
-        "kernel_ms_per_step": {n: round(float(v) / a.steps, 4) for n, v in zip(names, tot_ms)},
-        "kernel_launches": {n: int(v) for n, v in zip(names, tot_n)},
-        "k1_roofline": {"achieved": round(k1_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(k1_gbs / HBM_PEAK_GBS, 4)},
-        "single_batch": {"ms": round(float(latency[4]), 3),
-                         "gibs": round(batch_bytes / GIB / (float(latency[4]) * 1e-3), 3),
-                         "stages_ms": [round(float(x), 3) for x in latency]},
-        "cpu_baseline": cpu,
+        "data": f"synthetic: uniform random bytes generated on the device (torch Generator), {R} distinct "
+                f"resident batches per GPU, resident in HBM before timing",
+        "config": {"workload": f"{a.files} x {a.file_mib} MiB random buffers per step, rollsum split + MD5 "
+                               "block IDs + file content ids, device-resident (configs[1]"
+                               + (", sharded by file across GPUs: configs[2])" if world > 1 else ")"),
+                   "files_per_step": a.files, "files_per_gpu": nf, "file_bytes": fbytes,
+                   "md5_slice_blocks": B, "pipeline_depth": R, "launches_per_batch": need,
+                   "scan_lead": a.lead, "parallelism": f"file-sharded x{world} ({a.scaling} scaling; "
+                                                       "independent HIP streams, no data-path collective)"},
     }
-    if check is not None:
-        out["check_vs_oracle"] = check
+    out.update({k: v for k, v in head.items() if k not in ("value", "ms_per_step")})
+    out["single_batch"] = {"ms": round(float(latency[4]), 3),
+                           "gibs": round(sum(lens) / GIB / (float(latency[4]) * 1e-3), 3),
+                           "stages_ms": [round(float(x), 3) for x in latency]}
+    out["cpu_baseline"] = cpu
+    if "zipf" in lines and workloads[0] != "zipf":
+        out["zipf"] = dict(lines["zipf"], workload=f"{a.files} x {a.file_mib} MiB Zipf-duplicated buffers "
+                                                   "(configs[3] scheme), device-resident")
+    out["lib"] = _lib.identity()
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if host_pin is not None:
+        eng._L.hbx_free_pinned(host_pin)
     eng.close()
     if dist:
         dist.destroy_process_group()

@@ -9,8 +9,10 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# HBX_LIB overrides the in-tree library (A/B experiments with variant builds).
-LIB_PATH = os.environ.get("HBX_LIB") or os.path.join(HERE, "libhbxgpu.so")
+# The in-tree build only: no environment override, so a variant build can
+# never stand in for the product silently (A/B runs copy a variant over this
+# file explicitly, tools/gpu_ab.sh).
+LIB_PATH = os.path.join(HERE, "libhbxgpu.so")
 
 HBX_OK = 0
 ERRORS = {-1: "HBX_ERR_ARG", -2: "HBX_ERR_HIP", -3: "HBX_ERR_CAPACITY", -4: "HBX_ERR_IO",
@@ -63,6 +65,15 @@ class FileSummary(ctypes.Structure):
 BATCH_READY = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64)
 
 _lib = None
+
+
+def identity() -> dict:
+    """Which library this process runs: path and content hash (bench.py
+    prints it in its JSON line)."""
+    import hashlib
+    with open(LIB_PATH, "rb") as fh:
+        sha = hashlib.sha256(fh.read()).hexdigest()[:16]
+    return {"path": os.path.relpath(LIB_PATH, os.path.dirname(HERE)), "sha256_16": sha}
 
 
 def load() -> ctypes.CDLL:

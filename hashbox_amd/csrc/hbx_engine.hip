@@ -185,6 +185,12 @@ struct hbx_ctx {
 
   std::deque<Batch*> pending;  // submitted, not yet collected (FIFO)
   std::vector<Batch*> pool;
+  // A HIP error after a batch's device work was enqueued leaves chains of it
+  // in the carried order lists: the context refuses further pipelined work
+  // (HBX_ERR_STATE) and the batch's buffers are parked here, never reused,
+  // until hbx_ctx_destroy.
+  bool broken = false;
+  std::vector<Batch*> parked;
   std::vector<TimedLaunch> open_t;
   std::vector<hipEvent_t> ev_pool;
   double tot_ms[5] = {0, 0, 0, 0, 0};
@@ -430,11 +436,56 @@ int md5_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
   return HBX_OK;
 }
 
+// The order-list and planner buffers one more launch needs with `extra`
+// chains joining the unfinalized batches' chains.
+int ensure_plan_buffers(hbx_ctx* c, uint64_t extra) {
+  uint64_t bound = 64 + extra;  // entries <= chains of the unfinalized batches
+  for (Batch* b : c->pending)
+    if (!b->finalized) bound += b->caps;
+  int rc = HBX_OK;
+  for (int t = 0; t < 3 && !rc; t++) {
+    rc = ensure_shared(c, c->d_order[t], bound * sizeof(OrderEntry));
+    if (!rc) rc = ensure_shared(c, c->d_octl[t], 256);
+  }
+  if (!rc) rc = ensure_shared(c, c->d_plan, 2 * kPlanBins * sizeof(uint32_t));
+  return rc;
+}
+
+// A submit failed.  Before any device work of `b` was enqueued (`enqueued`
+// false) the batch simply returns to the pool.  After it, the batch leaves
+// the FIFO (so no later wait collects it into caller memory that may be
+// freed), the streams drain, its buffers are parked (its chains may still be
+// in the carried order lists) and the context refuses further pipelined work.
+int submit_abort(hbx_ctx* c, Batch* b, int rc, bool enqueued) {
+  const std::string keep = c->err;
+  for (auto it = c->pending.begin(); it != c->pending.end(); ++it)
+    if (*it == b) {
+      c->pending.erase(it);
+      break;
+    }
+  if (!enqueued) {
+    c->pool.push_back(b);
+    return rc;
+  }
+  for (hipStream_t s : {c->stream, c->cstream, c->hstream, c->rstream})
+    if (s) (void)hipStreamSynchronize(s);
+  c->parked.push_back(b);
+  c->broken = true;
+  c->err = keep + " (context is unusable for pipelined work; destroy it)";
+  return rc;
+}
+
+int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, const uint64_t* offs,
+                        const uint64_t* lens, uint32_t budget, uint64_t slices, size_t meta_bytes, int slot);
+
 // Plan + enqueue one device batch (K1, K2, first MD5 launch).  Results are
-// collected by wait_oldest in submission order.
+// collected by wait_oldest in submission order.  Every validation and
+// allocation happens before the batch joins the FIFO; a failure after that
+// removes it again (submit_abort), so a failed submit leaves no pending batch.
 int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* offs,
                  const uint64_t* lens, uint64_t* cut_ends, uint8_t* ids, const uint64_t* out_base,
                  const uint64_t* caps, hbx_file_summary* sums, uint32_t budget) {
+  if (c->broken) return c->fail(HBX_ERR_STATE, "context is unusable after a failed submit; destroy it");
   if (n > 0xFFFFFFFFull) return c->fail(HBX_ERR_ARG, "too many files");
   for (uint64_t f = 0; f < n; f++)
     if (offs[f] % HBX_ARENA_ALIGN) return c->fail(HBX_ERR_ARG, "file offset not 16-byte aligned");
@@ -474,7 +525,29 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
   // remainder fits
   const uint64_t nfull = (std::min<uint64_t>(longest, HBX_MAX_BLOCK_SIZE) + 8) >> 6;
   b->need = budget == kBudgetAll ? 1u : (uint32_t)std::max<uint64_t>(1, (nfull + budget - 1) / budget);
+  const uint64_t nt = c->h_tiles.size();
+  // meta block: off | len | slice_base | cut_base | tiles
+  const size_t meta_bytes = n * 8 * 4 + nt * sizeof(uint2);
+  const int slot = c->ssum_slot;
+  if (n) {  // every allocation first: the batch is not in the FIFO yet
+    int rc = HBX_OK;
+    for (hipError_t e : {b->h_meta.ensure(meta_bytes), b->d_meta.ensure(meta_bytes), b->d_cuts.ensure(tcaps * 8),
+                         b->d_count.ensure(n * 4), b->d_ids.ensure(tcaps * 16), b->d_cid.ensure(n * 16),
+                         b->d_ctype.ensure(n * 4), b->d_run.ensure(tcaps * sizeof(Chain)),
+                         b->d_fresh.ensure(tcaps * sizeof(OrderEntry)), b->d_fcnt.ensure(256),
+                         b->h_res.ensure(res_layout(n, tcaps).total)})
+      if (e != hipSuccess && !rc) rc = c->hip(e, "batch buffers");
+    if (!rc) rc = ensure_shared(c, c->d_ssum[slot], (slices + 1) * sizeof(uint2));  // +1: dummy slot
+    if (!rc) rc = ensure_plan_buffers(c, tcaps);
+    if (rc) return submit_abort(c, b, rc, false);
+  }
   c->pending.push_back(b);
+  const int rc = submit_batch_launch(c, b, d_arena, n, offs, lens, budget, slices, meta_bytes, slot);
+  return rc ? submit_abort(c, b, rc, true) : HBX_OK;
+}
+
+int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, const uint64_t* offs,
+                        const uint64_t* lens, uint32_t budget, uint64_t slices, size_t meta_bytes, int slot) {
   hipStream_t s = c->stream;
   if (n == 0) {
     for (int i = 0; i < 4; i++) HBX_TRY(c, hipEventRecord(b->ev[i], s));
@@ -483,31 +556,15 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
     return HBX_OK;
   }
   const uint64_t nt = c->h_tiles.size();
-  // meta block: off | len | slice_base | cut_base | tiles
-  const size_t meta_bytes = n * 8 * 4 + nt * sizeof(uint2);
-  HBX_TRY(c, b->h_meta.ensure(meta_bytes));
-  HBX_TRY(c, b->d_meta.ensure(meta_bytes));
   uint64_t* hm = b->h_meta.as<uint64_t>();
   std::memcpy(hm, offs, n * 8);
   std::memcpy(hm + n, lens, n * 8);
   std::memcpy(hm + 2 * n, c->h_slice_base.data(), n * 8);
   std::memcpy(hm + 3 * n, b->cut_base.data(), n * 8);
   if (nt) std::memcpy(hm + 4 * n, c->h_tiles.data(), nt * sizeof(uint2));
-  const int slot = c->ssum_slot;
   c->ssum_slot ^= 1;
   DevBuf& ssum = c->d_ssum[slot];
-  int rc = ensure_shared(c, ssum, (slices + 1) * sizeof(uint2));  // +1: dummy slot
-  if (rc) return rc;
-  HBX_TRY(c, b->d_cuts.ensure(tcaps * 8));
-  HBX_TRY(c, b->d_count.ensure(n * 4));
-  HBX_TRY(c, b->d_ids.ensure(tcaps * 16));
-  HBX_TRY(c, b->d_cid.ensure(n * 16));
-  HBX_TRY(c, b->d_ctype.ensure(n * 4));
-  HBX_TRY(c, b->d_run.ensure(tcaps * sizeof(Chain)));
-  HBX_TRY(c, b->d_fresh.ensure(tcaps * sizeof(OrderEntry)));
-  HBX_TRY(c, b->d_fcnt.ensure(256));
-  HBX_TRY(c, b->h_res.ensure(res_layout(n, tcaps).total));
-  if ((rc = ensure_shared(c, c->d_plan, 2 * kPlanBins * sizeof(uint32_t)))) return rc;
+  int rc = HBX_OK;
 
   HBX_TRY(c, hipMemcpyAsync(b->d_meta.p, hm, meta_bytes, hipMemcpyHostToDevice, s));
   const uint64_t* d_off = b->d_meta.as<uint64_t>();
@@ -563,12 +620,17 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
   return md5_launch(c, b, budget);
 }
 
+int submit_verify_launch(hbx_ctx* c, Batch* b, const uint8_t* arena, uint64_t n, const uint64_t* offs,
+                         const uint64_t* lens, const uint8_t* links, const uint64_t* link_base,
+                         const uint32_t* n_links, uint64_t nlinks_total, size_t meta_bytes, uint32_t budget);
+
 // Plan + enqueue a VerifyBlock batch: K6p hashes each block's prefix blocks
 // and turns the rest into K3 chains, which then share the time-sliced MD5
 // pipeline (and the FIFO of hbx_wait) with the chunking batches.
 int submit_verify(hbx_ctx* c, const uint8_t* arena, uint64_t n, const uint64_t* offs, const uint64_t* lens,
                   const uint8_t* links, const uint64_t* link_base, const uint32_t* n_links, uint8_t* ids,
                   const uint8_t* expect, uint8_t* ok, uint64_t* n_bad, uint32_t budget) {
+  if (c->broken) return c->fail(HBX_ERR_STATE, "context is unusable after a failed submit; destroy it");
   if (n > 0xFFFFFFFFull) return c->fail(HBX_ERR_ARG, "too many blocks");
   uint64_t nlinks_total = 0, longest = 0;
   for (uint64_t i = 0; i < n; i++) {
@@ -588,7 +650,26 @@ int submit_verify(hbx_ctx* c, const uint8_t* arena, uint64_t n, const uint64_t* 
   b->v_ok = ok;
   b->v_nbad = n_bad;
   b->need = budget == kBudgetAll ? 1u : (uint32_t)std::max<uint64_t>(1, (longest + budget - 1) / budget);
+  // meta block: descriptors | links
+  const size_t meta_bytes = n * sizeof(VerifyDesc) + 16 * nlinks_total;
+  if (n) {  // every allocation first: the batch is not in the FIFO yet
+    int rc = HBX_OK;
+    for (hipError_t e : {b->h_meta.ensure(meta_bytes), b->d_meta.ensure(meta_bytes), b->d_ids.ensure(n * 16),
+                         b->d_run.ensure(n * sizeof(Chain)), b->d_fresh.ensure(n * sizeof(OrderEntry)),
+                         b->d_fcnt.ensure(256), b->h_res.ensure(n * 16)})
+      if (e != hipSuccess && !rc) rc = c->hip(e, "verify batch buffers");
+    if (!rc) rc = ensure_plan_buffers(c, n);
+    if (rc) return submit_abort(c, b, rc, false);
+  }
   c->pending.push_back(b);
+  const int rc = submit_verify_launch(c, b, arena, n, offs, lens, links, link_base, n_links, nlinks_total,
+                                      meta_bytes, budget);
+  return rc ? submit_abort(c, b, rc, true) : HBX_OK;
+}
+
+int submit_verify_launch(hbx_ctx* c, Batch* b, const uint8_t* arena, uint64_t n, const uint64_t* offs,
+                         const uint64_t* lens, const uint8_t* links, const uint64_t* link_base,
+                         const uint32_t* n_links, uint64_t nlinks_total, size_t meta_bytes, uint32_t budget) {
   hipStream_t s = c->stream;
   if (n == 0) {
     for (int i = 0; i < 4; i++) HBX_TRY(c, hipEventRecord(b->ev[i], s));
@@ -596,15 +677,6 @@ int submit_verify(hbx_ctx* c, const uint8_t* arena, uint64_t n, const uint64_t* 
     HBX_TRY(c, hipEventRecord(b->ev[4], s));
     return HBX_OK;
   }
-  // meta block: descriptors | links
-  const size_t meta_bytes = n * sizeof(VerifyDesc) + 16 * nlinks_total;
-  HBX_TRY(c, b->h_meta.ensure(meta_bytes));
-  HBX_TRY(c, b->d_meta.ensure(meta_bytes));
-  HBX_TRY(c, b->d_ids.ensure(n * 16));
-  HBX_TRY(c, b->d_run.ensure(n * sizeof(Chain)));
-  HBX_TRY(c, b->d_fresh.ensure(n * sizeof(OrderEntry)));
-  HBX_TRY(c, b->d_fcnt.ensure(256));
-  HBX_TRY(c, b->h_res.ensure(n * 16));
   VerifyDesc* hd = b->h_meta.as<VerifyDesc>();
   uint8_t* dl = b->d_meta.as<uint8_t>() + n * sizeof(VerifyDesc);
   for (uint64_t i = 0; i < n; i++) {
@@ -684,6 +756,11 @@ int collect_batch(hbx_ctx* c, Batch* b) {
 int wait_oldest(hbx_ctx* c) {
   if (c->pending.empty()) return HBX_OK;
   Batch* b = c->pending.front();
+  if (c->broken) {  // drop it uncollected: its results are never written to the caller
+    c->pending.pop_front();
+    c->parked.push_back(b);
+    return c->fail(HBX_ERR_STATE, "context is unusable after a failed submit; destroy it");
+  }
   if (!b->finalized) {
     int rc = plan_launch(c, nullptr, kBudgetAll);
     if (!rc) rc = md5_launch(c, nullptr, kBudgetAll);
@@ -824,6 +901,7 @@ void hbx_ctx_destroy(hbx_ctx* c) {
   for (hipEvent_t e : c->h2d_done)
     if (e) (void)hipEventDestroy(e);
   for (Batch* b : c->pending) c->pool.push_back(b);
+  for (Batch* b : c->parked) c->pool.push_back(b);
   for (Batch* b : c->pool) {
     b->release();
     delete b;
@@ -858,6 +936,10 @@ int hbx_stage_times(hbx_ctx* c, float ms[5]) {
 int hbx_set_md5_slice(hbx_ctx* c, uint32_t blocks) {
   if (!c) return HBX_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
+  // a pending batch's launch count was fixed at submit from the slice of
+  // that moment: changing it now would finalize batches whose chains are
+  // not all hashed
+  if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
   c->md5_slice = blocks;
   return HBX_OK;
 }
@@ -978,9 +1060,11 @@ int hbx_chunk_hash(hbx_ctx* c, const uint8_t* data, uint64_t len, uint64_t* cut_
                    uint8_t* ids, uint64_t cap, uint64_t* n_chunks) {
   if (!c || (len && !data)) return HBX_ERR_ARG;
   const uint64_t base = 0;
-  hbx_file_summary s;
+  hbx_file_summary s{};
   int rc = hbx_chunk_hash_batch(c, 1, &data, &len, cut_ends, ids, &base, &cap, &s);
-  if (n_chunks) *n_chunks = s.n_chunks;
+  // the count is meaningful on success and on HBX_ERR_CAPACITY (the caller
+  // retries with that many slots); otherwise it is left untouched
+  if (n_chunks && (rc == HBX_OK || rc == HBX_ERR_CAPACITY)) *n_chunks = s.n_chunks;
   return rc;
 }
 

@@ -390,9 +390,10 @@ class Engine:
         oc = np.ascontiguousarray(caps, np.uint64)
         oo = np.zeros(n, np.uint64)
         oo[1:] = np.cumsum((oc[:-1] + 255) // 256 * 256)
-        d_in = torch.from_numpy(host).to("cuda:0")
-        d_out = torch.zeros(int(oo[-1] + oc[-1]) + 64, dtype=torch.uint8, device="cuda:0")
-        torch.cuda.synchronize()
+        dev = torch.device("cuda", self.device)  # this engine's GPU, not torch's current one
+        d_in = torch.from_numpy(host).to(dev)
+        d_out = torch.zeros(int(oo[-1] + oc[-1]) + 64, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize(dev)
         ol, st = self.inflate_blocks_device(d_in.data_ptr(), io, [a.size for a in arrs], d_out.data_ptr(), oo, oc)
         out = d_out.cpu().numpy()
         return [out[int(oo[i]):int(oo[i] + ol[i])].tobytes() if st[i] == 0 else None for i in range(n)], st

@@ -1,0 +1,73 @@
+"""Synthetic device-resident inputs for bench.py and the GPU tests (not part
+of the product path).
+
+* configs[1]: batches of 64 x 128 MiB uniform random bytes.
+* configs[3]: a Zipf-duplicated corpus (~50 % repeat content): segments of
+  64 KiB-4 MiB; each draw takes a fresh random segment with probability 1/2,
+  otherwise re-uses an earlier one chosen by Zipf(1.1) rank (rank 1 = the
+  first segment drawn).  Repeats may cross batches: the corpus is one stream
+  cut into the resident batches.  Same scheme as tools/validate_config4.py.
+
+Everything is generated on the device (torch), so a bench fills 260+ GiB of
+HBM in seconds; a host copy is taken only to run the CPU oracle.
+"""
+from __future__ import annotations
+
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+SEG_MIN = 64 * 1024
+SEG_MAX = 4 * 1024 * 1024
+
+
+def pack_layout(lens: Sequence[int], align: int = 256, slack: int = 65536) -> Tuple[np.ndarray, int]:
+    """Offsets of files packed into one arena (256-B aligned) and the bytes to
+    allocate (the engine reads up to 63 bytes past a file, K1 a halo)."""
+    offs = np.zeros(len(lens), np.uint64)
+    pos = 0
+    for i, n in enumerate(lens):
+        offs[i] = pos
+        pos += (int(n) + align - 1) // align * align
+    return offs, pos + slack
+
+
+def random_arenas(count: int, total: int, seed: int, device) -> list:
+    """`count` distinct arenas of `total` uniform random bytes."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    out = []
+    for _ in range(count):
+        t = torch.empty(total, dtype=torch.uint8, device=device)
+        t.random_(0, 256, generator=g)
+        out.append(t)
+    return out
+
+
+def zipf_fill(arenas: list, used: int, seed: int, fresh_p: float = 0.5, a: float = 1.1) -> float:
+    """Overwrite bytes [0, used) of every arena with one Zipf-duplicated
+    stream (configs[3] scheme).  Returns the repeat fraction: bytes of
+    second and later occurrences / all bytes."""
+    import torch
+    g = np.random.Generator(np.random.PCG64(seed))
+    tg = torch.Generator(device=arenas[0].device)
+    tg.manual_seed(seed)
+    segs: List[Tuple[int, int, int]] = []  # (arena, offset, size) of first occurrences
+    repeat = 0
+    for ai, arena in enumerate(arenas):
+        pos = 0
+        while pos < used:
+            if not segs or g.random() < fresh_p:
+                size = min(int(g.integers(SEG_MIN, SEG_MAX + 1)), used - pos)
+                arena[pos:pos + size].random_(0, 256, generator=tg)
+                segs.append((ai, pos, size))
+            else:
+                r = int(min(g.zipf(a), len(segs))) - 1
+                sa, so, size = segs[r]
+                size = min(size, used - pos)
+                arena[pos:pos + size].copy_(arenas[sa][so:so + size])
+                repeat += size
+            pos += size
+    torch.cuda.synchronize(arenas[0].device)
+    return repeat / (used * len(arenas))
