@@ -371,16 +371,17 @@ int finalize_batch(hbx_ctx* c, Batch* b) {
 int plan_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
   hipStream_t s = c->stream;
   const int slot = (int)(c->launches % 3), ps = (int)((c->launches + 2) % 3);
-  uint64_t bound = 64;  // entries <= chains of the unfinalized batches
-  for (Batch* b : c->pending)
-    if (!b->finalized) bound += b->caps;
-  int rc = ensure_shared(c, c->d_order[slot], bound * sizeof(OrderEntry));
-  if (!rc) rc = ensure_shared(c, c->d_octl[slot], 256);
-  if (!rc) rc = ensure_shared(c, c->d_plan, 2 * kPlanBins * sizeof(uint32_t));
+  int rc = ensure_plan_buffers(c, 0);  // nb (if any) is already in pending
   if (rc) return rc;
   // the K3 launch that read this slot three launches ago must be done
   if (c->order_used[slot] && c->hstream != s) HBX_TRY(c, hipStreamWaitEvent(s, c->order_free[slot], 0));
-  const bool has_prev = c->launches > 0;
+  // carried chains exist only while an older batch is unfinalized (a batch
+  // is finalized once every chain of it is hashed); without one the previous
+  // list is not read at all (hbx_reserve may have reallocated it)
+  bool has_prev = false;
+  for (Batch* b : c->pending)
+    if (b != nb && !b->finalized) has_prev = true;
+  has_prev = has_prev && c->launches > 0;
   const bool fresh = nb && nb->n;
   {
     StageTimer t(c, s, 2);
@@ -436,17 +437,17 @@ int md5_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
   return HBX_OK;
 }
 
-// The order-list and planner buffers one more launch needs with `extra`
-// chains joining the unfinalized batches' chains.
+// The order-list and planner buffers the next launch's plan writes, with
+// `extra` chains joining the unfinalized batches' chains.  Only the slot the
+// plan writes may grow: growing reallocates without copying, and the slot of
+// the previous launch holds the carried chains the plan reads.
 int ensure_plan_buffers(hbx_ctx* c, uint64_t extra) {
   uint64_t bound = 64 + extra;  // entries <= chains of the unfinalized batches
   for (Batch* b : c->pending)
     if (!b->finalized) bound += b->caps;
-  int rc = HBX_OK;
-  for (int t = 0; t < 3 && !rc; t++) {
-    rc = ensure_shared(c, c->d_order[t], bound * sizeof(OrderEntry));
-    if (!rc) rc = ensure_shared(c, c->d_octl[t], 256);
-  }
+  const int slot = (int)(c->launches % 3);
+  int rc = ensure_shared(c, c->d_order[slot], bound * sizeof(OrderEntry));
+  if (!rc) rc = ensure_shared(c, c->d_octl[slot], 256);
   if (!rc) rc = ensure_shared(c, c->d_plan, 2 * kPlanBins * sizeof(uint32_t));
   return rc;
 }
