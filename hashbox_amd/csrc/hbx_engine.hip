@@ -368,6 +368,8 @@ int finalize_batch(hbx_ctx* c, Batch* b) {
 // Plan launch j = c->launches on the scan stream: order[j%3] from
 // order[(j-1)%3] (advanced by the budget of launch j-1) plus the fresh chains
 // of batch nb (if any).  Needs no result of any K3 launch.
+int ensure_plan_buffers(hbx_ctx* c, uint64_t extra);
+
 int plan_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
   hipStream_t s = c->stream;
   const int slot = (int)(c->launches % 3), ps = (int)((c->launches + 2) % 3);
