@@ -258,10 +258,11 @@ def max_over_ranks(x, dist, dev, op="max"):
     return float(t.item())
 
 
-def run_workload(a, name, eng, arenas, offs, lens, R, B, need, lanes, dist, dev, world, rank,
+def run_workload(a, name, eng, arenas, offs, lens, R, B, need, lanes, dist, gpu, dev, world, rank,
                  job_batch_bytes, check_threads, before_submit=None):
-    """One steady-state measurement; returns the JSON fields of its line."""
-    r = steady(eng, arenas, offs, lens, R, a.steps, a.warmup, dist, dev, before_submit)
+    """One steady-state measurement; returns the JSON fields of its line.
+    `gpu` is this rank's device, `dev` the device of the reductions."""
+    r = steady(eng, arenas, offs, lens, R, a.steps, a.warmup, dist, gpu, before_submit)
     el = max_over_ranks(r["el"], dist, dev)
     tot_ms, tot_n = r["tot_ms"], r["tot_n"]
     k1_n, k3_n = int(tot_n[0]), int(tot_n[3])
@@ -413,7 +414,7 @@ def main():
     for wl in workloads:
         if wl == "zipf":
             zipf_repeat = W.zipf_fill(arenas, int(offs[-1]) + lens[-1], a.seed + 4 + 7919 * rank)
-        lines[wl] = run_workload(a, wl, eng, arenas, offs, lens, R, B, need, lanes, dist, red_dev,
+        lines[wl] = run_workload(a, wl, eng, arenas, offs, lens, R, B, need, lanes, dist, dev, red_dev,
                                  world, rank, job_batch, threads, before)
         if zipf_repeat is not None and wl == "zipf":
             lines[wl]["repeat_fraction"] = round(zipf_repeat, 4)
