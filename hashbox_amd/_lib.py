@@ -32,7 +32,7 @@ EXPORTS = [
     "hbx_deflate_bound", "hbx_deflate_blocks_device", "hbx_deflate_blocks",
     "hbx_deflate_file_bound", "hbx_store_paths_z",
     "hbx_wire_encode_id", "hbx_wire_encode_block_header", "hbx_wire_parse",
-    "hbx_verify_submit_device", "hbx_inflate_blocks_device", "hbx_store_paths_zcb",
+    "hbx_verify_submit_device", "hbx_inflate_blocks_device", "hbx_store_paths_zcb", "hbx_after_stream",
 ]
 # Functions returning something other than an int status.
 _NON_STATUS = ("hbx_ctx_destroy", "hbx_last_error", "hbx_max_chunks", "hbx_file_entry_size",
@@ -115,6 +115,7 @@ def load() -> ctypes.CDLL:
     L.hbx_arena_free.argtypes = [P, P]
     L.hbx_memcpy_h2d.argtypes = [P, P, P, U64]
     L.hbx_memcpy_h2d_async.argtypes = [P, P, P, U64]
+    L.hbx_after_stream.argtypes = [P, P]
     L.hbx_alloc_pinned.argtypes = [U64, ctypes.POINTER(P)]
     L.hbx_free_pinned.argtypes = [P]
     L.hbx_stage_times.argtypes = [P, ctypes.POINTER(ctypes.c_float)]

@@ -138,6 +138,7 @@ struct hbx_ctx {
   hipStream_t hstream = nullptr;  // hash stream: chain plan, K3
   hipStream_t rstream = nullptr;  // result stream: K4 + result D2H of batches whose chains are done
   hipEvent_t k3_done = nullptr;   // recorded on the hash stream after a K3 launch that completes batches
+  hipEvent_t producer = nullptr;  // hbx_after_stream: the caller's stream, waited for on the scan stream
   std::mutex mu;
   std::string err;
   // K1 tile = 256 x 64 KiB: fewer halo primes, and beside K3 fewer, longer
@@ -889,7 +890,7 @@ void hbx_ctx_destroy(hbx_ctx* c) {
   (void)hipSetDevice(c->device);
   for (hipStream_t s : {c->stream, c->cstream, c->hstream, c->rstream})
     if (s) (void)hipStreamSynchronize(s);
-  for (hipEvent_t e : {c->k3_done, c->ssum_free[0], c->ssum_free[1], c->plan_done[0], c->plan_done[1],
+  for (hipEvent_t e : {c->k3_done, c->producer, c->ssum_free[0], c->ssum_free[1], c->plan_done[0], c->plan_done[1],
                        c->plan_done[2], c->order_free[0], c->order_free[1], c->order_free[2]})
     if (e) (void)hipEventDestroy(e);
   for (DevBuf* b : {&c->d_ssum[0], &c->d_ssum[1], &c->d_order[0], &c->d_order[1], &c->d_order[2],
@@ -1497,6 +1498,16 @@ int hbx_memcpy_h2d_async(hbx_ctx* c, void* d, const void* h, uint64_t n) {
   std::lock_guard<std::mutex> g(c->mu);
   HBX_TRY(c, hipSetDevice(c->device));
   HBX_TRY(c, hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, c->stream));
+  return HBX_OK;
+}
+
+int hbx_after_stream(hbx_ctx* c, void* stream) {
+  if (!c) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  HBX_TRY(c, hipSetDevice(c->device));
+  if (!c->producer) HBX_TRY(c, hipEventCreateWithFlags(&c->producer, hipEventDisableTiming));
+  HBX_TRY(c, hipEventRecord(c->producer, static_cast<hipStream_t>(stream)));
+  HBX_TRY(c, hipStreamWaitEvent(c->stream, c->producer, 0));  // every input read starts on the scan stream
   return HBX_OK;
 }
 

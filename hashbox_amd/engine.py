@@ -74,16 +74,6 @@ def _p(a: np.ndarray) -> int:
     return a.ctypes.data if a.size else 0
 
 
-def _sync_producer():
-    """The engine's HIP streams do not wait for other streams: device data
-    written on torch's current stream (e.g. a tensor just filled) must be
-    complete before the engine reads it.  The device-pointer entry points
-    call this first."""
-    t = sys.modules.get("torch")
-    if t is not None and t.cuda.is_initialized():
-        t.cuda.current_stream().synchronize()
-
-
 class Engine:
     """One MI355X (one HIP stream) running the chunk + block-ID path."""
 
@@ -102,6 +92,19 @@ class Engine:
             self.set_md5_slice(md5_slice)
 
     # ----------------------------------------------------------- plumbing --
+    def _after_producer(self):
+        """The engine's HIP streams do not wait for other streams: device data
+        written on torch's current stream (e.g. a tensor just filled) must be
+        complete before the engine reads it.  The device-pointer entry points
+        call this first; the dependency is a GPU-side event wait
+        (hbx_after_stream), so the host never blocks and can submit batches
+        ahead of the device."""
+        t = sys.modules.get("torch")
+        if t is not None and t.cuda.is_initialized():
+            s = t.cuda.current_stream(self.device)
+            self._check(self._L.hbx_after_stream(self._ctx, ctypes.c_void_p(int(s.cuda_stream))),
+                        "hbx_after_stream")
+
     def close(self):
         if self._ctx:
             self._L.hbx_ctx_destroy(self._ctx)
@@ -168,7 +171,7 @@ class Engine:
         """Files resident in device memory (pointer ``d_arena``, e.g. a torch
         uint8 tensor's ``data_ptr()``).  Offsets 16-B aligned; each file must be
         followed by >= 64 readable bytes."""
-        _sync_producer()
+        self._after_producer()
         offs = np.ascontiguousarray(offs, np.uint64)
         lens = np.ascontiguousarray(lens, np.uint64)
         caps, base, cuts, ids, sums = self._alloc_out(lens)
@@ -181,7 +184,7 @@ class Engine:
         """Enqueue a device-resident batch and return at once.  Any number of
         batches may be in flight; :meth:`wait` completes the oldest.  The
         arena must stay untouched until then."""
-        _sync_producer()
+        self._after_producer()
         offs = np.ascontiguousarray(offs, np.uint64)
         lens = np.ascontiguousarray(lens, np.uint64)
         caps, base, cuts, ids, sums = self._alloc_out(lens)
@@ -210,7 +213,7 @@ class Engine:
         """Pipelined VerifyBlock of device-resident blocks (hbx_verify_submit_device):
         returns at once; :meth:`wait` (FIFO with chunking batches) returns
         (ids, ok, n_bad)."""
-        _sync_producer()
+        self._after_producer()
         offs = np.ascontiguousarray(offs, np.uint64)
         lens = np.ascontiguousarray(lens, np.uint64)
         n = int(lens.size)
@@ -311,7 +314,7 @@ class Engine:
                              expect: Optional[Sequence[bytes]] = None):
         """The same for blocks resident in device memory (each followed by
         >= 64 readable bytes)."""
-        _sync_producer()
+        self._after_producer()
         offs = np.ascontiguousarray(offs, np.uint64)
         lens = np.ascontiguousarray(lens, np.uint64)
         n = int(lens.size)
@@ -343,7 +346,7 @@ class Engine:
                               out_offs: Sequence[int], out_caps: Sequence[int]) -> np.ndarray:
         """Device form: block i = d_arena[offs[i] ..+lens[i]) -> zlib stream at
         d_out[out_offs[i] ..]; returns the stream lengths."""
-        _sync_producer()
+        self._after_producer()
         offs = np.ascontiguousarray(offs, np.uint64)
         lens = np.ascontiguousarray(lens, np.uint64)
         oo = np.ascontiguousarray(out_offs, np.uint64)
@@ -358,7 +361,7 @@ class Engine:
                               out_offs: Sequence[int], out_caps: Sequence[int]):
         """HashboxBlock.UncompressData (block.go:113-131) of many zlib streams on
         the device: returns (out_lens, status) (status 0 = ok)."""
-        _sync_producer()
+        self._after_producer()
         io = np.ascontiguousarray(in_offs, np.uint64)
         il = np.ascontiguousarray(in_lens, np.uint64)
         oo = np.ascontiguousarray(out_offs, np.uint64)

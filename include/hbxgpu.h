@@ -394,6 +394,13 @@ int hbx_memcpy_h2d(hbx_ctx *ctx, void *d_dst, const void *h_src, uint64_t bytes)
  * synchronous).  Use two contexts to overlap the next batch's copy with the
  * current batch's kernels. */
 int hbx_memcpy_h2d_async(hbx_ctx *ctx, void *d_dst, const void *h_src, uint64_t bytes);
+/* Order the context's next device work after everything enqueued so far on
+ * `stream` (a hipStream_t of the same device, e.g. the stream that filled an
+ * arena; NULL = the null stream).  The dependency is on the GPU (an event the
+ * context's streams wait for): the host never blocks, so a caller can keep
+ * submitting batches ahead of the device.  No reference counterpart: Go
+ * callers hand over host buffers. */
+int hbx_after_stream(hbx_ctx *ctx, void *stream);
 int hbx_alloc_pinned(uint64_t bytes, void **out);
 int hbx_free_pinned(void *p);
 
