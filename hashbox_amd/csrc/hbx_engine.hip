@@ -112,6 +112,7 @@ struct Batch {
   hbx_file_summary* sums = nullptr;
   std::vector<uint64_t> out_base, capv;
   uint32_t need = 1, done = 0;  // K3 launches its chains need / have had
+  bool joined = false;          // its chains are in the carried order lists (a plan took them)
   bool finalized = false;
   // a VerifyBlock batch (hbx_verify_submit_device) instead of files
   bool verify = false;
@@ -192,6 +193,11 @@ struct hbx_ctx {
   // until hbx_ctx_destroy.
   bool broken = false;
   std::vector<Batch*> parked;
+  // The batch whose chains are cut (K2r enqueued) but not yet in a plan: they
+  // join the K3 launch the NEXT submit issues (or a wait's drain), so K3
+  // launch j never waits for batch j's own scan and the scan stream always
+  // runs one step ahead of the hash stream.
+  Batch* unjoined = nullptr;
   std::vector<TimedLaunch> open_t;
   std::vector<hipEvent_t> ev_pool;
   double tot_ms[5] = {0, 0, 0, 0, 0};
@@ -317,6 +323,7 @@ Batch* acquire_batch(hbx_ctx* c) {
   b->n = b->caps = 0;
   b->need = 1;
   b->done = 0;
+  b->joined = false;
   b->finalized = false;
   b->cut_ends = nullptr;
   b->ids = nullptr;
@@ -383,7 +390,7 @@ int plan_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
   // list is not read at all (hbx_reserve may have reallocated it)
   bool has_prev = false;
   for (Batch* b : c->pending)
-    if (b != nb && !b->finalized) has_prev = true;
+    if (b != nb && b->joined && !b->finalized) has_prev = true;
   has_prev = has_prev && c->launches > 0;
   const bool fresh = nb && nb->n;
   {
@@ -425,7 +432,7 @@ int md5_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
   if (nb) HBX_TRY(c, hipEventRecord(nb->ev[3], s));
   bool forked = false;
   for (Batch* b : c->pending) {
-    if (b->finalized) continue;
+    if (b->finalized || !b->joined) continue;
     b->done++;
     if (budget == kBudgetAll || b->done >= b->need) {
       if (!forked && c->rstream != s) {  // the result stream picks up after this K3
@@ -438,6 +445,26 @@ int md5_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
     }
   }
   return HBX_OK;
+}
+
+// One pipeline step on the hash side: launch j = plan (the carried chains +
+// the chains of c->unjoined, the batch cut by the previous submit) then K3
+// with `budget` blocks per chain.  Issued by every submit BEFORE the new
+// batch's own scan is enqueued, and by wait_oldest with kBudgetAll to drain.
+// Nothing is launched when no chain is in flight.
+int md5_step(hbx_ctx* c, uint32_t budget) {
+  Batch* nb = c->unjoined;
+  bool live = nb != nullptr;
+  for (Batch* b : c->pending)
+    if (b->joined && !b->finalized) live = true;
+  if (!live) return HBX_OK;
+  int rc = plan_launch(c, nb, budget);
+  if (rc) return rc;
+  if (nb) {
+    nb->joined = true;
+    c->unjoined = nullptr;
+  }
+  return md5_launch(c, nb, budget);
 }
 
 // The order-list and planner buffers the next launch's plan writes, with
@@ -462,6 +489,7 @@ int ensure_plan_buffers(hbx_ctx* c, uint64_t extra) {
 // in the carried order lists) and the context refuses further pipelined work.
 int submit_abort(hbx_ctx* c, Batch* b, int rc, bool enqueued) {
   const std::string keep = c->err;
+  if (c->unjoined == b) c->unjoined = nullptr;
   for (auto it = c->pending.begin(); it != c->pending.end(); ++it)
     if (*it == b) {
       c->pending.erase(it);
@@ -553,6 +581,11 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
 int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, const uint64_t* offs,
                         const uint64_t* lens, uint32_t budget, uint64_t slices, size_t meta_bytes, int slot) {
   hipStream_t s = c->stream;
+  // launch j hashes the chains in flight plus the previous batch's; it is
+  // enqueued (plan on the scan stream) before this batch's K1, so it never
+  // waits for this batch's scan
+  int rc = md5_step(c, budget);
+  if (rc) return rc;
   if (n == 0) {
     for (int i = 0; i < 4; i++) HBX_TRY(c, hipEventRecord(b->ev[i], s));
     b->finalized = true;
@@ -568,7 +601,6 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   if (nt) std::memcpy(hm + 4 * n, c->h_tiles.data(), nt * sizeof(uint2));
   c->ssum_slot ^= 1;
   DevBuf& ssum = c->d_ssum[slot];
-  int rc = HBX_OK;
 
   HBX_TRY(c, hipMemcpyAsync(b->d_meta.p, hm, meta_bytes, hipMemcpyHostToDevice, s));
   const uint64_t* d_off = b->d_meta.as<uint64_t>();
@@ -617,11 +649,10 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
                      b->d_fcnt.as<uint32_t>());
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(b->ev[2], s2));
-  // the hash stream picks the batch up once its cuts exist; the scan stream
-  // is free for the next batch's K1/K2 while K3 runs
-  if (s2 != s) HBX_TRY(c, hipStreamWaitEvent(s, b->ev[2], 0));  // the plan reads K2r's entries
-  if ((rc = plan_launch(c, b, budget))) return rc;
-  return md5_launch(c, b, budget);
+  // the next plan (on the scan stream) reads K2r's entries
+  if (s2 != s) HBX_TRY(c, hipStreamWaitEvent(s, b->ev[2], 0));
+  c->unjoined = b;
+  return HBX_OK;
 }
 
 int submit_verify_launch(hbx_ctx* c, Batch* b, const uint8_t* arena, uint64_t n, const uint64_t* offs,
@@ -675,6 +706,8 @@ int submit_verify_launch(hbx_ctx* c, Batch* b, const uint8_t* arena, uint64_t n,
                          const uint64_t* lens, const uint8_t* links, const uint64_t* link_base,
                          const uint32_t* n_links, uint64_t nlinks_total, size_t meta_bytes, uint32_t budget) {
   hipStream_t s = c->stream;
+  int rc = md5_step(c, budget);  // launch j first, as in submit_batch_launch
+  if (rc) return rc;
   if (n == 0) {
     for (int i = 0; i < 4; i++) HBX_TRY(c, hipEventRecord(b->ev[i], s));
     b->finalized = true;
@@ -701,9 +734,8 @@ int submit_verify_launch(hbx_ctx* c, Batch* b, const uint8_t* arena, uint64_t n,
                      b->d_fresh.as<OrderEntry>(), b->d_fcnt.as<uint32_t>());
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(b->ev[2], s));
-  int rc = plan_launch(c, b, budget);
-  if (rc) return rc;
-  return md5_launch(c, b, budget);
+  c->unjoined = b;
+  return HBX_OK;
 }
 
 // Scatter a collected batch's pinned results into the caller's arrays.
@@ -765,9 +797,8 @@ int wait_oldest(hbx_ctx* c) {
     c->parked.push_back(b);
     return c->fail(HBX_ERR_STATE, "context is unusable after a failed submit; destroy it");
   }
-  if (!b->finalized) {
-    int rc = plan_launch(c, nullptr, kBudgetAll);
-    if (!rc) rc = md5_launch(c, nullptr, kBudgetAll);
+  if (!b->finalized) {  // drain: every chain in flight, the unjoined batch's included
+    int rc = md5_step(c, kBudgetAll);
     if (rc) return rc;
   }
   HBX_TRY(c, hipEventSynchronize(b->ev[4]));
@@ -1402,8 +1433,11 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
   // arena once its batch has been collected.
   const uint32_t budget = c->md5_slice ? c->md5_slice : kBudgetAll;
   const uint64_t nfull_max = (HBX_MAX_BLOCK_SIZE + 8ull) >> 6;
+  // a batch's chains join the launch of the next submit: it completes
+  // ceil(nfull/budget) submits after its own, so this many arenas keep the
+  // collect from forcing a drain
   const size_t depth = budget == kBudgetAll ? 2 : (size_t)std::min<uint64_t>(
-      64, (nfull_max + budget - 1) / budget + 1);
+      64, (nfull_max + budget - 1) / budget + 2);
   if (c->d_ring.size() < depth) c->d_ring.resize(depth);
   // size every staging buffer once, for the largest batch this call forms
   // (growing one later would re-pin host memory or drain the streams)
