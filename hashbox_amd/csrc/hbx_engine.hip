@@ -1539,6 +1539,17 @@ int hbx_after_stream(hbx_ctx* c, void* stream) {
   if (!c) return HBX_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   HBX_TRY(c, hipSetDevice(c->device));
+  if (!stream) {
+    // The null stream: a blocking scan stream (the CU-masked default) is
+    // already ordered after prior null-stream work by the legacy default-
+    // stream rule, on the GPU.  Recording an event on the null stream instead
+    // would hold the host until the scan stream drains (measured: every
+    // submit then waited for the previous batch's K1/K2, 0.3 ms hash-stream
+    // gaps per step).
+    unsigned flags = 0;
+    HBX_TRY(c, hipStreamGetFlags(c->stream, &flags));
+    if (!(flags & hipStreamNonBlocking)) return HBX_OK;
+  }
   if (!c->producer) HBX_TRY(c, hipEventCreateWithFlags(&c->producer, hipEventDisableTiming));
   HBX_TRY(c, hipEventRecord(c->producer, static_cast<hipStream_t>(stream)));
   HBX_TRY(c, hipStreamWaitEvent(c->stream, c->producer, 0));  // every input read starts on the scan stream

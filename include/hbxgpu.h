@@ -398,8 +398,10 @@ int hbx_memcpy_h2d_async(hbx_ctx *ctx, void *d_dst, const void *h_src, uint64_t 
  * `stream` (a hipStream_t of the same device, e.g. the stream that filled an
  * arena; NULL = the null stream).  The dependency is on the GPU (an event the
  * context's streams wait for): the host never blocks, so a caller can keep
- * submitting batches ahead of the device.  No reference counterpart: Go
- * callers hand over host buffers. */
+ * submitting batches ahead of the device.  For the null stream and a blocking
+ * scan stream (the default) the legacy default-stream ordering already holds
+ * and nothing is recorded.  No reference counterpart: Go callers hand over
+ * host buffers. */
 int hbx_after_stream(hbx_ctx *ctx, void *stream);
 int hbx_alloc_pinned(uint64_t bytes, void **out);
 int hbx_free_pinned(void *p);
