@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-step timeline of bench.py's timed window from a rocprofv3 kernel trace.
 
-usage: python tools/window_timeline.py <kernel_trace.csv> <steps> [--all]
+usage: python tools/window_timeline.py <kernel_trace.csv> <steps> [--all] [--seg a:b ...]
 
 The bench (one workload, e.g. --workload random) ends with one drain K3
 launch after the window, so the window holds the last `steps` K1 launches
@@ -40,6 +40,13 @@ print(f"K3 ms: mean {dur3.mean():.3f} median {np.median(dur3):.3f} min {dur3.min
 print(f"hash-stream gaps ms: sum {gap.sum():.2f} mean {gap.mean():.3f} max {gap.max():.3f}")
 d1 = np.array([ms(e - s) for s, e in w1])
 print(f"K1 ms: mean {d1.mean():.3f} first {d1[0]:.3f} max {d1.max():.3f}")
+for arg in sys.argv[3:]:
+    if arg.startswith("--seg="):
+        a, b = (int(x) for x in arg[6:].split(":"))
+        seg = ms(w3[b - 1][1] - w3[a][0]) / (b - a)
+        print(f"steps {a}..{b}: {seg:.3f} ms/step  K3 mean {dur3[a:b].mean():.3f}  K1 mean {d1[a:b].mean():.3f}  "
+              f"gaps {gap[max(a - 1, 0):b - 1].sum():.2f} ms  K1 start - K3 start mean "
+              f"{np.mean([ms(w1[i][0] - w3[i][0]) for i in range(a, b)]):.3f}")
 if "--all" in sys.argv or K <= 40:
     for i in range(K):
         wait = ms(w3[i][0] - w2[i][1])
