@@ -153,6 +153,12 @@ struct hbx_ctx {
   // 1255 GiB/s spread, 100 steps); 0 spreads them one per CU first
   uint32_t k3_dense = 1;
   uint32_t md5_slice = 16384; // K3 time slice: full MD5 blocks per chain per launch (0 = unlimited)
+  // K1 gate (hbx_k1_gate): a batch's K1 waits until every workgroup of the K3
+  // launch of the same submit has been dispatched.  k3_started counts K3
+  // workgroups on the device; k3_dispatched is the host's running total.
+  uint32_t k1_gate = 1;
+  DevBuf d_gate;
+  uint32_t k3_dispatched = 0;
   float stage_ms[5] = {0, 0, 0, 0, 0};
 
   // host-side plan scratch
@@ -423,9 +429,10 @@ int md5_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
     StageTimer t(c, s, 3);
     hipLaunchKernelGGL(hbx_k3_block_md5, dim3(c->md5_wgs), dim3(kK3Threads), 0, s,
                        c->d_order[slot].as<OrderEntry>(), static_cast<const uint32_t*>(c->d_octl[slot].as<uint32_t>()),
-                       budget, c->k3_dense);
+                       budget, c->k3_dense, c->d_gate.as<uint32_t>());
   }
   HBX_TRY(c, hipGetLastError());
+  c->k3_dispatched += c->md5_wgs;
   HBX_TRY(c, hipEventRecord(c->order_free[slot], s));
   c->order_used[slot] = true;
   c->launches++;
@@ -584,8 +591,10 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   // launch j hashes the chains in flight plus the previous batch's; it is
   // enqueued (plan on the scan stream) before this batch's K1, so it never
   // waits for this batch's scan
+  const uint64_t launches0 = c->launches;
   int rc = md5_step(c, budget);
   if (rc) return rc;
+  const bool gate = c->k1_gate && c->launches != launches0 && c->hstream != s;
   if (n == 0) {
     for (int i = 0; i < 4; i++) HBX_TRY(c, hipEventRecord(b->ev[i], s));
     b->finalized = true;
@@ -612,6 +621,11 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
 
   // the K2 that last read this summary slot (two batches back) must be done
   if (c->ssum_used[slot] && c->cstream != s) HBX_TRY(c, hipStreamWaitEvent(s, c->ssum_free[slot], 0));
+  if (gate) {  // K1 after the K3 launch above has all its workgroups on CUs (<= 10 ms)
+    hipLaunchKernelGGL(hbx_k1_gate, dim3(1), dim3(64), 0, s, static_cast<const uint32_t*>(c->d_gate.as<uint32_t>()),
+                       c->k3_dispatched, 1000000u);
+    HBX_TRY(c, hipGetLastError());
+  }
   HBX_TRY(c, hipEventRecord(b->ev[0], s));
   if (nt) {
     StageTimer t(c, s, 0);
@@ -881,6 +895,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = std::getenv("HBX_K3_DENSE")) c->k3_dense = std::atoi(v) ? 1u : 0u;
   if (const char* v = std::getenv("HBX_TILE_ITERS")) c->tile_iters = (uint32_t)std::min(1024, std::max(1, std::atoi(v)));
   if (const char* v = std::getenv("HBX_MD5_SLICE")) c->md5_slice = (uint32_t)std::max(0, std::atoi(v));
+  if (const char* v = std::getenv("HBX_K1_GATE")) c->k1_gate = std::atoi(v) ? 1u : 0u;
   if (hipSetDevice(device) != hipSuccess || make_stream(&c->stream, "HBX_SCAN_CUS", ncu, "0:4096") != hipSuccess) {
     delete c;
     return HBX_ERR_HIP;
@@ -899,7 +914,8 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
     hbx_ctx_destroy(c);
     return HBX_ERR_HIP;
   }
-  if (hipEventCreateWithFlags(&c->k3_done, hipEventDisableTiming) != hipSuccess ||
+  if (c->d_gate.ensure(256) != hipSuccess || hipMemset(c->d_gate.p, 0, 256) != hipSuccess ||
+      hipEventCreateWithFlags(&c->k3_done, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ssum_free[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ssum_free[1], hipEventDisableTiming) != hipSuccess) {
     hbx_ctx_destroy(c);
@@ -925,7 +941,7 @@ void hbx_ctx_destroy(hbx_ctx* c) {
                        c->plan_done[2], c->order_free[0], c->order_free[1], c->order_free[2]})
     if (e) (void)hipEventDestroy(e);
   for (DevBuf* b : {&c->d_ssum[0], &c->d_ssum[1], &c->d_order[0], &c->d_order[1], &c->d_order[2],
-                    &c->d_octl[0], &c->d_octl[1], &c->d_octl[2],
+                    &c->d_octl[0], &c->d_octl[1], &c->d_octl[2], &c->d_gate,
                     &c->d_stage, &c->d_msg, &c->d_plan, &c->d_vdesc, &c->d_vlinks,
                     &c->d_vout, &c->d_vexp, &c->d_zeros, &c->d_zblk, &c->d_zinfo, &c->d_zoff,
                     &c->d_zlen, &c->d_zout, &c->d_zimg, &c->d_idesc, &c->d_ires})

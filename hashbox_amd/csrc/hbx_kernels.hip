@@ -1338,10 +1338,13 @@ constexpr int kK3Threads = HBX_K3_THREADS;
 
 extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
     const OrderEntry* __restrict__ order, const uint32_t* __restrict__ n_order, uint32_t budget,
-    uint32_t dense) {
+    uint32_t dense, uint32_t* __restrict__ started) {
   // the MD5 chains are issue-bound: win the SIMD's issue arbitration against
   // co-resident waves of other kernels
   __builtin_amdgcn_s_setprio(3);
+  // dispatch counter for the next batch's K1 gate (hbx_k1_gate): one vector
+  // atomic per workgroup as it starts
+  if (started && threadIdx.x == 0) __hip_atomic_fetch_add(started, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t n_total = *n_order;
@@ -1391,6 +1394,25 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
       *reinterpret_cast<uint4*>(&chp->h[0]) = make_uint4(h[0], h[1], h[2], h[3]);
       chp->next = b0 + cnt;
     }
+  }
+}
+
+// K1 gate (scan stream, just before a batch's K1): holds the K1 back until
+// every workgroup of the K3 launch issued in the same submit has been
+// dispatched (K3's workgroups count themselves into *started), so K3's MD5
+// waves take their CUs before K1's 512 workgroups compete for them; K1 then
+// fills the CUs K3 leaves free.  One wave; lane 0 polls with vector loads.
+// The wait is bounded (limit in 100 MHz ticks of s_memrealtime): a gate
+// that times out only delays its K1.
+extern "C" __global__ __launch_bounds__(64) void hbx_k1_gate(const uint32_t* __restrict__ started,
+                                                              uint32_t target, uint32_t limit) {
+  if (threadIdx.x != 0) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    const uint32_t v = __hip_atomic_load(started, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if ((int32_t)(v - target) >= 0) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)limit) break;
+    __builtin_amdgcn_s_sleep(2);
   }
 }
 
