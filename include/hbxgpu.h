@@ -298,16 +298,23 @@ int hbx_store_paths_z(hbx_ctx *ctx, uint64_t n_files, const char *const *paths, 
                       hbx_file_summary *summaries, uint32_t io_threads, uint64_t batch_bytes,
                       uint8_t *zout, const uint64_t *zbase, uint64_t *zoff, uint64_t *zlen);
 
-/* ---- wire protocol, block-store subset ----------------------
+/* ---- wire protocol framing -----------------------------------
  * pkg/core/protocol.go: a message is u16 Num | u32 Type | its fields, big
  * endian (ProtocolMessage.Serialize, protocol.go:184-203).  Client types are
  * the lowercase constants; the server replies with Type & 0xDFDFDFDF
  * ("READ", "ACKN", "WRIT", "ERRS").  The StoreBlock exchange
  * (client.go:563-584, server.go:160-202): allo(id) -> READ(id) -> writ(block)
- * -> ACKN(id), or allo(id) -> ACKN(id) when the server has the block.  Pure
- * host code, no context. */
+ * -> ACKN(id), or allo(id) -> ACKN(id) when the server has the block.  The
+ * encoders cover that exchange; the parser frames every message type
+ * protocol.go:204-264 knows.  Pure host code, no context. */
+#define HBX_MSG_OLD_GREETING 0x686F6C61u /* "hola" */
 #define HBX_MSG_GREETING 0x68616C6Fu    /* "halo" */
+#define HBX_MSG_AUTHENTICATE 0x61757468u /* "auth" */
 #define HBX_MSG_GOODBYE 0x71756974u     /* "quit" */
+#define HBX_MSG_ACCOUNT_INFO 0x696E666Fu /* "info" */
+#define HBX_MSG_ADD_DATASET_STATE 0x61646473u /* "adds" */
+#define HBX_MSG_LIST_DATASET 0x6C697374u /* "list" */
+#define HBX_MSG_REMOVE_DATASET_STATE 0x64656C73u /* "dels" */
 #define HBX_MSG_ALLOCATE 0x616C6C6Fu    /* "allo" */
 #define HBX_MSG_READ 0x72656164u        /* "read" */
 #define HBX_MSG_WRITE 0x77726974u       /* "writ" */
@@ -324,8 +331,8 @@ typedef struct {
   uint32_t n_links;       /* writ/WRIT */
   const uint8_t *links;   /* writ/WRIT: into the input */
   uint8_t data_type;      /* writ/WRIT */
-  uint32_t data_len;      /* writ/WRIT data; ERRS text; halo: version */
-  const uint8_t *data;    /* writ/WRIT data, ERRS text: into the input */
+  uint32_t data_len;      /* writ/WRIT data; ERRS text; halo: version; others: payload bytes */
+  const uint8_t *data;    /* writ/WRIT data, ERRS text, other payloads (after the 6-byte header): into the input */
   uint64_t header_len;    /* bytes before the data */
   uint64_t total_len;     /* bytes of the whole message */
 } hbx_wire_msg;
