@@ -409,7 +409,8 @@ class Engine:
 
     def store_paths(self, paths: Sequence[Union[str, os.PathLike]], io_threads: int = 16,
                     batch_bytes: int = 1 << 30, compress: bool = False,
-                    on_batch: Optional[Callable[[int, int], None]] = None) -> List[FileChunks]:
+                    on_batch: Optional[Callable[[int, int], None]] = None,
+                    on_files: Optional[Callable[[int, List[FileChunks]], None]] = None) -> List[FileChunks]:
         """storeFile for many files on disk, end to end: the library reads them
         into pinned memory on ``io_threads`` threads and overlaps reading the
         next batch with the copy + kernels of the current one.  With
@@ -418,9 +419,11 @@ class Engine:
         ``FileChunks.zstreams``.  ``on_batch(first, count)`` (compress only)
         runs on this thread as soon as files [first, first+count) have their
         ids, summaries and zlib streams written (hbx_store_paths_zcb), so a
-        sender can ship them while later batches are still read and hashed."""
-        if on_batch is not None and not compress:
-            raise ValueError("on_batch needs compress=True (hbx_store_paths_zcb)")
+        sender can ship them while later batches are still read and hashed.
+        ``on_files(first, files)`` is the same callback handed the finished
+        FileChunks (ids, cut ends, zlib stream views) of those files."""
+        if (on_batch is not None or on_files is not None) and not compress:
+            raise ValueError("on_batch / on_files need compress=True (hbx_store_paths_zcb)")
         enc = [os.fsencode(p) for p in paths]
         lens = np.array([os.stat(p).st_size for p in enc], np.uint64)
         arr = (ctypes.c_char_p * max(len(enc), 1))(*enc)
@@ -440,7 +443,15 @@ class Engine:
         zargs = (self._ctx, len(enc), ctypes.cast(arr, ctypes.c_void_p), _p(lens), _p(cuts), _p(ids),
                  _p(base), _p(caps), sums, int(io_threads), int(batch_bytes), _p(zout), _p(zbase),
                  _p(zoff), _p(zlen))
-        if on_batch is None:
+        def view(f: int) -> FileChunks:  # file f's results, as soon as its batch is reported
+            s = sums[f]
+            k, b = int(s.n_chunks), int(base[f])
+            r = FileChunks(cuts[b:b + k].copy(), ids[b:b + k].copy(), int(s.content_type),
+                           bytes(s.content_id) if k else b"")
+            r.zstreams = [zout[int(zoff[b + i]):int(zoff[b + i] + zlen[b + i])] for i in range(k)]
+            return r
+
+        if on_batch is None and on_files is None:
             self._check(self._L.hbx_store_paths_z(*zargs), "hbx_store_paths_z")
         else:
             raised = []
@@ -449,7 +460,10 @@ class Engine:
                 if raised:
                     return
                 try:
-                    on_batch(int(first), int(count))
+                    if on_batch is not None:
+                        on_batch(int(first), int(count))
+                    if on_files is not None:
+                        on_files(int(first), [view(f) for f in range(int(first), int(first + count))])
                 except BaseException as e:  # never unwind through C
                     raised.append(e)
             cb = _lib.BATCH_READY(ready)

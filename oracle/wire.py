@@ -162,3 +162,73 @@ def error_msg(num: int, text: bytes) -> bytes:
 
 def greeting(num: int, version: int = 1) -> bytes:
     return serialize(num, GREETING, {"Version": version})
+
+
+class LoopbackSink:
+    """The server side of the block-store exchange, restated from
+    server/server.go:160-202 (test infrastructure: it stands in for the Go
+    server, which cannot be built here).  allo -> ACKN if the block is
+    stored, else READ; writ -> VerifyBlock (UncompressData + HashData,
+    pkg/core/block.go:152-174; every link must exist) -> store + ACKN, or
+    ERRS "Unable to verify blockID"; quit -> QUIT and close.  Messages are
+    read with this module's Unserialize restatement, not the product's
+    parser."""
+
+    def __init__(self, sock, preseed=()):
+        import threading
+        self.sock = sock
+        self.store = set(bytes(x) for x in preseed)
+        self.verified = 0
+        self.failed = 0
+        self.acked_allocs = 0
+        self.reads = 0
+        self.thread = threading.Thread(target=self._run, daemon=True)
+
+    def start(self):
+        self.thread.start()
+        return self
+
+    def _verify(self, block: dict) -> bool:
+        import zlib
+        from . import oracle as O
+        try:
+            data = zlib.decompress(block["Data"]) if block["DataType"] == ZLIB else block["Data"]
+        except zlib.error:
+            return False
+        if any(bytes(link) not in self.store for link in block["Links"]):
+            return False
+        return O.py_block_id(data, block["Links"]) == block["BlockID"]
+
+    def _run(self):
+        buf = b""
+        while True:
+            chunk = self.sock.recv(1 << 20)
+            if not chunk:
+                return
+            buf += chunk
+            while True:
+                try:
+                    num, mtype, data, used = unserialize(buf)
+                except EOFError:
+                    break
+                buf = buf[used:]
+                if mtype == ALLOCATE:
+                    bid = data["BlockID"]
+                    if bid in self.store:
+                        self.acked_allocs += 1
+                        self.sock.sendall(id_msg(num, ACKNOWLEDGE & SM, bid))
+                    else:
+                        self.reads += 1
+                        self.sock.sendall(id_msg(num, READ & SM, bid))
+                elif mtype == WRITE:
+                    b = data["Block"]
+                    if self._verify(b):
+                        self.verified += 1
+                        self.store.add(b["BlockID"])
+                        self.sock.sendall(id_msg(num, ACKNOWLEDGE & SM, b["BlockID"]))
+                    else:
+                        self.failed += 1
+                        self.sock.sendall(error_msg(num, b"Unable to verify blockID"))
+                elif mtype == GOODBYE:
+                    self.sock.sendall(header(num, GOODBYE & SM))
+                    return

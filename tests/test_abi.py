@@ -77,3 +77,20 @@ def test_oracle_inflate_strict_rejects_truncation():
         except (ValueError, zlib.error):
             continue
         raise AssertionError("accepted a bad stream")
+
+
+def test_plain_c_driver_links_and_reports_no_device(tmp_path):
+    """The C-ABI from plain C, as the cgo stub of INTEGRATION.md binds it: the
+    driver compiles against include/hbxgpu.h, links the in-tree library and,
+    without a GPU, every call reports a status instead of aborting."""
+    import pytest
+    from hashbox_amd import _lib
+    L = _lib.load()
+    n = ctypes.c_int(0)
+    if L.hbx_device_count(ctypes.byref(n)) == 0 and n.value > 0:
+        pytest.skip("a GPU is present: tests/test_gpu_abi.py runs the driver")
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "c"), f"OUT={tmp_path}"], check=True)
+    f = tmp_path / "in.bin"
+    f.write_bytes(b"hello")
+    r = subprocess.run([str(tmp_path / "abi_driver"), str(f), "--expect-nodev"], capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.strip() == "nodev ok", (r.returncode, r.stdout, r.stderr)

@@ -1,0 +1,58 @@
+"""GPU, more than one process: the N>1 paths run as the driver launches them
+(torch.distributed.run, one process per rank), here with gloo and every rank
+on cuda:0 of the one-GPU box.
+
+* bench.py --scaling strong (configs[2]: each step's files LPT-split across
+  the ranks) and --scaling weak, world 2, and strong at world 1: the window
+  holds exactly K K1/K3 launches per rank and every rank's checked batches
+  are bit-exact (check_vs_oracle, min over ranks).
+* hashbox_amd.multi.run_sharded driving the pipelined Engine on each rank:
+  the gathered per-file results equal the oracle's for every file."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _torchrun(nproc, args, timeout=240):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert lines, r.stdout[-2000:] + r.stderr[-2000:]
+    return json.loads(lines[-1])
+
+
+BENCH = ["bench.py", "--files", "4", "--file-mib", "16", "--steps", "6", "--warmup", "2", "--arenas", "8",
+         "--md5-slice", "32768", "--no-cpu-baseline", "--dist-backend", "gloo", "--cpu-threads", "4"]
+
+
+@pytest.mark.parametrize("nproc,scaling", [(2, "strong"), (2, "weak"), (1, "strong")])
+def test_bench_through_torchrun(nproc, scaling):
+    d = _torchrun(nproc, BENCH + ["--gpus", str(nproc), "--scaling", scaling])
+    assert d["n_gpus"] == nproc and d["scaling"] == scaling
+    assert d["check_vs_oracle"] is True and d["zipf"]["check_vs_oracle"] is True
+    assert d["window_launches"]["k1_digest_scan"] == 6 and d["window_launches"]["k3_block_md5"] == 6
+    assert d["config"]["files_per_gpu"] == (4 // nproc if scaling == "strong" else 4)
+    assert d["value"] > 0
+
+
+def test_run_sharded_engine_world2():
+    d = _torchrun(2, [os.path.join("tests", "mr_sharded_worker.py")])
+    assert d == {"ok": True, "files": 11, "world": 2}
