@@ -700,6 +700,9 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k2_cut_chain(
 }
 
 // -------------------------------------------------------------- MD5 -----
+#ifndef HBX_MD5_XAD
+#define HBX_MD5_XAD 1
+#endif
 namespace {
 
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int s) {
@@ -710,6 +713,31 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, int s) {
 #define HBX_H(b, c, d) __builtin_amdgcn_bitop3_b32((b), (c), (d), 0x96)  // b ^ c ^ d in one op
 #define HBX_I(b, c, d) ((c) ^ ((b) | ~(d)))
 #define HBX_STEP(FN, a, b, c, d, x, t, s) a = (b) + rotl((a) + (FN(b, c, d)) + (x) + (t), s)
+// A step's critical path is the chain through b (the previous step's result):
+// F(b,c,d) -> + (a+x+t) -> rotate -> + b, four dependent VALU ops.  In the H
+// rounds F = b ^ (c ^ d), and (b ^ cd) + t1 is ONE v_xad_u32 when c ^ d is
+// formed off the path (c and d are older than b): three dependent ops.  Both
+// are written as asm: the compiler would otherwise fold b ^ c ^ d back into
+// one v_bitop3 and add it with v_add3 (a, x and the constant).
+__device__ __forceinline__ uint32_t xor_offpath(uint32_t c, uint32_t d) {
+  uint32_t r;
+  asm("v_xor_b32 %0, %1, %2" : "=v"(r) : "v"(c), "v"(d));
+  return r;
+}
+__device__ __forceinline__ uint32_t xad(uint32_t b, uint32_t cd, uint32_t t1) {  // (b ^ cd) + t1
+  uint32_t r;
+  asm("v_xad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(cd), "v"(t1));
+  return r;
+}
+#if HBX_MD5_XAD
+#define HBX_STEP_H(a, b, c, d, x, t, s)                    \
+  {                                                        \
+    const uint32_t cd_ = xor_offpath(c, d);                \
+    a = (b) + rotl(xad((b), cd_, (a) + (x) + (t)), s);     \
+  }
+#else
+#define HBX_STEP_H(a, b, c, d, x, t, s) HBX_STEP(HBX_H, a, b, c, d, x, t, s)
+#endif
 
 __device__ __forceinline__ void md5_compress(uint32_t (&h)[4], const uint32_t (&m)[16]) {
   uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
@@ -745,22 +773,22 @@ __device__ __forceinline__ void md5_compress(uint32_t (&h)[4], const uint32_t (&
   HBX_STEP(HBX_G, d, a, b, c, m[2], 0xfcefa3f8u, 9);
   HBX_STEP(HBX_G, c, d, a, b, m[7], 0x676f02d9u, 14);
   HBX_STEP(HBX_G, b, c, d, a, m[12], 0x8d2a4c8au, 20);
-  HBX_STEP(HBX_H, a, b, c, d, m[5], 0xfffa3942u, 4);
-  HBX_STEP(HBX_H, d, a, b, c, m[8], 0x8771f681u, 11);
-  HBX_STEP(HBX_H, c, d, a, b, m[11], 0x6d9d6122u, 16);
-  HBX_STEP(HBX_H, b, c, d, a, m[14], 0xfde5380cu, 23);
-  HBX_STEP(HBX_H, a, b, c, d, m[1], 0xa4beea44u, 4);
-  HBX_STEP(HBX_H, d, a, b, c, m[4], 0x4bdecfa9u, 11);
-  HBX_STEP(HBX_H, c, d, a, b, m[7], 0xf6bb4b60u, 16);
-  HBX_STEP(HBX_H, b, c, d, a, m[10], 0xbebfbc70u, 23);
-  HBX_STEP(HBX_H, a, b, c, d, m[13], 0x289b7ec6u, 4);
-  HBX_STEP(HBX_H, d, a, b, c, m[0], 0xeaa127fau, 11);
-  HBX_STEP(HBX_H, c, d, a, b, m[3], 0xd4ef3085u, 16);
-  HBX_STEP(HBX_H, b, c, d, a, m[6], 0x04881d05u, 23);
-  HBX_STEP(HBX_H, a, b, c, d, m[9], 0xd9d4d039u, 4);
-  HBX_STEP(HBX_H, d, a, b, c, m[12], 0xe6db99e5u, 11);
-  HBX_STEP(HBX_H, c, d, a, b, m[15], 0x1fa27cf8u, 16);
-  HBX_STEP(HBX_H, b, c, d, a, m[2], 0xc4ac5665u, 23);
+  HBX_STEP_H(a, b, c, d, m[5], 0xfffa3942u, 4);
+  HBX_STEP_H(d, a, b, c, m[8], 0x8771f681u, 11);
+  HBX_STEP_H(c, d, a, b, m[11], 0x6d9d6122u, 16);
+  HBX_STEP_H(b, c, d, a, m[14], 0xfde5380cu, 23);
+  HBX_STEP_H(a, b, c, d, m[1], 0xa4beea44u, 4);
+  HBX_STEP_H(d, a, b, c, m[4], 0x4bdecfa9u, 11);
+  HBX_STEP_H(c, d, a, b, m[7], 0xf6bb4b60u, 16);
+  HBX_STEP_H(b, c, d, a, m[10], 0xbebfbc70u, 23);
+  HBX_STEP_H(a, b, c, d, m[13], 0x289b7ec6u, 4);
+  HBX_STEP_H(d, a, b, c, m[0], 0xeaa127fau, 11);
+  HBX_STEP_H(c, d, a, b, m[3], 0xd4ef3085u, 16);
+  HBX_STEP_H(b, c, d, a, m[6], 0x04881d05u, 23);
+  HBX_STEP_H(a, b, c, d, m[9], 0xd9d4d039u, 4);
+  HBX_STEP_H(d, a, b, c, m[12], 0xe6db99e5u, 11);
+  HBX_STEP_H(c, d, a, b, m[15], 0x1fa27cf8u, 16);
+  HBX_STEP_H(b, c, d, a, m[2], 0xc4ac5665u, 23);
   HBX_STEP(HBX_I, a, b, c, d, m[0], 0xf4292244u, 6);
   HBX_STEP(HBX_I, d, a, b, c, m[7], 0x432aff97u, 10);
   HBX_STEP(HBX_I, c, d, a, b, m[14], 0xab9423a7u, 15);
