@@ -89,6 +89,8 @@ def parse():
     ap.add_argument("--no-check", action="store_true",
                     help="skip the oracle check of the last collected and the last drained batch")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPUs; gloo for tests")
+    ap.add_argument("--single-alloc", action="store_true",
+                    help="the R arenas as views of one allocation instead of R allocations")
     return ap.parse_args()
 
 
@@ -379,7 +381,7 @@ def main():
     threads = a.cpu_threads or cores["usable"]
     if dist:  # ranks share the host's cores for the oracle check
         threads = max(1, threads // local_world)
-    arenas = W.random_arenas(R, total, a.seed + 7919 * rank, dev)
+    arenas = W.random_arenas(R, total, a.seed + 7919 * rank, dev, single=a.single_alloc)
     torch.cuda.synchronize(dev)
 
     eng = Engine(dev_idx, md5_slice=B)

@@ -32,12 +32,20 @@ def pack_layout(lens: Sequence[int], align: int = 256, slack: int = 65536) -> Tu
     return offs, pos + slack
 
 
-def random_arenas(count: int, total: int, seed: int, device) -> list:
-    """`count` distinct arenas of `total` uniform random bytes."""
+def random_arenas(count: int, total: int, seed: int, device, single: bool = False) -> list:
+    """`count` distinct arenas of `total` uniform random bytes (with `single`:
+    views of one allocation, 2 MiB-aligned)."""
     import torch
     g = torch.Generator(device=device)
     g.manual_seed(seed)
     out = []
+    if single:
+        step = (total + (2 << 20) - 1) // (2 << 20) * (2 << 20)
+        big = torch.empty(step * count, dtype=torch.uint8, device=device)
+        out = [big[i * step:i * step + total] for i in range(count)]
+        for t in out:
+            t.random_(0, 256, generator=g)
+        return out
     for _ in range(count):
         t = torch.empty(total, dtype=torch.uint8, device=device)
         t.random_(0, 256, generator=g)
