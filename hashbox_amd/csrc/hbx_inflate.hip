@@ -10,12 +10,13 @@
 // blocks, any window distance.
 //
 // A stream is serial, so a lane decodes one stream (64 per wave; the host
-// sorts streams longest first).  Huffman decoding is canonical: per code
-// length l, `cnt[l]` codes follow the first code of that length, and the
-// symbols of each table are listed in code order (RFC 1951 §3.2.2), as in
-// zlib's contrib/puff; the tables live in LDS per lane.  Every read and write
-// is bounds-checked: a corrupt stream sets its status and stops, it never
-// touches memory outside its input and output.
+// sorts streams longest first).  Huffman decoding is canonical (RFC 1951
+// §3.2.2): the codes of length l are the consecutive values [first[l],
+// limit[l]), so a decoder peeks 15 bits, bit-reverses them (codes are sent
+// most significant bit first) and takes the shortest l whose l-bit prefix is
+// below limit[l]; the symbol is sym[prefix + base[l]].  The tables live in LDS
+// per lane.  Every read and write is bounds-checked: a corrupt stream sets its
+// status and stops, it never touches memory outside its input and output.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -31,8 +32,17 @@ constexpr uint32_t kLenSyms = 288, kDistSyms = 32;
 constexpr uint32_t kOk = 0, kErrHeader = 1, kErrInput = 2, kErrOutput = 3, kErrCode = 4, kErrDist = 5,
                    kErrStored = 6;
 
+// One canonical code: limit[l] = first code of length l + number of codes
+// of length l (l-bit code space); base[l] = index in sym of the first symbol
+// of length l minus the first code of length l.
+struct Code {
+  uint16_t limit[16];
+  int16_t base[16];
+};
+
 struct LaneTables {
-  uint16_t lcnt[16], dcnt[16], offs[16];
+  Code lc, dc;
+  uint16_t next[16];  // placement cursors while a table is built
   uint16_t lsym[kLenSyms];
   uint16_t dsym[kDistSyms];
   uint8_t lens[320];  // code lengths while a dynamic table is built
@@ -75,43 +85,46 @@ struct Bits {
   }
 };
 
-// Canonical decode: codes are read MSB-first, one bit at a time (puff's
-// `decode`).  Returns the symbol, or -1 for an invalid code.
-__device__ __forceinline__ int decode(Bits& br, const uint16_t* cnt, const uint16_t* sym) {
-  int code = 0, first = 0, index = 0;
-  if (br.n < 16u) br.fill();
-  for (int len = 1; len <= 15; len++) {
-    code |= (int)(br.buf & 1u);
-    br.buf >>= 1;
-    br.n--;
-    const int count = cnt[len];
-    if (code - count < first) return sym[index + (code - first)];
-    index += count;
-    first += count;
-    first <<= 1;
-    code <<= 1;
+// Next symbol of `c`, or -1 if the next 15 bits start no code of it.
+__device__ __forceinline__ int decode(Bits& br, const Code& c, const uint16_t* sym) {
+  if (br.n < 15u) br.fill();
+  const uint32_t peek = __builtin_bitreverse32((uint32_t)br.buf) >> 17;  // first-sent bit on top
+  for (uint32_t l = 1; l <= 15u; l++) {
+    const uint32_t prefix = peek >> (15u - l);
+    if (prefix < c.limit[l]) {
+      br.buf >>= l;
+      br.n -= l;
+      return sym[(int)prefix + c.base[l]];
+    }
   }
   return -1;
 }
 
-// Tables from code lengths (puff's `construct`); returns false for an
-// over-subscribed set.  Incomplete sets are allowed (the decoder then meets an
-// invalid code only on corrupt input).
-__device__ __forceinline__ bool construct(uint16_t* cnt, uint16_t* sym, uint16_t* offs, const uint8_t* lens,
-                                          int n) {
-  for (int l = 0; l < 16; l++) cnt[l] = 0;
-  for (int s = 0; s < n; s++) cnt[lens[s]]++;
-  if (cnt[0] == n) return true;
-  int left = 1;
+// The code of `n` symbols with code lengths `lens` (RFC 1951 §3.2.2 steps
+// 1-3: count per length, first code per length, symbols in code order).
+// Returns false when the lengths over-subscribe the code space; incomplete
+// codes are accepted (a decoder meets a missing code only on corrupt input),
+// and all-zero lengths give a code that decodes nothing.
+__device__ __forceinline__ bool construct(Code& c, uint16_t* sym, uint16_t* next, const uint8_t* lens, int n) {
+  uint16_t count[16];
+  for (int l = 0; l < 16; l++) count[l] = 0;
+  for (int s = 0; s < n; s++) count[lens[s]]++;
+  count[0] = 0;
+  int room = 1;  // unused codes of the current length (Kraft)
+  uint32_t first = 0, start = 0;
+  c.limit[0] = 0;
+  c.base[0] = 0;
   for (int l = 1; l < 16; l++) {
-    left <<= 1;
-    left -= cnt[l];
-    if (left < 0) return false;
+    room = 2 * room - count[l];
+    if (room < 0) return false;
+    first = (first + count[l - 1]) << 1;
+    c.limit[l] = (uint16_t)(first + count[l]);
+    c.base[l] = (int16_t)((int)start - (int)first);
+    next[l] = (uint16_t)start;
+    start += count[l];
   }
-  offs[1] = 0;
-  for (int l = 1; l < 15; l++) offs[l + 1] = (uint16_t)(offs[l] + cnt[l]);
   for (int s = 0; s < n; s++)
-    if (lens[s]) sym[offs[lens[s]]++] = (uint16_t)s;
+    if (lens[s]) sym[next[lens[s]]++] = (uint16_t)s;
   return true;
 }
 
@@ -227,9 +240,9 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k8_inflate(const InflateDes
       for (int s = 144; s < 256; s++) T.lens[s] = 9;
       for (int s = 256; s < 280; s++) T.lens[s] = 7;
       for (int s = 280; s < 288; s++) T.lens[s] = 8;
-      construct(T.lcnt, T.lsym, T.offs, T.lens, 288);
+      construct(T.lc, T.lsym, T.next, T.lens, 288);
       for (int s = 0; s < 30; s++) T.lens[s] = 5;
-      construct(T.dcnt, T.dsym, T.offs, T.lens, 30);
+      construct(T.dc, T.dsym, T.next, T.lens, 30);
     } else {  // dynamic (RFC 1951 §3.2.7)
       const uint32_t nlen = br.get(5) + 257u, ndist = br.get(5) + 1u, ncode = br.get(4) + 4u;
       if (nlen > 286u || ndist > 30u) {
@@ -238,14 +251,14 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k8_inflate(const InflateDes
       }
       for (int s = 0; s < 19; s++) T.lens[s] = 0;
       for (uint32_t s = 0; s < ncode; s++) T.lens[kOrder[s]] = (uint8_t)br.get(3);
-      if (!construct(T.lcnt, T.lsym, T.offs, T.lens, 19)) {
+      if (!construct(T.lc, T.lsym, T.next, T.lens, 19)) {
         st = kErrCode;
         break;
       }
       uint32_t idx = 0;
       bool bad = false;
       while (idx < nlen + ndist) {
-        int sym = decode(br, T.lcnt, T.lsym);
+        int sym = decode(br, T.lc, T.lsym);
         if (sym < 0) {
           bad = true;
           break;
@@ -280,18 +293,18 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k8_inflate(const InflateDes
       // distance lengths first (they sit after the literal/length ones in lens)
       for (uint32_t s = 0; s < 30u; s++) T.dlens[s] = s < ndist ? T.lens[nlen + s] : 0u;
       for (uint32_t s = nlen; s < 288u; s++) T.lens[s] = 0u;
-      if (!construct(T.lcnt, T.lsym, T.offs, T.lens, 288)) {
+      if (!construct(T.lc, T.lsym, T.next, T.lens, 288)) {
         st = kErrCode;
         break;
       }
-      if (!construct(T.dcnt, T.dsym, T.offs, T.dlens, 30)) {
+      if (!construct(T.dc, T.dsym, T.next, T.dlens, 30)) {
         st = kErrCode;
         break;
       }
     }
     // the block's symbols
     for (;;) {
-      const int sym = decode(br, T.lcnt, T.lsym);
+      const int sym = decode(br, T.lc, T.lsym);
       if (sym < 0) {
         st = kErrCode;
         break;
@@ -311,7 +324,7 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k8_inflate(const InflateDes
           break;
         }
         const uint32_t len = len_base(ls) + br.get(len_extra(ls));
-        const int ds = decode(br, T.dcnt, T.dsym);
+        const int ds = decode(br, T.dc, T.dsym);
         if (ds < 0 || ds >= 30) {
           st = kErrCode;
           break;
