@@ -1189,118 +1189,6 @@ __device__ void md5_coop(uint8_t* wl, const uint8_t* c, uint32_t (&h)[4], uint32
 #endif
 }
 
-// Cooperative streaming, LDS-DMA form (default, HBX_K3_DMA): the same stage
-// loads (instruction q fetches 256 contiguous bytes of each of chains
-// 4q..4q+3) land straight in LDS by global_load_lds_dwordx4, with no register
-// staging and no ds_write pass, which frees the 128 staging VGPRs for a
-// one-block read-ahead of each lane's message words (the LDS read latency is
-// then hidden behind the previous block's 64 steps).  The DMA writes lane i's
-// 16 bytes at base + 16 i, so a chain's 256-B row is contiguous; granule g of
-// chain c sits in slot (g + c) & 15 of its row (the SOURCE address carries
-// the rotation), which makes every per-lane ds_read_b128 conflict-free.  Two
-// 16 KiB halves per wave: stage s+1 lands while stage s is hashed; the wait
-// for it is one s_waitcnt per stage, hand-counted (the compiler does not see
-// asm loads).
-constexpr uint32_t kDmaStage = 64u * 256u;        // one stage: 4 blocks of 64 chains
-constexpr uint32_t kDmaWaveLds = 2u * kDmaStage;  // two stages per wave
-
-// 16 LDS-DMA of 1 KiB each: lane i's 16 bytes from a[q] to dst + 1024 q + 16 i.
-// One statement, M0 stepped in place (hipcc does not preserve M0 around asm).
-#define HBX_GLDS(k) "s_nop 0\n\tglobal_load_lds_dwordx4 %" #k ", off\n\ts_add_u32 m0, m0, 0x400\n\t"
-__device__ __forceinline__ void glds16x16(const uint64_t (&a)[16], uint32_t dst) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %17\n\t"
-      HBX_GLDS(1) HBX_GLDS(2) HBX_GLDS(3) HBX_GLDS(4) HBX_GLDS(5) HBX_GLDS(6) HBX_GLDS(7) HBX_GLDS(8)
-      HBX_GLDS(9) HBX_GLDS(10) HBX_GLDS(11) HBX_GLDS(12) HBX_GLDS(13) HBX_GLDS(14) HBX_GLDS(15) HBX_GLDS(16)
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(a[8]),
-        "v"(a[9]), "v"(a[10]), "v"(a[11]), "v"(a[12]), "v"(a[13]), "v"(a[14]), "v"(a[15]), "s"(dst)
-      : "memory", "scc");
-}
-#undef HBX_GLDS
-
-#ifndef HBX_COOP_NOINLINE
-#define HBX_COOP_NOINLINE 1
-#endif
-#if HBX_COOP_NOINLINE
-__device__ __noinline__
-#else
-__device__
-#endif
-void md5_coop_dma(uint8_t* wl, const uint8_t* c, uint32_t (&h)[4], uint32_t b1, uint32_t R) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t S = reinterpret_cast<uint64_t>(c) + 64ull * b1 - 8ull;  // message block b1
-  const uint32_t ngr = 4u * R;                                           // granules of R blocks
-  const uint32_t nst = (ngr + 15u) / 16u;
-  const uint32_t sub = lane >> 4, p = lane & 15u;
-  const uint32_t lds0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)wl);
-  // DMA instruction q: this lane fills slot p of chain 4q+sub's row with
-  // granule (p - chain) & 15 of that chain's stage
-  uint64_t Q[16];
-  uint32_t G[16];
-#pragma unroll
-  for (int q = 0; q < 16; q++) {
-    const uint32_t ch = 4u * (uint32_t)q + sub;
-    G[q] = (p - ch) & 15u;
-    Q[q] = shfl64(S, ch) + 16ull * G[q];
-  }
-  // this lane's row: granule g at slot (g + lane) & 15
-  uint32_t rdo[16];
-#pragma unroll
-  for (int g = 0; g < 16; g++) rdo[g] = lds0 + 256u * lane + 16u * (((uint32_t)g + lane) & 15u);
-  auto issue = [&](uint32_t st, uint32_t half) {  // 16 DMA, stage st into half
-    uint64_t a[16];
-    if (16u * (st + 1u) <= ngr) {
-#pragma unroll
-      for (int q = 0; q < 16; q++) a[q] = Q[q] + 256ull * st;
-    } else {  // the last stage: granules past the last needed one re-read it (always in the chunk)
-#pragma unroll
-      for (int q = 0; q < 16; q++) a[q] = Q[q] - 16ull * G[q] + 16ull * min(16u * st + G[q], ngr - 1u);
-    }
-    glds16x16(a, lds0 + half * kDmaStage);
-  };
-  typedef __attribute__((address_space(3))) const u32x4 l_u32x4;
-  auto read = [&](uint32_t half, uint32_t u, u32x4 (&W)[4]) {  // ds_read_b128, half as an immediate
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-      W[i] = *reinterpret_cast<l_u32x4*>((uintptr_t)(rdo[4u * u + (uint32_t)i] + half * kDmaStage));
-  };
-  issue(0u, 0u);
-  if (nst > 1u) issue(1u, 1u);
-  if (nst > 1u)
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // stage 0 landed, stage 1 in flight
-  else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  u32x4 W[4], Wn[4];
-  read(0u, 0u, W);
-  for (uint32_t s = 0; s < nst; s++) {
-    const uint32_t half = s & 1u;
-#pragma unroll
-    for (uint32_t u = 0; u < 4u; u++) {
-      const uint32_t blk = 4u * s + u;
-      if (blk >= R) break;  // wave-uniform
-      if (u < 3u && blk + 1u < R) read(half, u + 1u, Wn);  // read-ahead inside the stage
-      const uint32_t m[16] = {W[0].x, W[0].y, W[0].z, W[0].w, W[1].x, W[1].y, W[1].z, W[1].w,
-                              W[2].x, W[2].y, W[2].z, W[2].w, W[3].x, W[3].y, W[3].z, W[3].w};
-      md5_compress(h, m);
-      if (u < 3u) {
-#pragma unroll
-        for (int i = 0; i < 4; i++) W[i] = Wn[i];
-      }
-    }
-    if (s + 1u < nst) {  // stage s+1 (the only DMA in flight) has landed; its half is read next
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      read(half ^ 1u, 0u, W);
-      // every read of this stage's half has returned (each was waited for at
-      // its use): stage s+2 may land in it
-      if (s + 2u < nst) issue(s + 2u, half);
-    }
-  }
-}
-
 }  // namespace
 
 // ------------------------------------------------------ MD5 chain table --
@@ -1473,10 +1361,6 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
 #ifndef HBX_K3_COOP
 #define HBX_K3_COOP 1
 #endif
-// ... landed in LDS by LDS-DMA (md5_coop_dma) instead of through registers
-#ifndef HBX_K3_DMA
-#define HBX_K3_DMA 1
-#endif
 constexpr uint32_t kCoopMinBudget = 8u;
 constexpr int kK3Threads = HBX_K3_THREADS;
 
@@ -1494,11 +1378,7 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
   const uint32_t n_total = *n_order;
 #if HBX_K3_COOP
   static_assert(kK3Threads == 256, "cooperative K3 path sized for 4 waves per workgroup");
-#if HBX_K3_DMA
-  __shared__ __attribute__((aligned(1024))) uint8_t k3_lds[kK3Threads / 64][kDmaWaveLds];
-#else
   __shared__ __attribute__((aligned(16))) uint8_t k3_lds[kK3Threads / 64][kCoopWaveLds];
-#endif
 #endif
   const uint32_t groups = (n_total + 63u) / 64u;
   const uint32_t nwaves = gridDim.x * (kK3Threads / 64);
@@ -1527,11 +1407,7 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
     const uint32_t R = ~wave_max_all(active ? ~cnt : 0u);
     if (R >= kCoopMinBudget) {  // wave-uniform
       md5_block_at(src, ch.len, h, ch.next);  // every lane now at a block >= 1
-#if HBX_K3_DMA
-      md5_coop_dma(k3_lds[wave], src, h, ch.next + 1u, R - 1u);
-#else
       md5_coop(k3_lds[wave], src, h, ch.next + 1u, R - 1u);
-#endif
       md5_run(src, len, h, b0 + R, active ? cnt - R : 0u, finish);
     } else {
       md5_run(src, len, h, b0, cnt, finish);
