@@ -89,6 +89,8 @@ def parse():
     ap.add_argument("--no-check", action="store_true",
                     help="skip the oracle check of the last collected and the last drained batch")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPUs; gloo for tests")
+    ap.add_argument("--ballast-gib", type=float, default=0.0,
+                    help="diagnostics: hold this much extra device memory (written once, never read)")
     ap.add_argument("--single-alloc", action="store_true",
                     help="the R arenas as views of one allocation instead of R allocations")
     return ap.parse_args()
@@ -382,6 +384,7 @@ def main():
     if dist:  # ranks share the host's cores for the oracle check
         threads = max(1, threads // local_world)
     arenas = W.random_arenas(R, total, a.seed + 7919 * rank, dev, single=a.single_alloc)
+    ballast = torch.zeros(int(a.ballast_gib * GIB), dtype=torch.uint8, device=dev) if a.ballast_gib else None
     torch.cuda.synchronize(dev)
 
     eng = Engine(dev_idx, md5_slice=B)
