@@ -93,6 +93,8 @@ struct PinBuf {
 
 // Per-kernel cumulative timing: one event pair per launch, harvested once the
 // end event has completed (hbx_stage_totals).
+constexpr uint32_t kK1CtrWord = 32;  // d_gate: word 0 = K3 dispatch counter, word 32 = K1 tile queue
+
 struct TimedLaunch {
   hipEvent_t a, b;
   int stage;
@@ -159,6 +161,7 @@ struct hbx_ctx {
   uint32_t k1_gate = 1;
   DevBuf d_gate;
   uint32_t k3_dispatched = 0;
+  uint32_t k1_ctr = 0;  // K1 tile queue: fetches issued by all earlier K1 launches (d_gate word kK1CtrWord)
   float stage_ms[5] = {0, 0, 0, 0, 0};
 
   // host-side plan scratch
@@ -633,9 +636,13 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
       hipLaunchKernelGGL(hbx_k1_digest_scan_lite, dim3((uint32_t)nt), dim3(kK1LThreads), 0, s,
                          arena, d_off, d_len, d_sb, d_tiles,
                          c->tile_iters * (HBX_MIN_BLOCK_SIZE / kK1LSpan), ssum.as<uint2>(), slices);
-    else if (c->k1_mode == 1)
-      hipLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3((uint32_t)nt), dim3(kK1Threads), 0, s,
-                         arena, d_off, d_len, d_sb, d_tiles, c->tile_iters, ssum.as<uint2>(), slices);
+    else if (c->k1_mode == 1) {
+      const uint32_t grid = (uint32_t)std::min<uint64_t>(nt, c->md5_wgs);  // at most one workgroup per CU
+      hipLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3(grid), dim3(kK1Threads), 0, s,
+                         arena, d_off, d_len, d_sb, d_tiles, c->tile_iters, ssum.as<uint2>(), slices,
+                         c->d_gate.as<uint32_t>() + kK1CtrWord, c->k1_ctr, (uint32_t)nt);
+      c->k1_ctr += (uint32_t)nt + grid;  // every tile once, plus one failed fetch per workgroup
+    }
     else
       hipLaunchKernelGGL(hbx_k1_digest_scan, dim3((uint32_t)nt), dim3(kK1Threads), 0, s, arena,
                          d_off, d_len, d_sb, d_tiles, c->tile_iters, ssum.as<uint2>(), slices);
