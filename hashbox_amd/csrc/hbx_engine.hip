@@ -148,7 +148,6 @@ struct hbx_ctx {
   // K1 workgroups (2,139-2,146 vs 2,088-2,108 GiB/s for 64, 3 A/B pairs,
   // tools/gpu_ab_tile.sh; 8-32 are slower)
   uint32_t tile_iters = 256;
-  uint32_t k1_mode = 1;       // K1: 0 register prefetch, 1 LDS-DMA landing, 2 K1-lite (co-resides with K3)
   uint32_t md5_wgs = 256;     // K3 grid: one 256-thread workgroup per CU (set from the device)
   // K3 wave placement: 1 packs the busy waves into the fewest CUs (4 per CU,
   // one per SIMD), leaving whole CUs to the next batch's K1 (measured 1510 vs
@@ -166,7 +165,7 @@ struct hbx_ctx {
 
   // host-side plan scratch
   std::vector<uint64_t> h_slice_base;
-  std::vector<uint2> h_tiles;
+  std::vector<uint4> h_tiles, h_tail_tiles;
 
   // K1 -> K2 slice summaries, two slots used by alternate batches: K1 of
   // batch i+1 (scan stream) overlaps K2 of batch i (cut stream)
@@ -520,6 +519,22 @@ int submit_abort(hbx_ctx* c, Batch* b, int rc, bool enqueued) {
 int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, const uint64_t* offs,
                         const uint64_t* lens, uint32_t budget, uint64_t slices, size_t meta_bytes, int slot);
 
+// K1 tiles of one file of `iters` 64 KiB iterations: long tiles of
+// c->tile_iters over the first seven eighths (h_tiles), then 1 MiB tiles over
+// the rest (h_tail_tiles, queued after every long tile of the batch).
+constexpr uint32_t kTailTileIters = 16;
+void k1_tiles(hbx_ctx* c, uint32_t f, uint32_t iters) {
+  uint32_t tail = 0;
+  if (iters > c->tile_iters) {
+    tail = std::min(iters, std::max(kTailTileIters, (iters / 8 + kTailTileIters - 1) / kTailTileIters * kTailTileIters));
+  }
+  const uint32_t head = iters - tail;
+  for (uint32_t i = 0; i < head; i += c->tile_iters)
+    c->h_tiles.push_back(make_uint4(f, i, std::min(c->tile_iters, head - i), 0u));
+  for (uint32_t i = head; i < iters; i += kTailTileIters)
+    c->h_tail_tiles.push_back(make_uint4(f, i, std::min(kTailTileIters, iters - i), 0u));
+}
+
 // Plan + enqueue one device batch (K1, K2, first MD5 launch).  Results are
 // collected by wait_oldest in submission order.  Every validation and
 // allocation happens before the batch joins the FIFO; a failure after that
@@ -542,8 +557,8 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
   b->cut_base.resize(n);
   c->h_slice_base.resize(n);
   c->h_tiles.clear();
+  c->h_tail_tiles.clear();
   uint64_t slices = 0, tcaps = 0, longest = 0;
-  const uint64_t tile_bytes = (uint64_t)c->tile_iters * HBX_MIN_BLOCK_SIZE;
   for (uint64_t f = 0; f < n; f++) {
     const uint64_t N = lens[f];
     longest = std::max(longest, N);
@@ -552,14 +567,15 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
     tcaps += max_chunks(N);
     if (N > 2ull * HBX_MIN_BLOCK_SIZE) {  // only files with split candidates scan
       slices += (N + kSlice - 1) / kSlice;
-      const uint64_t nt = (N + tile_bytes - 1) / tile_bytes;
-      if (nt > 0xFFFFFFFFull) {
+      const uint64_t iters = (N + HBX_MIN_BLOCK_SIZE - 1) / HBX_MIN_BLOCK_SIZE;
+      if (iters > 0xFFFFFFFFull) {
         c->pool.push_back(b);
         return c->fail(HBX_ERR_ARG, "file too large");
       }
-      for (uint64_t t = 0; t < nt; t++) c->h_tiles.push_back(make_uint2((uint32_t)f, (uint32_t)t));
+      k1_tiles(c, (uint32_t)f, (uint32_t)iters);
     }
   }
+  c->h_tiles.insert(c->h_tiles.end(), c->h_tail_tiles.begin(), c->h_tail_tiles.end());
   b->caps = tcaps;
   // launches this batch's chains need: a chunk is <= min(longest file, MAX)
   // bytes, i.e. <= nfull full message blocks, and each launch advances it by
@@ -569,7 +585,7 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
   b->need = budget == kBudgetAll ? 1u : (uint32_t)std::max<uint64_t>(1, (nfull + budget - 1) / budget);
   const uint64_t nt = c->h_tiles.size();
   // meta block: off | len | slice_base | cut_base | tiles
-  const size_t meta_bytes = n * 8 * 4 + nt * sizeof(uint2);
+  const size_t meta_bytes = n * 8 * 4 + nt * sizeof(uint4);
   const int slot = c->ssum_slot;
   if (n) {  // every allocation first: the batch is not in the FIFO yet
     int rc = HBX_OK;
@@ -610,7 +626,7 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   std::memcpy(hm + n, lens, n * 8);
   std::memcpy(hm + 2 * n, c->h_slice_base.data(), n * 8);
   std::memcpy(hm + 3 * n, b->cut_base.data(), n * 8);
-  if (nt) std::memcpy(hm + 4 * n, c->h_tiles.data(), nt * sizeof(uint2));
+  if (nt) std::memcpy(hm + 4 * n, c->h_tiles.data(), nt * sizeof(uint4));
   c->ssum_slot ^= 1;
   DevBuf& ssum = c->d_ssum[slot];
 
@@ -619,7 +635,7 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   const uint64_t* d_len = d_off + n;
   const uint64_t* d_sb = d_off + 2 * n;
   const uint64_t* d_cb = d_off + 3 * n;
-  const uint2* d_tiles = reinterpret_cast<const uint2*>(d_off + 4 * n);
+  const uint4* d_tiles = reinterpret_cast<const uint4*>(d_off + 4 * n);
   const uint8_t* arena = static_cast<const uint8_t*>(d_arena);
 
   // the K2 that last read this summary slot (two batches back) must be done
@@ -632,20 +648,11 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   HBX_TRY(c, hipEventRecord(b->ev[0], s));
   if (nt) {
     StageTimer t(c, s, 0);
-    if (c->k1_mode == 2)
-      hipLaunchKernelGGL(hbx_k1_digest_scan_lite, dim3((uint32_t)nt), dim3(kK1LThreads), 0, s,
-                         arena, d_off, d_len, d_sb, d_tiles,
-                         c->tile_iters * (HBX_MIN_BLOCK_SIZE / kK1LSpan), ssum.as<uint2>(), slices);
-    else if (c->k1_mode == 1) {
-      const uint32_t grid = (uint32_t)std::min<uint64_t>(nt, c->md5_wgs);  // at most one workgroup per CU
-      hipLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3(grid), dim3(kK1Threads), 0, s,
-                         arena, d_off, d_len, d_sb, d_tiles, c->tile_iters, ssum.as<uint2>(), slices,
-                         c->d_gate.as<uint32_t>() + kK1CtrWord, c->k1_ctr, (uint32_t)nt);
-      c->k1_ctr += (uint32_t)nt + grid;  // every tile once, plus one failed fetch per workgroup
-    }
-    else
-      hipLaunchKernelGGL(hbx_k1_digest_scan, dim3((uint32_t)nt), dim3(kK1Threads), 0, s, arena,
-                         d_off, d_len, d_sb, d_tiles, c->tile_iters, ssum.as<uint2>(), slices);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(nt, c->md5_wgs);  // at most one workgroup per CU
+    hipLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3(grid), dim3(kK1Threads), 0, s, arena, d_off, d_len, d_sb,
+                       d_tiles, ssum.as<uint2>(), slices, c->d_gate.as<uint32_t>() + kK1CtrWord, c->k1_ctr,
+                       (uint32_t)nt);
+    c->k1_ctr += (uint32_t)nt + grid;  // every tile once, plus one failed fetch per workgroup
   }
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(b->ev[1], s));
@@ -896,8 +903,6 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   int ncu = 0;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->md5_wgs = (uint32_t)(ncu = prop.multiProcessorCount);
-  if (const char* v = std::getenv("HBX_K1_DMA")) c->k1_mode = std::atoi(v) ? 1u : 0u;
-  if (const char* v = std::getenv("HBX_K1_MODE")) c->k1_mode = (uint32_t)std::min(2, std::max(0, std::atoi(v)));
   if (const char* v = std::getenv("HBX_MD5_WGS")) c->md5_wgs = (uint32_t)std::max(1, std::atoi(v));
   if (const char* v = std::getenv("HBX_K3_DENSE")) c->k3_dense = std::atoi(v) ? 1u : 0u;
   if (const char* v = std::getenv("HBX_TILE_ITERS")) c->tile_iters = (uint32_t)std::min(1024, std::max(1, std::atoi(v)));
@@ -1007,11 +1012,12 @@ int hbx_reserve(hbx_ctx* c, uint32_t batches, uint64_t files, uint64_t bytes) {
   std::lock_guard<std::mutex> g(c->mu);
   if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
   HBX_TRY(c, hipSetDevice(c->device));
-  const uint64_t tile_bytes = (uint64_t)c->tile_iters * HBX_MIN_BLOCK_SIZE;
   const uint64_t caps = bytes / HBX_MIN_BLOCK_SIZE + files;  // >= sum of max_chunks over the files
-  const uint64_t tiles = bytes / tile_bytes + files;
+  // long tiles + 1 MiB tail tiles over at most an eighth (+1) of each file
+  const uint64_t tiles = bytes / ((uint64_t)c->tile_iters * HBX_MIN_BLOCK_SIZE) +
+                         bytes / (8ull * kTailTileIters * HBX_MIN_BLOCK_SIZE) + 3 * files;
   const uint64_t slices = bytes / kSlice + files;
-  const size_t meta_bytes = files * 8 * 4 + tiles * sizeof(uint2);
+  const size_t meta_bytes = files * 8 * 4 + tiles * sizeof(uint4);
   int rc = HBX_OK;
   for (int t = 0; t < 2 && !rc; t++) rc = ensure_shared(c, c->d_ssum[t], (slices + 1) * sizeof(uint2));
   if (!rc) rc = ensure_shared(c, c->d_plan, 2 * kPlanBins * sizeof(uint32_t));

@@ -247,58 +247,6 @@ __device__ __forceinline__ void k1_store_slice(uint2* __restrict__ ssum, uint64_
   if (l < 2u) reinterpret_cast<uint32_t*>(ssum + idx)[l] = l ? sprev : smax;
 }
 
-// tiles[t] = {file index, tile index within file}; a tile is tile_iters
-// consecutive 64 KiB iterations of one file.  ssum[slice_base[f] + j] =
-// {max digest of slice j, digest before slice j}; ssum[dummy] absorbs the
-// writes of slices past a file's end.
-extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan(
-    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
-    const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ slice_base,
-    const uint2* __restrict__ tiles, uint32_t tile_iters, uint2* __restrict__ ssum,
-    uint64_t dummy) {
-  __shared__ uint2 wtot[2][16];
-  const uint2 td = tiles[blockIdx.x];
-  const uint32_t f = td.x;
-  const uint64_t N = file_len[f];
-  const uint64_t q0 = (uint64_t)td.y * tile_iters * kMinBlock;
-  const uint8_t* fb = arena + file_off[f];
-  const uint64_t sb = slice_base[f];
-
-  const uint32_t tid = threadIdx.x;
-  const uint32_t l = tid & 63u;
-  const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
-  const uint32_t e_l = w * kSlice + l * 64u;  // iteration-relative first position of this lane
-
-  const uint64_t rem = N - q0;
-  const uint32_t n_it = (uint32_t)umin64(tile_iters, (rem + kMinBlock - 1) / kMinBlock);
-  // rounded up to 16 B: every dwordx4 is entirely in or out of range (the
-  // arena guarantees HBX_ARENA_SLACK readable bytes after each file)
-  const uint32_t nbytes = (uint32_t)((umin64(rem, (uint64_t)n_it * kMinBlock) + 15ull) & ~15ull);
-  const __amdgpu_buffer_rsrc_t rs = make_rsrc_u(fb + q0, nbytes);
-
-  uint32_t out[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) out[k] = 0u;
-  if (q0 != 0) load_run64(make_rsrc_u(fb + q0 - kMinBlock, kMinBlock), e_l, 0u, out);
-  K1State st = k1_prime(out, q0 == 0, wtot, w, l, e_l);
-
-  uint32_t cur[16], nxt[16];
-  load_run64(rs, e_l, 0u, cur);
-  for (uint32_t it = 0; it < n_it; it++) {
-    if (it + 1 < n_it) load_run64(rs, e_l, (it + 1) * kMinBlock, nxt);
-    const uint64_t qs = q0 + (uint64_t)it * kMinBlock;  // iteration start position
-    uint32_t smax, sprev;
-    k1_iteration(cur, out, st, wtot, it, w, l, e_l, qs, N, smax, sprev);
-    const bool ok = qs + (uint64_t)w * kSlice < N;
-    k1_store_slice(ssum, ok ? sb + ((qs >> kSliceShift) + w) : dummy, l, smax, sprev);
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-      out[k] = cur[k];
-      cur[k] = nxt[k];
-    }
-  }
-}
-
 // ---------------------------------------------------------- K1 (LDS-DMA) --
 // Same scan; the runs land in LDS by buffer_load ... lds (no VGPR staging),
 // two iterations in flight per CU (128 KiB), instead of one in registers.
@@ -345,17 +293,21 @@ constexpr uint32_t kDmaSlot = 4096;  // bytes per wave per iteration
 
 // Tiles come from a work queue (tile_ctr, a running counter: this launch's
 // tiles are ctr_base .. ctr_base + n_tiles - 1), and the grid is at most one
-// workgroup per CU.  A fixed grid of one workgroup per tile finished in
-// whole rounds over the CUs K3 leaves free: 512 tiles on 128 free CUs take 4
-// rounds, on 127 CUs 5 (the "residency cliff": K1 3.2 -> 4.0 ms as soon as
-// K3's chains needed a 129th CU).  From the queue every workgroup keeps
-// taking tiles until none is left, so K1 ends within one tile of its work /
-// free CUs, and every workgroup exits after one failed fetch.
+// workgroup per CU.  Equal tiles finish in whole rounds over the CUs K3
+// leaves free: 512 tiles of 16 MiB on 128 free CUs take 4 rounds, on 127 CUs
+// 5 (the "residency cliff": K1 3.2 -> 3.9 ms as soon as K3's chains needed a
+// 129th CU).  The host queues each file's long tiles first and its last
+// eighth as 1 MiB tiles after every long tile, so the workgroups that finish
+// their long tiles early take the short ones and the launch ends within one
+// short tile of work / free CUs.  Every workgroup exits after one failed fetch.
+// tiles[t] = {file, first 64 KiB iteration, iterations, 0}; ssum[slice_base[f]
+// + j] = {max digest of slice j, digest before slice j}; ssum[dummy] absorbs
+// the writes of slices past a file's end.
 extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_dma(
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
     const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ slice_base,
-    const uint2* __restrict__ tiles, uint32_t tile_iters, uint2* __restrict__ ssum,
-    uint64_t dummy, uint32_t* __restrict__ tile_ctr, uint32_t ctr_base, uint32_t n_tiles) {
+    const uint4* __restrict__ tiles, uint2* __restrict__ ssum, uint64_t dummy,
+    uint32_t* __restrict__ tile_ctr, uint32_t ctr_base, uint32_t n_tiles) {
   __shared__ uint2 wtot[2][16];
   __shared__ __attribute__((aligned(1024))) uint8_t land[kK1Threads / 64][2][kDmaSlot];
   __shared__ uint32_t next_tile;
@@ -364,10 +316,11 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_d
   __syncthreads();
   const uint32_t tile = next_tile;
   if (tile >= n_tiles) break;  // the same for every thread of the workgroup
-  const uint2 td = tiles[tile];
+  const uint4 td = tiles[tile];
   const uint32_t f = td.x;
   const uint64_t N = file_len[f];
-  const uint64_t q0 = (uint64_t)td.y * tile_iters * kMinBlock;
+  const uint64_t q0 = (uint64_t)td.y * kMinBlock;
+  const uint32_t tile_iters = td.z;
   const uint8_t* fb = arena + file_off[f];
   const uint64_t sb = slice_base[f];
 
@@ -441,135 +394,6 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_d
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the tile (or the workgroup) ends
   __syncthreads();  // every thread has read next_tile and used the landing slots
-  }
-}
-
-// ------------------------------------------------------------ K1 (lite) --
-// The same scan sized to co-reside with K3: 256 threads (one
-// wave per SIMD), no LDS staging, ~150 VGPRs, so a CU running K3's MD5 waves
-// (136 KiB LDS, 324 registers on one SIMD) still fits K1-lite workgroups on
-// its spare SIMDs and the next batch's scan overlaps the hashing.
-// An iteration spans 16 KiB (one 4 KiB slice per wave); the bytes MIN
-// earlier are the same thread's run 4 iterations back, kept in a 4-deep
-// register ring with their aggregates (the loop is unrolled by 4 so the ring
-// index is static).  The state update across a 16 KiB span keeps the
-// 16384*S1 term that vanishes mod 2^16 for a 64 KiB span.
-constexpr int kK1LThreads = 256;
-constexpr uint32_t kK1LSpan = 16384u;
-
-// <= 168 VGPRs (3 waves per SIMD): fits beside a K3 wave's 324 registers
-extern "C" __global__ __launch_bounds__(kK1LThreads) __attribute__((amdgpu_waves_per_eu(3)))
-void hbx_k1_digest_scan_lite(
-    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
-    const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ slice_base,
-    const uint2* __restrict__ tiles, uint32_t tile_iters, uint2* __restrict__ ssum,
-    uint64_t dummy) {
-  __shared__ uint2 wtot[2][4];
-  const uint2 td = tiles[blockIdx.x];
-  const uint32_t f = td.x;
-  const uint64_t N = file_len[f];
-  const uint64_t q0 = (uint64_t)td.y * tile_iters * kK1LSpan;
-  const uint8_t* fb = arena + file_off[f];
-  const uint64_t sb = slice_base[f];
-
-  const uint32_t tid = threadIdx.x;
-  const uint32_t l = tid & 63u;
-  const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
-  const uint32_t e_l = w * kSlice + l * 64u;  // iteration-relative first position of this lane
-
-  const uint64_t rem = N - q0;
-  const uint32_t n_it = (uint32_t)umin64(tile_iters, (rem + kK1LSpan - 1) / kK1LSpan);
-  const uint32_t nbytes = (uint32_t)((umin64(rem, (uint64_t)n_it * kK1LSpan) + 15ull) & ~15ull);
-  const __amdgpu_buffer_rsrc_t rs = make_rsrc_u(fb + q0, nbytes);
-
-  // ring[j]: this thread's run of the iteration j (mod 4) back; at the tile
-  // start the 64 KiB halo before q0 (virtual zeros at the file start)
-  uint32_t ring[4][16];
-  uint32_t S1c = 0u, s2c = 0x8000u;
-  if (q0 != 0) {
-    const __amdgpu_buffer_rsrc_t rh = make_rsrc_u(fb + q0 - kMinBlock, kMinBlock);
-    uint32_t hA = 0u, hC = 0u;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      load_run64(rh, (uint32_t)j * kK1LSpan + e_l, 0u, ring[j]);
-      const RunAgg g = run_aggregates(ring[j]);
-      hA += g.af;
-      hC += ((uint32_t)j * kK1LSpan + e_l) * g.af + g.jf;
-    }
-    const uint32_t iA = wave_incl_sum(hA), iC = wave_incl_sum(hC);
-    if (l == 63u) wtot[1][w] = make_uint2(iA, iC);
-    __syncthreads();
-    uint32_t tA = 0u, tC = 0u;
-#pragma unroll
-    for (int v = 0; v < 4; v++) {
-      tA += wtot[1][v].x;
-      tC += wtot[1][v].y;
-    }
-    S1c = tA;
-    s2c = 0x8000u - tC;  // virtual-zero start: s2 = 2^15 - sum k*x_k over the window
-  } else {
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-#pragma unroll
-      for (int k = 0; k < 16; k++) ring[j][k] = 0u;
-    }
-  }
-
-  uint32_t cur[16];
-  load_run64(rs, e_l, 0u, cur);
-  auto iteration = [&](auto jc, uint32_t it) {
-    constexpr int J = decltype(jc)::value;  // ring slot = it % 4
-    uint32_t nxt[16];
-    if (it + 1 < n_it) load_run64(rs, e_l, (it + 1) * kK1LSpan, nxt);
-    const uint64_t qs = q0 + (uint64_t)it * kK1LSpan;
-    const RunAgg ca = run_aggregates(cur);
-    const RunAgg pa = run_aggregates(ring[J]);  // recomputed: cheaper than 16 registers
-    const uint32_t A_hA = ca.ah - pa.ah, J_hA = ca.jh - pa.jh;
-    const uint32_t A_l = ca.af - pa.af, J_l = ca.jf - pa.jf;
-    const uint32_t C_l = e_l * A_l + J_l;
-    const uint32_t iA = wave_incl_sum(A_l);
-    const uint32_t iC = wave_incl_sum(C_l);
-    if (l == 63u) wtot[it & 1u][w] = make_uint2(iA, iC);
-    __syncthreads();
-    uint32_t WA = 0u, WC = 0u, totA = 0u, totC = 0u;
-#pragma unroll
-    for (int v = 0; v < 4; v++) {
-      const uint2 t = wtot[it & 1u][v];
-      WA += (uint32_t)v < w ? t.x : 0u;
-      WC += (uint32_t)v < w ? t.y : 0u;
-      totA += t.x;
-      totC += t.y;
-    }
-    const uint32_t A_pre = WA + (iA - A_l), C_pre = WC + (iC - C_l);
-    const uint32_t S1_t = S1c + A_pre;
-    const uint32_t s2_t = s2c + e_l * S1_t - C_pre;
-    const uint32_t A_pre2 = A_pre + A_hA, C_pre2 = C_pre + e_l * A_hA + J_hA;
-    const uint32_t S1_b = S1c + A_pre2;
-    const uint32_t s2_b = s2c + (e_l + 32u) * S1_b - C_pre2;
-    const uint32_t sprev = readlane((s2_t << 16) | (S1_t & 0xffffu), 0);
-    const uint32_t XA = (s2_t << 16) | (S1_t & 0xffffu), XB = (s2_b << 16) | (S1_b & 0xffffu);
-    uint32_t M;
-    if (qs + kK1LSpan <= N)
-      M = digest_pass_sdwa<false>(cur, ring[J], XA, XB, e_l, 0u);
-    else
-      M = digest_pass_sdwa<true>(cur, ring[J], XA, XB, e_l, (uint32_t)(N - qs));
-    const uint32_t smax = readlane(wave_max_to_lane63(M), 63);
-    const bool ok = qs + (uint64_t)w * kSlice < N;
-    k1_store_slice(ssum, ok ? sb + ((qs >> kSliceShift) + w) : dummy, l, smax, sprev);
-    // state after the 16 KiB span: S1 += totA; s2 += span*S1' - totC
-    S1c += totA;
-    s2c = s2c + kK1LSpan * S1c - totC;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-      ring[J][k] = cur[k];
-      cur[k] = nxt[k];
-    }
-  };
-  for (uint32_t it = 0; it < n_it; it += 4u) {
-    iteration(std::integral_constant<int, 0>{}, it);
-    if (it + 1u < n_it) iteration(std::integral_constant<int, 1>{}, it + 1u);
-    if (it + 2u < n_it) iteration(std::integral_constant<int, 2>{}, it + 2u);
-    if (it + 3u < n_it) iteration(std::integral_constant<int, 3>{}, it + 3u);
   }
 }
 
