@@ -93,8 +93,6 @@ struct PinBuf {
 
 // Per-kernel cumulative timing: one event pair per launch, harvested once the
 // end event has completed (hbx_stage_totals).
-constexpr uint32_t kK1CtrWord = 32;  // d_gate: word 0 = K3 dispatch counter, word 32 = K1 tile queue
-
 struct TimedLaunch {
   hipEvent_t a, b;
   int stage;
@@ -160,7 +158,6 @@ struct hbx_ctx {
   uint32_t k1_gate = 1;
   DevBuf d_gate;
   uint32_t k3_dispatched = 0;
-  uint32_t k1_ctr = 0;  // K1 tile queue: fetches issued by all earlier K1 launches (d_gate word kK1CtrWord)
   float stage_ms[5] = {0, 0, 0, 0, 0};
 
   // host-side plan scratch
@@ -648,11 +645,8 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   HBX_TRY(c, hipEventRecord(b->ev[0], s));
   if (nt) {
     StageTimer t(c, s, 0);
-    const uint32_t grid = (uint32_t)std::min<uint64_t>(nt, c->md5_wgs);  // at most one workgroup per CU
-    hipLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3(grid), dim3(kK1Threads), 0, s, arena, d_off, d_len, d_sb,
-                       d_tiles, ssum.as<uint2>(), slices, c->d_gate.as<uint32_t>() + kK1CtrWord, c->k1_ctr,
-                       (uint32_t)nt);
-    c->k1_ctr += (uint32_t)nt + grid;  // every tile once, plus one failed fetch per workgroup
+    hipLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3((uint32_t)nt), dim3(kK1Threads), 0, s, arena, d_off, d_len,
+                       d_sb, d_tiles, ssum.as<uint2>(), slices);
   }
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(b->ev[1], s));

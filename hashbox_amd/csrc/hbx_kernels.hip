@@ -291,32 +291,24 @@ __device__ __forceinline__ void dma16(s32x4 srd, uint32_t voff, uint32_t soff, u
 
 constexpr uint32_t kDmaSlot = 4096;  // bytes per wave per iteration
 
-// Tiles come from a work queue (tile_ctr, a running counter: this launch's
-// tiles are ctr_base .. ctr_base + n_tiles - 1), and the grid is at most one
-// workgroup per CU.  Equal tiles finish in whole rounds over the CUs K3
-// leaves free: 512 tiles of 16 MiB on 128 free CUs take 4 rounds, on 127 CUs
-// 5 (the "residency cliff": K1 3.2 -> 3.9 ms as soon as K3's chains needed a
-// 129th CU).  The host queues each file's long tiles first and its last
-// eighth as 1 MiB tiles after every long tile, so the workgroups that finish
-// their long tiles early take the short ones and the launch ends within one
-// short tile of work / free CUs.  Every workgroup exits after one failed fetch.
+// One workgroup per tile.  Equal tiles finish in whole rounds over the CUs
+// K3 leaves free: 512 tiles of 16 MiB on 128 free CUs take 4 rounds, on 127
+// CUs 5 (the "residency cliff": K1 3.2 -> 3.9 ms as soon as K3's chains
+// needed a 129th CU).  The host lists each file's long tiles first and its
+// last eighth as 1 MiB tiles after every long tile of the batch; workgroups
+// are dispatched in that order, so the CUs that finish their long tiles
+// early take the short ones and the launch ends within about one short tile
+// of work / free CUs.
 // tiles[t] = {file, first 64 KiB iteration, iterations, 0}; ssum[slice_base[f]
 // + j] = {max digest of slice j, digest before slice j}; ssum[dummy] absorbs
 // the writes of slices past a file's end.
 extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_dma(
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
     const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ slice_base,
-    const uint4* __restrict__ tiles, uint2* __restrict__ ssum, uint64_t dummy,
-    uint32_t* __restrict__ tile_ctr, uint32_t ctr_base, uint32_t n_tiles) {
+    const uint4* __restrict__ tiles, uint2* __restrict__ ssum, uint64_t dummy) {
   __shared__ uint2 wtot[2][16];
   __shared__ __attribute__((aligned(1024))) uint8_t land[kK1Threads / 64][2][kDmaSlot];
-  __shared__ uint32_t next_tile;
-  for (;;) {
-  if (threadIdx.x == 0) next_tile = atomicAdd(tile_ctr, 1u) - ctr_base;
-  __syncthreads();
-  const uint32_t tile = next_tile;
-  if (tile >= n_tiles) break;  // the same for every thread of the workgroup
-  const uint4 td = tiles[tile];
+  const uint4 td = tiles[blockIdx.x];
   const uint32_t f = td.x;
   const uint64_t N = file_len[f];
   const uint64_t q0 = (uint64_t)td.y * kMinBlock;
@@ -392,9 +384,7 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_d
     step(it, run_b, out);
     if (it + 1u < n_it) step(it + 1u, out, run_b);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the tile (or the workgroup) ends
-  __syncthreads();  // every thread has read next_tile and used the landing slots
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup exits
 }
 
 // ------------------------------------------------------------------ K2 --
