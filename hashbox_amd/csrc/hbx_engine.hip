@@ -162,7 +162,7 @@ struct hbx_ctx {
 
   // host-side plan scratch
   std::vector<uint64_t> h_slice_base;
-  std::vector<uint4> h_tiles, h_tail_tiles;
+  std::vector<uint4> h_tiles;
 
   // K1 -> K2 slice summaries, two slots used by alternate batches: K1 of
   // batch i+1 (scan stream) overlaps K2 of batch i (cut stream)
@@ -516,20 +516,14 @@ int submit_abort(hbx_ctx* c, Batch* b, int rc, bool enqueued) {
 int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, const uint64_t* offs,
                         const uint64_t* lens, uint32_t budget, uint64_t slices, size_t meta_bytes, int slot);
 
-// K1 tiles of one file of `iters` 64 KiB iterations: long tiles of
-// c->tile_iters over the first seven eighths (h_tiles), then 1 MiB tiles over
-// the rest (h_tail_tiles, queued after every long tile of the batch).
-constexpr uint32_t kTailTileIters = 16;
+// K1 tiles of one file of `iters` 64 KiB iterations: c->tile_iters each.
+// (Queuing each file's last eighth as 1 MiB tiles after the long ones, to
+// round off K1's last pass over the CUs K3 leaves free, measured slower: K1
+// 3.18 -> 3.33 ms beside K3 at 33 resident batches, from the extra halos and
+// workgroups.)
 void k1_tiles(hbx_ctx* c, uint32_t f, uint32_t iters) {
-  uint32_t tail = 0;
-  if (iters > c->tile_iters) {
-    tail = std::min(iters, std::max(kTailTileIters, (iters / 8 + kTailTileIters - 1) / kTailTileIters * kTailTileIters));
-  }
-  const uint32_t head = iters - tail;
-  for (uint32_t i = 0; i < head; i += c->tile_iters)
-    c->h_tiles.push_back(make_uint4(f, i, std::min(c->tile_iters, head - i), 0u));
-  for (uint32_t i = head; i < iters; i += kTailTileIters)
-    c->h_tail_tiles.push_back(make_uint4(f, i, std::min(kTailTileIters, iters - i), 0u));
+  for (uint32_t i = 0; i < iters; i += c->tile_iters)
+    c->h_tiles.push_back(make_uint4(f, i, std::min(c->tile_iters, iters - i), 0u));
 }
 
 // Plan + enqueue one device batch (K1, K2, first MD5 launch).  Results are
@@ -554,7 +548,6 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
   b->cut_base.resize(n);
   c->h_slice_base.resize(n);
   c->h_tiles.clear();
-  c->h_tail_tiles.clear();
   uint64_t slices = 0, tcaps = 0, longest = 0;
   for (uint64_t f = 0; f < n; f++) {
     const uint64_t N = lens[f];
@@ -572,7 +565,6 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
       k1_tiles(c, (uint32_t)f, (uint32_t)iters);
     }
   }
-  c->h_tiles.insert(c->h_tiles.end(), c->h_tail_tiles.begin(), c->h_tail_tiles.end());
   b->caps = tcaps;
   // launches this batch's chains need: a chunk is <= min(longest file, MAX)
   // bytes, i.e. <= nfull full message blocks, and each launch advances it by
@@ -1007,9 +999,7 @@ int hbx_reserve(hbx_ctx* c, uint32_t batches, uint64_t files, uint64_t bytes) {
   if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
   HBX_TRY(c, hipSetDevice(c->device));
   const uint64_t caps = bytes / HBX_MIN_BLOCK_SIZE + files;  // >= sum of max_chunks over the files
-  // long tiles + 1 MiB tail tiles over at most an eighth (+1) of each file
-  const uint64_t tiles = bytes / ((uint64_t)c->tile_iters * HBX_MIN_BLOCK_SIZE) +
-                         bytes / (8ull * kTailTileIters * HBX_MIN_BLOCK_SIZE) + 3 * files;
+  const uint64_t tiles = bytes / ((uint64_t)c->tile_iters * HBX_MIN_BLOCK_SIZE) + files;
   const uint64_t slices = bytes / kSlice + files;
   const size_t meta_bytes = files * 8 * 4 + tiles * sizeof(uint4);
   int rc = HBX_OK;

@@ -291,14 +291,10 @@ __device__ __forceinline__ void dma16(s32x4 srd, uint32_t voff, uint32_t soff, u
 
 constexpr uint32_t kDmaSlot = 4096;  // bytes per wave per iteration
 
-// One workgroup per tile.  Equal tiles finish in whole rounds over the CUs
-// K3 leaves free: 512 tiles of 16 MiB on 128 free CUs take 4 rounds, on 127
-// CUs 5 (the "residency cliff": K1 3.2 -> 3.9 ms as soon as K3's chains
-// needed a 129th CU).  The host lists each file's long tiles first and its
-// last eighth as 1 MiB tiles after every long tile of the batch; workgroups
-// are dispatched in that order, so the CUs that finish their long tiles
-// early take the short ones and the launch ends within about one short tile
-// of work / free CUs.
+// One workgroup per tile.  Equal tiles finish in whole rounds over the CUs K3
+// leaves free: 512 tiles of 16 MiB on 128 free CUs take 4 rounds, on 127 CUs
+// 5 — the measured "residency cliff" (K1 3.2 -> 3.9 ms beside K3 as soon as
+// 34+ resident batches put K3's chains on a 129th CU).
 // tiles[t] = {file, first 64 KiB iteration, iterations, 0}; ssum[slice_base[f]
 // + j] = {max digest of slice j, digest before slice j}; ssum[dummy] absorbs
 // the writes of slices past a file's end.
