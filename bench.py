@@ -80,9 +80,12 @@ def parse():
     ap.add_argument("--hbm-frac", type=float, default=0.95,
                     help="fraction of free HBM given to resident batches; throughput ~ resident bytes "
                          "/ batch lifetime (the longest chunk's serial MD5)")
-    ap.add_argument("--lead", type=int, default=2,
-                    help="launches between a batch's completion and its collection (the scan stream's "
-                         "slack): R = launches per batch + lead")
+    ap.add_argument("--join-lag", type=int, default=0,
+                    help="submits between a batch's own and the K3 launch its chains join "
+                         "(hbx_set_join_lag; 0 = auto: 2 below 64 files per GPU, else 1)")
+    ap.add_argument("--lead", type=int, default=-1,
+                    help="launches between a batch's completion and its collection (the scan side's "
+                         "slack): R = launches per batch + lead (-1 = join lag + 1)")
     ap.add_argument("--e2e", action="store_true",
                     help="host-inclusive mode: each step's batch is copied from pinned host memory "
                          "(H2D on the engine's scan stream, overlapped with the pipeline)")
@@ -360,6 +363,8 @@ def main():
     if not lens:
         raise SystemExit(f"rank {rank} has no files: --files {a.files} < world {world}")
     nf = len(lens)
+    lag = a.join_lag if a.join_lag > 0 else (2 if nf < 64 else 1)
+    lead = a.lead if a.lead >= 0 else lag + 1
     offs, total = W.pack_layout(lens)
     job_batch = (sum(job_lens) if a.scaling == "strong" else sum(job_lens) * world)
     # launches a batch needs before its chains are all hashed
@@ -367,18 +372,19 @@ def main():
     # ranks sharing one device (tests) share its HBM
     share = max(1, -(-local_world // max(ndev, 1)))
     free, _ = torch.cuda.mem_get_info(dev)
-    r_fit = max(a.lead + 1, int(free * a.hbm_frac / share) // (total + (64 << 20)))
+    r_fit = max(lead + 1, int(free * a.hbm_frac / share) // (total + (64 << 20)))
     if a.e2e:
-        r_fit = min(r_fit, a.lead + 2)  # PCIe-bound: a shallow pipeline suffices
+        r_fit = min(r_fit, lead + 2)  # PCIe-bound: a shallow pipeline suffices
     if a.md5_slice < 0:
         R = a.arenas if a.arenas > 0 else r_fit
-        B = -(-nfull // max(1, R - a.lead))
+        B = -(-nfull // max(1, R - lead))
     else:
         B = a.md5_slice
-        R = a.arenas if a.arenas > 0 else min((1 if B == 0 else -(-nfull // B)) + a.lead, r_fit)
+        R = a.arenas if a.arenas > 0 else min((1 if B == 0 else -(-nfull // B)) + lead, r_fit)
     need = 1 if B == 0 else -(-nfull // B)
-    if need + 1 > R:
-        raise SystemExit(f"pipeline depth {R} < launches per batch {need} + 1: raise --arenas or the slice")
+    if need + lag > R:
+        raise SystemExit(f"pipeline depth {R} < launches per batch {need} + join lag {lag}: raise --arenas "
+                         "or the slice")
     cores = cpu_info()
     threads = a.cpu_threads or cores["usable"]
     if dist:  # ranks share the host's cores for the oracle check
@@ -387,7 +393,7 @@ def main():
     ballast = torch.zeros(int(a.ballast_gib * GIB), dtype=torch.uint8, device=dev) if a.ballast_gib else None
     torch.cuda.synchronize(dev)
 
-    eng = Engine(dev_idx, md5_slice=B)
+    eng = Engine(dev_idx, md5_slice=B, join_lag=lag)
     # every batch slot, chain table and summary buffer of the pipeline is
     # allocated now: an allocation inside the timed region would drain the streams
     eng.reserve(R + 1, nf, sum(lens))
@@ -460,7 +466,7 @@ def main():
                                + (", sharded by file across GPUs: configs[2])" if world > 1 else ")"),
                    "files_per_step": a.files, "files_per_gpu": nf, "file_bytes": fbytes,
                    "md5_slice_blocks": B, "pipeline_depth": R, "launches_per_batch": need,
-                   "scan_lead": a.lead, "parallelism": f"file-sharded x{world} ({a.scaling} scaling; "
+                   "scan_lead": lead, "join_lag": lag, "parallelism": f"file-sharded x{world} ({a.scaling} scaling; "
                                                        "independent HIP streams, no data-path collective)"},
     }
     out.update({k: v for k, v in head.items() if k not in ("value", "ms_per_step")})

@@ -142,10 +142,21 @@ struct hbx_ctx {
   hipEvent_t producer = nullptr;  // hbx_after_stream: the caller's stream, waited for on the scan stream
   std::mutex mu;
   std::string err;
-  // K1 tile = 256 x 64 KiB: fewer halo primes, and beside K3 fewer, longer
-  // K1 workgroups (2,139-2,146 vs 2,088-2,108 GiB/s for 64, 3 A/B pairs,
-  // tools/gpu_ab_tile.sh; 8-32 are slower)
-  uint32_t tile_iters = 256;
+  // K1 tile length in 64 KiB iterations; 0 = per batch (k1_tile_iters):
+  // about two tiles per CU, 16..256.  At 8 GiB batches that is 256 (fewer
+  // halo primes and, beside K3, fewer, longer K1 workgroups: 2,139-2,146 vs
+  // 2,088-2,108 GiB/s for 64); a 1 GiB batch gets 32 so that its K1 still
+  // spreads over every CU K3 leaves
+  uint32_t tile_iters = 0;
+  uint32_t join_lag = 1;      // hbx_set_join_lag
+  // where and when K2c plans run (plan_mode_of): 0 on the scan stream, by
+  // the submit that launches; 1 the same on the hash stream; 2 on the scan
+  // stream one launch ahead (preplan).  -1 = 2 at join lag >= 2, else 0
+  // (HBX_PLAN_MODE for A/B).
+  int plan_mode = -1;
+  bool preplanned = false;    // the plan of launch `launches` is enqueued (mode 2)
+  Batch* pre_nb = nullptr;    // the batch whose chains that plan adds
+  int k2_own = -1;            // ensure_cut_stream: -1 = by join lag (HBX_K2_STREAM for A/B)
   uint32_t md5_wgs = 256;     // K3 grid: one 256-thread workgroup per CU (set from the device)
   // K3 wave placement: 1 packs the busy waves into the fewest CUs (4 per CU,
   // one per SIMD), leaving whole CUs to the next batch's K1 (measured 1510 vs
@@ -198,11 +209,11 @@ struct hbx_ctx {
   // until hbx_ctx_destroy.
   bool broken = false;
   std::vector<Batch*> parked;
-  // The batch whose chains are cut (K2r enqueued) but not yet in a plan: they
-  // join the K3 launch the NEXT submit issues (or a wait's drain), so K3
-  // launch j never waits for batch j's own scan and the scan stream always
-  // runs one step ahead of the hash stream.
-  Batch* unjoined = nullptr;
+  // Batches whose chains are cut (K2r enqueued) but not yet in a plan, oldest
+  // first: a batch joins the K3 launch issued `join_lag` submits after its
+  // own (or a wait's drain), so K3 launch j never waits for batch j's own
+  // scan and the scan side runs join_lag steps ahead of the hash stream.
+  std::deque<Batch*> unjoined;
   std::vector<TimedLaunch> open_t;
   std::vector<hipEvent_t> ev_pool;
   double tot_ms[5] = {0, 0, 0, 0, 0};
@@ -383,8 +394,42 @@ int finalize_batch(hbx_ctx* c, Batch* b) {
 // of batch nb (if any).  Needs no result of any K3 launch.
 int ensure_plan_buffers(hbx_ctx* c, uint64_t extra);
 
+// Where and when plans run (the plan of launch j+1 adds batch j+1-lag).
+// * lag 1, mode 0: submit j+1 enqueues it on the scan stream, after batch j's
+//   K1 (and K2), whose chains it adds.
+// * lag 2, mode 1: the batch was cut a step earlier, so the plan can go on the
+//   hash stream between K3 j and K3 j+1, off the scan stream (which then
+//   carries only the K1 gate and K1).  Costs ~0.06 ms of dispatch gaps per
+//   step on the hash stream.
+// * lag >= 3, mode 2 (preplan): submit j enqueues it on the scan stream right
+//   after launching K3 j and BEFORE batch j's K1; the batch it adds (j-2 or
+//   older) was cut during the previous step, so the plan never waits for a K2
+//   and the hash stream carries nothing but K3 launches.  At lag 2 the same
+//   schedule would make K1 j wait for K2 of batch j-1 (measured 1,575 GiB/s at
+//   8 files per GPU, vs 1,890 for mode 1).
+int plan_mode_of(const hbx_ctx* c) {
+  if (c->plan_mode >= 0) return c->plan_mode;
+  return c->join_lag >= 3 ? 2 : c->join_lag == 2 ? 1 : 0;
+}
+hipStream_t plan_stream(const hbx_ctx* c) { return plan_mode_of(c) == 1 ? c->hstream : c->stream; }
+
+// K2 + K2r get a stream of their own once the join lag allows it (or
+// HBX_K2_STREAM=1): K1 of the next batch then no longer queues behind this
+// batch's K2 (at 8 files per GPU, 1,578 -> 1,825 GiB/s).  At lag 1 the plan
+// needs K2r right away, and a fourth stream of ours shares one of the
+// GPU_MAX_HW_QUEUES = 4 hardware queues (measured +0.2 ms hash-stream gap),
+// so K2 stays on the scan stream.  Created once; never dropped.
+int ensure_cut_stream(hbx_ctx* c) {
+  const bool want = c->k2_own < 0 ? c->join_lag >= 2 : c->k2_own > 0;
+  if (!want || c->cstream != c->stream || c->hstream == c->stream) return HBX_OK;
+  hipStream_t s = nullptr;
+  HBX_TRY(c, hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  c->cstream = s;
+  return HBX_OK;
+}
+
 int plan_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
-  hipStream_t s = c->stream;
+  hipStream_t s = plan_stream(c);
   const int slot = (int)(c->launches % 3), ps = (int)((c->launches + 2) % 3);
   int rc = ensure_plan_buffers(c, 0);  // nb (if any) is already in pending
   if (rc) return rc;
@@ -398,6 +443,8 @@ int plan_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
     if (b != nb && b->joined && !b->finalized) has_prev = true;
   has_prev = has_prev && c->launches > 0;
   const bool fresh = nb && nb->n;
+  // the joining batch's chains come from K2r (cut stream) or K6p (scan stream)
+  if (fresh && !(s == c->stream && c->cstream == s)) HBX_TRY(c, hipStreamWaitEvent(s, nb->ev[2], 0));
   {
     StageTimer t(c, s, 2);
     HBX_TRY(c, hipMemsetAsync(c->d_plan.p, 0, 2 * kPlanBins * sizeof(uint32_t), s));
@@ -412,7 +459,6 @@ int plan_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
   }
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(c->plan_done[slot], s));
-  c->last_budget = budget;
   return HBX_OK;
 }
 
@@ -423,7 +469,7 @@ int plan_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
 int md5_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
   hipStream_t s = c->hstream;
   const int slot = (int)(c->launches % 3);
-  if (s != c->stream) HBX_TRY(c, hipStreamWaitEvent(s, c->plan_done[slot], 0));
+  if (s != plan_stream(c)) HBX_TRY(c, hipStreamWaitEvent(s, c->plan_done[slot], 0));
   {
     StageTimer t(c, s, 3);
     hipLaunchKernelGGL(hbx_k3_block_md5, dim3(c->md5_wgs), dim3(kK3Threads), 0, s,
@@ -432,6 +478,7 @@ int md5_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
   }
   HBX_TRY(c, hipGetLastError());
   c->k3_dispatched += c->md5_wgs;
+  c->last_budget = budget;  // what the next plan advances this list by
   HBX_TRY(c, hipEventRecord(c->order_free[slot], s));
   c->order_used[slot] = true;
   c->launches++;
@@ -454,12 +501,21 @@ int md5_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
 }
 
 // One pipeline step on the hash side: launch j = plan (the carried chains +
-// the chains of c->unjoined, the batch cut by the previous submit) then K3
-// with `budget` blocks per chain.  Issued by every submit BEFORE the new
-// batch's own scan is enqueued, and by wait_oldest with kBudgetAll to drain.
-// Nothing is launched when no chain is in flight.
-int md5_step(hbx_ctx* c, uint32_t budget) {
-  Batch* nb = c->unjoined;
+// the chains of the oldest unjoined batch once it is join_lag submits old)
+// then K3 with `budget` blocks per chain.  Issued by every submit BEFORE the
+// new batch's own scan is enqueued, and by wait_oldest (`drain`, with
+// kBudgetAll: the oldest unjoined batch joins whatever its age).  Nothing is
+// launched when no chain is in flight.
+int md5_step(hbx_ctx* c, uint32_t budget, bool drain = false) {
+  if (c->preplanned) {  // planned one launch ahead (mode 2): any budget may run it
+    Batch* nb = c->pre_nb;
+    c->preplanned = false;
+    c->pre_nb = nullptr;
+    if (nb) nb->joined = true;
+    return md5_launch(c, nb, budget);
+  }
+  Batch* nb = nullptr;
+  if (!c->unjoined.empty() && (drain || c->unjoined.size() >= c->join_lag)) nb = c->unjoined.front();
   bool live = nb != nullptr;
   for (Batch* b : c->pending)
     if (b->joined && !b->finalized) live = true;
@@ -468,9 +524,31 @@ int md5_step(hbx_ctx* c, uint32_t budget) {
   if (rc) return rc;
   if (nb) {
     nb->joined = true;
-    c->unjoined = nullptr;
+    c->unjoined.pop_front();
   }
   return md5_launch(c, nb, budget);
+}
+
+// Mode 2: enqueue the plan of the NEXT launch now, on the scan stream, before
+// the submitting batch's own K1.  It adds the oldest unjoined batch once that
+// is join_lag submits old at the next submit (the submitting batch is not in
+// the FIFO yet, hence the + 1).  Nothing is planned when no chain would be in
+// flight; the next submit then plans inline.
+int preplan(hbx_ctx* c, uint32_t budget) {
+  if (plan_mode_of(c) != 2 || c->preplanned || c->hstream == c->stream) return HBX_OK;
+  Batch* nb = nullptr;
+  if (!c->unjoined.empty() && c->unjoined.size() + 1 >= c->join_lag && c->join_lag >= 2) nb = c->unjoined.front();
+  bool live = nb != nullptr;
+  for (Batch* b : c->pending)
+    if (b->joined && !b->finalized) live = true;
+  if (!live) return HBX_OK;
+  int rc = ensure_plan_buffers(c, 0);  // its slot's last reader (K3 three launches back) is waited for
+  if (!rc) rc = plan_launch(c, nb, budget);
+  if (rc) return rc;
+  if (nb) c->unjoined.pop_front();
+  c->pre_nb = nb;
+  c->preplanned = true;
+  return HBX_OK;
 }
 
 // The order-list and planner buffers the next launch's plan writes, with
@@ -478,6 +556,7 @@ int md5_step(hbx_ctx* c, uint32_t budget) {
 // plan writes may grow: growing reallocates without copying, and the slot of
 // the previous launch holds the carried chains the plan reads.
 int ensure_plan_buffers(hbx_ctx* c, uint64_t extra) {
+  if (c->preplanned) return HBX_OK;  // that slot holds the next launch's list already
   uint64_t bound = 64 + extra;  // entries <= chains of the unfinalized batches
   for (Batch* b : c->pending)
     if (!b->finalized) bound += b->caps;
@@ -495,7 +574,11 @@ int ensure_plan_buffers(hbx_ctx* c, uint64_t extra) {
 // in the carried order lists) and the context refuses further pipelined work.
 int submit_abort(hbx_ctx* c, Batch* b, int rc, bool enqueued) {
   const std::string keep = c->err;
-  if (c->unjoined == b) c->unjoined = nullptr;
+  for (auto it = c->unjoined.begin(); it != c->unjoined.end(); ++it)
+    if (*it == b) {
+      c->unjoined.erase(it);
+      break;
+    }
   for (auto it = c->pending.begin(); it != c->pending.end(); ++it)
     if (*it == b) {
       c->pending.erase(it);
@@ -516,14 +599,27 @@ int submit_abort(hbx_ctx* c, Batch* b, int rc, bool enqueued) {
 int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, const uint64_t* offs,
                         const uint64_t* lens, uint32_t budget, uint64_t slices, size_t meta_bytes, int slot);
 
-// K1 tiles of one file of `iters` 64 KiB iterations: c->tile_iters each.
+// K1 tiles of one file of `iters` 64 KiB iterations: `tile` each.
 // (Queuing each file's last eighth as 1 MiB tiles after the long ones, to
 // round off K1's last pass over the CUs K3 leaves free, measured slower: K1
 // 3.18 -> 3.33 ms beside K3 at 33 resident batches, from the extra halos and
 // workgroups.)
-void k1_tiles(hbx_ctx* c, uint32_t f, uint32_t iters) {
-  for (uint32_t i = 0; i < iters; i += c->tile_iters)
-    c->h_tiles.push_back(make_uint4(f, i, std::min(c->tile_iters, iters - i), 0u));
+void k1_tiles(hbx_ctx* c, uint32_t f, uint32_t iters, uint32_t tile) {
+  for (uint32_t i = 0; i < iters; i += tile) c->h_tiles.push_back(make_uint4(f, i, std::min(tile, iters - i), 0u));
+}
+
+constexpr uint32_t kTileItersMin = 16, kTileItersMax = 256;
+
+// K1 tile length for a batch of `total` iterations (c->tile_iters, or about
+// two tiles per CU when that is 0)
+uint32_t k1_tile_iters(const hbx_ctx* c, uint64_t total) {
+  if (c->tile_iters) return c->tile_iters;
+  const uint64_t t = (total + 2ull * c->md5_wgs - 1) / (2ull * c->md5_wgs);
+  return (uint32_t)std::min<uint64_t>(kTileItersMax, std::max<uint64_t>(kTileItersMin, t));
+}
+
+inline uint64_t scan_iters(uint64_t N) {  // K1 iterations of a file (0: no split candidates)
+  return N > 2ull * HBX_MIN_BLOCK_SIZE ? (N + HBX_MIN_BLOCK_SIZE - 1) / HBX_MIN_BLOCK_SIZE : 0;
 }
 
 // Plan + enqueue one device batch (K1, K2, first MD5 launch).  Results are
@@ -548,21 +644,25 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
   b->cut_base.resize(n);
   c->h_slice_base.resize(n);
   c->h_tiles.clear();
-  uint64_t slices = 0, tcaps = 0, longest = 0;
+  uint64_t slices = 0, tcaps = 0, longest = 0, total_iters = 0;
+  for (uint64_t f = 0; f < n; f++) {
+    const uint64_t iters = scan_iters(lens[f]);
+    if (iters > 0xFFFFFFFFull) {
+      c->pool.push_back(b);
+      return c->fail(HBX_ERR_ARG, "file too large");
+    }
+    total_iters += iters;
+  }
+  const uint32_t tile = k1_tile_iters(c, total_iters);
   for (uint64_t f = 0; f < n; f++) {
     const uint64_t N = lens[f];
     longest = std::max(longest, N);
     c->h_slice_base[f] = slices;
     b->cut_base[f] = tcaps;
     tcaps += max_chunks(N);
-    if (N > 2ull * HBX_MIN_BLOCK_SIZE) {  // only files with split candidates scan
+    if (const uint64_t iters = scan_iters(N)) {  // only files with split candidates scan
       slices += (N + kSlice - 1) / kSlice;
-      const uint64_t iters = (N + HBX_MIN_BLOCK_SIZE - 1) / HBX_MIN_BLOCK_SIZE;
-      if (iters > 0xFFFFFFFFull) {
-        c->pool.push_back(b);
-        return c->fail(HBX_ERR_ARG, "file too large");
-      }
-      k1_tiles(c, (uint32_t)f, (uint32_t)iters);
+      k1_tiles(c, (uint32_t)f, (uint32_t)iters, tile);
     }
   }
   b->caps = tcaps;
@@ -601,6 +701,7 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   // waits for this batch's scan
   const uint64_t launches0 = c->launches;
   int rc = md5_step(c, budget);
+  if (!rc) rc = preplan(c, budget);
   if (rc) return rc;
   const bool gate = c->k1_gate && c->launches != launches0 && c->hstream != s;
   if (n == 0) {
@@ -662,10 +763,10 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
                      b->d_ids.as<uint32_t>(), b->d_run.as<Chain>(), b->d_fresh.as<OrderEntry>(),
                      b->d_fcnt.as<uint32_t>());
   HBX_TRY(c, hipGetLastError());
+  // the plan this batch joins waits for ev[2] (plan_launch), so with a join
+  // lag of 2 the scan stream never waits for this K2
   HBX_TRY(c, hipEventRecord(b->ev[2], s2));
-  // the next plan (on the scan stream) reads K2r's entries
-  if (s2 != s) HBX_TRY(c, hipStreamWaitEvent(s, b->ev[2], 0));
-  c->unjoined = b;
+  c->unjoined.push_back(b);
   return HBX_OK;
 }
 
@@ -721,6 +822,7 @@ int submit_verify_launch(hbx_ctx* c, Batch* b, const uint8_t* arena, uint64_t n,
                          const uint32_t* n_links, uint64_t nlinks_total, size_t meta_bytes, uint32_t budget) {
   hipStream_t s = c->stream;
   int rc = md5_step(c, budget);  // launch j first, as in submit_batch_launch
+  if (!rc) rc = preplan(c, budget);
   if (rc) return rc;
   if (n == 0) {
     for (int i = 0; i < 4; i++) HBX_TRY(c, hipEventRecord(b->ev[i], s));
@@ -748,7 +850,7 @@ int submit_verify_launch(hbx_ctx* c, Batch* b, const uint8_t* arena, uint64_t n,
                      b->d_fresh.as<OrderEntry>(), b->d_fcnt.as<uint32_t>());
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(b->ev[2], s));
-  c->unjoined = b;
+  c->unjoined.push_back(b);
   return HBX_OK;
 }
 
@@ -811,9 +913,13 @@ int wait_oldest(hbx_ctx* c) {
     c->parked.push_back(b);
     return c->fail(HBX_ERR_STATE, "context is unusable after a failed submit; destroy it");
   }
-  if (!b->finalized) {  // drain: every chain in flight, the unjoined batch's included
-    int rc = md5_step(c, kBudgetAll);
+  // drain: every chain in flight; a pre-planned launch runs first (with an
+  // unlimited budget), then b joins if it had not yet (b is the oldest)
+  for (int k = 0; !b->finalized; k++) {
+    const uint64_t l0 = c->launches;
+    int rc = md5_step(c, kBudgetAll, true);
     if (rc) return rc;
+    if (c->launches == l0 || k > 2) return c->fail(HBX_ERR_STATE, "drain launched nothing (internal)");
   }
   HBX_TRY(c, hipEventSynchronize(b->ev[4]));
   c->pending.pop_front();
@@ -891,7 +997,9 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
     c->md5_wgs = (uint32_t)(ncu = prop.multiProcessorCount);
   if (const char* v = std::getenv("HBX_MD5_WGS")) c->md5_wgs = (uint32_t)std::max(1, std::atoi(v));
   if (const char* v = std::getenv("HBX_K3_DENSE")) c->k3_dense = std::atoi(v) ? 1u : 0u;
-  if (const char* v = std::getenv("HBX_TILE_ITERS")) c->tile_iters = (uint32_t)std::min(1024, std::max(1, std::atoi(v)));
+  if (const char* v = std::getenv("HBX_TILE_ITERS")) c->tile_iters = (uint32_t)std::min(1024, std::max(0, std::atoi(v)));
+  if (const char* v = std::getenv("HBX_JOIN_LAG")) c->join_lag = (uint32_t)std::min(4, std::max(1, std::atoi(v)));
+  if (const char* v = std::getenv("HBX_PLAN_MODE")) c->plan_mode = std::min(2, std::max(0, std::atoi(v)));
   if (const char* v = std::getenv("HBX_MD5_SLICE")) c->md5_slice = (uint32_t)std::max(0, std::atoi(v));
   if (const char* v = std::getenv("HBX_K1_GATE")) c->k1_gate = std::atoi(v) ? 1u : 0u;
   if (hipSetDevice(device) != hipSuccess || make_stream(&c->stream, "HBX_SCAN_CUS", ncu, "0:4096") != hipSuccess) {
@@ -899,16 +1007,12 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
     return HBX_ERR_HIP;
   }
   const char* one = std::getenv("HBX_ONE_STREAM");  // A/B: scan, hash and results on one stream
-  // K2 on its own stream is optional: with GPU_MAX_HW_QUEUES = 4 a fourth
-  // stream of ours shares a hardware queue (measured: +0.2 ms hash-stream gap)
-  const char* k2s = std::getenv("HBX_K2_STREAM");
-  const bool own_k2 = k2s && std::atoi(k2s);
+  if (const char* v = std::getenv("HBX_K2_STREAM")) c->k2_own = std::atoi(v) ? 1 : 0;
+  c->cstream = c->stream;
   if (one && std::atoi(one)) {
-    c->cstream = c->hstream = c->rstream = c->stream;
-  } else if ((own_k2 ? hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking)
-                     : (c->cstream = c->stream, hipSuccess)) != hipSuccess ||
-             make_stream(&c->hstream, "HBX_HASH_CUS", ncu) != hipSuccess ||
-             make_stream(&c->rstream, "HBX_RES_CUS", ncu) != hipSuccess) {
+    c->hstream = c->rstream = c->stream;
+  } else if (make_stream(&c->hstream, "HBX_HASH_CUS", ncu) != hipSuccess ||
+             make_stream(&c->rstream, "HBX_RES_CUS", ncu) != hipSuccess || ensure_cut_stream(c) != HBX_OK) {
     hbx_ctx_destroy(c);
     return HBX_ERR_HIP;
   }
@@ -969,10 +1073,20 @@ void hbx_ctx_destroy(hbx_ctx* c) {
 const char* hbx_last_error(const hbx_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 int hbx_set_tile_iters(hbx_ctx* c, uint32_t iters) {
-  if (!c || iters == 0 || iters > 1024) return HBX_ERR_ARG;
+  if (!c || iters > 1024) return HBX_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   c->tile_iters = iters;
   return HBX_OK;
+}
+
+int hbx_set_join_lag(hbx_ctx* c, uint32_t lag) {
+  if (!c || lag < 1 || lag > 4) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  // pending batches were counted against the lag of their submit
+  if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
+  HBX_TRY(c, hipSetDevice(c->device));
+  c->join_lag = lag;
+  return ensure_cut_stream(c);
 }
 
 int hbx_stage_times(hbx_ctx* c, float ms[5]) {
@@ -999,7 +1113,7 @@ int hbx_reserve(hbx_ctx* c, uint32_t batches, uint64_t files, uint64_t bytes) {
   if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
   HBX_TRY(c, hipSetDevice(c->device));
   const uint64_t caps = bytes / HBX_MIN_BLOCK_SIZE + files;  // >= sum of max_chunks over the files
-  const uint64_t tiles = bytes / ((uint64_t)c->tile_iters * HBX_MIN_BLOCK_SIZE) + files;
+  const uint64_t tiles = bytes / ((uint64_t)(c->tile_iters ? c->tile_iters : kTileItersMin) * HBX_MIN_BLOCK_SIZE) + files;
   const uint64_t slices = bytes / kSlice + files;
   const size_t meta_bytes = files * 8 * 4 + tiles * sizeof(uint4);
   int rc = HBX_OK;
@@ -1446,11 +1560,11 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
   // arena once its batch has been collected.
   const uint32_t budget = c->md5_slice ? c->md5_slice : kBudgetAll;
   const uint64_t nfull_max = (HBX_MAX_BLOCK_SIZE + 8ull) >> 6;
-  // a batch's chains join the launch of the next submit: it completes
-  // ceil(nfull/budget) submits after its own, so this many arenas keep the
-  // collect from forcing a drain
+  // a batch's chains join the launch join_lag submits later: it completes
+  // join_lag - 1 + ceil(nfull/budget) submits after its own, so this many
+  // arenas keep the collect from forcing a drain
   const size_t depth = budget == kBudgetAll ? 2 : (size_t)std::min<uint64_t>(
-      64, (nfull_max + budget - 1) / budget + 2);
+      64, (nfull_max + budget - 1) / budget + c->join_lag + 1);
   if (c->d_ring.size() < depth) c->d_ring.resize(depth);
   // size every staging buffer once, for the largest batch this call forms
   // (growing one later would re-pin host memory or drain the streams)

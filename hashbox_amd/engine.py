@@ -78,7 +78,7 @@ class Engine:
     """One MI355X (one HIP stream) running the chunk + block-ID path."""
 
     def __init__(self, device: int = 0, tile_iters: Optional[int] = None,
-                 md5_slice: Optional[int] = None):
+                 md5_slice: Optional[int] = None, join_lag: Optional[int] = None):
         self._L = _lib.load()
         self._ctx = ctypes.c_void_p()
         rc = self._L.hbx_ctx_create(int(device), ctypes.byref(self._ctx))
@@ -90,6 +90,8 @@ class Engine:
             self._check(self._L.hbx_set_tile_iters(self._ctx, int(tile_iters)), "set_tile_iters")
         if md5_slice is not None:
             self.set_md5_slice(md5_slice)
+        if join_lag is not None:
+            self.set_join_lag(join_lag)
 
     # ----------------------------------------------------------- plumbing --
     def _after_producer(self):
@@ -243,6 +245,11 @@ class Engine:
     def set_md5_slice(self, blocks: int):
         """MD5 blocks per chain per K3 launch (0 = unlimited)."""
         self._check(self._L.hbx_set_md5_slice(self._ctx, int(blocks)), "hbx_set_md5_slice")
+
+    def set_join_lag(self, lag: int):
+        """Submits between a batch's own and the MD5 launch its chains join
+        (1..4; 2 gives a small batch's scan a whole extra step)."""
+        self._check(self._L.hbx_set_join_lag(self._ctx, int(lag)), "hbx_set_join_lag")
 
     def reserve(self, batches: int, files: int, nbytes: int):
         """Pre-size the pipeline for ``batches`` batches in flight of up to

@@ -134,8 +134,8 @@ int hbx_wait(hbx_ctx *ctx);
 int hbx_pending(hbx_ctx *ctx);
 /* Time slice of the block-MD5 stage: full 64-byte MD5 blocks each chain in
  * flight advances per launch (default 16384 = 1 MiB; 0 = unlimited, one
- * launch per batch).  A submitted batch is complete after
- * ceil(min(longest file, 8 MiB)/64 / blocks) further launches; results are
+ * launch per batch).  A submitted batch is complete after join lag (below)
+ * + ceil(min(longest file, 8 MiB)/64 / blocks) - 1 further launches; results are
  * identical for every setting. */
 int hbx_set_md5_slice(hbx_ctx *ctx, uint32_t blocks);
 /* Optional: pre-size the pipeline for `batches` batches in flight of up to
@@ -423,8 +423,17 @@ int hbx_stage_times(hbx_ctx *ctx, float ms[5]);
  * [0] K1 scan, [1] K2 cut chain, [2] K2c chain plan, [3] K3 block MD5,
  * [4] K4 content id.  reset != 0 zeroes the totals after reading. */
 int hbx_stage_totals(hbx_ctx *ctx, double ms[5], uint64_t launches[5], int reset);
-/* Tile length of K1 in 64 KiB iterations (default 64 = 4 MiB tiles). */
+/* Tile length of K1 in 64 KiB iterations, 1..1024; 0 (the default) sizes
+ * tiles per batch: about two per CU, 16..256 iterations (1-16 MiB). */
 int hbx_set_tile_iters(hbx_ctx *ctx, uint32_t iters);
+/* Pipeline join lag, 1..4 (default 1): a batch's chains join the block-MD5
+ * launch issued `lag` submits after it, so its cut stage (K1 scan + K2 cut
+ * chain) has `lag` pipeline steps to finish before the hash stage needs it.
+ * Lag 2 suits small batches, whose scan is latency- rather than
+ * throughput-bound.  Results are identical for every setting; a batch is
+ * complete `lag` - 1 launches later.  Fails with HBX_ERR_STATE while batches
+ * are pending. */
+int hbx_set_join_lag(hbx_ctx *ctx, uint32_t lag);
 
 #ifdef __cplusplus
 }

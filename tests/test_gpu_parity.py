@@ -74,10 +74,11 @@ def test_batch_mixed(engine, oracle):
         _check(r, oracle.store_file(f, fast=True))
 
 
-@pytest.mark.parametrize("tile_iters", [1, 3, 32, 64, 256, 1024])
+@pytest.mark.parametrize("tile_iters", [0, 1, 3, 32, 64, 256, 1024])
 def test_tile_sizes(oracle, tile_iters):
     from hashbox_amd import Engine
-    # several tiles per file up to 256 iterations (16 MiB tiles); 1024 = one tile
+    # several tiles per file up to 256 iterations (16 MiB tiles); 1024 = one
+    # tile; 0 = sized per batch (16 iterations for this one)
     n = 37 * MIN + 999 if tile_iters < 64 else (5 * tile_iters * MIN) // 2 + 999 if tile_iters <= 256 else 20 * MAXB + 5
     with Engine(0, tile_iters=tile_iters) as e:
         x = oracle.random_bytes(n, 77)
@@ -181,14 +182,16 @@ def _device_batches(oracle, nb, seed):
     return out
 
 
-@pytest.mark.parametrize("md5_slice", [1, 3, 64, 16384])
-def test_pipelined_batches_time_sliced(oracle, md5_slice):
+@pytest.mark.parametrize("md5_slice,join_lag", [(1, 1), (3, 1), (64, 1), (16384, 1), (3, 2), (64, 2), (64, 3),
+                                                (16384, 4)])
+def test_pipelined_batches_time_sliced(oracle, md5_slice, join_lag):
     """Several batches in flight on one context with the block-MD5 stage
     time-sliced: chains resume across many K3 launches, new batches' chunks
-    join carried chains, results come back in FIFO order, bit-exact."""
+    join carried chains (join_lag submits later), results come back in FIFO
+    order, bit-exact."""
     from hashbox_amd import Engine
     batches = _device_batches(oracle, 4, 31 + md5_slice % 7)
-    with Engine(0, md5_slice=md5_slice) as e:
+    with Engine(0, md5_slice=md5_slice, join_lag=join_lag) as e:
         for dev, offs, sizes, _ in batches[:3]:
             e.submit_device(dev.data_ptr(), offs, sizes)
         assert e.pending() == 3
@@ -210,22 +213,32 @@ def test_pipelined_batches_time_sliced(oracle, md5_slice):
         assert n[3] >= 1 and ms[3] > 0
 
 
-def test_pipelined_steady_state(oracle):
+@pytest.mark.parametrize("join_lag,plan_mode", [(1, None), (2, None), (3, None), (2, "0"), (2, "1"), (1, "1")])
+def test_pipelined_steady_state(oracle, monkeypatch, join_lag, plan_mode):
     """A deep pipeline as bench.py drives it: submit, and wait only once
     `depth` batches are pending, so batches complete through the slice
-    schedule rather than a forced drain."""
+    schedule rather than a forced drain.  Join lags 1-3, with the plans one
+    launch ahead (the default at lag >= 2), inline on the scan stream or on
+    the hash stream (HBX_PLAN_MODE 0/1: schedule only)."""
     from hashbox_amd import Engine
+    if plan_mode is not None:
+        monkeypatch.setenv("HBX_PLAN_MODE", plan_mode)
     batches = _device_batches(oracle, 3, 57)
     got = []
-    with Engine(0, md5_slice=4096) as e:  # 256 KiB per chain per launch: 32 launches per 8 MiB
+    with Engine(0, md5_slice=4096, join_lag=join_lag) as e:  # 256 KiB per chain per launch: 32 per 8 MiB
         order = [i % 3 for i in range(40)]
         for i in order:
             dev, offs, sizes, _ = batches[i]
             e.submit_device(dev.data_ptr(), offs, sizes)
-            if e.pending() > 34:
+            if e.pending() >= 32 + join_lag + 1:
                 got.append(e.wait())
         while e.pending():
             got.append(e.wait())
+        with pytest.raises(Exception):  # the lag is fixed while batches are pending
+            e.submit_device(batches[0][0].data_ptr(), batches[0][1], batches[0][2])
+            e.set_join_lag(1)
+        got.append(e.wait())
+        order.append(0)
     assert len(got) == len(order)
     for i, g in zip(order, got):
         for a, r in zip(g, batches[i][3]):
