@@ -82,7 +82,7 @@ def parse():
                          "/ batch lifetime (the longest chunk's serial MD5)")
     ap.add_argument("--join-lag", type=int, default=0,
                     help="submits between a batch's own and the K3 launch its chains join "
-                         "(hbx_set_join_lag; 0 = auto: 2 below 64 files per GPU, else 1)")
+                         "(hbx_set_join_lag; 0 = auto: 3 below 64 files per GPU, else 1)")
     ap.add_argument("--lead", type=int, default=-1,
                     help="launches between a batch's completion and its collection (the scan side's "
                          "slack): R = launches per batch + lead (-1 = join lag + 1)")
@@ -208,21 +208,25 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
     + submit one), then the drain.  Returns timings, the window's launch
     counts and results."""
     order = deque()  # arena index of every pending batch, oldest first
-    state = {"j": 0}
+    state = {"j": 0, "t_sub": 0.0, "t_col": 0.0}
     arena_res = {}
 
     def submit():
+        t = time.perf_counter()
         i = state["j"] % R
         if before_submit:
             before_submit(i)
         eng.submit_device(arenas[i].data_ptr(), offs, lens)
         order.append(i)
         state["j"] += 1
+        state["t_sub"] += time.perf_counter() - t
 
     def collect():
+        t = time.perf_counter()
         i = order.popleft()
         res = eng.wait()
         arena_res[i] = res
+        state["t_col"] += time.perf_counter() - t
         return i, res
 
     torch.cuda.synchronize(dev)
@@ -236,6 +240,8 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
         dist.barrier()
     torch.cuda.synchronize(dev)
     eng.stage_totals(reset=True)  # everything before the window is complete and harvested
+    state["t_sub"] = state["t_col"] = 0.0
+    eng.wait_s = 0.0
     t0 = time.perf_counter()
     last = None
     for _ in range(steps):
@@ -243,6 +249,8 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
         submit()
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
+    host = {"submit_ms": state["t_sub"] / steps * 1e3, "collect_ms": state["t_col"] / steps * 1e3,
+            "in_hbx_wait_ms": eng.wait_s / steps * 1e3}
     if dist:
         dist.barrier()
     tot_ms, tot_n = eng.stage_totals()
@@ -254,7 +262,7 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
     t2 = time.perf_counter()
     return {"el": t1 - t0, "drain": t2 - t_d, "fill_to_drained": t2 - t_fill,
             "batches_total": state["j"], "tot_ms": tot_ms, "tot_n": tot_n,
-            "last": last, "drained": drained, "arena_res": arena_res}
+            "last": last, "drained": drained, "arena_res": arena_res, "host": host}
 
 
 def max_over_ranks(x, dist, dev, op="max"):
@@ -325,6 +333,8 @@ def run_workload(a, name, eng, arenas, offs, lens, R, B, need, lanes, dist, gpu,
         "k3_lanes": lane_occupancy(r["arena_res"], R, B, need, lanes),
         "kernel_ms_per_step": {n: round(float(v) / a.steps, 4) for n, v in zip(KNAMES, tot_ms)},
         "window_launches": {n: int(v) for n, v in zip(KNAMES, tot_n)},
+        # host time per step inside the window (rank 0's): submit, and collect (incl. any wait)
+        "host_ms_per_step": {k: round(v, 4) for k, v in r["host"].items()},
     }
     if check is not None:
         out["check_vs_oracle"] = check
@@ -363,7 +373,10 @@ def main():
     if not lens:
         raise SystemExit(f"rank {rank} has no files: --files {a.files} < world {world}")
     nf = len(lens)
-    lag = a.join_lag if a.join_lag > 0 else (2 if nf < 64 else 1)
+    # small per-GPU batches (strong scaling) are scan-latency-bound at lag 1:
+    # lag 3 plans each launch a step ahead (tools/gpu_pipe_sweep.sh: 8 files
+    # 1,576 -> 1,976 GiB/s, 16 files 1,752 -> 2,185); at 64 files lag 1 is best
+    lag = a.join_lag if a.join_lag > 0 else (3 if nf < 64 else 1)
     lead = a.lead if a.lead >= 0 else lag + 1
     offs, total = W.pack_layout(lens)
     job_batch = (sum(job_lens) if a.scaling == "strong" else sum(job_lens) * world)

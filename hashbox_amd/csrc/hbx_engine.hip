@@ -98,13 +98,34 @@ struct TimedLaunch {
   int stage;
 };
 
+// Layout of a batch's results, the same on the device (d_res) and in the
+// pinned host block (h_res), so one copy moves them all.
+struct ResLayout {
+  size_t counts = 0, cuts = 0, ids = 0, cid = 0, ctype = 0, total = 0;
+};
+inline size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
+ResLayout res_layout(uint64_t n_files, uint64_t total_cap) {
+  ResLayout r;
+  r.cuts = al256(n_files * 4);
+  r.ids = r.cuts + al256(total_cap * 8);
+  r.cid = r.ids + al256(total_cap * 16);
+  r.ctype = r.cid + al256(n_files * 16);
+  r.total = r.ctype + al256(n_files * 4);
+  return r;
+}
+
 // One submitted batch.  Its device buffers live until its results are
 // collected: K3 writes BlockIDs into d_ids across several launches when the
 // MD5 stage is time-sliced.
 struct Batch {
   uint64_t n = 0, caps = 0;
   std::vector<uint64_t> cut_base;
-  DevBuf d_meta, d_cuts, d_count, d_ids, d_cid, d_ctype;
+  DevBuf d_meta, d_res;  // d_res: cut counts | cut ends | ids | content ids | types (rl)
+  ResLayout rl;
+  uint8_t* res(size_t off) const { return static_cast<uint8_t*>(d_res.p) + off; }
+  uint64_t* cuts_d() const { return reinterpret_cast<uint64_t*>(res(rl.cuts)); }
+  uint32_t* count_d() const { return reinterpret_cast<uint32_t*>(res(rl.counts)); }
+  uint32_t* ids_d() const { return reinterpret_cast<uint32_t*>(res(rl.ids)); }
   DevBuf d_run, d_fresh, d_fcnt;  // the batch's MD5 chains (K2r), their order entries, count
   PinBuf h_meta, h_res;
   uint64_t* cut_ends = nullptr;
@@ -122,7 +143,7 @@ struct Batch {
   uint64_t* v_nbad = nullptr;
   hipEvent_t ev[5] = {};  // K1 start | K1 end | K2 end | plan+K3 end (first) | results ready
   void release() {
-    for (DevBuf* d : {&d_meta, &d_cuts, &d_count, &d_ids, &d_cid, &d_ctype, &d_run, &d_fresh, &d_fcnt}) d->release();
+    for (DevBuf* d : {&d_meta, &d_res, &d_run, &d_fresh, &d_fcnt}) d->release();
     h_meta.release();
     h_res.release();
     for (auto& e : ev)
@@ -156,6 +177,7 @@ struct hbx_ctx {
   int plan_mode = -1;
   bool preplanned = false;    // the plan of launch `launches` is enqueued (mode 2)
   Batch* pre_nb = nullptr;    // the batch whose chains that plan adds
+  uint32_t k4_window = 1024;  // K4's LDS window of ids (HBX_K4_WINDOW, 1..1024: tests)
   int k2_own = -1;            // ensure_cut_stream: -1 = by join lag (HBX_K2_STREAM for A/B)
   uint32_t md5_wgs = 256;     // K3 grid: one 256-thread workgroup per CU (set from the device)
   // K3 wave placement: 1 packs the busy waves into the fewest CUs (4 per CU,
@@ -283,12 +305,21 @@ struct StageTimer {
   }
 };
 
+// Timed launches of one stage run on one stream, so they complete in order:
+// once one is still running, the later ones of its stage are not queried (a
+// host far ahead of the device keeps many open, and each query costs µs).
 void harvest_timings(hbx_ctx* c) {
   size_t keep = 0;
+  bool open[5] = {false, false, false, false, false};
   for (size_t i = 0; i < c->open_t.size(); i++) {
     TimedLaunch& t = c->open_t[i];
     float ms = 0.f;
-    if (hipEventQuery(t.b) == hipSuccess && hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) {
+    bool done = false;
+    if (!open[t.stage]) {
+      done = hipEventQuery(t.b) == hipSuccess && hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess;
+      open[t.stage] = !done;
+    }
+    if (done) {
       c->tot_ms[t.stage] += ms;
       c->tot_n[t.stage] += 1;
       c->ev_pool.push_back(t.a);
@@ -300,26 +331,6 @@ void harvest_timings(hbx_ctx* c) {
   c->open_t.resize(keep);
 }
 
-// Layout of the pinned result block of a batch.
-struct ResLayout {
-  size_t counts, cuts, ids, cid, ctype, total;
-};
-ResLayout res_layout(uint64_t n_files, uint64_t total_cap) {
-  ResLayout r;
-  size_t o = 0;
-  r.counts = o;
-  o += ((n_files * 4 + 255) & ~size_t(255));
-  r.cuts = o;
-  o += total_cap * 8;
-  r.ids = o;
-  o += total_cap * 16;
-  r.cid = o;
-  o += n_files * 16;
-  r.ctype = o;
-  o += ((n_files * 4 + 255) & ~size_t(255));
-  r.total = o;
-  return r;
-}
 
 Batch* acquire_batch(hbx_ctx* c) {
   Batch* b;
@@ -339,6 +350,7 @@ Batch* acquire_batch(hbx_ctx* c) {
   b->n = b->caps = 0;
   b->need = 1;
   b->done = 0;
+  b->rl = ResLayout{};  // a verify batch keeps its ids at offset 0 of d_res
   b->joined = false;
   b->finalized = false;
   b->cut_ends = nullptr;
@@ -359,7 +371,7 @@ int finalize_batch(hbx_ctx* c, Batch* b) {
   hipStream_t s = c->rstream;
   b->finalized = true;
   if (b->verify) {
-    if (b->n) HBX_TRY(c, hipMemcpyAsync(b->h_res.p, b->d_ids.p, b->n * 16, hipMemcpyDeviceToHost, s));
+    if (b->n) HBX_TRY(c, hipMemcpyAsync(b->h_res.p, b->d_res.p, b->n * 16, hipMemcpyDeviceToHost, s));
     HBX_TRY(c, hipEventRecord(b->ev[4], s));
     return HBX_OK;
   }
@@ -368,18 +380,13 @@ int finalize_batch(hbx_ctx* c, Batch* b) {
     const uint64_t* d_cb = b->d_meta.as<uint64_t>() + 3 * n;
     {
       StageTimer t(c, s, 4);
-      hipLaunchKernelGGL(hbx_k4_content_id, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, s,
-                         (uint32_t)n, d_cb, b->d_count.as<uint32_t>(), b->d_ids.as<uint32_t>(),
-                         b->d_cid.as<uint32_t>(), b->d_ctype.as<int32_t>());
+      hipLaunchKernelGGL(hbx_k4_content_id, dim3((uint32_t)n), dim3(64), 0, s,
+                         (uint32_t)n, d_cb, b->count_d(), b->ids_d(), reinterpret_cast<uint32_t*>(b->res(b->rl.cid)),
+                         reinterpret_cast<int32_t*>(b->res(b->rl.ctype)), c->k4_window);
     }
     HBX_TRY(c, hipGetLastError());
-    const ResLayout rl = res_layout(n, b->caps);
-    uint8_t* hr = b->h_res.as<uint8_t>();
-    HBX_TRY(c, hipMemcpyAsync(hr + rl.counts, b->d_count.p, n * 4, hipMemcpyDeviceToHost, s));
-    HBX_TRY(c, hipMemcpyAsync(hr + rl.cuts, b->d_cuts.p, b->caps * 8, hipMemcpyDeviceToHost, s));
-    HBX_TRY(c, hipMemcpyAsync(hr + rl.ids, b->d_ids.p, b->caps * 16, hipMemcpyDeviceToHost, s));
-    HBX_TRY(c, hipMemcpyAsync(hr + rl.cid, b->d_cid.p, n * 16, hipMemcpyDeviceToHost, s));
-    HBX_TRY(c, hipMemcpyAsync(hr + rl.ctype, b->d_ctype.p, n * 4, hipMemcpyDeviceToHost, s));
+    // one copy for every result (5 copies before: each a dispatch on this stream)
+    HBX_TRY(c, hipMemcpyAsync(b->h_res.p, b->d_res.p, b->rl.total, hipMemcpyDeviceToHost, s));
   }
   HBX_TRY(c, hipEventRecord(b->ev[4], s));
   return HBX_OK;
@@ -678,11 +685,11 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
   const int slot = c->ssum_slot;
   if (n) {  // every allocation first: the batch is not in the FIFO yet
     int rc = HBX_OK;
-    for (hipError_t e : {b->h_meta.ensure(meta_bytes), b->d_meta.ensure(meta_bytes), b->d_cuts.ensure(tcaps * 8),
-                         b->d_count.ensure(n * 4), b->d_ids.ensure(tcaps * 16), b->d_cid.ensure(n * 16),
-                         b->d_ctype.ensure(n * 4), b->d_run.ensure(tcaps * sizeof(Chain)),
+    b->rl = res_layout(n, tcaps);
+    for (hipError_t e : {b->h_meta.ensure(meta_bytes), b->d_meta.ensure(meta_bytes), b->d_res.ensure(b->rl.total),
+                         b->d_run.ensure(tcaps * sizeof(Chain)),
                          b->d_fresh.ensure(tcaps * sizeof(OrderEntry)), b->d_fcnt.ensure(256),
-                         b->h_res.ensure(res_layout(n, tcaps).total)})
+                         b->h_res.ensure(b->rl.total)})
       if (e != hipSuccess && !rc) rc = c->hip(e, "batch buffers");
     if (!rc) rc = ensure_shared(c, c->d_ssum[slot], (slices + 1) * sizeof(uint2));  // +1: dummy slot
     if (!rc) rc = ensure_plan_buffers(c, tcaps);
@@ -750,8 +757,7 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   {
     StageTimer t(c, s2, 1);
     hipLaunchKernelGGL(hbx_k2_cut_chain, dim3((uint32_t)n), dim3(64), 0, s2, arena, d_off, d_len,
-                       d_sb, ssum.as<uint2>(), d_cb, b->d_cuts.as<uint64_t>(),
-                       b->d_count.as<uint32_t>());
+                       d_sb, ssum.as<uint2>(), d_cb, b->cuts_d(), b->count_d());
   }
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(c->ssum_free[slot], s2));
@@ -759,8 +765,7 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   // K2r: the batch's chains and their order entries
   HBX_TRY(c, hipMemsetAsync(b->d_fcnt.p, 0, 4, s2));
   hipLaunchKernelGGL(hbx_k2r_new_chains, dim3((uint32_t)((n * kPlanLanesPerFile + 255) / 256)), dim3(256), 0, s2,
-                     (uint32_t)n, arena, d_off, d_cb, b->d_cuts.as<uint64_t>(), b->d_count.as<uint32_t>(),
-                     b->d_ids.as<uint32_t>(), b->d_run.as<Chain>(), b->d_fresh.as<OrderEntry>(),
+                     (uint32_t)n, arena, d_off, d_cb, b->cuts_d(), b->count_d(), b->ids_d(), b->d_run.as<Chain>(), b->d_fresh.as<OrderEntry>(),
                      b->d_fcnt.as<uint32_t>());
   HBX_TRY(c, hipGetLastError());
   // the plan this batch joins waits for ev[2] (plan_launch), so with a join
@@ -804,7 +809,7 @@ int submit_verify(hbx_ctx* c, const uint8_t* arena, uint64_t n, const uint64_t* 
   const size_t meta_bytes = n * sizeof(VerifyDesc) + 16 * nlinks_total;
   if (n) {  // every allocation first: the batch is not in the FIFO yet
     int rc = HBX_OK;
-    for (hipError_t e : {b->h_meta.ensure(meta_bytes), b->d_meta.ensure(meta_bytes), b->d_ids.ensure(n * 16),
+    for (hipError_t e : {b->h_meta.ensure(meta_bytes), b->d_meta.ensure(meta_bytes), b->d_res.ensure(n * 16),
                          b->d_run.ensure(n * sizeof(Chain)), b->d_fresh.ensure(n * sizeof(OrderEntry)),
                          b->d_fcnt.ensure(256), b->h_res.ensure(n * 16)})
       if (e != hipSuccess && !rc) rc = c->hip(e, "verify batch buffers");
@@ -846,7 +851,7 @@ int submit_verify_launch(hbx_ctx* c, Batch* b, const uint8_t* arena, uint64_t n,
   HBX_TRY(c, hipMemsetAsync(b->d_fcnt.p, 0, 4, s));
   HBX_TRY(c, hipEventRecord(b->ev[1], s));
   hipLaunchKernelGGL(hbx_k6p_verify_chains, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
-                     b->d_meta.as<VerifyDesc>(), (uint32_t)n, b->d_ids.as<uint32_t>(), b->d_run.as<Chain>(),
+                     b->d_meta.as<VerifyDesc>(), (uint32_t)n, b->ids_d(), b->d_run.as<Chain>(),
                      b->d_fresh.as<OrderEntry>(), b->d_fcnt.as<uint32_t>());
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(b->ev[2], s));
@@ -871,7 +876,7 @@ int collect_batch(hbx_ctx* c, Batch* b) {
     if (b->v_nbad) *b->v_nbad = bad;
     return HBX_OK;
   }
-  const ResLayout rl = res_layout(n, b->caps);
+  const ResLayout& rl = b->rl;
   const uint8_t* hr = b->h_res.as<uint8_t>();
   const uint32_t* counts = reinterpret_cast<const uint32_t*>(hr + rl.counts);
   const uint64_t* cuts = reinterpret_cast<const uint64_t*>(hr + rl.cuts);
@@ -999,6 +1004,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = std::getenv("HBX_K3_DENSE")) c->k3_dense = std::atoi(v) ? 1u : 0u;
   if (const char* v = std::getenv("HBX_TILE_ITERS")) c->tile_iters = (uint32_t)std::min(1024, std::max(0, std::atoi(v)));
   if (const char* v = std::getenv("HBX_JOIN_LAG")) c->join_lag = (uint32_t)std::min(4, std::max(1, std::atoi(v)));
+  if (const char* v = std::getenv("HBX_K4_WINDOW")) c->k4_window = (uint32_t)std::min(1024, std::max(1, std::atoi(v)));
   if (const char* v = std::getenv("HBX_PLAN_MODE")) c->plan_mode = std::min(2, std::max(0, std::atoi(v)));
   if (const char* v = std::getenv("HBX_MD5_SLICE")) c->md5_slice = (uint32_t)std::max(0, std::atoi(v));
   if (const char* v = std::getenv("HBX_K1_GATE")) c->k1_gate = std::atoi(v) ? 1u : 0u;
@@ -1129,10 +1135,10 @@ int hbx_reserve(hbx_ctx* c, uint32_t batches, uint64_t files, uint64_t bytes) {
     Batch* b = acquire_batch(c);  // pooled first, then new
     if (!b) break;
     ready.push_back(b);
-    for (auto r : {b->h_meta.ensure(meta_bytes), b->d_meta.ensure(meta_bytes), b->d_cuts.ensure(caps * 8),
-                   b->d_count.ensure(files * 4), b->d_ids.ensure(caps * 16), b->d_cid.ensure(files * 16),
-                   b->d_ctype.ensure(files * 4), b->d_run.ensure(caps * sizeof(Chain)),
-                   b->d_fresh.ensure(caps * sizeof(OrderEntry)), b->d_fcnt.ensure(256), b->h_res.ensure(res_layout(files, caps).total)})
+    const size_t rbytes = res_layout(files, caps).total;
+    for (auto r : {b->h_meta.ensure(meta_bytes), b->d_meta.ensure(meta_bytes), b->d_res.ensure(rbytes),
+                   b->d_run.ensure(caps * sizeof(Chain)), b->d_fresh.ensure(caps * sizeof(OrderEntry)),
+                   b->d_fcnt.ensure(256), b->h_res.ensure(rbytes)})
       if (r != hipSuccess && !rc) rc = c->hip(r, "hbx_reserve");
     if (rc) break;
   }

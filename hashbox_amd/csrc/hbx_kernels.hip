@@ -1270,26 +1270,42 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k1_gate(const uint32_t* __r
   }
 }
 
-// Lane per file: ContentBlockID (store.go:187-196).
+// ContentBlockID (store.go:187-196), one wave per file.  The file's ids are
+// staged into LDS by all 64 lanes at once (kK4Window per round trip) and the
+// chain-block message is generated from there: the ids are read twice
+// (once as BlockIDs, once as FileChainBlock links), and a lane fetching them
+// one 16-B load per step paid a dependent memory round trip per message block,
+// which beside K1's HBM stream made K4 take 0.2-0.45 ms for 8 files.  Every
+// lane runs the same MD5 (uniform control flow); lane 0 stores it.
+constexpr uint32_t kK4Window = 1024u;  // ids per LDS window (16 KiB); `window` <= this (tests shrink it)
+
 extern "C" __global__ __launch_bounds__(64) void hbx_k4_content_id(
     uint32_t n_files, const uint64_t* __restrict__ cut_base, const uint32_t* __restrict__ cut_count,
     const uint32_t* __restrict__ ids, uint32_t* __restrict__ content_ids,
-    int32_t* __restrict__ content_type) {
-  const uint32_t f = blockIdx.x * 64u + threadIdx.x;
+    int32_t* __restrict__ content_type, uint32_t window) {
+  __shared__ uint4 win[kK4Window];
+  const uint32_t f = blockIdx.x;
   if (f >= n_files) return;
   const uint32_t k = cut_count[f];
   const uint4* id = reinterpret_cast<const uint4*>(ids) + cut_base[f];
   uint4* co = reinterpret_cast<uint4*>(content_ids) + f;
-  if (k == 0u) {
-    *co = make_uint4(0u, 0u, 0u, 0u);
-    content_type[f] = 0;
+  if (k <= 1u) {
+    if (threadIdx.x == 0) {
+      *co = k ? id[0] : make_uint4(0u, 0u, 0u, 0u);
+      content_type[f] = k ? 2 : 0;  // ContentTypeFileData / none
+    }
     return;
   }
-  if (k == 1u) {
-    *co = id[0];
-    content_type[f] = 2;  // ContentTypeFileData
-    return;
-  }
+  uint32_t w0 = 0xFFFFFFFFu;  // first id index in the window (none yet)
+  auto get = [&](uint32_t i) -> uint4 {
+    if (i < w0 || i - w0 >= window) {  // uniform: every lane asks for the same word
+      __syncthreads();
+      for (uint32_t t = threadIdx.x; t < window && i + t < k; t += 64u) win[t] = id[i + t];
+      __syncthreads();
+      w0 = i;
+    }
+    return win[i - w0];
+  };
   // Message words (little-endian u32 view of the hashed byte stream):
   //   BE32(k) | id_1..id_k | BE32(8+32k) | "fchn" | BE32(k) | (id_i | 0^16)*k
   const uint32_t nw = 12u * k + 4u;
@@ -1306,7 +1322,7 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k4_content_id(
       if (j == 0u) {
         v = bswap32(k);
       } else if (j <= 4u * k) {
-        const uint4 q = id[(j - 1u) >> 2];
+        const uint4 q = get((j - 1u) >> 2);
         const uint32_t r = (j - 1u) & 3u;
         v = r == 0 ? q.x : r == 1 ? q.y : r == 2 ? q.z : q.w;
       } else if (j == 4u * k + 1u) {
@@ -1319,7 +1335,7 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k4_content_id(
         const uint32_t t = j - (4u * k + 4u);
         const uint32_t r = t & 7u;
         if (r < 4u) {
-          const uint4 q = id[t >> 3];
+          const uint4 q = get(t >> 3);
           v = r == 0 ? q.x : r == 1 ? q.y : r == 2 ? q.z : q.w;
         } else {
           v = 0u;
@@ -1338,8 +1354,10 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k4_content_id(
     }
     md5_compress(h, m);
   }
-  *co = make_uint4(h[0], h[1], h[2], h[3]);
-  content_type[f] = 3;  // ContentTypeFileChain
+  if (threadIdx.x == 0) {
+    *co = make_uint4(h[0], h[1], h[2], h[3]);
+    content_type[f] = 3;  // ContentTypeFileChain
+  }
 }
 
 // Plain MD5 over a device buffer (used by hbx_block_id for arbitrary blocks

@@ -20,6 +20,7 @@ from __future__ import annotations
 import ctypes
 import os
 import sys
+import time
 from collections import deque
 from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence, Union
@@ -86,6 +87,7 @@ class Engine:
             raise HbxError(f"hbx_ctx_create(device={device}) failed: {_lib.ERRORS.get(rc, rc)}")
         self.device = device
         self._pending = deque()
+        self.wait_s = 0.0
         if tile_iters is not None:
             self._check(self._L.hbx_set_tile_iters(self._ctx, int(tile_iters)), "set_tile_iters")
         if md5_slice is not None:
@@ -202,7 +204,10 @@ class Engine:
         if not self._pending:
             return []
         item = self._pending.popleft()
-        self._check(self._L.hbx_wait(self._ctx), "hbx_wait")
+        t = time.perf_counter()
+        rc = self._L.hbx_wait(self._ctx)
+        self.wait_s += time.perf_counter() - t  # time inside hbx_wait (bench diagnostics)
+        self._check(rc, "hbx_wait")
         if isinstance(item[0], str):  # ("verify", ...)
             _, n, ids, ok, bad, keep = item
             return ids[:n], (ok[:n].astype(bool) if keep[1] is not None else None), int(bad.value)

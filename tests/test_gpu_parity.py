@@ -60,6 +60,21 @@ def test_periodic_ties(engine, oracle):
     _check(engine.chunk_hash(x), oracle.store_file(x, fast=True))
 
 
+@pytest.mark.parametrize("window", [1, 3, 16])
+def test_content_id_windows(oracle, monkeypatch, window):
+    """K4 stages a file's ids through an LDS window (1,024 ids; shrunk here
+    with HBX_K4_WINDOW) and reads them twice, as ids and as links: files of
+    many more chunks than the window restage it on both passes."""
+    from hashbox_amd import Engine
+    monkeypatch.setenv("HBX_K4_WINDOW", str(window))
+    files = [oracle.random_bytes(n, 60 + i) for i, n in enumerate([9 * MAXB + 3, 40 * MAXB + 11, 3 * MIN])]
+    with Engine(0) as e:
+        got = e.chunk_hash_batch(files)
+    assert got[1].n_chunks > 3 * window
+    for f, r in zip(files, got):
+        _check(r, oracle.store_file(f, fast=True))
+
+
 def test_zipf_duplicates(engine, oracle):
     x = oracle.zipf_corpus(48 * 1024 * 1024, 7)
     _check(engine.chunk_hash(x), oracle.store_file(x, fast=True))

@@ -15,8 +15,8 @@ for cfg in "$@"; do
   python - $out/$tag.json $tag <<'PY'
 import json,sys
 d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
-k=d["kernel_ms_per_step"]; c=d["config"]
+k=d["kernel_ms_per_step"]; c=d["config"]; h=d.get("host_ms_per_step", {})
 print(f"{sys.argv[2]:24s} R={c['pipeline_depth']} B={c['md5_slice_blocks']} lead={c['scan_lead']} "
-      f"{d['value']:.1f} GiB/s {d['ms_per_step']:.3f} ms  " + " ".join(f"{n[:6]}={v:.3f}" for n,v in k.items()), flush=True)
+      f"{d['value']:.1f} GiB/s {d['ms_per_step']:.3f} ms  host sub {h.get('submit_ms',0):.3f} col {h.get('collect_ms',0):.3f} (wait {h.get('in_hbx_wait_ms',0):.3f})  " + " ".join(f"{n[:6]}={v:.3f}" for n,v in k.items()), flush=True)
 PY
 done
