@@ -2,7 +2,7 @@
 # Round-2 first pass: GPU parity suite, smoke, the driver's bench command and a
 # long steady-state bench (the two headlines must agree within a few %).
 set -o pipefail
-O=gpurun_out/r02a
+O=gpurun_out/${TAG:-r02a}
 mkdir -p $O
 nproc > $O/nproc.txt; cat /sys/fs/cgroup/cpu.max >> $O/nproc.txt 2>&1; python3 -c "import os;print(len(os.sched_getaffinity(0)))" >> $O/nproc.txt
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
