@@ -155,9 +155,13 @@ def test_kat_block_ids_on_device(engine):
         assert engine.block_id(bytes.fromhex(r["data_hex"])).hex() == r["id"]
 
 
-def test_store_paths_end_to_end(engine, oracle, tmp_path):
+@pytest.mark.parametrize("join_lag", [1, 3])
+def test_store_paths_end_to_end(oracle, tmp_path, join_lag):
     """Files on disk -> pinned -> HBM -> results, in small batches so the
-    two-stream double buffering and batch boundaries are exercised."""
+    two-stream double buffering and batch boundaries are exercised (the
+    arena ring is as deep as the slice schedule plus the join lag)."""
+    from hashbox_amd import Engine
+    engine = Engine(0, md5_slice=4096, join_lag=join_lag)
     sizes = [0, 1, 4096, 2 * MIN + 1, 3 * MAXB + 7, 700_001, 5 * MIN, 12345, 9 * 1024 * 1024]
     paths, datas = [], []
     for i, n in enumerate(sizes * 3):
@@ -174,6 +178,7 @@ def test_store_paths_end_to_end(engine, oracle, tmp_path):
     from hashbox_amd import HbxError
     with _pt.raises((HbxError, FileNotFoundError)):
         engine.store_paths([str(tmp_path / "missing.bin")])
+    engine.close()
 
 
 def _device_batches(oracle, nb, seed):
