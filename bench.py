@@ -94,6 +94,8 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPUs; gloo for tests")
     ap.add_argument("--ballast-gib", type=float, default=0.0,
                     help="diagnostics: hold this much extra device memory (written once, never read)")
+    ap.add_argument("--k3-probe", action="store_true",
+                    help="diagnostics: per-wave timeline of the window's last K3 launch (HBX_K3_PROBE)")
     ap.add_argument("--single-alloc", action="store_true",
                     help="the R arenas as views of one allocation instead of R allocations")
     return ap.parse_args()
@@ -254,6 +256,7 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
     if dist:
         dist.barrier()
     tot_ms, tot_n = eng.stage_totals()
+    probe = k3_probe_stats(eng.k3_wave_times()) if os.environ.get("HBX_K3_PROBE") == "1" else None
     t_d = time.perf_counter()
     drained = None
     while order:
@@ -262,7 +265,24 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
     t2 = time.perf_counter()
     return {"el": t1 - t0, "drain": t2 - t_d, "fill_to_drained": t2 - t_fill,
             "batches_total": state["j"], "tot_ms": tot_ms, "tot_n": tot_n,
-            "last": last, "drained": drained, "arena_res": arena_res, "host": host}
+            "last": last, "drained": drained, "arena_res": arena_res, "host": host, "probe": probe}
+
+
+def k3_probe_stats(w):
+    """Summary of one K3 launch's per-wave records (engine.k3_wave_times), µs."""
+    busy = w[w[:, 1] != 0]
+    if not len(busy):
+        return None
+    t0 = int(w[w[:, 0] != 0][:, 0].min())
+    us = lambda x: np.round(np.asarray(x, np.float64) * 0.01, 1)  # noqa: E731  100 MHz ticks
+    start = us(busy[:, 0].astype(np.int64) - t0)
+    setup = us(busy[:, 1].astype(np.int64) - busy[:, 0].astype(np.int64))
+    end = us(busy[:, 2].astype(np.int64) - t0)
+    R = (busy[:, 3] & 0xffffffff).astype(np.int64)
+    q = lambda a: [float(np.min(a)), float(np.median(a)), float(np.max(a))]  # noqa: E731
+    return {"busy_waves": int(len(busy)), "span_us": float(us(int(w[:, 2].max()) - t0)),
+            "start_us_min_med_max": q(start), "startup_us_min_med_max": q(setup), "end_us_min_med_max": q(end),
+            "R_min_med_max": q(R)}
 
 
 def max_over_ranks(x, dist, dev, op="max"):
@@ -336,6 +356,8 @@ def run_workload(a, name, eng, arenas, offs, lens, R, B, need, lanes, dist, gpu,
         # host time per step inside the window (rank 0's): submit, and collect (incl. any wait)
         "host_ms_per_step": {k: round(v, 4) for k, v in r["host"].items()},
     }
+    if r["probe"] is not None:
+        out["k3_probe"] = r["probe"]
     if check is not None:
         out["check_vs_oracle"] = check
     return out
@@ -406,6 +428,8 @@ def main():
     ballast = torch.zeros(int(a.ballast_gib * GIB), dtype=torch.uint8, device=dev) if a.ballast_gib else None
     torch.cuda.synchronize(dev)
 
+    if a.k3_probe:
+        os.environ["HBX_K3_PROBE"] = "1"
     eng = Engine(dev_idx, md5_slice=B, join_lag=lag)
     # every batch slot, chain table and summary buffer of the pipeline is
     # allocated now: an allocation inside the timed region would drain the streams

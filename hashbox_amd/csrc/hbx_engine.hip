@@ -134,6 +134,8 @@ struct Batch {
   std::vector<uint64_t> out_base, capv;
   uint32_t need = 1, done = 0;  // K3 launches its chains need / have had
   bool joined = false;          // its chains are in the carried order lists (a plan took them)
+  bool ev3 = false;             // ev[3] recorded (synchronous batches only)
+  uint64_t final_launch = 0;    // index of the K3 launch after which it was finalized
   bool finalized = false;
   // a VerifyBlock batch (hbx_verify_submit_device) instead of files
   bool verify = false;
@@ -153,13 +155,14 @@ struct Batch {
 
 }  // namespace
 
+constexpr uint32_t kK3TimeRing = 4096;  // hbx_ctx::h_k3t slots (2 x u64 each)
+
 struct hbx_ctx {
   int device = 0;
   hipStream_t stream = nullptr;   // scan stream: input copies, K1, K2 (and hbx_block_id)
   hipStream_t cstream = nullptr;  // cut stream: K2 (after its batch's K1 on the scan stream)
   hipStream_t hstream = nullptr;  // hash stream: chain plan, K3
   hipStream_t rstream = nullptr;  // result stream: K4 + result D2H of batches whose chains are done
-  hipEvent_t k3_done = nullptr;   // recorded on the hash stream after a K3 launch that completes batches
   hipEvent_t producer = nullptr;  // hbx_after_stream: the caller's stream, waited for on the scan stream
   std::mutex mu;
   std::string err;
@@ -191,6 +194,17 @@ struct hbx_ctx {
   uint32_t k1_gate = 1;
   DevBuf d_gate;
   uint32_t k3_dispatched = 0;
+  // K3 launch times measured on the device (no timing events on the hash
+  // stream, which carries only K3 and its completion event): K3's first
+  // workgroup and its last wave stamp s_memrealtime into slot (launch %
+  // kK3TimeRing) of this pinned ring; tickets from d_gate[0] (workgroups
+  // started) and d_gate[1] (waves ended).  Harvested once a launch is known
+  // complete (k3_done_upto: launches [0, k3_done_upto) are).
+  PinBuf h_k3t;
+  PinBuf h_probe;  // HBX_K3_PROBE: per-wave times of the latest K3 launch (hbx_k3_wave_times)
+  uint32_t k3_waves = 0;
+  std::deque<uint64_t> k3_open;
+  uint64_t k3_done_upto = 0;
   float stage_ms[5] = {0, 0, 0, 0, 0};
 
   // host-side plan scratch
@@ -332,6 +346,19 @@ void harvest_timings(hbx_ctx* c) {
 }
 
 
+// Add the device-measured K3 launches known complete to the totals.
+void harvest_k3(hbx_ctx* c) {
+  while (!c->k3_open.empty() && c->k3_open.front() < c->k3_done_upto) {
+    const volatile uint64_t* t = c->h_k3t.as<uint64_t>() + 2 * (c->k3_open.front() % kK3TimeRing);
+    const uint64_t a = t[0], e = t[1];
+    if (a && e >= a) {
+      c->tot_ms[3] += (double)(e - a) * 1e-5;  // s_memrealtime: 100 MHz
+      c->tot_n[3] += 1;
+    }
+    c->k3_open.pop_front();
+  }
+}
+
 Batch* acquire_batch(hbx_ctx* c) {
   Batch* b;
   if (!c->pool.empty()) {
@@ -352,6 +379,8 @@ Batch* acquire_batch(hbx_ctx* c) {
   b->done = 0;
   b->rl = ResLayout{};  // a verify batch keeps its ids at offset 0 of d_res
   b->joined = false;
+  b->ev3 = false;
+  b->final_launch = 0;
   b->finalized = false;
   b->cut_ends = nullptr;
   b->ids = nullptr;
@@ -365,7 +394,7 @@ Batch* acquire_batch(hbx_ctx* c) {
 }
 
 // K4 + D2H of one batch whose chains are all hashed, on the result stream
-// (after c->k3_done), so the hash stream goes straight on with the next plan
+// (after the finalizing K3's completion event), so the hash stream goes straight on with the next plan
 // and K3 launch.
 int finalize_batch(hbx_ctx* c, Batch* b) {
   hipStream_t s = c->rstream;
@@ -477,29 +506,48 @@ int md5_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
   hipStream_t s = c->hstream;
   const int slot = (int)(c->launches % 3);
   if (s != plan_stream(c)) HBX_TRY(c, hipStreamWaitEvent(s, c->plan_done[slot], 0));
-  {
-    StageTimer t(c, s, 3);
-    hipLaunchKernelGGL(hbx_k3_block_md5, dim3(c->md5_wgs), dim3(kK3Threads), 0, s,
-                       c->d_order[slot].as<OrderEntry>(), static_cast<const uint32_t*>(c->d_octl[slot].as<uint32_t>()),
-                       budget, c->k3_dense, c->d_gate.as<uint32_t>());
+  // the device-timing slot of this launch (its previous user, kK3TimeRing
+  // launches back, must have been harvested)
+  const uint64_t L = c->launches;
+  if (!c->k3_open.empty() && c->k3_open.front() + kK3TimeRing <= L) {
+    HBX_TRY(c, hipStreamSynchronize(s));
+    c->k3_done_upto = L;
+    harvest_k3(c);
   }
+  uint64_t* tslot = nullptr;
+  if (c->h_k3t.p) {
+    tslot = c->h_k3t.as<uint64_t>() + 2 * (L % kK3TimeRing);
+    tslot[0] = tslot[1] = 0;
+    c->k3_open.push_back(L);
+  }
+  const uint32_t waves = c->md5_wgs * (kK3Threads / 64);
+  hipLaunchKernelGGL(hbx_k3_block_md5, dim3(c->md5_wgs), dim3(kK3Threads), 0, s,
+                     c->d_order[slot].as<OrderEntry>(), static_cast<const uint32_t*>(c->d_octl[slot].as<uint32_t>()),
+                     budget, c->k3_dense, c->d_gate.as<uint32_t>(), c->k3_dispatched, c->k3_waves + waves - 1u, tslot,
+                     c->h_probe.p ? c->h_probe.as<uint64_t>() : nullptr);
   HBX_TRY(c, hipGetLastError());
   c->k3_dispatched += c->md5_wgs;
+  c->k3_waves += waves;
   c->last_budget = budget;  // what the next plan advances this list by
+  // the launch's one completion event: the plan three launches on waits for
+  // it, and so does the result stream for the batches it completes
   HBX_TRY(c, hipEventRecord(c->order_free[slot], s));
   c->order_used[slot] = true;
   c->launches++;
-  if (nb) HBX_TRY(c, hipEventRecord(nb->ev[3], s));
+  if (nb && budget == kBudgetAll) {  // per-batch stage times of a synchronous batch (hbx_stage_times)
+    HBX_TRY(c, hipEventRecord(nb->ev[3], s));
+    nb->ev3 = true;
+  }
   bool forked = false;
   for (Batch* b : c->pending) {
     if (b->finalized || !b->joined) continue;
     b->done++;
     if (budget == kBudgetAll || b->done >= b->need) {
       if (!forked && c->rstream != s) {  // the result stream picks up after this K3
-        HBX_TRY(c, hipEventRecord(c->k3_done, s));
-        HBX_TRY(c, hipStreamWaitEvent(c->rstream, c->k3_done, 0));
+        HBX_TRY(c, hipStreamWaitEvent(c->rstream, c->order_free[slot], 0));
         forked = true;
       }
+      b->final_launch = L;
       int rc = finalize_batch(c, b);
       if (rc) return rc;
     }
@@ -902,7 +950,9 @@ int collect_batch(hbx_ctx* c, Batch* b) {
   float ms = 0.f;
   for (int i = 0; i < 4; i++) {
     c->stage_ms[i] = 0.f;
-    if (hipEventElapsedTime(&ms, b->ev[i], b->ev[i + 1]) == hipSuccess) c->stage_ms[i] = ms;
+    // a pipelined batch has no ev[3]: [2] then spans K2 end -> results ready
+    const int e = (i == 2 && !b->ev3) ? 4 : i + 1;
+    if ((i != 3 || b->ev3) && hipEventElapsedTime(&ms, b->ev[i], b->ev[e]) == hipSuccess) c->stage_ms[i] = ms;
   }
   if (hipEventElapsedTime(&ms, b->ev[0], b->ev[4]) == hipSuccess) c->stage_ms[4] = ms;
   return rc;
@@ -928,9 +978,12 @@ int wait_oldest(hbx_ctx* c) {
   }
   HBX_TRY(c, hipEventSynchronize(b->ev[4]));
   c->pending.pop_front();
+  // ev[4] follows the K3 launch that finalized b (the result stream waited for it)
+  if (b->joined) c->k3_done_upto = std::max<uint64_t>(c->k3_done_upto, b->final_launch + 1);
   int rc = collect_batch(c, b);
   c->pool.push_back(b);
   harvest_timings(c);
+  harvest_k3(c);
   return rc;
 }
 
@@ -1022,8 +1075,11 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
     hbx_ctx_destroy(c);
     return HBX_ERR_HIP;
   }
+  if (c->h_k3t.ensure(kK3TimeRing * 16) == hipSuccess) std::memset(c->h_k3t.p, 0, kK3TimeRing * 16);
+  if (const char* v = std::getenv("HBX_K3_PROBE"))
+    if (std::atoi(v) && c->h_probe.ensure((size_t)c->md5_wgs * (kK3Threads / 64) * 32) == hipSuccess)
+      std::memset(c->h_probe.p, 0, (size_t)c->md5_wgs * (kK3Threads / 64) * 32);
   if (c->d_gate.ensure(256) != hipSuccess || hipMemset(c->d_gate.p, 0, 256) != hipSuccess ||
-      hipEventCreateWithFlags(&c->k3_done, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ssum_free[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ssum_free[1], hipEventDisableTiming) != hipSuccess) {
     hbx_ctx_destroy(c);
@@ -1045,7 +1101,7 @@ void hbx_ctx_destroy(hbx_ctx* c) {
   (void)hipSetDevice(c->device);
   for (hipStream_t s : {c->stream, c->cstream, c->hstream, c->rstream})
     if (s) (void)hipStreamSynchronize(s);
-  for (hipEvent_t e : {c->k3_done, c->producer, c->ssum_free[0], c->ssum_free[1], c->plan_done[0], c->plan_done[1],
+  for (hipEvent_t e : {c->producer, c->ssum_free[0], c->ssum_free[1], c->plan_done[0], c->plan_done[1],
                        c->plan_done[2], c->order_free[0], c->order_free[1], c->order_free[2]})
     if (e) (void)hipEventDestroy(e);
   for (DevBuf* b : {&c->d_ssum[0], &c->d_ssum[1], &c->d_order[0], &c->d_order[1], &c->d_order[2],
@@ -1056,6 +1112,8 @@ void hbx_ctx_destroy(hbx_ctx* c) {
     b->release();
   for (PinBuf& h : c->h_read) h.release();
   c->h_zstage.release();
+  c->h_k3t.release();
+  c->h_probe.release();
   for (DevBuf& d : c->d_ring) d.release();
   for (hipEvent_t e : c->h2d_done)
     if (e) (void)hipEventDestroy(e);
@@ -1093,6 +1151,19 @@ int hbx_set_join_lag(hbx_ctx* c, uint32_t lag) {
   HBX_TRY(c, hipSetDevice(c->device));
   c->join_lag = lag;
   return ensure_cut_stream(c);
+}
+
+int hbx_k3_wave_times(hbx_ctx* c, uint64_t* out, uint32_t max_waves, uint32_t* n_waves) {
+  if (!c || !n_waves) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  *n_waves = 0;
+  if (!c->h_probe.p) return c->fail(HBX_ERR_STATE, "K3 probe not enabled (HBX_K3_PROBE=1 at context creation)");
+  HBX_TRY(c, hipSetDevice(c->device));
+  HBX_TRY(c, hipStreamSynchronize(c->hstream));
+  const uint32_t n = c->md5_wgs * (kK3Threads / 64);
+  if (out) std::memcpy(out, c->h_probe.p, (size_t)std::min(n, max_waves) * 32);
+  *n_waves = n;
+  return HBX_OK;
 }
 
 int hbx_stage_times(hbx_ctx* c, float ms[5]) {
@@ -1151,6 +1222,8 @@ int hbx_stage_totals(hbx_ctx* c, double ms[5], uint64_t launches[5], int reset) 
   if (!c) return HBX_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   harvest_timings(c);
+  if (c->hstream && hipStreamQuery(c->hstream) == hipSuccess) c->k3_done_upto = c->launches;
+  harvest_k3(c);
   for (int i = 0; i < 5; i++) {
     if (ms) ms[i] = c->tot_ms[i];
     if (launches) launches[i] = c->tot_n[i];

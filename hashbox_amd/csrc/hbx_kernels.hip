@@ -1192,13 +1192,20 @@ constexpr int kK3Threads = HBX_K3_THREADS;
 
 extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
     const OrderEntry* __restrict__ order, const uint32_t* __restrict__ n_order, uint32_t budget,
-    uint32_t dense, uint32_t* __restrict__ started) {
+    uint32_t dense, uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last,
+    uint64_t* __restrict__ tslot, uint64_t* __restrict__ probe) {
   // the MD5 chains are issue-bound: win the SIMD's issue arbitration against
   // co-resident waves of other kernels
   __builtin_amdgcn_s_setprio(3);
   // dispatch counter for the next batch's K1 gate (hbx_k1_gate): one vector
-  // atomic per workgroup as it starts
-  if (started && threadIdx.x == 0) __hip_atomic_fetch_add(started, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  // atomic per workgroup as it starts.  Its ticket also times the launch: the
+  // workgroup that draws t_first (the launch's first) stamps the start, the
+  // wave that draws t_last on started[1] (the launch's last) the end, into
+  // tslot (pinned host memory; hbx_engine harvest_k3)
+  if (started && threadIdx.x == 0) {
+    const uint32_t tk = __hip_atomic_fetch_add(started, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (tslot && tk == t_first) tslot[0] = __builtin_amdgcn_s_memrealtime();
+  }
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t n_total = *n_order;
@@ -1218,6 +1225,11 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
   // short waves on every CU: K3 3.52 -> 3.41 ms but K1 3.25 -> 3.54 ms beside
   // it, 2,235 -> 2,091 GiB/s at 33 resident batches.)
   const uint32_t g0 = dense ? blockIdx.x * (kK3Threads / 64) + wave : wave * gridDim.x + blockIdx.x;
+  // diagnostics (HBX_K3_PROBE): per wave its start, the end of its first
+  // group's start-up (loads + prologue), its end, R and the largest count
+  const uint64_t pt0 = probe ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  uint64_t pt1 = 0ull;
+  uint32_t pR = 0u, pmax = 0u;
   for (uint32_t g = g0; g < groups; g += nwaves) {
     const uint32_t k = 64u * g + lane;
     const bool active = k < n_total;
@@ -1238,6 +1250,11 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
     const uint32_t R = ~wave_max_all(active ? ~cnt : 0u);
     if (R >= kCoopMinBudget) {  // wave-uniform
       md5_block_at(src, ch.len, h, ch.next);  // every lane now at a block >= 1
+      if (probe && g == g0) {
+        pt1 = __builtin_amdgcn_s_memrealtime();
+        pR = R;
+        pmax = wave_max_all(cnt);
+      }
       md5_coop(k3_lds[wave], src, h, ch.next + 1u, R - 1u);
       md5_run(src, len, h, b0 + R, active ? cnt - R : 0u, finish);
     } else {
@@ -1253,6 +1270,17 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
       *reinterpret_cast<uint4*>(&chp->h[0]) = make_uint4(h[0], h[1], h[2], h[3]);
       chp->next = b0 + cnt;
     }
+  }
+  if (probe && (threadIdx.x & 63u) == 0u) {
+    uint64_t* p = probe + 4u * (blockIdx.x * (kK3Threads / 64) + wave);
+    p[0] = pt0;
+    p[1] = pt1;
+    p[2] = __builtin_amdgcn_s_memrealtime();
+    p[3] = (uint64_t)pR | ((uint64_t)pmax << 32);
+  }
+  if (started && tslot && (threadIdx.x & 63u) == 0u) {
+    const uint32_t tk = __hip_atomic_fetch_add(started + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (tk == t_last) tslot[1] = __builtin_amdgcn_s_memrealtime();
   }
 }
 

@@ -256,6 +256,16 @@ class Engine:
         (1..4; 2 gives a small batch's scan a whole extra step)."""
         self._check(self._L.hbx_set_join_lag(self._ctx, int(lag)), "hbx_set_join_lag")
 
+    def k3_wave_times(self) -> np.ndarray:
+        """Diagnostics (HBX_K3_PROBE=1 at creation): per-wave records of the
+        latest K3 launch, shape (waves, 4): start, start-up end, end (100 MHz
+        ticks), R | max count << 32."""
+        n = ctypes.c_uint32(0)
+        self._check(self._L.hbx_k3_wave_times(self._ctx, None, 0, ctypes.byref(n)), "hbx_k3_wave_times")
+        out = np.zeros((max(n.value, 1), 4), np.uint64)
+        self._check(self._L.hbx_k3_wave_times(self._ctx, _p(out), n.value, ctypes.byref(n)), "hbx_k3_wave_times")
+        return out[:n.value]
+
     def reserve(self, batches: int, files: int, nbytes: int):
         """Pre-size the pipeline for ``batches`` batches in flight of up to
         ``files`` files / ``nbytes`` bytes each, so the steady state never

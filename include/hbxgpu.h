@@ -26,7 +26,8 @@
  *   hbx_directory_block_* and storeDir's block id (store.go:201-234)
  *   hbx_deflate_blocks    HashboxBlock.CompressData, zlib (block.go:133-184)
  *   hbx_inflate_blocks_device  UncompressData (block.go:113-131), on the device
- *   hbx_wire_*            allo/READ/writ/ACKN framing (pkg/core/protocol.go)
+ *   hbx_wire_*            ProtocolMessage framing of every message type
+ *                         (pkg/core/protocol.go:184-264), block-store encoders
  *
  * Conventions
  *   - Every function returns an int status: 0 = OK, negative = error
@@ -39,7 +40,7 @@
  *     where the device arena and the output arrays must stay valid (use
  *     hbx_alloc_pinned memory from cgo: cgo forbids C from retaining Go
  *     pointers).
- *   - One context = one GPU + one HIP stream.  Calls on one context are
+ *   - One context = one GPU and its own HIP streams.  Calls on one context are
  *     serialised by an internal lock; use one context per GPU (or per
  *     goroutine) to run in parallel.
  *   - Block IDs are 16 raw MD5 bytes, exactly Go's core.Byte128 (core.go:26).
@@ -47,9 +48,10 @@
  *     starts at cut_ends[i-1] (0 for i = 0).
  *   - Capacity: every chunk except the last is >= 64 KiB, so a file of len
  *     bytes has at most hbx_max_chunks(len) = len/65536 + 1 chunks.
- *   - Device inputs must be complete when the call is made: the library's
- *     HIP streams are non-blocking and do not wait for the caller's streams
- *     (synchronize the producing stream first).
+ *   - Device inputs must be complete when the engine reads them: its HIP
+ *     streams do not wait for the caller's streams.  Synchronize the producing
+ *     stream first, or call hbx_after_stream(ctx, stream) before the submit
+ *     (a GPU-side wait; the host does not block).
  */
 #ifndef HBXGPU_H
 #define HBXGPU_H
@@ -414,15 +416,24 @@ int hbx_alloc_pinned(uint64_t bytes, void **out);
 int hbx_free_pinned(void *p);
 
 /* Device time (ms) of the last completed batch per stage:
- * [0] K1 window-digest scan, [1] K2 cut chain, [2] chain plan + first K3
- * launch, [3] later K3 launches + K4 content id, [4] whole batch on the
- * stream.  For a synchronous call [2] is all of K3 and [3] is K4. */
+ * [0] K1 window-digest scan, [1] K2 cut chain, [2] K2 end -> results ready
+ * (the batch's share of the pipelined MD5 launches, K4 and the copy),
+ * [3] 0, [4] whole batch.  For a synchronous call [2] is the plan and K3
+ * and [3] is K4 + the result copy. */
 int hbx_stage_times(hbx_ctx *ctx, float ms[5]);
 /* Cumulative device time (ms) and launch count per kernel since the context
- * was created (or last reset), for completed launches:
+ * was created (or last reset), for completed launches (K3 launches are timed
+ * on the device and counted once known complete: after the wait that
+ * collects a batch they finished, or once the hash stream is idle):
  * [0] K1 scan, [1] K2 cut chain, [2] K2c chain plan, [3] K3 block MD5,
  * [4] K4 content id.  reset != 0 zeroes the totals after reading. */
 int hbx_stage_totals(hbx_ctx *ctx, double ms[5], uint64_t launches[5], int reset);
+/* Diagnostics: with HBX_K3_PROBE=1 in the environment at context creation,
+ * every K3 launch records per wave {start, end of its start-up (first
+ * group's loads and prologue block), end, R | max count << 32} (s_memrealtime
+ * ticks, 100 MHz).  Copies the latest launch's records (4 x u64 per wave, up
+ * to max_waves) after the hash stream drains; *n_waves = waves per launch. */
+int hbx_k3_wave_times(hbx_ctx *ctx, uint64_t *out, uint32_t max_waves, uint32_t *n_waves);
 /* Tile length of K1 in 64 KiB iterations, 1..1024; 0 (the default) sizes
  * tiles per batch: about two per CU, 16..256 iterations (1-16 MiB). */
 int hbx_set_tile_iters(hbx_ctx *ctx, uint32_t iters);

@@ -36,6 +36,7 @@ int main(int argc, char **argv) {
     if (rc_dev != HBX_ERR_NODEV || nd != 0 || rc_ctx != HBX_ERR_NODEV || ctx) return 3;
     if (hbx_chunk_hash(NULL, NULL, 0, NULL, NULL, 0, NULL) != HBX_ERR_ARG) return 4;
     if (hbx_max_chunks(131072) != 3) return 5;
+    if (hbx_set_join_lag(NULL, 1) != HBX_ERR_ARG) return 6;
     printf("nodev ok\n");
     return 0;
   }
@@ -84,11 +85,14 @@ int main(int argc, char **argv) {
   meta[1] = n;
   meta[2] = 0;
   uint64_t capv = cap;
+  /* a join lag of 3 (the bench's small-batch setting): the wait's drain joins the batch */
+  if ((rc = hbx_set_join_lag(ctx, 3)) != HBX_OK) return fail("hbx_set_join_lag", rc, ctx);
   if ((rc = hbx_submit_device(ctx, arena, 1, &meta[0], &meta[1], acuts, aids, &meta[2], &capv, sum)) != HBX_OK)
     return fail("hbx_submit_device", rc, ctx);
   if (hbx_pending(ctx) != 1) return fail("hbx_pending", hbx_pending(ctx), ctx);
   /* the slice is fixed while a batch is pending */
   if (hbx_set_md5_slice(ctx, 7) != HBX_ERR_STATE) return fail("hbx_set_md5_slice while pending", 0, ctx);
+  if (hbx_set_join_lag(ctx, 1) != HBX_ERR_STATE) return fail("hbx_set_join_lag while pending", 0, ctx);
   if ((rc = hbx_wait(ctx)) != HBX_OK) return fail("hbx_wait", rc, ctx);
   if (sum->n_chunks != k) return fail("async chunk count", (int)sum->n_chunks, ctx);
   for (uint64_t i = 0; i < k; i++) {
