@@ -270,19 +270,33 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
 
 def k3_probe_stats(w):
     """Summary of one K3 launch's per-wave records (engine.k3_wave_times), µs."""
+    w = w.astype(np.int64)
     busy = w[w[:, 1] != 0]
     if not len(busy):
         return None
     t0 = int(w[w[:, 0] != 0][:, 0].min())
     us = lambda x: np.round(np.asarray(x, np.float64) * 0.01, 1)  # noqa: E731  100 MHz ticks
-    start = us(busy[:, 0].astype(np.int64) - t0)
-    setup = us(busy[:, 1].astype(np.int64) - busy[:, 0].astype(np.int64))
-    end = us(busy[:, 2].astype(np.int64) - t0)
-    R = (busy[:, 3] & 0xffffffff).astype(np.int64)
+    low56 = (1 << 56) - 1
+    start = us(busy[:, 0] - t0)
+    setup = us((busy[:, 1] & low56) - busy[:, 0])
+    end = us(busy[:, 2] - t0)
+    R = busy[:, 3] & 0xffff
+    xcc = busy[:, 1] >> 56
+    hw = busy[:, 3] >> 32
+    simd, cu, se = (hw >> 4) & 3, (hw >> 8) & 0xf, (hw >> 13) & 3
     q = lambda a: [float(np.min(a)), float(np.median(a)), float(np.max(a))]  # noqa: E731
-    return {"busy_waves": int(len(busy)), "span_us": float(us(int(w[:, 2].max()) - t0)),
-            "start_us_min_med_max": q(start), "startup_us_min_med_max": q(setup), "end_us_min_med_max": q(end),
-            "R_min_med_max": q(R)}
+    full = R == R.max()
+    out = {"busy_waves": int(len(busy)), "span_us": float(us(int(w[:, 2].max()) - t0)),
+           "start_us_min_med_max": q(start), "startup_us_min_med_max": q(setup), "end_us_min_med_max": q(end),
+           "R_min_med_max": q(R), "full_slice_waves": int(full.sum()),
+           "full_slice_end_us_min_med_max": q(end[full]) if full.any() else None}
+    for name, key in (("xcc", xcc), ("se", se), ("simd", simd)):
+        out[f"full_end_us_by_{name}"] = {int(k): q(end[full & (key == k)]) for k in np.unique(key[full])}
+    # slowest full-slice waves: where they ran
+    order = np.argsort(-end)
+    out["slowest10"] = [{"end_us": float(end[i]), "xcc": int(xcc[i]), "se": int(se[i]), "cu": int(cu[i]),
+                         "simd": int(simd[i]), "R": int(R[i])} for i in order[:10]]
+    return out
 
 
 def max_over_ranks(x, dist, dev, op="max"):

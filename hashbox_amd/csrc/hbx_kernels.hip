@@ -1256,7 +1256,33 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
         pmax = wave_max_all(cnt);
       }
       md5_coop(k3_lds[wave], src, h, ch.next + 1u, R - 1u);
-      md5_run(src, len, h, b0 + R, active ? cnt - R : 0u, finish);
+      // A group that straddles two order bins mixes counts (e.g. 4,229 and
+      // 4,093 blocks): the lanes still holding blocks go on cooperatively
+      // while the others shadow the first of them and discard (the lane-mode
+      // path would take ~1.5x per block, and such a wave was the launch's
+      // last by 120 us: bench --k3-probe).
+      uint32_t pos = b0 + R, rem = active ? cnt - R : 0u;
+      for (int round = 0; round < 4; round++) {
+        const uint32_t mx = wave_max_all(rem ? ~rem : 0u);
+        if (mx == 0u || ~mx < kCoopMinBudget) break;  // wave-uniform
+        const uint32_t R2 = ~mx;
+        const bool part = rem != 0u;
+        const int L = __builtin_ctzll(__builtin_amdgcn_ballot_w64(part));
+        const uint64_t s_sh = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(reinterpret_cast<uint64_t>(src) >> 32), L) << 32) |
+                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)reinterpret_cast<uint64_t>(src), L);
+        const uint32_t p_sh = (uint32_t)__builtin_amdgcn_readlane((int)pos, L);
+        uint32_t hk[4] = {h[0], h[1], h[2], h[3]};
+        md5_coop(k3_lds[wave], part ? src : reinterpret_cast<const uint8_t*>(s_sh), hk, part ? pos : p_sh, R2);
+        if (part) {
+          h[0] = hk[0];
+          h[1] = hk[1];
+          h[2] = hk[2];
+          h[3] = hk[3];
+          pos += R2;
+          rem -= R2;
+        }
+      }
+      md5_run(src, len, h, pos, rem, finish);
     } else {
       md5_run(src, len, h, b0, cnt, finish);
     }
@@ -1273,10 +1299,13 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
   }
   if (probe && (threadIdx.x & 63u) == 0u) {
     uint64_t* p = probe + 4u * (blockIdx.x * (kK3Threads / 64) + wave);
+    // hardware placement: HW_ID (wave, SIMD, CU, SH, SE) and XCC_ID
+    const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+    const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11)) & 0xfu;
     p[0] = pt0;
-    p[1] = pt1;
+    p[1] = pt1 | ((uint64_t)xcc << 56);
     p[2] = __builtin_amdgcn_s_memrealtime();
-    p[3] = (uint64_t)pR | ((uint64_t)pmax << 32);
+    p[3] = (uint64_t)min(pR, 0xffffu) | ((uint64_t)min(pmax, 0xffffu) << 16) | ((uint64_t)hw << 32);
   }
   if (started && tslot && (threadIdx.x & 63u) == 0u) {
     const uint32_t tk = __hip_atomic_fetch_add(started + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);

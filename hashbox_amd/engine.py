@@ -258,8 +258,8 @@ class Engine:
 
     def k3_wave_times(self) -> np.ndarray:
         """Diagnostics (HBX_K3_PROBE=1 at creation): per-wave records of the
-        latest K3 launch, shape (waves, 4): start, start-up end, end (100 MHz
-        ticks), R | max count << 32."""
+        latest K3 launch, shape (waves, 4): start, start-up end | XCC << 56,
+        end (100 MHz ticks), R | max count << 16 | HW_ID << 32."""
         n = ctypes.c_uint32(0)
         self._check(self._L.hbx_k3_wave_times(self._ctx, None, 0, ctypes.byref(n)), "hbx_k3_wave_times")
         out = np.zeros((max(n.value, 1), 4), np.uint64)

@@ -430,8 +430,9 @@ int hbx_stage_times(hbx_ctx *ctx, float ms[5]);
 int hbx_stage_totals(hbx_ctx *ctx, double ms[5], uint64_t launches[5], int reset);
 /* Diagnostics: with HBX_K3_PROBE=1 in the environment at context creation,
  * every K3 launch records per wave {start, end of its start-up (first
- * group's loads and prologue block), end, R | max count << 32} (s_memrealtime
- * ticks, 100 MHz).  Copies the latest launch's records (4 x u64 per wave, up
+ * group's loads and prologue block) | XCC id << 56, end, R | max count << 16
+ * | HW_ID << 32} (times in s_memrealtime ticks, 100 MHz; R and the count
+ * saturate at 65535).  Copies the latest launch's records (4 x u64 per wave, up
  * to max_waves) after the hash stream drains; *n_waves = waves per launch. */
 int hbx_k3_wave_times(hbx_ctx *ctx, uint64_t *out, uint32_t max_waves, uint32_t *n_waves);
 /* Tile length of K1 in 64 KiB iterations, 1..1024; 0 (the default) sizes
