@@ -271,7 +271,7 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
 def k3_probe_stats(w):
     """Summary of one K3 launch's per-wave records (engine.k3_wave_times), µs."""
     w = w.astype(np.int64)
-    busy = w[w[:, 1] != 0]
+    busy = w[(w[:, 1] & ((1 << 56) - 1)) != 0]  # waves that ran a group (start-up stamped)
     if not len(busy):
         return None
     t0 = int(w[w[:, 0] != 0][:, 0].min())
