@@ -2042,9 +2042,9 @@ int hbx_inflate_blocks_device(hbx_ctx* c, const void* d_in, uint64_t n, const ui
   std::lock_guard<std::mutex> g(c->mu);
   if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
   if (n == 0) return HBX_OK;
-  if (n > 0xFFFFFFFFull) return c->fail(HBX_ERR_ARG, "too many streams");
+  if (n > 0x7FFFFFFFull) return c->fail(HBX_ERR_ARG, "too many streams");
   HBX_TRY(c, hipSetDevice(c->device));
-  // longest stream first: a wave's 64 lanes then decode about equally long streams
+  // one wave per stream, longest first (the long ones start first)
   std::vector<uint32_t> perm(n);
   for (uint64_t i = 0; i < n; i++) {
     if (in_lens[i] > 0xFFFFFFFFull || out_caps[i] > 0xFFFFFFFFull) return c->fail(HBX_ERR_ARG, "stream too large");
@@ -2064,8 +2064,22 @@ int hbx_inflate_blocks_device(hbx_ctx* c, const void* d_in, uint64_t n, const ui
   HBX_TRY(c, c->d_ires.ensure(n * 8));
   HBX_TRY(c, hipMemcpyAsync(c->d_idesc.p, desc.data(), n * sizeof(InflateDesc), hipMemcpyHostToDevice, s));
   uint32_t* dres = c->d_ires.as<uint32_t>();
-  hipLaunchKernelGGL(hbx_k8_inflate, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, s, c->d_idesc.as<InflateDesc>(),
-                     (uint32_t)n, dres, dres + n);
+  // a wave per stream, except for tens of thousands of short compressible
+  // streams, where 64 streams per wave (one per lane) keep more streams in
+  // flight (hbx_inflate.hip); HBX_K8_MODE=lane|wave forces one (tests)
+  uint64_t tin = 0, tcap = 0;
+  for (uint64_t k = 0; k < n; k++) {
+    tin += desc[k].len;
+    tcap += desc[k].cap;
+  }
+  bool lanes = n >= 8192 && tin * 10 < tcap * 7 && tcap / n <= (256u << 10);
+  if (const char* m = std::getenv("HBX_K8_MODE")) lanes = std::strcmp(m, "lane") == 0;
+  if (lanes)
+    hipLaunchKernelGGL(hbx_k8_inflate_lanes, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, s,
+                       c->d_idesc.as<InflateDesc>(), (uint32_t)n, dres, dres + n);
+  else
+    hipLaunchKernelGGL(hbx_k8_inflate, dim3((uint32_t)n), dim3(64), 0, s, c->d_idesc.as<InflateDesc>(),
+                       (uint32_t)n, dres, dres + n);
   HBX_TRY(c, hipGetLastError());
   std::vector<uint32_t> res(2 * n);
   HBX_TRY(c, hipMemcpyAsync(res.data(), dres, n * 8, hipMemcpyDeviceToHost, s));

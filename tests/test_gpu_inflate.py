@@ -14,6 +14,14 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["wave", "lane"])
+def k8_mode(request, monkeypatch):
+    """Both decoders: a wave per stream (the default) and a lane per stream
+    (picked for tens of thousands of short compressible streams)."""
+    monkeypatch.setenv("HBX_K8_MODE", request.param)
+    return request.param
+
+
 def _text(n, seed):
     rng = np.random.default_rng(seed)
     words = [bytes(rng.integers(97, 123, int(k), dtype=np.uint8)) for k in rng.integers(2, 10, 300)]
