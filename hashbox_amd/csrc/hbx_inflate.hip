@@ -191,6 +191,69 @@ __device__ __forceinline__ int wave_decode(WaveBits& br, const Code& c, const ui
   return -1;
 }
 
+// The same reader run by the whole wave in lockstep on uniform (scalar)
+// values: every LDS value it reads is made uniform with readfirstlane, so
+// its state lives in SGPRs and its branches are scalar (no exec-mask
+// bookkeeping, which dominated the lane-0 loop: PMC ~50 SALU per token).
+__device__ __forceinline__ uint32_t ufirst(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t ufirst64(uint64_t v) {
+  return ((uint64_t)ufirst((uint32_t)(v >> 32)) << 32) | ufirst((uint32_t)v);
+}
+
+struct UBits {
+  uint64_t buf;
+  uint32_t n;
+  uint32_t p;  // next stream byte to load (streams are < 4 GiB)
+  __device__ __forceinline__ void fill(const uint8_t* in, uint32_t base, uint32_t len) {
+    if (n > 56u) return;
+    const uint32_t q = p - base;
+    uint64_t v = 0ull;
+    if (q <= kInBuf) {  // (see WaveBits::fill)
+      const uint64_t* w = reinterpret_cast<const uint64_t*>(in + (q & ~7u));
+      const uint32_t sh = (q & 7u) * 8u;
+      const uint64_t w0 = ufirst64(w[0]), w1 = ufirst64(w[1]);
+      v = sh ? (w0 >> sh) | (w1 << (64u - sh)) : w0;
+    }
+    if (p + 8u > len) {
+      const uint32_t keep = len > p ? len - p : 0u;
+      v &= keep ? (~0ull >> (64u - 8u * keep)) : 0ull;
+    }
+    const uint32_t take = (64u - n) >> 3;
+    buf |= v << n;
+    p += take;
+    n += 8u * take;
+  }
+  __device__ __forceinline__ uint32_t get(uint32_t k, const uint8_t* in, uint32_t base, uint32_t len) {
+    if (n < k) fill(in, base, len);
+    const uint32_t v = (uint32_t)(buf & ((1ull << k) - 1ull));
+    buf >>= k;
+    n -= k;
+    return v;
+  }
+};
+
+__device__ __forceinline__ int u_decode(UBits& br, const Code& c, const uint16_t* sym, const uint16_t* lut,
+                                        const uint8_t* in, uint32_t base, uint32_t len) {
+  if (br.n < 15u) br.fill(in, base, len);
+  const uint32_t e = ufirst(lut[br.buf & ((1u << kLutBits) - 1u)]);
+  if (e) {
+    const uint32_t l = e & 15u;
+    br.buf >>= l;
+    br.n -= l;
+    return (int)(e >> 4);
+  }
+  const uint32_t peek = __builtin_bitreverse32((uint32_t)br.buf) >> 17;
+  for (uint32_t l = kLutBits + 1; l <= 15u; l++) {
+    const uint32_t prefix = peek >> (15u - l);
+    if (prefix < ufirst(c.limit[l])) {
+      br.buf >>= l;
+      br.n -= l;
+      return (int)ufirst(sym[(int)prefix + (int16_t)ufirst((uint32_t)(uint16_t)c.base[l])]);
+    }
+  }
+  return -1;
+}
+
 __device__ __forceinline__ uint64_t bcast64(uint64_t v) {
   return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
@@ -249,52 +312,54 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k8_inflate(const InflateDes
   // write tokens [0, nt) (all lanes).  Tokens come off LDS 64 at a time,
   // one per lane; the wave walks them from registers (readlane / shuffle),
   // so a token costs no dependent LDS round trip of its own.
-  auto expand = [&](uint32_t nt) {
+  auto expand_chunk = [&](uint32_t mytok, uint32_t cn) {  // cn tokens, token t in lane t
+    const uint64_t litmask = __builtin_amdgcn_ballot_w64(lane < cn && (mytok >> 31) != 0u);
+    uint32_t t = 0;
+    while (t < cn) {
+      if ((litmask >> t) & 1ull) {  // a run of literals, one per lane
+        const uint64_t rest = ~(litmask >> t);
+        const uint32_t run = min(rest ? (uint32_t)__builtin_ctzll(rest) : 64u - t, cn - t);
+        const uint32_t b = (uint32_t)__shfl((int)mytok, (int)(t + lane), 64) & 0xFFu;
+        if (lane < run) put(o + lane, b);
+        o += run;
+        t += run;
+        step_done();
+        continue;
+      }
+      const uint32_t tk = (uint32_t)__builtin_amdgcn_readlane((int)mytok, (int)t);
+      const uint32_t L = tk >> 16, D = tk & 0xFFFFu ? tk & 0xFFFFu : 65536u;
+      if (D >= 64u) {
+        for (uint32_t j0 = 0; j0 < L; j0 += 64u) {
+          const uint32_t j = j0 + lane;
+          if (j < L) put(o + j, W.ring[(o - D + j) & (kWin - 1u)]);
+          step_done();
+        }
+      } else {  // pattern of period D: byte j = byte (j mod D) of the last D
+        const float rD = __builtin_amdgcn_rcpf((float)D);
+        auto mod_small = [&](uint32_t x) {  // x mod D for x < 2^12: a reciprocal, one correction
+          uint32_t r = x - D * (uint32_t)((float)x * rD);
+          return r >= D ? r - D : r;
+        };
+        const uint32_t m = mod_small(lane), r64 = mod_small(64u);
+        uint32_t c = 0;
+        for (uint32_t j0 = 0; j0 < L; j0 += 64u) {
+          const uint32_t j = j0 + lane;
+          uint32_t k = c + m;
+          if (k >= D) k -= D;
+          if (j < L) put(o + j, W.ring[(o - D + k) & (kWin - 1u)]);
+          c += r64;
+          if (c >= D) c -= D;
+          step_done();
+        }
+      }
+      o += L;
+      t++;
+    }
+  };
+  auto expand = [&](uint32_t nt) {  // tokens [0, nt) from W.tok
     for (uint32_t t0 = 0; t0 < nt; t0 += 64u) {
       const uint32_t cn = min(64u, nt - t0);
-      const uint32_t mytok = lane < cn ? W.tok[t0 + lane] : 0u;
-      const uint64_t litmask = __builtin_amdgcn_ballot_w64(lane < cn && (mytok >> 31) != 0u);
-      uint32_t t = 0;
-      while (t < cn) {
-        if ((litmask >> t) & 1ull) {  // a run of literals, one per lane
-          const uint64_t rest = ~(litmask >> t);
-          const uint32_t run = min(rest ? (uint32_t)__builtin_ctzll(rest) : 64u - t, cn - t);
-          const uint32_t b = (uint32_t)__shfl((int)mytok, (int)(t + lane), 64) & 0xFFu;
-          if (lane < run) put(o + lane, b);
-          o += run;
-          t += run;
-          step_done();
-          continue;
-        }
-        const uint32_t tk = (uint32_t)__builtin_amdgcn_readlane((int)mytok, (int)t);
-        const uint32_t L = tk >> 16, D = tk & 0xFFFFu ? tk & 0xFFFFu : 65536u;
-        if (D >= 64u) {
-          for (uint32_t j0 = 0; j0 < L; j0 += 64u) {
-            const uint32_t j = j0 + lane;
-            if (j < L) put(o + j, W.ring[(o - D + j) & (kWin - 1u)]);
-            step_done();
-          }
-        } else {  // pattern of period D: byte j = byte (j mod D) of the last D
-          const float rD = __builtin_amdgcn_rcpf((float)D);
-          auto mod_small = [&](uint32_t x) {  // x mod D for x < 2^12: a reciprocal, one correction
-            uint32_t r = x - D * (uint32_t)((float)x * rD);
-            return r >= D ? r - D : r;
-          };
-          const uint32_t m = mod_small(lane), r64 = mod_small(64u);
-          uint32_t c = 0;
-          for (uint32_t j0 = 0; j0 < L; j0 += 64u) {
-            const uint32_t j = j0 + lane;
-            uint32_t k = c + m;
-            if (k >= D) k -= D;
-            if (j < L) put(o + j, W.ring[(o - D + k) & (kWin - 1u)]);
-            c += r64;
-            if (c >= D) c -= D;
-            step_done();
-          }
-        }
-        o += L;
-        t++;
-      }
+      expand_chunk(lane < cn ? W.tok[t0 + lane] : 0u, cn);
     }
   };
 
@@ -419,50 +484,50 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k8_inflate(const InflateDes
       W.dlut[e] = lut_entry(W.dc, W.dsym, e);
     }
     __syncthreads();
+    // the symbols: the whole wave decodes in lockstep on uniform values, 64
+    // tokens at a time into a register (token t in lane t), then writes them
+    UBits ub{bcast64(br.buf), bcast32(br.n), (uint32_t)bcast64(br.p)};
+    const uint32_t len32 = (uint32_t)len;
     for (;;) {
-      uint32_t why = 0;
-      ntok = 0;
-      if (lane == 0) {
-        uint64_t ov = o;  // output including the tokens of this batch
-        for (;;) {
-          if (ntok >= kTok) {
-            why = kTokFull;
+      const uint32_t b32 = (uint32_t)base;
+      // past lim the next token could need bytes beyond the staged window
+      const uint32_t lim = base + kInBuf < len + 16u ? b32 + kInBuf - 16u : 0xFFFFFFFFu;
+      uint32_t toks = 0, cnt = 0, why = 0;
+      uint64_t ov = o;  // output including this chunk's tokens
+      while (cnt < 64u) {
+        if (ub.p > lim) {
+          why = kNeedInput;
+          break;
+        }
+        const int sym = u_decode(ub, W.lc, W.lsym, W.llut, W.in, b32, len32);
+        uint32_t tv;
+        if (sym < 0) {
+          st = kErrCode;
+          break;
+        }
+        if (sym < 256) {
+          if (ov >= cap) {
+            st = kErrOutput;
             break;
           }
-          if (br.p + 16u > base + kInBuf && base + kInBuf < len + 16u) {
-            why = kNeedInput;
-            break;
-          }
-          const int sym = wave_decode(br, W.lc, W.lsym, W.llut, W.in, base, len);
-          if (sym < 0) {
-            st = kErrCode;
-            break;
-          }
-          if (sym < 256) {
-            if (ov >= cap) {
-              st = kErrOutput;
-              break;
-            }
-            W.tok[ntok++] = 0x80000000u | (uint32_t)sym;
-            ov++;
-            continue;
-          }
-          if (sym == 256) {
-            why = kEndOfBlock;
-            break;
-          }
+          tv = 0x80000000u | (uint32_t)sym;
+          ov++;
+        } else if (sym == 256) {
+          why = kEndOfBlock;
+          break;
+        } else {
           const uint32_t ls = (uint32_t)sym - 257u;
           if (ls >= 29u) {
             st = kErrCode;
             break;
           }
-          const uint32_t L = len_base(ls) + br.get(len_extra(ls), W.in, base, len);
-          const int ds = wave_decode(br, W.dc, W.dsym, W.dlut, W.in, base, len);
+          const uint32_t L = len_base(ls) + ub.get(len_extra(ls), W.in, b32, len32);
+          const int ds = u_decode(ub, W.dc, W.dsym, W.dlut, W.in, b32, len32);
           if (ds < 0 || ds >= 30) {
             st = kErrCode;
             break;
           }
-          const uint32_t D = dist_base((uint32_t)ds) + br.get(dist_extra((uint32_t)ds), W.in, base, len);
+          const uint32_t D = dist_base((uint32_t)ds) + ub.get(dist_extra((uint32_t)ds), W.in, b32, len32);
           if (D > ov) {
             st = kErrDist;
             break;
@@ -471,20 +536,20 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k8_inflate(const InflateDes
             st = kErrOutput;
             break;
           }
-          W.tok[ntok++] = (L << 16) | (D & 0xFFFFu);  // D = 32768 is stored as 0x8000; never 0
+          tv = (L << 16) | (D & 0xFFFFu);  // D = 32768 is stored as 0x8000; never 0
           ov += L;
         }
+        toks = lane == cnt ? tv : toks;
+        cnt++;
       }
-      __syncthreads();
-      st = bcast32(st);
-      why = bcast32(why);
-      ntok = bcast32(ntok);
       if (st != kOk) break;
-      expand(ntok);
+      expand_chunk(toks, cnt);
       if (why == kEndOfBlock) break;
-      if (why == kNeedInput) stage(bcast64(br.p) & ~15ull);
-      __syncthreads();
+      if (why == kNeedInput) stage(ub.p & ~15u);
     }
+    br.buf = ub.buf;  // lane 0's reader takes over for the next block header
+    br.n = ub.n;
+    br.p = ub.p;
     if (st != kOk) break;
     if (lane == 0) {  // consumed past the input?
       if (8ull * br.p - br.n > 8ull * len) st = kErrInput;
