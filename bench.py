@@ -84,8 +84,10 @@ def parse():
                     help="submits between a batch's own and the K3 launch its chains join "
                          "(hbx_set_join_lag; 0 = auto: 3 below 64 files per GPU, else 1)")
     ap.add_argument("--lead", type=int, default=-1,
-                    help="launches between a batch's completion and its collection (the scan side's "
-                         "slack): R = launches per batch + lead (-1 = join lag + 1)")
+                    help="steps an arena stays resident beyond the launches its batch needs: R = launches "
+                         "per batch + lead (-1 = join lag + 1).  Lead = join lag is the least that lets the next "
+                         "batch's scan overlap the launch finishing the old one (hbx_input_after_oldest), but at "
+                         "the auto residency it puts 32 batches' chains in flight, past K3's 128-CU cliff")
     ap.add_argument("--e2e", action="store_true",
                     help="host-inclusive mode: each step's batch is copied from pinned host memory "
                          "(H2D on the engine's scan stream, overlapped with the pipeline)")
@@ -206,9 +208,13 @@ def lane_occupancy(arena_res, R, B, need, lanes):
 
 
 def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=None):
-    """Fill to R in flight, W warm-up steps, K timed steps (collect the oldest
-    + submit one), then the drain.  Returns timings, the window's launch
-    counts and results."""
+    """Fill to R in flight, W warm-up steps, K timed steps (submit one into
+    the next arena of the ring, then collect the oldest batch), then the
+    drain.  A batch reuses the arena of the batch R before it while that one
+    is still in the pipeline: hbx_input_after_oldest orders its scan (and an
+    --e2e copy) after the launch that finishes the older batch, on the GPU,
+    so the host collecting later never holds an arena back.  Returns
+    timings, the window's launch counts and results."""
     order = deque()  # arena index of every pending batch, oldest first
     state = {"j": 0, "t_sub": 0.0, "t_col": 0.0}
     arena_res = {}
@@ -216,6 +222,8 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
     def submit():
         t = time.perf_counter()
         i = state["j"] % R
+        if len(order) >= R:  # arena i still holds the oldest pending batch
+            eng.input_after_oldest()
         if before_submit:
             before_submit(i)
         eng.submit_device(arenas[i].data_ptr(), offs, lens)
@@ -236,8 +244,8 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
     for _ in range(R):
         submit()
     for _ in range(warmup):
-        collect()
         submit()
+        collect()
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -247,8 +255,8 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
     t0 = time.perf_counter()
     last = None
     for _ in range(steps):
-        last = collect()
         submit()
+        last = collect()
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     host = {"submit_ms": state["t_sub"] / steps * 1e3, "collect_ms": state["t_col"] / steps * 1e3,
@@ -447,7 +455,7 @@ def main():
     eng = Engine(dev_idx, md5_slice=B, join_lag=lag)
     # every batch slot, chain table and summary buffer of the pipeline is
     # allocated now: an allocation inside the timed region would drain the streams
-    eng.reserve(R + 1, nf, sum(lens))
+    eng.reserve(R + 2, nf, sum(lens))
     for _ in range(2):  # single-batch latency (one batch alone, synchronous call), untimed
         eng.chunk_hash_device(arenas[0].data_ptr(), offs, lens)
     latency = eng.stage_times()

@@ -1741,6 +1741,29 @@ int hbx_memcpy_h2d_async(hbx_ctx* c, void* d, const void* h, uint64_t n) {
   return HBX_OK;
 }
 
+int hbx_input_after_oldest(hbx_ctx* c) {
+  if (!c) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->broken) return c->fail(HBX_ERR_STATE, "context is unusable after a failed submit; destroy it");
+  if (c->pending.empty()) return HBX_OK;
+  HBX_TRY(c, hipSetDevice(c->device));
+  Batch* x = c->pending.front();
+  // its last MD5 launch must have been issued: drain until it is (a caller
+  // that reuses memory this early gets correct results, only slower)
+  for (int k = 0; !x->finalized; k++) {
+    const uint64_t l0 = c->launches;
+    int rc = md5_step(c, kBudgetAll, true);
+    if (rc) return rc;
+    if (c->launches == l0 || k > 2) return c->fail(HBX_ERR_STATE, "drain launched nothing (internal)");
+  }
+  if (!x->joined || c->hstream == c->stream) return HBX_OK;  // (empty batch / one stream: in order already)
+  // the completion event of the launch that finished it (or of a later one,
+  // if that slot has been recorded again since)
+  const uint64_t L = c->launches - x->final_launch <= 3 ? x->final_launch : c->launches - 1;
+  HBX_TRY(c, hipStreamWaitEvent(c->stream, c->order_free[L % 3], 0));
+  return HBX_OK;
+}
+
 int hbx_after_stream(hbx_ctx* c, void* stream) {
   if (!c) return HBX_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);

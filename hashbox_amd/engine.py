@@ -251,6 +251,12 @@ class Engine:
         """MD5 blocks per chain per K3 launch (0 = unlimited)."""
         self._check(self._L.hbx_set_md5_slice(self._ctx, int(blocks)), "hbx_set_md5_slice")
 
+    def input_after_oldest(self):
+        """The next input copy / batch may reuse the oldest pending batch's
+        device memory: a GPU-side wait for its hashing to finish
+        (hbx_input_after_oldest)."""
+        self._check(self._L.hbx_input_after_oldest(self._ctx), "hbx_input_after_oldest")
+
     def set_join_lag(self, lag: int):
         """Submits between a batch's own and the MD5 launch its chains join
         (1..4; 2 gives a small batch's scan a whole extra step)."""

@@ -140,6 +140,15 @@ int hbx_pending(hbx_ctx *ctx);
  * + ceil(min(longest file, 8 MiB)/64 / blocks) - 1 further launches; results are
  * identical for every setting. */
 int hbx_set_md5_slice(hbx_ctx *ctx, uint32_t blocks);
+/* Reuse the input memory of the OLDEST pending batch: enqueue on the
+ * engine's input (scan) stream a GPU-side wait for the MD5 launch that
+ * finishes that batch, so input copies (hbx_memcpy_h2d_async) and batches
+ * submitted afterwards read it only once the batch's last chain is hashed —
+ * before the batch is collected with hbx_wait, and without blocking the
+ * host.  A ring of device arenas then needs no slot for results still on
+ * their way to the host.  If that batch's last launch has not been issued
+ * yet, the chains in flight are drained first (correct, only slower). */
+int hbx_input_after_oldest(hbx_ctx *ctx);
 /* Optional: pre-size the pipeline for `batches` batches in flight of up to
  * `files` files and `bytes` bytes each.  The batch pool, the MD5 chain tables
  * and the slice summaries are allocated now, so the steady state never

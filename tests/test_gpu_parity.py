@@ -312,3 +312,53 @@ def test_stream_cu_sets(oracle, monkeypatch, scan, hash_):
     for i, g in zip(order, got):
         for a, r in zip(g, batches[i][3]):
             _check(a, r)
+
+
+@pytest.mark.parametrize("md5_slice", [65536, 4096])
+def test_input_after_oldest_ring(oracle, md5_slice):
+    """A ring of 3 device arenas refilled with NEW data while earlier batches
+    are still pending: hbx_input_after_oldest orders each refill (an H2D copy
+    on the engine's input stream) and the batch after the oldest pending
+    batch's last MD5 launch, on the GPU.  With slice 65536 that launch was
+    issued already (no drain); with 4096 it was not (the call drains).
+    Every batch must match the oracle on ITS data, never the data that
+    replaced it."""
+    import ctypes
+    import torch
+    from hashbox_amd import Engine, _lib, pack_arena_layout
+    L = _lib.load()
+    rng = np.random.default_rng(71)
+    sizes = [9 * MAXB + 5, 3 * MIN + 7, 2 * MAXB + 99]
+    offs, total = pack_arena_layout(sizes)
+    datas = []
+    for j in range(6):
+        host = np.zeros(total, np.uint8)
+        for k, (o, n) in enumerate(zip(offs, sizes)):
+            host[int(o):int(o) + n] = rng.integers(0, 256, n, dtype=np.uint8)
+        datas.append(host)
+    refs = [[oracle.store_file(h[int(o):int(o) + n], fast=True) for o, n in zip(offs, sizes)] for h in datas]
+    pin = ctypes.c_void_p()
+    assert L.hbx_alloc_pinned(total * 6, ctypes.byref(pin)) == 0
+    staged = np.ctypeslib.as_array((ctypes.c_uint8 * (total * 6)).from_address(pin.value))
+    for j, h in enumerate(datas):
+        staged[j * total:(j + 1) * total] = h
+    ring = [torch.empty(total, dtype=torch.uint8, device="cuda:0") for _ in range(3)]
+    torch.cuda.synchronize()
+    got, order = [], []
+    with Engine(0, md5_slice=md5_slice) as e:
+        for j in range(12):
+            if e.pending() >= 3:
+                e.input_after_oldest()
+            d = j % 6
+            e.memcpy_h2d_async(ring[j % 3].data_ptr(), pin.value + d * total, total)
+            e.submit_device(ring[j % 3].data_ptr(), offs, sizes)
+            order.append(d)
+            if e.pending() > 3:
+                got.append(e.wait())
+        while e.pending():
+            got.append(e.wait())
+    L.hbx_free_pinned(pin)
+    assert len(got) == 12
+    for d, res in zip(order, got):
+        for g, r in zip(res, refs[d]):
+            _check(g, r)
