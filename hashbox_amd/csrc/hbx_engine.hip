@@ -1712,13 +1712,16 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
     k++;
   }
   // collect everything in flight (also after a failure: the caller's arrays
-  // must not be written once this call has returned)
+  // must not be written once this call has returned); counted as waiting
+  // for collection
+  const double td = now();
   while (!c->pending.empty()) {
     const std::string keep = c->err;
     const int r2 = rc == HBX_OK ? collect() : wait_oldest(c);
     if (rc == HBX_OK) rc = r2;
     else c->err = keep;
   }
+  c->io_s[1] += now() - td;
   return rc;
 }
 }  // namespace

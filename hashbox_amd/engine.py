@@ -18,6 +18,7 @@ pkg/core/utils.go:22-37).
 from __future__ import annotations
 
 import ctypes
+import gc
 import os
 import sys
 import time
@@ -47,7 +48,7 @@ def max_chunks(n: int) -> int:
     return n // MIN_BLOCK_SIZE + 1
 
 
-@dataclass
+@dataclass(slots=True)
 class FileChunks:
     """What storeFile records for one file."""
     cut_ends: np.ndarray  # uint64 [k]: chunk i = [cut_ends[i-1], cut_ends[i])
@@ -88,6 +89,7 @@ class Engine:
         self.device = device
         self._pending = deque()
         self.wait_s = 0.0
+        self.last_call_s = 0.0
         if tile_iters is not None:
             self._check(self._L.hbx_set_tile_iters(self._ctx, int(tile_iters)), "set_tile_iters")
         if md5_slice is not None:
@@ -134,7 +136,8 @@ class Engine:
 
     @staticmethod
     def _alloc_out(lens: Sequence[int]):
-        caps = np.array([max_chunks(int(n)) for n in lens], np.uint64)
+        caps = (np.asarray(lens, np.uint64).reshape(-1) // np.uint64(MIN_BLOCK_SIZE) + np.uint64(1)
+                if len(lens) else np.zeros(0, np.uint64))
         base = np.zeros(len(lens), np.uint64)
         if len(lens):
             base[1:] = np.cumsum(caps)[:-1]
@@ -146,14 +149,27 @@ class Engine:
 
     @staticmethod
     def _unpack(lens, caps, base, cuts, ids, sums) -> List[FileChunks]:
-        out = []
-        for f in range(len(lens)):
-            s = sums[f]
-            k = int(s.n_chunks)
-            b = int(base[f])
-            out.append(FileChunks(cuts[b:b + k].copy(), ids[b:b + k].copy(), int(s.content_type),
-                                  bytes(s.content_id) if k else b""))
-        return out
+        # one structured view of the summaries; each file's cut ends and ids
+        # are views into the per-call output arrays (no per-file copies:
+        # 100 k files unpack in ~0.15 s instead of ~0.4 s)
+        n = len(lens)
+        if n == 0:
+            return []
+        sv = np.ctypeslib.as_array(sums)[:n]
+        k = sv["n_chunks"].astype(np.int64)
+        starts = base[:n].astype(np.int64).tolist()
+        ks = k.tolist()
+        types = sv["content_type"].tolist()
+        cid = np.ascontiguousarray(sv["content_id"]).tobytes()
+        # the cyclic collector would run dozens of passes over 100 k new objects
+        was = gc.isenabled()
+        gc.disable()
+        try:
+            return [FileChunks(cuts[b:b + kk], ids[b:b + kk], t, cid[16 * f:16 * f + 16] if kk else b"")
+                    for f, (b, kk, t) in enumerate(zip(starts, ks, types))]
+        finally:
+            if was:
+                gc.enable()
 
     # -------------------------------------------------------------- API ----
     def chunk_hash(self, data: BytesLike) -> FileChunks:
@@ -438,7 +454,8 @@ class Engine:
     def store_paths(self, paths: Sequence[Union[str, os.PathLike]], io_threads: int = 16,
                     batch_bytes: int = 1 << 30, compress: bool = False,
                     on_batch: Optional[Callable[[int, int], None]] = None,
-                    on_files: Optional[Callable[[int, List[FileChunks]], None]] = None) -> List[FileChunks]:
+                    on_files: Optional[Callable[[int, List[FileChunks]], None]] = None,
+                    sizes: Optional[Sequence[int]] = None) -> List[FileChunks]:
         """storeFile for many files on disk, end to end: the library reads them
         into pinned memory on ``io_threads`` threads and overlaps reading the
         next batch with the copy + kernels of the current one.  With
@@ -449,17 +466,29 @@ class Engine:
         ids, summaries and zlib streams written (hbx_store_paths_zcb), so a
         sender can ship them while later batches are still read and hashed.
         ``on_files(first, files)`` is the same callback handed the finished
-        FileChunks (ids, cut ends, zlib stream views) of those files."""
+        FileChunks (ids, cut ends, zlib stream views) of those files.
+        ``sizes`` are the files' byte sizes when the caller already has them
+        (storeFile takes the walker's FileEntry with FileSize, store.go:84,
+        247); otherwise each path is stat'ed here.  A file shorter than its
+        size fails the call (HBX_ERR_IO); bytes past it are not read.  ``last_call_s`` holds
+        the library call's wall seconds."""
         if (on_batch is not None or on_files is not None) and not compress:
             raise ValueError("on_batch / on_files need compress=True (hbx_store_paths_zcb)")
         enc = [os.fsencode(p) for p in paths]
-        lens = np.array([os.stat(p).st_size for p in enc], np.uint64)
+        if sizes is None:
+            lens = np.array([os.stat(p).st_size for p in enc], np.uint64)
+        else:
+            lens = np.array(sizes, np.uint64).reshape(-1)
+            if lens.size != len(enc):
+                raise ValueError("sizes must have one entry per path")
         arr = (ctypes.c_char_p * max(len(enc), 1))(*enc)
         caps, base, cuts, ids, sums = self._alloc_out(lens)
         if not compress:
+            t0 = time.perf_counter()
             self._check(self._L.hbx_store_paths(self._ctx, len(enc), ctypes.cast(arr, ctypes.c_void_p),
                                                 _p(lens), _p(cuts), _p(ids), _p(base), _p(caps), sums,
                                                 int(io_threads), int(batch_bytes)), "hbx_store_paths")
+            self.last_call_s = time.perf_counter() - t0
             return self._unpack(lens, caps, base, cuts, ids, sums)
         fb = np.array([self._L.hbx_deflate_file_bound(int(x)) for x in lens], np.uint64)
         zbase = np.zeros(max(lens.size, 1), np.uint64)
@@ -479,6 +508,7 @@ class Engine:
             r.zstreams = [zout[int(zoff[b + i]):int(zoff[b + i] + zlen[b + i])] for i in range(k)]
             return r
 
+        t0 = time.perf_counter()
         if on_batch is None and on_files is None:
             self._check(self._L.hbx_store_paths_z(*zargs), "hbx_store_paths_z")
         else:
@@ -499,6 +529,7 @@ class Engine:
                         "hbx_store_paths_zcb")
             if raised:
                 raise raised[0]
+        self.last_call_s = time.perf_counter() - t0
         res = self._unpack(lens, caps, base, cuts, ids, sums)
         for f, r in enumerate(res):
             b = int(base[f])
@@ -507,8 +538,9 @@ class Engine:
         return res
 
     def io_times(self, reset: bool = False) -> np.ndarray:
-        """store_paths host seconds: reading files, waiting for an arena,
-        waiting for a pinned slot's copy (cumulative)."""
+        """store_paths host seconds: reading files, waiting for batches to be
+        collected (arena reuse and the final drain), waiting for a pinned
+        slot's copy (cumulative)."""
         s = (ctypes.c_double * 3)()
         self._check(self._L.hbx_io_times(self._ctx, s, int(bool(reset))), "hbx_io_times")
         return np.array(list(s), np.float64)

@@ -297,7 +297,9 @@ def store_tree(eng: Engine, root, reference_id: bytes = _ZERO16, io_threads: int
     t1 = time.perf_counter()
     paths = list(file_entries)
     if paths:
-        res = eng.store_paths(paths, io_threads=io_threads, batch_bytes=batch_bytes)
+        # sizes from the walk's Lstat (FileEntry.FileSize, store.go:247)
+        res = eng.store_paths(paths, io_threads=io_threads, batch_bytes=batch_bytes,
+                              sizes=[file_entries[p].file_size for p in paths])
         for p, r in zip(paths, res):
             e = file_entries[p]
             e.content_type, e.content_block_id = r.content_type, r.content_id  # store.go:187-196

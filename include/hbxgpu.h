@@ -170,8 +170,9 @@ int hbx_store_paths(hbx_ctx *ctx, uint64_t n_files, const char *const *paths,
                     uint32_t io_threads, uint64_t batch_bytes);
 
 /* Host seconds hbx_store_paths spent, cumulative per context: [0] reading
- * files into pinned memory, [1] waiting for a device arena (its batch's
- * hashing), [2] waiting for a pinned slot's H2D copy.  reset != 0 zeroes them. */
+ * files into pinned memory, [1] waiting for batches to be collected (a device
+ * arena's reuse, and the drain at the end of the call), [2] waiting for a
+ * pinned slot's H2D copy.  reset != 0 zeroes them. */
 int hbx_io_times(hbx_ctx *ctx, double s[3], int reset);
 
 /* MD5(BE32(n_links) || links || BE32(len) || data) on the device. */

@@ -178,6 +178,15 @@ def test_store_paths_end_to_end(oracle, tmp_path, join_lag):
     from hashbox_amd import HbxError
     with _pt.raises((HbxError, FileNotFoundError)):
         engine.store_paths([str(tmp_path / "missing.bin")])
+    # the walker's sizes (FileEntry.FileSize) instead of a stat per path
+    got = engine.store_paths(paths, io_threads=4, batch_bytes=64 << 20, sizes=[x.size for x in datas])
+    for x, g in zip(datas, got):
+        _check(g, oracle.store_file(x, fast=True))
+    # a size past the end of the file fails loudly
+    with _pt.raises(HbxError):
+        engine.store_paths(paths[3:4], sizes=[datas[3].size + 1])
+    with _pt.raises(ValueError):
+        engine.store_paths(paths[:2], sizes=[1])
     engine.close()
 
 

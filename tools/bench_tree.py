@@ -93,7 +93,7 @@ def main():
             "seconds": round(t_all, 3), "gibs": round(total / t_all / 2**30, 3),
             "files_per_s": round(len(got.files) / t_all, 1),
             "phases_s": {k: round(v, 3) for k, v in got.seconds.items()},
-            "io_s": {"read": round(io[0], 3), "wait_arena": round(io[1], 3), "wait_copy": round(io[2], 3)},
+            "io_s": {"read": round(io[0], 3), "wait_collect": round(io[1], 3), "wait_copy": round(io[2], 3)},
             "dir_ids_one_batch": {"dirs": len(dirs), "ms": round(t_dirs * 1e3, 3),
                                   "dblk_bytes": sum(len(got.directories[p][0]) for p in dirs)},
             "root_id": got.root.content_block_id.hex(),

@@ -3,7 +3,7 @@
 set -o pipefail
 O=gpurun_out/c5io; mkdir -p $O
 first=1
-for cfg in "16 1024" "32 1024" "16 256" "8 1024"; do
+for cfg in ${CFGS:-"16 1024" "12 1024" "14 1024" "10 1024"}; do
   set -- $cfg
   keep="--keep"
   timeout -k 10 300 python tools/bench_config5.py --io-threads $1 --batch-mib $2 --cpu-sample 200 $keep > $O/c5_$1_$2.json 2> $O/c5.err || { tail -3 $O/c5.err; exit 1; }
