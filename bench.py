@@ -98,6 +98,10 @@ def parse():
                     help="diagnostics: hold this much extra device memory (written once, never read)")
     ap.add_argument("--k3-probe", action="store_true",
                     help="diagnostics: per-wave timeline of the window's last K3 launch (HBX_K3_PROBE)")
+    ap.add_argument("--alias-depth", type=int, default=0,
+                    help="diagnostics: D batches in flight over the physical arenas (batch j reads arena "
+                         "j %% R; inputs are read-only, so aliasing emulates the residency a paged arena would "
+                         "free).  Never the headline: the line is marked 'aliased'")
     ap.add_argument("--single-alloc", action="store_true",
                     help="the R arenas as views of one allocation instead of R allocations")
     return ap.parse_args()
@@ -207,7 +211,7 @@ def lane_occupancy(arena_res, R, B, need, lanes):
             "occupancy_max": round(max(active) / lanes, 4)}
 
 
-def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=None):
+def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=None, aliased=False):
     """Fill to R in flight, W warm-up steps, K timed steps (submit one into
     the next arena of the ring, then collect the oldest batch), then the
     drain.  A batch reuses the arena of the batch R before it while that one
@@ -222,7 +226,7 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
     def submit():
         t = time.perf_counter()
         i = state["j"] % R
-        if len(order) >= R:  # arena i still holds the oldest pending batch
+        if len(order) >= R and not aliased:  # arena i still holds the oldest pending batch
             eng.input_after_oldest()
         if before_submit:
             before_submit(i)
@@ -319,7 +323,8 @@ def run_workload(a, name, eng, arenas, offs, lens, R, B, need, lanes, dist, gpu,
                  job_batch_bytes, check_threads, before_submit=None):
     """One steady-state measurement; returns the JSON fields of its line.
     `gpu` is this rank's device, `dev` the device of the reductions."""
-    r = steady(eng, arenas, offs, lens, R, a.steps, a.warmup, dist, gpu, before_submit)
+    r = steady(eng, arenas, offs, lens, R, a.steps, a.warmup, dist, gpu, before_submit,
+               aliased=a.alias_depth > 0)
     el = max_over_ranks(r["el"], dist, dev)
     tot_ms, tot_n = r["tot_ms"], r["tot_n"]
     k1_n, k3_n = int(tot_n[0]), int(tot_n[3])
@@ -447,6 +452,13 @@ def main():
     if dist:  # ranks share the host's cores for the oracle check
         threads = max(1, threads // local_world)
     arenas = W.random_arenas(R, total, a.seed + 7919 * rank, dev, single=a.single_alloc)
+    if a.alias_depth > 0:  # diagnostics: D in flight over the R physical arenas
+        n_phys = R
+        R = a.alias_depth
+        arenas = [arenas[i % n_phys] for i in range(R)]
+        if a.md5_slice < 0:
+            B = -(-nfull // max(1, R - lead))
+        need = 1 if B == 0 else -(-nfull // B)
     ballast = torch.zeros(int(a.ballast_gib * GIB), dtype=torch.uint8, device=dev) if a.ballast_gib else None
     torch.cuda.synchronize(dev)
 
@@ -536,6 +548,9 @@ def main():
     if "zipf" in lines and workloads[0] != "zipf":
         out["zipf"] = dict(lines["zipf"], workload=f"{a.files} x {a.file_mib} MiB Zipf-duplicated buffers "
                                                    "(configs[3] scheme), device-resident")
+    if a.alias_depth > 0:
+        out["aliased"] = {"depth": R, "physical_arenas": n_phys,
+                          "note": "diagnostic: in-flight batches share arenas; not a headline"}
     out["lib"] = _lib.identity()
     if rank == 0:
         print(json.dumps(out), flush=True)
