@@ -98,6 +98,8 @@ def parse():
                     help="diagnostics: hold this much extra device memory (written once, never read)")
     ap.add_argument("--k3-probe", action="store_true",
                     help="diagnostics: per-wave timeline of the window's last K3 launch (HBX_K3_PROBE)")
+    ap.add_argument("--k3-waves", type=int, default=1, choices=[1, 2],
+                    help="block-MD5 kernel waves per SIMD (hbx_set_k3_waves)")
     ap.add_argument("--alias-depth", type=int, default=0,
                     help="diagnostics: D batches in flight over the physical arenas (batch j reads arena "
                          "j %% R; inputs are read-only, so aliasing emulates the residency a paged arena would "
@@ -464,7 +466,7 @@ def main():
 
     if a.k3_probe:
         os.environ["HBX_K3_PROBE"] = "1"
-    eng = Engine(dev_idx, md5_slice=B, join_lag=lag)
+    eng = Engine(dev_idx, md5_slice=B, join_lag=lag, k3_waves=a.k3_waves)
     # every batch slot, chain table and summary buffer of the pipeline is
     # allocated now: an allocation inside the timed region would drain the streams
     eng.reserve(R + 2, nf, sum(lens))
@@ -537,7 +539,7 @@ def main():
                                + (", sharded by file across GPUs: configs[2])" if world > 1 else ")"),
                    "files_per_step": a.files, "files_per_gpu": nf, "file_bytes": fbytes,
                    "md5_slice_blocks": B, "pipeline_depth": R, "launches_per_batch": need,
-                   "scan_lead": lead, "join_lag": lag, "parallelism": f"file-sharded x{world} ({a.scaling} scaling; "
+                   "scan_lead": lead, "join_lag": lag, "k3_waves_per_simd": a.k3_waves, "parallelism": f"file-sharded x{world} ({a.scaling} scaling; "
                                                        "independent HIP streams, no data-path collective)"},
     }
     out.update({k: v for k, v in head.items() if k not in ("value", "ms_per_step")})

@@ -187,6 +187,7 @@ struct hbx_ctx {
   // one per SIMD), leaving whole CUs to the next batch's K1 (measured 1510 vs
   // 1255 GiB/s spread, 100 steps); 0 spreads them one per CU first
   uint32_t k3_dense = 1;
+  uint32_t k3_threads = 256;  // K3 workgroup: 256 = one wave per SIMD (hbx_k3_block_md5), 512 = two (_w2)
   uint32_t md5_slice = 16384; // K3 time slice: full MD5 blocks per chain per launch (0 = unlimited)
   // K1 gate (hbx_k1_gate): a batch's K1 waits until every workgroup of the K3
   // launch of the same submit has been dispatched.  k3_started counts K3
@@ -520,8 +521,9 @@ int md5_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
     tslot[0] = tslot[1] = 0;
     c->k3_open.push_back(L);
   }
-  const uint32_t waves = c->md5_wgs * (kK3Threads / 64);
-  hipLaunchKernelGGL(hbx_k3_block_md5, dim3(c->md5_wgs), dim3(kK3Threads), 0, s,
+  const uint32_t waves = c->md5_wgs * (c->k3_threads / 64);
+  hipLaunchKernelGGL(c->k3_threads == (uint32_t)kK3Threads2 ? hbx_k3_block_md5_w2 : hbx_k3_block_md5,
+                     dim3(c->md5_wgs), dim3(c->k3_threads), 0, s,
                      c->d_order[slot].as<OrderEntry>(), static_cast<const uint32_t*>(c->d_octl[slot].as<uint32_t>()),
                      budget, c->k3_dense, c->d_gate.as<uint32_t>(), c->k3_dispatched, c->k3_waves + waves - 1u, tslot,
                      c->h_probe.p ? c->h_probe.as<uint64_t>() : nullptr);
@@ -1055,6 +1057,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
     c->md5_wgs = (uint32_t)(ncu = prop.multiProcessorCount);
   if (const char* v = std::getenv("HBX_MD5_WGS")) c->md5_wgs = (uint32_t)std::max(1, std::atoi(v));
   if (const char* v = std::getenv("HBX_K3_DENSE")) c->k3_dense = std::atoi(v) ? 1u : 0u;
+  if (const char* v = std::getenv("HBX_K3_WAVES")) c->k3_threads = std::atoi(v) == 2 ? kK3Threads2 : kK3Threads;
   if (const char* v = std::getenv("HBX_TILE_ITERS")) c->tile_iters = (uint32_t)std::min(1024, std::max(0, std::atoi(v)));
   if (const char* v = std::getenv("HBX_JOIN_LAG")) c->join_lag = (uint32_t)std::min(4, std::max(1, std::atoi(v)));
   if (const char* v = std::getenv("HBX_K4_WINDOW")) c->k4_window = (uint32_t)std::min(1024, std::max(1, std::atoi(v)));
@@ -1077,8 +1080,8 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   }
   if (c->h_k3t.ensure(kK3TimeRing * 16) == hipSuccess) std::memset(c->h_k3t.p, 0, kK3TimeRing * 16);
   if (const char* v = std::getenv("HBX_K3_PROBE"))
-    if (std::atoi(v) && c->h_probe.ensure((size_t)c->md5_wgs * (kK3Threads / 64) * 32) == hipSuccess)
-      std::memset(c->h_probe.p, 0, (size_t)c->md5_wgs * (kK3Threads / 64) * 32);
+    if (std::atoi(v) && c->h_probe.ensure((size_t)c->md5_wgs * (kK3Threads2 / 64) * 32) == hipSuccess)
+      std::memset(c->h_probe.p, 0, (size_t)c->md5_wgs * (kK3Threads2 / 64) * 32);
   if (c->d_gate.ensure(256) != hipSuccess || hipMemset(c->d_gate.p, 0, 256) != hipSuccess ||
       hipEventCreateWithFlags(&c->ssum_free[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ssum_free[1], hipEventDisableTiming) != hipSuccess) {
@@ -1160,7 +1163,7 @@ int hbx_k3_wave_times(hbx_ctx* c, uint64_t* out, uint32_t max_waves, uint32_t* n
   if (!c->h_probe.p) return c->fail(HBX_ERR_STATE, "K3 probe not enabled (HBX_K3_PROBE=1 at context creation)");
   HBX_TRY(c, hipSetDevice(c->device));
   HBX_TRY(c, hipStreamSynchronize(c->hstream));
-  const uint32_t n = c->md5_wgs * (kK3Threads / 64);
+  const uint32_t n = c->md5_wgs * (c->k3_threads / 64);
   if (out) std::memcpy(out, c->h_probe.p, (size_t)std::min(n, max_waves) * 32);
   *n_waves = n;
   return HBX_OK;
@@ -1181,6 +1184,16 @@ int hbx_set_md5_slice(hbx_ctx* c, uint32_t blocks) {
   // not all hashed
   if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
   c->md5_slice = blocks;
+  return HBX_OK;
+}
+
+int hbx_set_k3_waves(hbx_ctx* c, uint32_t waves_per_simd) {
+  if (!c || (waves_per_simd != 1u && waves_per_simd != 2u)) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  // the K1 gate of a pending batch counts the workgroups and waves of the
+  // K3 launch it follows
+  if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
+  c->k3_threads = waves_per_simd == 2u ? kK3Threads2 : kK3Threads;
   return HBX_OK;
 }
 

@@ -700,9 +700,9 @@ __device__ __forceinline__ u32x4 md5_load(g_u32x4* p) {
   return *p;
 #endif
 }
+template <int RING = HBX_MD5_RING>  // blocks of prefetch (16 VGPRs each)
 __device__ void md5_run(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32_t b0, uint32_t cnt,
                         bool finish) {
-  constexpr int RING = HBX_MD5_RING;  // blocks of prefetch (16 VGPRs each)
   const uint32_t sh = (uint32_t)reinterpret_cast<uintptr_t>(c) & 3u;
   g_u32* va = gptr32(c - sh);  // raw R[r] = va[r]
   // prefetches clamp to the last block this lane compresses; a lane with
@@ -862,16 +862,27 @@ __device__ void md5_block_at(const uint8_t* c, uint32_t len, uint32_t (&h)[4], u
 // Cooperative streaming for a wave whose 64 lanes all advance exactly R
 // blocks, lane j from block b1_j >= 1 of its own chain.  Lane-mode loads put
 // 64 chains (64 pages) in every load instruction and the per-CU address
-// translation thrashes (89 % UTCL1 misses); here load
-// instruction q fetches 256 contiguous bytes of each of 4 chains, so it
-// touches ~4 pages.  Each chain's message stream is read dword-aligned from
-// S_j = chunk + 64*b1 - 8 - (chunk & 3), staged 4 blocks (16 granules of 16
-// B) at a time through registers into LDS (rows of 272 B: conflict-free, all
-// offsets immediate), two stages resident (the current one and the next),
-// and each lane reads its own row with 4 aligned ds_read_b128 per block.
-constexpr uint32_t kCoopRow = 272u;              // 256 B of one chain's stage + 16 B pad
-constexpr uint32_t kCoopHalf = 64u * kCoopRow;   // one stage of the wave's 64 chains
-constexpr uint32_t kCoopWaveLds = 2u * kCoopHalf;
+// translation thrashes (89 % UTCL1 misses); here a load
+// instruction fetches 16*G contiguous bytes of each of C = 64/G chains, so it
+// touches ~C pages.  Each chain's message stream is read from its exact byte
+// address S_j = chunk + 64*b1 - 8 (16-B loads at any byte offset; the
+// hardware splits them), so the words land aligned and a block needs no
+// v_alignbyte.  A stage is G granules (16 B) of every chain = G/4 blocks,
+// staged through registers into LDS rows of 16*G + 16 bytes (conflict-free
+// ds_read_b128 of a lane's own row), two stages resident (the current one and
+// the next); each lane reads its row with 4 aligned ds_read_b128 per block.
+//   G = 16: 4-block stages, 272-B rows, 34 KiB per wave (one wave per SIMD);
+//   G = 8:  2-block stages, 144-B rows, 18 KiB per wave (two waves per SIMD
+//           fit the CU's 160 KiB of LDS).
+template <int G>
+struct Coop {
+  static constexpr uint32_t C = 64u / G;          // chains per load instruction
+  static constexpr uint32_t Row = 16u * G + 16u;  // one chain's stage + 16 B pad
+  static constexpr uint32_t Half = 64u * Row;     // one stage of the wave's 64 chains
+  static constexpr uint32_t WaveLds = 2u * Half;
+  static constexpr uint32_t BPS = G / 4u;         // message blocks per stage
+};
+constexpr uint32_t kCoopWaveLds = Coop<16>::WaveLds;
 
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src_lane) {
   const int lo = __builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)(uint32_t)v);
@@ -879,140 +890,100 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src_lane) {
   return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 
-template <int HALF>
-__device__ __forceinline__ void coop_write(uint8_t* wl, uint32_t wr, const u32x4 (&G)[16]) {
+// Stage registers into LDS half `half` (lane: granule t of the rows C*q+sub).
+template <int G>
+__device__ __forceinline__ void coop_write(uint8_t* wl, uint32_t wr, uint32_t half, const u32x4 (&Gs)[G]) {
 #pragma unroll
-  for (int q = 0; q < 16; q++)
-    *reinterpret_cast<u32x4*>(wl + wr + (uint32_t)HALF * kCoopHalf + 1088u * (uint32_t)q) = G[q];
+  for (int q = 0; q < G; q++)
+    *reinterpret_cast<u32x4*>(wl + wr + half * Coop<G>::Half + Coop<G>::C * Coop<G>::Row * (uint32_t)q) = Gs[q];
 }
 
-// Loads of stage `st` (granules 16*st .. 16*st+15 of every chain) into G.
+// Loads of stage `st` (granules G*st .. G*st+G-1 of every chain) into Gs.
 // Branch-free, so the compiler's vmcnt bookkeeping stays exact through the
 // stage loop and a wait covers only the register set it needs: a granule
 // past the last needed one (>= ngr) re-reads granule ngr-1, which every
 // chain holds.
-__device__ __forceinline__ void coop_load(u32x4 (&G)[16], const uint64_t (&Q)[16], uint32_t st,
-                                          uint32_t t, uint32_t ngr) {
-  const uint32_t g = min(16u * st + t, ngr - 1u);  // this lane's granule
-  const uint64_t off = 16ull * (g - t);            // Q[q] already holds + 16 t
+template <int G>
+__device__ __forceinline__ void coop_load(u32x4 (&Gs)[G], const uint64_t (&Q)[G], uint32_t st, uint32_t t,
+                                          uint32_t ngr) {
+  const uint32_t g = min((uint32_t)G * st + t, ngr - 1u);  // this lane's granule
+  const uint64_t off = 16ull * (g - t);                     // Q[q] already holds + 16 t
 #pragma unroll
-  for (int q = 0; q < 16; q++) G[q] = md5_load(gptr128(Q[q] + off));
+  for (int q = 0; q < G; q++) Gs[q] = md5_load(gptr128(Q[q] + off));
 }
 
-// 1: each chain's message stream is read from its exact byte address (16-B
-// loads at any byte offset; the hardware splits them), so the words land in
-// LDS aligned and a block needs no v_alignbyte.  0: dword-aligned reads plus
-// 16 v_alignbyte per block.
-#ifndef HBX_COOP_BYTE
-#define HBX_COOP_BYTE 1
-#endif
-#ifndef HBX_COOP_SETS
-#define HBX_COOP_SETS 2  // register sets of cooperative loads in flight (2 or 3; 3 needs HBX_COOP_BYTE)
-#endif
+// The G/4 blocks of stage s from LDS half `half` (blocks past R skipped).
+template <int G>
+__device__ __forceinline__ void coop_hash(const uint8_t* wl, uint32_t rd, uint32_t half, uint32_t s, uint32_t R,
+                                          uint32_t (&h)[4]) {
+  const uint8_t* hb = wl + rd + half * Coop<G>::Half;
+#pragma unroll
+  for (int u = 0; u < (int)Coop<G>::BPS; u++) {
+    const uint32_t blk = Coop<G>::BPS * s + (uint32_t)u;
+    if (blk >= R) break;  // wave-uniform
+    u32x4 W[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) W[i] = *reinterpret_cast<const u32x4*>(hb + 16u * (4u * u + (uint32_t)i));
+    const uint32_t m[16] = {W[0].x, W[0].y, W[0].z, W[0].w, W[1].x, W[1].y, W[1].z, W[1].w,
+                            W[2].x, W[2].y, W[2].z, W[2].w, W[3].x, W[3].y, W[3].z, W[3].w};
+    md5_compress(h, m);
+  }
+}
 
+// SETS register sets of loads in flight: stages s+1 .. s+SETS while stage s
+// is hashed (2 or 3).
+template <int G, int SETS>
 __device__ void md5_coop(uint8_t* wl, const uint8_t* c, uint32_t (&h)[4], uint32_t b1, uint32_t R) {
+  static_assert(G == 8 || G == 16, "stage of 2 or 4 blocks");
+  static_assert(SETS == 2 || SETS == 3, "2 or 3 register sets");
   const uint32_t lane = threadIdx.x & 63u;
-#if HBX_COOP_BYTE
   const uint64_t S = reinterpret_cast<uint64_t>(c) + 64ull * b1 - 8ull;  // message block b1
   const uint32_t ngr = 4u * R;                                           // granules of R blocks
-#else
-  const uint32_t sh = (uint32_t)reinterpret_cast<uintptr_t>(c) & 3u;
-  const uint64_t S = reinterpret_cast<uint64_t>(c) + 64ull * b1 - 8ull - sh;
-  const uint32_t ngr = 4u * R + 1u;  // granules holding dwords 0 .. 16R
-#endif
-  const uint32_t t = lane & 15u, sub = lane >> 4;
-  uint64_t Q[16];  // role q: chain 4q+sub, granule t of each stage
+  const uint32_t t = lane % (uint32_t)G, sub = lane / (uint32_t)G;
+  uint64_t Q[G];  // role q: chain C*q+sub, granule t of each stage
 #pragma unroll
-  for (int q = 0; q < 16; q++) Q[q] = shfl64(S, 4u * (uint32_t)q + sub) + 16ull * t;
-  const uint32_t wr = sub * kCoopRow + 16u * t;  // + 1088 q: row 4q+sub, granule t
-  const uint32_t rd = lane * kCoopRow;           // this lane's row
-  const uint32_t nst = (ngr + 15u) / 16u;
-  // Two register sets of loads in flight (stages s+1 and s+2 while stage s
-  // is hashed), so a load has two stages (~8 blocks) to land.  Stages past
-  // the last re-read it (coop_load clamps).
-  u32x4 GA[16], GB[16];
-  coop_load(GA, Q, 0u, t, ngr);
-  coop_load(GB, Q, 1u, t, ngr);
-  coop_write<0>(wl, wr, GA);
-  coop_load(GA, Q, 2u, t, ngr);
-#if !HBX_COOP_BYTE
-  // window: granules g..g+4 of the current block (W[0] carried)
-  u32x4 W0 = *reinterpret_cast<const u32x4*>(wl + rd);
-#endif
-  auto stage_pair = [&](auto half_c, uint32_t s, u32x4(&Gn)[16]) {
-    constexpr int HALF = decltype(half_c)::value;
+  for (int q = 0; q < G; q++) Q[q] = shfl64(S, Coop<G>::C * (uint32_t)q + sub) + 16ull * t;
+  const uint32_t wr = sub * Coop<G>::Row + 16u * t;
+  const uint32_t rd = lane * Coop<G>::Row;  // this lane's row
+  const uint32_t nst = (ngr + (uint32_t)G - 1u) / (uint32_t)G;
+  constexpr uint32_t BPS = Coop<G>::BPS;
+  // Stages past the last re-read it (coop_load clamps); their writes land in
+  // a half never read again.
+  u32x4 GA[G], GB[G];
+  coop_load<G>(GA, Q, 0u, t, ngr);
+  coop_load<G>(GB, Q, 1u, t, ngr);
+  coop_write<G>(wl, wr, 0u, GA);
+  coop_load<G>(GA, Q, 2u, t, ngr);
+  if constexpr (SETS == 2) {
     // start of stage s: stage s+1 (in Gn) into the other half, then Gn's
-    // registers take the loads of stage s+3.  Unconditional: past the last
-    // stage the loads repeat it and the write lands in a half never read
-    // again.
-    coop_write<HALF ^ 1>(wl, wr, Gn);
-    coop_load(Gn, Q, min(s + 3u, nst - 1u), t, ngr);
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const uint32_t blk = 4u * s + (uint32_t)u;
-      if (blk >= R) break;  // wave-uniform
-      const uint8_t* hb = wl + rd + (uint32_t)HALF * kCoopHalf;
-#if HBX_COOP_BYTE
-      u32x4 W[4];
-#pragma unroll
-      for (int i = 0; i < 4; i++) W[i] = *reinterpret_cast<const u32x4*>(hb + 16u * (4u * u + (uint32_t)i));
-      const uint32_t m[16] = {W[0].x, W[0].y, W[0].z, W[0].w, W[1].x, W[1].y, W[1].z, W[1].w,
-                              W[2].x, W[2].y, W[2].z, W[2].w, W[3].x, W[3].y, W[3].z, W[3].w};
-      md5_compress(h, m);
-#else
-      const u32x4 W1 = *reinterpret_cast<const u32x4*>(hb + 16u * (4u * u + 1u));
-      const u32x4 W2 = *reinterpret_cast<const u32x4*>(hb + 16u * (4u * u + 2u));
-      const u32x4 W3 = *reinterpret_cast<const u32x4*>(hb + 16u * (4u * u + 3u));
-      const u32x4 W4 = u < 3 ? *reinterpret_cast<const u32x4*>(hb + 16u * (4u * u + 4u))
-                             : *reinterpret_cast<const u32x4*>(wl + rd + (uint32_t)(HALF ^ 1) * kCoopHalf);
-      const uint32_t D[17] = {W0.x, W0.y, W0.z, W0.w, W1.x, W1.y, W1.z, W1.w, W2.x,
-                              W2.y, W2.z, W2.w, W3.x, W3.y, W3.z, W3.w, W4.x};
-      uint32_t m[16];
-#pragma unroll
-      for (int i = 0; i < 16; i++) m[i] = alignbyte(D[i + 1], D[i], sh);
-      md5_compress(h, m);
-      W0 = W4;
-#endif
+    // registers take the loads of stage s+3
+    auto stage = [&](auto half_c, uint32_t s, u32x4(&Gn)[G]) {
+      constexpr uint32_t HALF = decltype(half_c)::value;
+      coop_write<G>(wl, wr, HALF ^ 1u, Gn);
+      coop_load<G>(Gn, Q, min(s + 3u, nst - 1u), t, ngr);
+      coop_hash<G>(wl, rd, HALF, s, R, h);
+    };
+    for (uint32_t s = 0; BPS * s < R; s += 2u) {
+      stage(std::integral_constant<uint32_t, 0>{}, s, GB);
+      stage(std::integral_constant<uint32_t, 1>{}, s + 1u, GA);  // hashes nothing past block R
     }
-  };
-#if HBX_COOP_SETS == 3
-  // Three register sets in flight (stages s+1..s+3 while stage s is hashed):
-  // the sets rotate statically (unrolled by 3), the LDS half alternates at
-  // run time.
-  (void)stage_pair;
-  u32x4 GC[16];
-  coop_load(GC, Q, 3u, t, ngr);  // GA holds stage 2, GB stage 1, stage 0 is in half 0
-  auto stage_rt = [&](uint32_t s, u32x4(&Gn)[16]) {
-    const uint32_t half = s & 1u;
-    // stage s+1 (in Gn) into the other half, then Gn takes the loads of s+4
-#pragma unroll
-    for (int q = 0; q < 16; q++)
-      *reinterpret_cast<u32x4*>(wl + wr + (half ^ 1u) * kCoopHalf + 1088u * (uint32_t)q) = Gn[q];
-    coop_load(Gn, Q, min(s + 4u, nst - 1u), t, ngr);
-    const uint8_t* hb = wl + rd + half * kCoopHalf;
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const uint32_t blk = 4u * s + (uint32_t)u;
-      if (blk >= R) break;  // wave-uniform
-      u32x4 W[4];
-#pragma unroll
-      for (int i = 0; i < 4; i++) W[i] = *reinterpret_cast<const u32x4*>(hb + 16u * (4u * u + (uint32_t)i));
-      const uint32_t m[16] = {W[0].x, W[0].y, W[0].z, W[0].w, W[1].x, W[1].y, W[1].z, W[1].w,
-                              W[2].x, W[2].y, W[2].z, W[2].w, W[3].x, W[3].y, W[3].z, W[3].w};
-      md5_compress(h, m);
+  } else {
+    // the sets rotate statically (unrolled by 3), the LDS half alternates at
+    // run time
+    u32x4 GC[G];
+    coop_load<G>(GC, Q, 3u, t, ngr);  // GA holds stage 2, GB stage 1, stage 0 is in half 0
+    auto stage = [&](uint32_t s, u32x4(&Gn)[G]) {
+      const uint32_t half = s & 1u;
+      coop_write<G>(wl, wr, half ^ 1u, Gn);  // stage s+1
+      coop_load<G>(Gn, Q, min(s + 4u, nst - 1u), t, ngr);
+      coop_hash<G>(wl, rd, half, s, R, h);
+    };
+    for (uint32_t s = 0; BPS * s < R; s += 3u) {
+      stage(s, GB);       // GB: stage s+1
+      stage(s + 1u, GA);  // GA: stage s+2
+      stage(s + 2u, GC);  // GC: stage s+3 (hashes nothing past block R)
     }
-  };
-  for (uint32_t s = 0; 4u * s < R; s += 3u) {
-    stage_rt(s, GB);       // GB: stage s+1
-    stage_rt(s + 1u, GA);  // GA: stage s+2
-    stage_rt(s + 2u, GC);  // GC: stage s+3 (hashes nothing past block R)
   }
-#else
-  for (uint32_t s = 0; 4u * s < R; s += 2u) {
-    stage_pair(std::integral_constant<int, 0>{}, s, GB);
-    stage_pair(std::integral_constant<int, 1>{}, s + 1u, GA);  // hashes nothing past block R
-  }
-#endif
 }
 
 }  // namespace
@@ -1175,23 +1146,24 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
 // in the planner's order).  Each lane resumes its chain at `next`,
 // compresses up to `budget` full blocks and either finishes (tail blocks,
 // BlockID stored at `out`, entry marked done) or saves the state for the
-// next launch.  grid = one 256-thread workgroup per CU; placement of groups
-// on waves: see `dense`.  The MD5 chain is bound by the issue rate of one
-// wave (DESIGN.md "K3"; tools/experiments/md5_wave_mode.hip for what did not
-// pay).  256 threads = one wave per SIMD, which lets the compiler use the
-// whole register file (VGPR + AGPR) for the prefetch ring without spilling.
-#ifndef HBX_K3_THREADS
-#define HBX_K3_THREADS 256
-#endif
+// next launch.  grid = one workgroup per CU (256 threads = one wave per SIMD,
+// or 512 = two); placement of groups on waves: see `dense`.  The MD5 chain
+// is bound by the issue rate of one wave (DESIGN.md "K3").
+//
 // cooperative (page-local) loads for waves of full-slice chains
 #ifndef HBX_K3_COOP
 #define HBX_K3_COOP 1
 #endif
 constexpr uint32_t kCoopMinBudget = 8u;
-constexpr int kK3Threads = HBX_K3_THREADS;
+constexpr int kK3Threads = 256;    // hbx_k3_block_md5: one wave per SIMD
+constexpr int kK3Threads2 = 512;   // hbx_k3_block_md5_w2: two waves per SIMD
 
-extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
-    const OrderEntry* __restrict__ order, const uint32_t* __restrict__ n_order, uint32_t budget,
+// The body of both K3 variants: THREADS per workgroup (one per CU), the
+// cooperative stage of G granules with SETS register sets in flight, the
+// lane path's prefetch ring of RING blocks.  `wl` = this wave's LDS.
+template <int THREADS, int G, int SETS, int RING>
+__device__ __forceinline__ void k3_body(
+    uint8_t* wl, const OrderEntry* __restrict__ order, const uint32_t* __restrict__ n_order, uint32_t budget,
     uint32_t dense, uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last,
     uint64_t* __restrict__ tslot, uint64_t* __restrict__ probe) {
   // the MD5 chains are issue-bound: win the SIMD's issue arbitration against
@@ -1209,12 +1181,8 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t n_total = *n_order;
-#if HBX_K3_COOP
-  static_assert(kK3Threads == 256, "cooperative K3 path sized for 4 waves per workgroup");
-  __shared__ __attribute__((aligned(16))) uint8_t k3_lds[kK3Threads / 64][kCoopWaveLds];
-#endif
   const uint32_t groups = (n_total + 63u) / 64u;
-  const uint32_t nwaves = gridDim.x * (kK3Threads / 64);
+  const uint32_t nwaves = gridDim.x * (THREADS / 64);
   // spread: group g on wave (g / grid) % W of workgroup g % grid (one busy
   // wave per CU first); dense: group g on wave g % W of workgroup g / W, so
   // the busy waves fill the fewest CUs and whole CUs stay free for the scan
@@ -1224,7 +1192,7 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
   // to a multiple of the 8 XCDs, to even out K3's CUs per XCD, mixed long and
   // short waves on every CU: K3 3.52 -> 3.41 ms but K1 3.25 -> 3.54 ms beside
   // it, 2,235 -> 2,091 GiB/s at 33 resident batches.)
-  const uint32_t g0 = dense ? blockIdx.x * (kK3Threads / 64) + wave : wave * gridDim.x + blockIdx.x;
+  const uint32_t g0 = dense ? blockIdx.x * (THREADS / 64) + wave : wave * gridDim.x + blockIdx.x;
   // diagnostics (HBX_K3_PROBE): per wave its start, the end of its first
   // group's start-up (loads + prologue), its end, R and the largest count
   const uint64_t pt0 = probe ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -1255,7 +1223,7 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
         pR = R;
         pmax = wave_max_all(cnt);
       }
-      md5_coop(k3_lds[wave], src, h, ch.next + 1u, R - 1u);
+      md5_coop<G, SETS>(wl, src, h, ch.next + 1u, R - 1u);
       // A group that straddles two order bins mixes counts (e.g. 4,229 and
       // 4,093 blocks): the lanes still holding blocks go on cooperatively
       // while the others shadow the first of them and discard (the lane-mode
@@ -1272,7 +1240,7 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)reinterpret_cast<uint64_t>(src), L);
         const uint32_t p_sh = (uint32_t)__builtin_amdgcn_readlane((int)pos, L);
         uint32_t hk[4] = {h[0], h[1], h[2], h[3]};
-        md5_coop(k3_lds[wave], part ? src : reinterpret_cast<const uint8_t*>(s_sh), hk, part ? pos : p_sh, R2);
+        md5_coop<G, SETS>(wl, part ? src : reinterpret_cast<const uint8_t*>(s_sh), hk, part ? pos : p_sh, R2);
         if (part) {
           h[0] = hk[0];
           h[1] = hk[1];
@@ -1282,12 +1250,13 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
           rem -= R2;
         }
       }
-      md5_run(src, len, h, pos, rem, finish);
+      md5_run<RING>(src, len, h, pos, rem, finish);
     } else {
-      md5_run(src, len, h, b0, cnt, finish);
+      md5_run<RING>(src, len, h, b0, cnt, finish);
     }
 #else
-    md5_run(src, len, h, b0, cnt, finish);
+    (void)wl;
+    md5_run<RING>(src, len, h, b0, cnt, finish);
 #endif
     if (finish) {
       *(__attribute__((address_space(1))) u32x4*)ch.out = u32x4{h[0], h[1], h[2], h[3]};
@@ -1298,7 +1267,7 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
     }
   }
   if (probe && (threadIdx.x & 63u) == 0u) {
-    uint64_t* p = probe + 4u * (blockIdx.x * (kK3Threads / 64) + wave);
+    uint64_t* p = probe + 4u * (blockIdx.x * (THREADS / 64) + wave);
     // hardware placement: HW_ID (wave, SIMD, CU, SH, SE) and XCC_ID
     const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));
     const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11)) & 0xfu;
@@ -1311,6 +1280,34 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
     const uint32_t tk = __hip_atomic_fetch_add(started + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     if (tk == t_last) tslot[1] = __builtin_amdgcn_s_memrealtime();
   }
+}
+
+
+// One wave per SIMD: 4-block stages, two register sets, an 8-block lane ring
+// (VGPR + AGPR, 346 registers, no scratch).
+extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
+    const OrderEntry* __restrict__ order, const uint32_t* __restrict__ n_order, uint32_t budget,
+    uint32_t dense, uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last,
+    uint64_t* __restrict__ tslot, uint64_t* __restrict__ probe) {
+  __shared__ __attribute__((aligned(16))) uint8_t k3_lds[kK3Threads / 64][Coop<16>::WaveLds];
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  k3_body<kK3Threads, 16, 2, HBX_MD5_RING>(k3_lds[wave], order, n_order, budget, dense, started, t_first, t_last,
+                                           tslot, probe);
+}
+
+// Two waves per SIMD (the MD5 chain runs at one wave's issue rate, and two
+// waves of a SIMD each keep that rate: tools/ubench/valu_latency), so the
+// same chains fill half the CUs and leave the rest to the next batch's K1:
+// 2-block stages (18 KiB of LDS per wave), three register sets, a 4-block
+// lane ring, at most 256 registers.
+extern "C" __global__ __launch_bounds__(kK3Threads2, 2) void hbx_k3_block_md5_w2(
+    const OrderEntry* __restrict__ order, const uint32_t* __restrict__ n_order, uint32_t budget,
+    uint32_t dense, uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last,
+    uint64_t* __restrict__ tslot, uint64_t* __restrict__ probe) {
+  __shared__ __attribute__((aligned(16))) uint8_t k3_lds[kK3Threads2 / 64][Coop<8>::WaveLds];
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  k3_body<kK3Threads2, 8, 3, 4>(k3_lds[wave], order, n_order, budget, dense, started, t_first, t_last, tslot,
+                                probe);
 }
 
 // K1 gate (scan stream, just before a batch's K1): holds the K1 back until
@@ -1532,9 +1529,9 @@ extern "C" __global__ __launch_bounds__(64, 1) void hbx_k6_hash_blocks(
   // the longest), the per-lane remainder through the lane path
   const uint32_t R = ~wave_max_all(active ? ~cnt : 0u);
   const uint32_t Rc = R >= kCoopMinBudget ? R : 0u;  // wave-uniform
-  if (Rc) md5_coop(k6_lds, vs, h, hb, Rc);
+  if (Rc) md5_coop<16, 2>(k6_lds, vs, h, hb, Rc);
   const uint32_t rest = cnt - Rc;
-  md5_run(rest ? vs : zeros + 64, rest ? len + p - 8u : 0u, h, rest ? hb + Rc : 1u, rest, false);
+  md5_run<>(rest ? vs : zeros + 64, rest ? len + p - 8u : 0u, h, rest ? hb + Rc : 1u, rest, false);
   if (fast) md5_tail(vs, len + p - 8u, h, true);
   if (active) {
     *reinterpret_cast<uint4*>(ids + 4u * i) = make_uint4(h[0], h[1], h[2], h[3]);

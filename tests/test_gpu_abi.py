@@ -47,6 +47,8 @@ def test_state_rules(oracle):
         e.submit_device(dev.data_ptr(), offs, sizes)
         with pytest.raises(HbxError):
             e.set_md5_slice(3)
+        with pytest.raises(HbxError):  # the K3 variant is fixed while batches are pending
+            e.set_k3_waves(2)
         with pytest.raises(HbxError):  # offset not 16-byte aligned
             e.submit_device(dev.data_ptr(), offs + np.uint64(4), sizes)
         assert e.pending() == 1
@@ -54,6 +56,9 @@ def test_state_rules(oracle):
         got = [e.wait(), e.wait()]
         assert e.pending() == 0
         e.set_md5_slice(3)  # allowed once drained
+        e.set_k3_waves(2)
+        with pytest.raises(HbxError):
+            e.set_k3_waves(3)
         e.submit_device(dev.data_ptr(), offs, sizes)
         got.append(e.wait())
     for g in got:

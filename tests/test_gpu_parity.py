@@ -211,16 +211,17 @@ def _device_batches(oracle, nb, seed):
     return out
 
 
-@pytest.mark.parametrize("md5_slice,join_lag", [(1, 1), (3, 1), (64, 1), (16384, 1), (3, 2), (64, 2), (64, 3),
-                                                (16384, 4)])
-def test_pipelined_batches_time_sliced(oracle, md5_slice, join_lag):
+@pytest.mark.parametrize("md5_slice,join_lag,k3_waves", [(1, 1, 1), (3, 1, 1), (64, 1, 1), (16384, 1, 1), (3, 2, 1),
+                                                         (64, 2, 1), (64, 3, 1), (16384, 4, 1), (1, 1, 2),
+                                                         (9, 1, 2), (64, 3, 2), (16384, 1, 2)])
+def test_pipelined_batches_time_sliced(oracle, md5_slice, join_lag, k3_waves):
     """Several batches in flight on one context with the block-MD5 stage
     time-sliced: chains resume across many K3 launches, new batches' chunks
     join carried chains (join_lag submits later), results come back in FIFO
     order, bit-exact."""
     from hashbox_amd import Engine
     batches = _device_batches(oracle, 4, 31 + md5_slice % 7)
-    with Engine(0, md5_slice=md5_slice, join_lag=join_lag) as e:
+    with Engine(0, md5_slice=md5_slice, join_lag=join_lag, k3_waves=k3_waves) as e:
         for dev, offs, sizes, _ in batches[:3]:
             e.submit_device(dev.data_ptr(), offs, sizes)
         assert e.pending() == 3
@@ -274,8 +275,8 @@ def test_pipelined_steady_state(oracle, monkeypatch, join_lag, plan_mode):
             _check(a, r)
 
 
-@pytest.mark.parametrize("dense", ["0", "1"])
-def test_reserved_pipeline_placements(oracle, monkeypatch, dense):
+@pytest.mark.parametrize("dense,k3_waves", [("0", 1), ("1", 1), ("0", 2), ("1", 2)])
+def test_reserved_pipeline_placements(oracle, monkeypatch, dense, k3_waves):
     """hbx_reserve pre-sizes the pool, chain tables and summaries; both K3
     wave placements (HBX_K3_DENSE) give the same bit-exact results through a
     pipeline that runs its scan stream two steps ahead."""
@@ -283,7 +284,7 @@ def test_reserved_pipeline_placements(oracle, monkeypatch, dense):
     monkeypatch.setenv("HBX_K3_DENSE", dense)
     batches = _device_batches(oracle, 2, 43)
     got, order = [], [i % 2 for i in range(12)]
-    with Engine(0, md5_slice=2048) as e:
+    with Engine(0, md5_slice=2048, k3_waves=k3_waves) as e:
         e.reserve(10, max(len(b[2]) for b in batches), max(int(sum(b[2])) for b in batches))
         for i in order:
             dev, offs, sizes, _ = batches[i]
