@@ -46,7 +46,18 @@ import torch  # noqa: E402
 
 METRIC = "device-resident GiB/s chunked+hashed at 1/2/4/8 MI355X; % HBM roofline"
 K3_VALU_PER_BLOCK = 325
-VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
+# The path is VALU-issue-bound (DESIGN.md §6 "The bound"): PMC SQ_INSTS_VALU
+# per launch of the default workload (profiles/r02b_pmc_summary.txt) gives
+# the wave-instructions per input byte of K1 (6.825e8 / 8 GiB) and K3
+# (6.887e8 / 8 GiB); a SIMD retires at most one wave64 VALU instruction per
+# ~4.84 cycles on this integer mix (K3 one wave per SIMD: 1.21 quad-cycles
+# per VALU at 91 % issue-active; K1 alone, four waves per SIMD, the same
+# per-SIMD rate; K3 with two waves per SIMD, --k3-waves 2, takes 1.87x as
+# long per launch).  Peak = 1024 SIMDs x 2.4 GHz (spec clock) / 4.84.
+K1_WAVE_VALU_PER_BYTE = 6.825e8 / (8 << 30)
+K3_WAVE_VALU_PER_BYTE = 6.887e8 / (8 << 30)
+SIMD_CYCLES_PER_VALU = 4.84
+VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / SIMD_CYCLES_PER_VALU
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md), GB/s
 GIB = 1 << 30
 KNAMES = ["k1_digest_scan", "k2_cut_chain", "k2c_chain_plan", "k3_block_md5", "k4_content_id"]
@@ -375,10 +386,19 @@ def run_workload(a, name, eng, arenas, offs, lens, R, B, need, lanes, dist, gpu,
         # K3 is VALU-issue work: ~325 VALU per 64-B block on the cooperative
         # path (5 per MD5 step); chip peak 256 CU x 4 SIMD-32 x 32 lanes x
         # 2.4 GHz; one wave issues at most one VALU per 4 cycles.
-        "k3_valu": {"valu_per_block": K3_VALU_PER_BLOCK,
-                    "achieved_tops": round(k3_bps * K3_VALU_PER_BLOCK / 64 / 1e12, 3),
-                    "peak_tops": round(VALU_PEAK_LANE_OPS / 1e12, 2),
-                    "frac": round(k3_bps * K3_VALU_PER_BLOCK / 64 / VALU_PEAK_LANE_OPS, 4)},
+        # the whole path's bound: K1 + K3 VALU wave-instructions per step over
+        # the chip's measured issue capacity at the spec clock (the box runs
+        # power-capped at ~2.09 GHz while pipelined)
+        "valu_roofline": {"bound": "valu-issue", "unit": "wave-instr/s",
+                          "achieved": round(rank_batch * (K1_WAVE_VALU_PER_BYTE + K3_WAVE_VALU_PER_BYTE)
+                                            / (el / a.steps), 0),
+                          "peak": round(VALU_PEAK_WAVE_INSTR, 0),
+                          "frac": round(rank_batch * (K1_WAVE_VALU_PER_BYTE + K3_WAVE_VALU_PER_BYTE)
+                                        / (el / a.steps) / VALU_PEAK_WAVE_INSTR, 4),
+                          "k1_valu_per_byte": round(K1_WAVE_VALU_PER_BYTE * 64, 3),
+                          "k3_valu_per_byte": round(K3_WAVE_VALU_PER_BYTE * 64, 3),
+                          "simd_cycles_per_valu": SIMD_CYCLES_PER_VALU,
+                          "source": "profiles/r02b_pmc_summary.txt (SQ_INSTS_VALU), profiles/r02g_k3w2"},
         "k3_lanes": lane_occupancy(r["arena_res"], R, B, need, lanes),
         "kernel_ms_per_step": {n: round(float(v) / a.steps, 4) for n, v in zip(KNAMES, tot_ms)},
         "window_launches": {n: int(v) for n, v in zip(KNAMES, tot_n)},
