@@ -187,6 +187,7 @@ struct hbx_ctx {
   // one per SIMD), leaving whole CUs to the next batch's K1 (measured 1510 vs
   // 1255 GiB/s spread, 100 steps); 0 spreads them one per CU first
   uint32_t k3_dense = 1;
+  uint32_t k1_run = 64;       // K1 bytes per thread per iteration: 64 (1024 threads) or 128 (512, K1b)
   uint32_t k3_threads = 256;  // K3 workgroup: 256 = one wave per SIMD (hbx_k3_block_md5), 512 = two (_w2)
   uint32_t md5_slice = 16384; // K3 time slice: full MD5 blocks per chain per launch (0 = unlimited)
   // K1 gate (hbx_k1_gate): a batch's K1 waits until every workgroup of the K3
@@ -795,8 +796,12 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   HBX_TRY(c, hipEventRecord(b->ev[0], s));
   if (nt) {
     StageTimer t(c, s, 0);
-    hipLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3((uint32_t)nt), dim3(kK1Threads), 0, s, arena, d_off, d_len,
-                       d_sb, d_tiles, ssum.as<uint2>(), slices);
+    if (c->k1_run == 128u)
+      hipLaunchKernelGGL(hbx_k1_digest_scan_dma2, dim3((uint32_t)nt), dim3(kK1bThreads), 0, s, arena, d_off, d_len,
+                         d_sb, d_tiles, ssum.as<uint2>(), slices);
+    else
+      hipLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3((uint32_t)nt), dim3(kK1Threads), 0, s, arena, d_off, d_len,
+                         d_sb, d_tiles, ssum.as<uint2>(), slices);
   }
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(b->ev[1], s));
@@ -1057,6 +1062,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
     c->md5_wgs = (uint32_t)(ncu = prop.multiProcessorCount);
   if (const char* v = std::getenv("HBX_MD5_WGS")) c->md5_wgs = (uint32_t)std::max(1, std::atoi(v));
   if (const char* v = std::getenv("HBX_K3_DENSE")) c->k3_dense = std::atoi(v) ? 1u : 0u;
+  if (const char* v = std::getenv("HBX_K1_RUN")) c->k1_run = std::atoi(v) == 128 ? 128u : 64u;
   if (const char* v = std::getenv("HBX_K3_WAVES")) c->k3_threads = std::atoi(v) == 2 ? kK3Threads2 : kK3Threads;
   if (const char* v = std::getenv("HBX_TILE_ITERS")) c->tile_iters = (uint32_t)std::min(1024, std::max(0, std::atoi(v)));
   if (const char* v = std::getenv("HBX_JOIN_LAG")) c->join_lag = (uint32_t)std::min(4, std::max(1, std::atoi(v)));

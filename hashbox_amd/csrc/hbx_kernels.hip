@@ -383,6 +383,241 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_d
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup exits
 }
 
+// ------------------------------------------- K1b (128-byte runs, LDS-DMA) --
+// The same scan with half the per-byte overhead: 512 threads (8 waves, two
+// per SIMD), each owning 128 contiguous positions of a 64 KiB iteration, so
+// the run aggregates, the two wave scans, the cross-wave exchange, the
+// barrier and the slice maxima are paid once per 128 positions instead of 64
+// (K1's digest loop is 3.5 VALU per position, the rest was ~1.6 per byte;
+// the path is VALU-issue-bound, DESIGN.md §6 "The bound").  A wave covers two
+// slices (lanes 0-31, 32-63).  Four digest streams per lane (positions 0-31,
+// 32-63, 64-95, 96-127).  The wave's 8 KiB land in LDS by DMA in a swizzled
+// image: DMA op k fetches lane rows 8k..8k+7 (1 KiB contiguous in the file),
+// and row r's granule g sits at column g ^ ((r >> 1) & 7), so each lane's
+// ds_read_b128 of its own row is bank-conflict-free (every 16-lane group of
+// ds_read_b128 hits 16 distinct 4-bank columns; MI355X_MICROARCH.md LDS).
+constexpr int kK1bThreads = 512;
+constexpr uint32_t kK1bSlot = 8192;  // bytes per wave per iteration
+
+struct RunAgg4 {
+  uint32_t a[4], j[4];  // in-aggregates of positions [0, 32(s+1)) of the run
+};
+__device__ __forceinline__ RunAgg4 run_aggregates128(const uint32_t (&v)[32]) {
+  RunAgg4 r;
+  uint32_t a = 0, j = 0;
+#pragma unroll
+  for (int s = 0; s < 4; s++) {
+#pragma unroll
+    for (int k = 8 * s; k < 8 * s + 8; k++) {
+      a = dot4(v[k], 0x01010101u, a);
+      j = dot4(v[k], jw(k), j);
+    }
+    r.a[s] = a;
+    r.j[s] = j;
+  }
+  return r;
+}
+
+template <bool TAIL>
+__device__ __forceinline__ uint32_t digest_pass128(const uint32_t (&in)[32], const uint32_t (&out)[32],
+                                                   uint32_t (&X)[4], uint32_t e_l, uint32_t lim) {
+  uint32_t M = 0;
+  if (!TAIL) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      HBX_SDWA_DWORD(X[0], X[1], M, in[k], out[k], in[8 + k], out[8 + k]);
+      HBX_SDWA_DWORD(X[2], X[3], M, in[16 + k], out[16 + k], in[24 + k], out[24 + k]);
+    }
+    return M;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+#define HBX_SDWA_PAIR4(B)                                                            \
+    {                                                                                \
+      HBX_SDWA_STEP(X[0], in[k], out[k], B);                                         \
+      HBX_SDWA_STEP(X[1], in[8 + k], out[8 + k], B);                                 \
+      HBX_SDWA_STEP(X[2], in[16 + k], out[16 + k], B);                               \
+      HBX_SDWA_STEP(X[3], in[24 + k], out[24 + k], B);                               \
+      const uint32_t p = e_l + 4u * k + B;                                           \
+      const uint32_t D0 = p < lim ? X[0] : 0u, D1 = p + 32u < lim ? X[1] : 0u;       \
+      const uint32_t D2 = p + 64u < lim ? X[2] : 0u, D3 = p + 96u < lim ? X[3] : 0u; \
+      asm("v_max3_u32 %0, %0, %1, %2" : "+v"(M) : "v"(D0), "v"(D1));                \
+      asm("v_max3_u32 %0, %0, %1, %2" : "+v"(M) : "v"(D2), "v"(D3));                \
+    }
+    HBX_SDWA_PAIR4(0) HBX_SDWA_PAIR4(1) HBX_SDWA_PAIR4(2) HBX_SDWA_PAIR4(3)
+#undef HBX_SDWA_PAIR4
+  }
+  return M;
+}
+
+struct K1bState {
+  uint32_t S1c, s2c;  // state before the iteration's first position
+  RunAgg4 pa;         // in-aggregates of the previous run (= this run's "out")
+};
+
+// Half-wave max: lane 31 = max of lanes 0-31, lane 63 = max of lanes 32-63.
+__device__ __forceinline__ uint32_t half_max_to_31_63(uint32_t x) {
+  x = max(x, dpp<kRowShr1>(x));
+  x = max(x, dpp<kRowShr2>(x));
+  x = max(x, dpp<kRowShr4>(x));
+  x = max(x, dpp<kRowShr8>(x));
+  x = max(x, dpp<kRowBcast15, 0xa>(x));
+  return x;
+}
+
+extern "C" __global__ __launch_bounds__(kK1bThreads, 2) void hbx_k1_digest_scan_dma2(
+    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
+    const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ slice_base,
+    const uint4* __restrict__ tiles, uint2* __restrict__ ssum, uint64_t dummy) {
+  constexpr uint32_t W = kK1bThreads / 64;
+  __shared__ uint2 wtot[2][W];
+  __shared__ __attribute__((aligned(1024))) uint8_t land[W][2][kK1bSlot];
+  const uint4 td = tiles[blockIdx.x];
+  const uint32_t f = td.x;
+  const uint64_t N = file_len[f];
+  const uint64_t q0 = (uint64_t)td.y * kMinBlock;
+  const uint32_t tile_iters = td.z;
+  const uint8_t* fb = arena + file_off[f];
+  const uint64_t sb = slice_base[f];
+
+  const uint32_t tid = threadIdx.x;
+  const uint32_t l = tid & 63u;
+  const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+  const uint32_t e_l = w * kK1bSlot + l * 128u;
+
+  const uint64_t rem = N - q0;
+  const uint32_t n_it = (uint32_t)umin64(tile_iters, (rem + kMinBlock - 1) / kMinBlock);
+  const uint32_t nbytes = (uint32_t)((umin64(rem, (uint64_t)n_it * kMinBlock) + 15ull) & ~15ull);
+  const s32x4 srd = make_srd(fb + q0, nbytes);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)&land[w][0][0];
+  const uint32_t lds1 = (uint32_t)(uintptr_t)&land[w][1][0];
+  // DMA op k, lane i: row r = 8k + i/8 of the wave, column i%8 holds granule
+  // (i%8) ^ ((r>>1)&7); the offsets do not depend on the iteration
+  uint32_t voff[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint32_t r = 8u * (uint32_t)k + (l >> 3);
+    voff[k] = w * kK1bSlot + r * 128u + 16u * ((l & 7u) ^ ((r >> 1) & 7u));
+  }
+  auto issue = [&](uint32_t it, uint32_t lds) {  // 8 DMA ops, always issued
+#pragma unroll
+    for (int k = 0; k < 8; k++) dma16(srd, voff[k], it * kMinBlock, lds + 1024u * k);
+  };
+  const uint32_t xr = (l >> 1) & 7u;  // this lane's row swizzle
+  auto land_read = [&](uint32_t slot, uint32_t (&v)[32]) {
+    const uint8_t* row = &land[w][slot][l * 128u];
+#pragma unroll
+    for (int g = 0; g < 8; g++) {
+      const u32x4 t = *reinterpret_cast<const u32x4*>(row + 16u * ((uint32_t)g ^ xr));
+      v[4 * g + 0] = t.x;
+      v[4 * g + 1] = t.y;
+      v[4 * g + 2] = t.z;
+      v[4 * g + 3] = t.w;
+    }
+  };
+
+  uint32_t out[32];
+#pragma unroll
+  for (int k = 0; k < 32; k++) out[k] = 0u;
+  K1bState st;
+  if (q0 != 0) {  // prime: the state at q0-1 from the MIN bytes before q0
+    const __amdgpu_buffer_rsrc_t rh = make_rsrc_u(fb + q0 - kMinBlock, kMinBlock);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const u32x4 t = bload16(rh, e_l + 16u * k, 0u);
+      out[4 * k + 0] = t.x;
+      out[4 * k + 1] = t.y;
+      out[4 * k + 2] = t.z;
+      out[4 * k + 3] = t.w;
+    }
+    st.pa = run_aggregates128(out);
+    const uint32_t iA = wave_incl_sum(st.pa.a[3]);
+    const uint32_t iC = wave_incl_sum(e_l * st.pa.a[3] + st.pa.j[3]);
+    if (l == 63u) wtot[1][w] = make_uint2(iA, iC);
+    __syncthreads();
+    const uint2 t = (l < W) ? wtot[1][l] : make_uint2(0u, 0u);
+    const uint32_t sA = row_incl_sum(t.x), sC = row_incl_sum(t.y);
+    st.S1c = readlane(sA, 15);
+    st.s2c = 0x8000u - readlane(sC, 15);  // virtual-zero start: s2 = 2^15 - sum k*x_k
+  } else {
+#pragma unroll
+    for (int s = 0; s < 4; s++) st.pa.a[s] = st.pa.j[s] = 0u;
+    st.S1c = 0u;
+    st.s2c = 0x8000u;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  issue(0u, lds0);
+  issue(1u, lds1);  // past the tile end: out-of-range reads land zeros, never read
+  uint32_t run_b[32];
+  auto step = [&](uint32_t it, uint32_t (&cur)[32], const uint32_t (&prev)[32]) {
+    // outstanding, oldest first: DMA(it) x8, store(it-2), DMA(it+1) x8, store(it-1)
+    if (it == 0)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (it == 1)
+      asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    land_read(it & 1u, cur);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot consumed before it is refilled
+    issue(it + 2u, (it & 1u) ? lds1 : lds0);
+    const uint64_t qs = q0 + (uint64_t)it * kMinBlock;
+    // --- one iteration (k1_iteration with four streams per lane)
+    const RunAgg4 ca = run_aggregates128(cur);
+    uint32_t Ac[4], Jc[4];
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+      Ac[s] = ca.a[s] - st.pa.a[s];
+      Jc[s] = ca.j[s] - st.pa.j[s];
+    }
+    const uint32_t A_l = Ac[3], C_l = e_l * Ac[3] + Jc[3];
+    const uint32_t iA = wave_incl_sum(A_l);
+    const uint32_t iC = wave_incl_sum(C_l);
+    if (l == 63u) wtot[it & 1u][w] = make_uint2(iA, iC);
+    __syncthreads();
+    const uint2 t = (l < W) ? wtot[it & 1u][l] : make_uint2(0u, 0u);
+    const uint32_t sA = row_incl_sum(t.x), sC = row_incl_sum(t.y);
+    const uint32_t WA = w ? readlane(sA, (int)w - 1) : 0u;
+    const uint32_t WC = w ? readlane(sC, (int)w - 1) : 0u;
+    const uint32_t totA = readlane(sA, 15), totC = readlane(sC, 15);
+    const uint32_t A_pre = WA + (iA - A_l), C_pre = WC + (iC - C_l);
+    uint32_t X[4];
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+      const uint32_t Ap = A_pre + (s ? Ac[s - 1] : 0u);
+      const uint32_t Cp = C_pre + (s ? e_l * Ac[s - 1] + Jc[s - 1] : 0u);
+      const uint32_t S1 = st.S1c + Ap;
+      const uint32_t s2 = st.s2c + (e_l + 32u * (uint32_t)s) * S1 - Cp;
+      X[s] = (s2 << 16) | (S1 & 0xffffu);
+    }
+    const uint32_t sprev0 = readlane(X[0], 0), sprev1 = readlane(X[0], 32);
+    uint32_t M;
+    if (qs + kMinBlock <= N) {
+      M = digest_pass128<false>(cur, prev, X, e_l, 0u);
+    } else {
+      M = digest_pass128<true>(cur, prev, X, e_l, (uint32_t)(N - qs));
+    }
+    const uint32_t hm = half_max_to_31_63(M);
+    const uint32_t smax0 = readlane(hm, 31), smax1 = readlane(hm, 63);
+    st.S1c += totA;
+    st.s2c -= totC;  // 65536*(...) vanishes mod 2^16
+    st.pa = ca;
+    // slice summaries of the wave's two slices: ONE store instruction (lanes
+    // 0-3), always issued (slices past the file end go to the dummy slot)
+    const uint64_t sl = (qs >> kSliceShift) + 2u * w + (l >> 1);
+    const bool ok = (sl << kSliceShift) < N;
+    if (l < 4u) {
+      const uint32_t v = (l == 0u) ? smax0 : (l == 1u) ? sprev0 : (l == 2u) ? smax1 : sprev1;
+      reinterpret_cast<uint32_t*>(ssum + (ok ? sb + sl : dummy))[l & 1u] = v;
+    }
+  };
+  for (uint32_t it = 0; it < n_it; it += 2u) {
+    step(it, run_b, out);
+    if (it + 1u < n_it) step(it + 1u, out, run_b);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup exits
+}
+
 // ------------------------------------------------------------------ K2 --
 namespace {
 
