@@ -234,7 +234,14 @@ struct hbx_ctx {
   DevBuf d_zblk, d_zinfo, d_zoff, d_zlen, d_zout, d_zimg;  // hbx_deflate_blocks*
   DevBuf d_idesc, d_ires;                                  // hbx_inflate_blocks_device
   PinBuf h_read[2];         // hbx_store_paths: pinned landing slots for file reads
-  PinBuf h_zstage;          // hbx_store_paths_z: compressed streams of one batch
+  PinBuf h_zstage;          // hbx_store_paths_z: compressed streams of one batch (synchronous form)
+  // hbx_store_paths_z: two compression stages in flight on their own stream
+  struct ZStage {
+    DevBuf blk, info, off, len, img, out;
+    PinBuf desc, lens, stage;
+    hipEvent_t done = nullptr;
+  } zs[2];
+  hipStream_t zstream = nullptr;
   hipEvent_t h2d_done[2] = {nullptr, nullptr};  // slot's H2D copy has completed
   std::vector<DevBuf> d_ring;  // hbx_store_paths: device arenas of the batches in flight
   double io_s[3] = {0, 0, 0};  // hbx_store_paths: reading files | waiting for an arena | waiting for a copy
@@ -1121,6 +1128,15 @@ void hbx_ctx_destroy(hbx_ctx* c) {
     b->release();
   for (PinBuf& h : c->h_read) h.release();
   c->h_zstage.release();
+  if (c->zstream) (void)hipStreamSynchronize(c->zstream);
+  for (auto& z : c->zs) {
+    for (DevBuf* b : {&z.blk, &z.info, &z.off, &z.len, &z.img, &z.out}) b->release();
+    z.desc.release();
+    z.lens.release();
+    z.stage.release();
+    if (z.done) (void)hipEventDestroy(z.done);
+  }
+  if (c->zstream) (void)hipStreamDestroy(c->zstream);
   c->h_k3t.release();
   c->h_probe.release();
   for (DevBuf& d : c->d_ring) d.release();
@@ -1544,56 +1560,105 @@ struct ZJob {
   std::vector<uint64_t> offs;
 };
 
-// CompressData of every chunk of a collected batch (client.go:249-258): K7
-// on the batch's arena, one copy of the streams back, packed per file at
-// zout[zbase[f] ..].
-int deflate_batch(hbx_ctx* c, const ZJob& j, const uint64_t* cut_ends, const uint64_t* out_base,
-                  const hbx_file_summary* sums, const ZOut& z, uint32_t threads) {
-  std::vector<uint64_t> src, len, dst;
-  uint64_t d = 0;
-  for (uint64_t i = 0; i < j.count; i++) {
-    const uint64_t f = j.first + i;
+// CompressData of every chunk of a collected batch (client.go:249-258),
+// asynchronous: K7 reads the batch's arena on the engine's compression
+// stream and the streams come back in one D2H copy into a pinned stage, while
+// the caller's loop goes on reading and copying later batches.  Two stages
+// rotate; a stage is unpacked (streams placed per file at zout[zbase[f] ..],
+// the batch's callback) before it is reused, and every job is unpacked in
+// FIFO order before hbx_store_paths_z returns.
+struct ZPend {
+  ZJob job;
+  int stage = 0;
+  std::vector<uint64_t> dst;  // stream offset of each chunk in the stage
+};
+
+int z_start(hbx_ctx* c, ZPend& zp, const uint64_t* cut_ends, const uint64_t* out_base,
+            const hbx_file_summary* sums) {
+  auto& Z = c->zs[zp.stage];
+  std::vector<hbxz::ZBlock> zb;
+  uint64_t d = 0, nseg = 0;
+  for (uint64_t i = 0; i < zp.job.count; i++) {
+    const uint64_t f = zp.job.first + i;
     uint64_t start = 0;
     for (uint32_t q = 0; q < sums[f].n_chunks; q++) {
       const uint64_t e = cut_ends[out_base[f] + q];
-      src.push_back(reinterpret_cast<uint64_t>(j.arena + j.offs[i] + start));
-      len.push_back(e - start);
-      dst.push_back(d);
-      d += (hbx_deflate_bound(e - start) + 15) & ~uint64_t(15);
+      const uint64_t len = e - start, ns = (len + hbxz::kSeg - 1) / hbxz::kSeg;
+      zb.push_back(hbxz::ZBlock{reinterpret_cast<uint64_t>(zp.job.arena + zp.job.offs[i] + start), d, len,
+                                (uint32_t)nseg, (uint32_t)ns});
+      zp.dst.push_back(d);
+      d += (hbx_deflate_bound(len) + 15) & ~uint64_t(15);
+      nseg += ns;
       start = e;
     }
   }
-  const uint64_t nc = src.size();
-  if (nc == 0) return HBX_OK;
-  HBX_TRY(c, c->d_zout.ensure(d + 64));
-  HBX_TRY(c, c->h_zstage.ensure(d + 64));
-  std::vector<uint64_t> dabs(nc), ol(nc);
-  for (uint64_t i = 0; i < nc; i++) dabs[i] = reinterpret_cast<uint64_t>(c->d_zout.as<uint8_t>() + dst[i]);
-  const int rc = deflate_device(c, nc, src.data(), len.data(), dabs.data(), ol.data());
-  if (rc) return rc;
-  HBX_TRY(c, hipMemcpy(c->h_zstage.p, c->d_zout.p, d, hipMemcpyDeviceToHost));
-  const uint8_t* h = c->h_zstage.as<uint8_t>();
-  // placement (serial, cheap), then the copies out of the pinned stage on
-  // `threads` threads (one thread copies a few GB/s)
-  std::vector<uint64_t> to(nc);
-  uint64_t k = 0;
-  for (uint64_t i = 0; i < j.count; i++) {
-    const uint64_t f = j.first + i;
-    uint64_t run = z.zbase[f];
-    for (uint32_t q = 0; q < sums[f].n_chunks; q++, k++) {
-      to[k] = run;
-      z.zoff[out_base[f] + q] = run;
-      z.zlen[out_base[f] + q] = ol[k];
-      run += ol[k];
+  const uint64_t n = zb.size();
+  if (n == 0) return HBX_OK;
+  if (nseg > 0x7FFFFFFFull) return c->fail(HBX_ERR_ARG, "too much data in one batch");
+  if (!c->zstream) HBX_TRY(c, hipStreamCreateWithFlags(&c->zstream, hipStreamNonBlocking));
+  if (!Z.done) HBX_TRY(c, hipEventCreateWithFlags(&Z.done, hipEventDisableTiming));
+  HBX_TRY(c, Z.out.ensure(d + 64));
+  HBX_TRY(c, Z.stage.ensure(d + 64));
+  HBX_TRY(c, Z.desc.ensure(n * sizeof(hbxz::ZBlock)));
+  HBX_TRY(c, Z.lens.ensure(n * 8));
+  HBX_TRY(c, Z.blk.ensure(n * sizeof(hbxz::ZBlock)));
+  HBX_TRY(c, Z.info.ensure(std::max<uint64_t>(nseg, 1) * sizeof(hbxz::SegInfo)));
+  HBX_TRY(c, Z.off.ensure(std::max<uint64_t>(nseg, 1) * 8));
+  HBX_TRY(c, Z.len.ensure(n * 8));
+  HBX_TRY(c, Z.img.ensure(std::max<uint64_t>(nseg, 1) * hbxz::kSlot));
+  const uint64_t base = reinterpret_cast<uint64_t>(Z.out.p);
+  for (auto& x : zb) x.dst += base;  // stage offsets -> device addresses
+  std::memcpy(Z.desc.p, zb.data(), n * sizeof(hbxz::ZBlock));
+  hipStream_t s = c->zstream;
+  HBX_TRY(c, hipMemcpyAsync(Z.blk.p, Z.desc.p, n * sizeof(hbxz::ZBlock), hipMemcpyHostToDevice, s));
+  const hbxz::ZBlock* dz = Z.blk.as<hbxz::ZBlock>();
+  hipLaunchKernelGGL(hbx_k7_deflate_size, dim3((uint32_t)nseg), dim3(hbxz::kThreads), 0, s, dz, (uint32_t)n,
+                     (uint32_t)nseg, Z.info.as<hbxz::SegInfo>(), Z.img.as<uint32_t>());
+  HBX_TRY(c, hipGetLastError());
+  hipLaunchKernelGGL(hbx_k7_deflate_plan, dim3((uint32_t)n), dim3(64), 0, s, dz, (uint32_t)n,
+                     Z.info.as<hbxz::SegInfo>(), Z.off.as<uint64_t>(), Z.len.as<uint64_t>());
+  HBX_TRY(c, hipGetLastError());
+  hipLaunchKernelGGL(hbx_k7_deflate_write, dim3((uint32_t)nseg), dim3(hbxz::kThreads), 0, s, (uint32_t)nseg,
+                     Z.info.as<hbxz::SegInfo>(), Z.img.as<uint32_t>(), Z.off.as<uint64_t>());
+  HBX_TRY(c, hipGetLastError());
+  HBX_TRY(c, hipMemcpyAsync(Z.lens.p, Z.len.p, n * 8, hipMemcpyDeviceToHost, s));
+  HBX_TRY(c, hipMemcpyAsync(Z.stage.p, Z.out.p, d, hipMemcpyDeviceToHost, s));
+  HBX_TRY(c, hipEventRecord(Z.done, s));
+  return HBX_OK;
+}
+
+// Wait for a started job, place its streams and call the batch back.
+int z_finish(hbx_ctx* c, const ZPend& zp, const uint64_t* out_base, const hbx_file_summary* sums, const ZOut& z,
+             uint32_t threads) {
+  const auto& Z = c->zs[zp.stage];
+  const uint64_t nc = zp.dst.size();
+  if (nc) {
+    HBX_TRY(c, hipEventSynchronize(Z.done));
+    const uint8_t* h = Z.stage.as<uint8_t>();
+    const uint64_t* ol = Z.lens.as<uint64_t>();
+    // placement (serial, cheap), then the copies out of the pinned stage on
+    // `threads` threads (one thread copies a few GB/s)
+    std::vector<uint64_t> to(nc);
+    uint64_t k = 0;
+    for (uint64_t i = 0; i < zp.job.count; i++) {
+      const uint64_t f = zp.job.first + i;
+      uint64_t run = z.zbase[f];
+      for (uint32_t q = 0; q < sums[f].n_chunks; q++, k++) {
+        to[k] = run;
+        z.zoff[out_base[f] + q] = run;
+        z.zlen[out_base[f] + q] = ol[k];
+        run += ol[k];
+      }
     }
+    const uint32_t nt = std::max<uint32_t>(1u, std::min<uint32_t>(threads, 64u));
+    std::vector<std::thread> pool;
+    for (uint32_t t = 0; t < nt; t++)
+      pool.emplace_back([&, t] {
+        for (uint64_t i = t; i < nc; i += nt) std::memcpy(z.zout + to[i], h + zp.dst[i], ol[i]);
+      });
+    for (auto& th : pool) th.join();
   }
-  const uint32_t nt = std::max<uint32_t>(1u, std::min<uint32_t>(threads, 64u));
-  std::vector<std::thread> pool;
-  for (uint32_t t = 0; t < nt; t++)
-    pool.emplace_back([&, t] {
-      for (uint64_t i = t; i < nc; i += nt) std::memcpy(z.zout + to[i], h + dst[i], ol[i]);
-    });
-  for (auto& th : pool) th.join();
+  if (z.ready) z.ready(z.user, zp.job.first, zp.job.count);
   return HBX_OK;
 }
 
@@ -1686,15 +1751,33 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
   std::vector<uint64_t> offs;
   uint64_t f = 0, k = 0;
   int rc = HBX_OK;
-  // with compression, each collected batch is compressed from its arena
-  // before the arena takes the next batch (FIFO, like the collection)
+  // with compression, each collected batch is compressed from its arena on
+  // the compression stream (z_start); the next batch copied into that arena
+  // waits for it on the GPU, and the host unpacks a stage (z_finish, FIFO)
+  // before reusing it and at the end
   std::deque<ZJob> jobs;
+  std::deque<ZPend> zq;
+  uint64_t zjobs = 0;
+  int arena_zstage = -1;  // the stage that reads the arena just freed by collect()
+  auto zdrain_one = [&]() -> int {
+    const int r = z_finish(c, zq.front(), out_base, sums, z, io_threads);
+    zq.pop_front();
+    return r;
+  };
   auto collect = [&]() -> int {
     int r = wait_oldest(c);
-    if (z.zout) {
-      if (!r && !jobs.empty()) r = deflate_batch(c, jobs.front(), cut_ends, out_base, sums, z, io_threads);
-      if (!r && !jobs.empty() && z.ready) z.ready(z.user, jobs.front().first, jobs.front().count);
-      if (!jobs.empty()) jobs.pop_front();
+    arena_zstage = -1;
+    if (z.zout && !jobs.empty()) {
+      if (!r && zq.size() >= 2) r = zdrain_one();  // the stage this job takes
+      if (!r) {
+        ZPend zp;
+        zp.job = std::move(jobs.front());
+        zp.stage = (int)(zjobs++ & 1u);
+        r = z_start(c, zp, cut_ends, out_base, sums);
+        arena_zstage = zp.stage;
+        zq.push_back(std::move(zp));
+      }
+      jobs.pop_front();
     }
     return r;
   };
@@ -1720,6 +1803,11 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
     c->io_s[1] += t1 - t0;
     c->io_s[2] += t2 - t1;
     if (rc) break;
+    // the arena's previous batch may still be read by its compression job
+    if (arena_zstage >= 0 && c->zs[arena_zstage].done &&
+        (rc = c->hip(hipStreamWaitEvent(c->stream, c->zs[arena_zstage].done, 0), "hipStreamWaitEvent")))
+      break;
+    arena_zstage = -1;
     if ((rc = c->hip(hipMemcpyAsync(arena.p, c->h_read[p].p, tot, hipMemcpyHostToDevice, c->stream),
                      "hipMemcpyAsync")))
       break;
@@ -1739,6 +1827,16 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
     const int r2 = rc == HBX_OK ? collect() : wait_oldest(c);
     if (rc == HBX_OK) rc = r2;
     else c->err = keep;
+  }
+  // every compression job unpacked (also after a failure: the stages must be
+  // idle before the arena ring is reused)
+  while (!zq.empty()) {
+    if (rc == HBX_OK) {
+      rc = zdrain_one();
+    } else {
+      if (c->zs[zq.front().stage].done) (void)hipEventSynchronize(c->zs[zq.front().stage].done);
+      zq.pop_front();
+    }
   }
   c->io_s[1] += now() - td;
   return rc;
