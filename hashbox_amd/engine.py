@@ -76,6 +76,21 @@ def _p(a: np.ndarray) -> int:
     return a.ctypes.data if a.size else 0
 
 
+def _huge_host_buffer(nbytes: int) -> np.ndarray:
+    """A host byte buffer the library fills once (the compressed streams of a
+    whole store_paths call): an anonymous mapping advised for transparent
+    huge pages, so its first touch costs one fault per 2 MiB instead of per
+    4 KiB (60 GB of 4 KiB first-touch faults cost ~1.4 s on 16 threads)."""
+    import mmap
+    m = mmap.mmap(-1, max(nbytes, 1), flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+    if hasattr(mmap, "MADV_HUGEPAGE"):
+        try:
+            m.madvise(mmap.MADV_HUGEPAGE)
+        except OSError:
+            pass
+    return np.frombuffer(m, np.uint8)  # the array keeps the mapping alive
+
+
 class Engine:
     """One MI355X (one HIP stream) running the chunk + block-ID path."""
 
@@ -501,7 +516,7 @@ class Engine:
         zbase = np.zeros(max(lens.size, 1), np.uint64)
         if lens.size > 1:
             zbase[1:lens.size] = np.cumsum(fb[:-1])
-        zout = np.empty(int(fb.sum()) + 16, np.uint8)
+        zout = _huge_host_buffer(int(fb.sum()) + 16)
         zoff = np.zeros(max(int(caps.sum()), 1), np.uint64)
         zlen = np.zeros_like(zoff)
         zargs = (self._ctx, len(enc), ctypes.cast(arr, ctypes.c_void_p), _p(lens), _p(cuts), _p(ids),
