@@ -240,8 +240,8 @@ struct hbx_ctx {
     DevBuf blk, info, off, len, img, out;
     PinBuf desc, lens, stage;
     hipEvent_t done = nullptr;
+    hipStream_t stream = nullptr;  // one per stage: one job's K7 overlaps the other's copy-back
   } zs[2];
-  hipStream_t zstream = nullptr;
   hipEvent_t h2d_done[2] = {nullptr, nullptr};  // slot's H2D copy has completed
   std::vector<DevBuf> d_ring;  // hbx_store_paths: device arenas of the batches in flight
   double io_s[3] = {0, 0, 0};  // hbx_store_paths: reading files | waiting for an arena | waiting for a copy
@@ -1128,15 +1128,16 @@ void hbx_ctx_destroy(hbx_ctx* c) {
     b->release();
   for (PinBuf& h : c->h_read) h.release();
   c->h_zstage.release();
-  if (c->zstream) (void)hipStreamSynchronize(c->zstream);
+  for (auto& z : c->zs)
+    if (z.stream) (void)hipStreamSynchronize(z.stream);
   for (auto& z : c->zs) {
     for (DevBuf* b : {&z.blk, &z.info, &z.off, &z.len, &z.img, &z.out}) b->release();
     z.desc.release();
     z.lens.release();
     z.stage.release();
     if (z.done) (void)hipEventDestroy(z.done);
+    if (z.stream) (void)hipStreamDestroy(z.stream);
   }
-  if (c->zstream) (void)hipStreamDestroy(c->zstream);
   c->h_k3t.release();
   c->h_probe.release();
   for (DevBuf& d : c->d_ring) d.release();
@@ -1562,7 +1563,7 @@ struct ZJob {
 
 // CompressData of every chunk of a collected batch (client.go:249-258),
 // asynchronous: K7 reads the batch's arena on the engine's compression
-// stream and the streams come back in one D2H copy into a pinned stage, while
+// streams (one per stage) and the streams come back in one D2H copy into a pinned stage, while
 // the caller's loop goes on reading and copying later batches.  Two stages
 // rotate; a stage is unpacked (streams placed per file at zout[zbase[f] ..],
 // the batch's callback) before it is reused, and every job is unpacked in
@@ -1595,7 +1596,7 @@ int z_start(hbx_ctx* c, ZPend& zp, const uint64_t* cut_ends, const uint64_t* out
   const uint64_t n = zb.size();
   if (n == 0) return HBX_OK;
   if (nseg > 0x7FFFFFFFull) return c->fail(HBX_ERR_ARG, "too much data in one batch");
-  if (!c->zstream) HBX_TRY(c, hipStreamCreateWithFlags(&c->zstream, hipStreamNonBlocking));
+  if (!Z.stream) HBX_TRY(c, hipStreamCreateWithFlags(&Z.stream, hipStreamNonBlocking));
   if (!Z.done) HBX_TRY(c, hipEventCreateWithFlags(&Z.done, hipEventDisableTiming));
   HBX_TRY(c, Z.out.ensure(d + 64));
   HBX_TRY(c, Z.stage.ensure(d + 64));
@@ -1609,7 +1610,7 @@ int z_start(hbx_ctx* c, ZPend& zp, const uint64_t* cut_ends, const uint64_t* out
   const uint64_t base = reinterpret_cast<uint64_t>(Z.out.p);
   for (auto& x : zb) x.dst += base;  // stage offsets -> device addresses
   std::memcpy(Z.desc.p, zb.data(), n * sizeof(hbxz::ZBlock));
-  hipStream_t s = c->zstream;
+  hipStream_t s = Z.stream;
   HBX_TRY(c, hipMemcpyAsync(Z.blk.p, Z.desc.p, n * sizeof(hbxz::ZBlock), hipMemcpyHostToDevice, s));
   const hbxz::ZBlock* dz = Z.blk.as<hbxz::ZBlock>();
   hipLaunchKernelGGL(hbx_k7_deflate_size, dim3((uint32_t)nseg), dim3(hbxz::kThreads), 0, s, dz, (uint32_t)n,
