@@ -1630,11 +1630,13 @@ int z_start(hbx_ctx* c, ZPend& zp, const uint64_t* cut_ends, const uint64_t* out
 
 // Wait for a started job, place its streams and call the batch back.
 int z_finish(hbx_ctx* c, const ZPend& zp, const uint64_t* out_base, const hbx_file_summary* sums, const ZOut& z,
-             uint32_t threads) {
+             uint32_t threads, double& t_sync) {
   const auto& Z = c->zs[zp.stage];
   const uint64_t nc = zp.dst.size();
   if (nc) {
+    const auto t0 = std::chrono::steady_clock::now();
     HBX_TRY(c, hipEventSynchronize(Z.done));
+    t_sync += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     const uint8_t* h = Z.stage.as<uint8_t>();
     const uint64_t* ol = Z.lens.as<uint64_t>();
     // placement (serial, cheap), then the copies out of the pinned stage on
@@ -1759,14 +1761,19 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
   std::deque<ZJob> jobs;
   std::deque<ZPend> zq;
   uint64_t zjobs = 0;
+  double zt[4] = {0, 0, 0, 0};  // HBX_ZDIAG: wait_oldest | z_start | z_finish | its event waits
   int arena_zstage = -1;  // the stage that reads the arena just freed by collect()
   auto zdrain_one = [&]() -> int {
-    const int r = z_finish(c, zq.front(), out_base, sums, z, io_threads);
+    const double t0 = now();
+    const int r = z_finish(c, zq.front(), out_base, sums, z, io_threads, zt[3]);
+    zt[2] += now() - t0;
     zq.pop_front();
     return r;
   };
   auto collect = [&]() -> int {
+    const double t0 = now();
     int r = wait_oldest(c);
+    zt[0] += now() - t0;
     arena_zstage = -1;
     if (z.zout && !jobs.empty()) {
       if (!r && zq.size() >= 2) r = zdrain_one();  // the stage this job takes
@@ -1774,7 +1781,9 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
         ZPend zp;
         zp.job = std::move(jobs.front());
         zp.stage = (int)(zjobs++ & 1u);
+        const double t1 = now();
         r = z_start(c, zp, cut_ends, out_base, sums);
+        zt[1] += now() - t1;
         arena_zstage = zp.stage;
         zq.push_back(std::move(zp));
       }
@@ -1840,6 +1849,9 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
     }
   }
   c->io_s[1] += now() - td;
+  if (z.zout && std::getenv("HBX_ZDIAG"))
+    std::fprintf(stderr, "zdiag: wait_oldest %.3f s, z_start %.3f s, z_finish %.3f s (event waits %.3f s), jobs %llu\n",
+                 zt[0], zt[1], zt[2], zt[3], (unsigned long long)zjobs);
   return rc;
 }
 }  // namespace
