@@ -1734,7 +1734,7 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
   if (c->d_ring.size() < depth) c->d_ring.resize(depth);
   // size every staging buffer once, for the largest batch this call forms
   // (growing one later would re-pin host memory or drain the streams)
-  uint64_t biggest = 0;
+  uint64_t biggest = 0, zbytes = 0, zchunks = 0, zsegs = 0;
   for (uint64_t i = 0; i < n;) {
     uint64_t tot = 0, cnt = 0;
     while (i < n && (cnt == 0 || tot + lens[i] <= batch_bytes) && cnt < 65536) {
@@ -1743,8 +1743,26 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
       cnt++;
     }
     biggest = std::max(biggest, tot);
+    // compression stage bounds of this batch: chunks <= a file's
+    // max_chunks, a chunk's stream <= hbx_deflate_bound rounded to 16 B
+    const uint64_t nch = tot / HBX_MIN_BLOCK_SIZE + cnt;
+    zchunks = std::max(zchunks, nch);
+    zsegs = std::max(zsegs, tot / hbxz::kSeg + nch);
+    zbytes = std::max<uint64_t>(zbytes, tot + 5ull * (tot / hbxz::kSeg) + 31ull * nch + 64);
   }
   for (PinBuf& h : c->h_read) HBX_TRY(c, h.ensure(biggest + 65536));
+  if (z.zout)  // every compression stage sized once (growing one would re-pin or drain the device)
+    for (auto& Z : c->zs) {
+      HBX_TRY(c, Z.out.ensure(zbytes));
+      HBX_TRY(c, Z.stage.ensure(zbytes));
+      HBX_TRY(c, Z.desc.ensure(zchunks * sizeof(hbxz::ZBlock)));
+      HBX_TRY(c, Z.lens.ensure(zchunks * 8));
+      HBX_TRY(c, Z.blk.ensure(zchunks * sizeof(hbxz::ZBlock)));
+      HBX_TRY(c, Z.info.ensure(std::max<uint64_t>(zsegs, 1) * sizeof(hbxz::SegInfo)));
+      HBX_TRY(c, Z.off.ensure(std::max<uint64_t>(zsegs, 1) * 8));
+      HBX_TRY(c, Z.len.ensure(zchunks * 8));
+      HBX_TRY(c, Z.img.ensure(std::max<uint64_t>(zsegs, 1) * hbxz::kSlot));
+    }
   for (size_t i = 0; i < depth; i++) {
     int r0 = ensure_shared(c, c->d_ring[i], biggest + 65536);
     if (r0) return r0;
