@@ -22,6 +22,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <future>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -1572,6 +1573,8 @@ struct ZPend {
   ZJob job;
   int stage = 0;
   std::vector<uint64_t> dst;  // stream offset of each chunk in the stage
+  std::shared_future<int> fin;  // its unpack (z_finish), on a worker thread
+  double t_sync = 0.0;          // HBX_ZDIAG: time that unpack waited for the GPU
 };
 
 int z_start(hbx_ctx* c, ZPend& zp, const uint64_t* cut_ends, const uint64_t* out_base,
@@ -1783,8 +1786,9 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
   int arena_zstage = -1;  // the stage that reads the arena just freed by collect()
   auto zdrain_one = [&]() -> int {
     const double t0 = now();
-    const int r = z_finish(c, zq.front(), out_base, sums, z, io_threads, zt[3]);
+    const int r = zq.front().fin.get();
     zt[2] += now() - t0;
+    zt[3] += zq.front().t_sync;
     zq.pop_front();
     return r;
   };
@@ -1803,7 +1807,26 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
         r = z_start(c, zp, cut_ends, out_base, sums);
         zt[1] += now() - t1;
         arena_zstage = zp.stage;
+        // the unpack runs on a worker thread while this loop reads and copies
+        // the next batches; each waits for its predecessor (FIFO callbacks)
+        std::shared_future<int> prev = zq.empty() ? std::shared_future<int>() : zq.back().fin;
         zq.push_back(std::move(zp));
+        if (!r) {
+          ZPend* zpp = &zq.back();  // a deque keeps element addresses on push_back / pop_front
+          const uint32_t ut = std::max<uint32_t>(1u, io_threads / 2u);
+          zpp->fin = std::async(std::launch::async, [c, zpp, prev, out_base, sums, &z, ut]() -> int {
+                       if (prev.valid()) {
+                         const int r0 = prev.get();
+                         if (r0) return r0;
+                       }
+                       (void)hipSetDevice(c->device);
+                       return z_finish(c, *zpp, out_base, sums, z, ut, zpp->t_sync);
+                     }).share();
+        } else {
+          std::promise<int> pr;
+          pr.set_value(r);
+          zq.back().fin = pr.get_future().share();
+        }
       }
       jobs.pop_front();
     }
@@ -1862,7 +1885,7 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
     if (rc == HBX_OK) {
       rc = zdrain_one();
     } else {
-      if (c->zs[zq.front().stage].done) (void)hipEventSynchronize(c->zs[zq.front().stage].done);
+      zq.front().fin.wait();  // its worker must be done before the stages and arenas go
       zq.pop_front();
     }
   }
