@@ -236,13 +236,14 @@ struct hbx_ctx {
   DevBuf d_idesc, d_ires;                                  // hbx_inflate_blocks_device
   PinBuf h_read[2];         // hbx_store_paths: pinned landing slots for file reads
   PinBuf h_zstage;          // hbx_store_paths_z: compressed streams of one batch (synchronous form)
-  // hbx_store_paths_z: two compression stages in flight on their own stream
+  // hbx_store_paths_z: compression stages in flight, each on its own stream
+  static constexpr int kZStages = 3;
   struct ZStage {
     DevBuf blk, info, off, len, img, out;
     PinBuf desc, lens, stage;
     hipEvent_t done = nullptr;
-    hipStream_t stream = nullptr;  // one per stage: one job's K7 overlaps the other's copy-back
-  } zs[2];
+    hipStream_t stream = nullptr;  // one per stage: one job's K7 overlaps another's copy-back
+  } zs[kZStages];
   hipEvent_t h2d_done[2] = {nullptr, nullptr};  // slot's H2D copy has completed
   std::vector<DevBuf> d_ring;  // hbx_store_paths: device arenas of the batches in flight
   double io_s[3] = {0, 0, 0};  // hbx_store_paths: reading files | waiting for an arena | waiting for a copy
@@ -1565,7 +1566,7 @@ struct ZJob {
 // CompressData of every chunk of a collected batch (client.go:249-258),
 // asynchronous: K7 reads the batch's arena on the engine's compression
 // streams (one per stage) and the streams come back in one D2H copy into a pinned stage, while
-// the caller's loop goes on reading and copying later batches.  Two stages
+// the caller's loop goes on reading and copying later batches.  Three stages
 // rotate; a stage is unpacked (streams placed per file at zout[zbase[f] ..],
 // the batch's callback) before it is reused, and every job is unpacked in
 // FIFO order before hbx_store_paths_z returns.
@@ -1798,11 +1799,11 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
     zt[0] += now() - t0;
     arena_zstage = -1;
     if (z.zout && !jobs.empty()) {
-      if (!r && zq.size() >= 2) r = zdrain_one();  // the stage this job takes
+      if (!r && zq.size() >= (size_t)hbx_ctx::kZStages) r = zdrain_one();  // the stage this job takes
       if (!r) {
         ZPend zp;
         zp.job = std::move(jobs.front());
-        zp.stage = (int)(zjobs++ & 1u);
+        zp.stage = (int)(zjobs++ % (uint64_t)hbx_ctx::kZStages);
         const double t1 = now();
         r = z_start(c, zp, cut_ends, out_base, sums);
         zt[1] += now() - t1;
