@@ -398,10 +398,12 @@ int hbx_inflate_blocks_device(hbx_ctx *ctx, const void *d_in, uint64_t n, const 
                               const uint64_t *out_caps, uint64_t *out_lens, uint32_t *status);
 
 /* hbx_store_paths_z with a callback per collected batch: ready(user, first,
- * count) runs on the calling thread as soon as files [first, first+count)
- * have their cut_ends, ids, summaries and zlib streams written, so a sender
- * can put those blocks on the wire while later batches are still read and
- * hashed.  It must return quickly and must not call into the same context. */
+ * count) runs as soon as files [first, first+count) have their cut_ends, ids,
+ * summaries and zlib streams written, so a sender can put those blocks on the
+ * wire while later batches are still read and hashed.  The calls come from
+ * an engine worker thread (the one that unpacked the batch's compressed
+ * streams), one at a time and in file order, all before this function
+ * returns.  It must return quickly and must not call into the same context. */
 typedef void (*hbx_batch_ready_fn)(void *user, uint64_t first_file, uint64_t n_files);
 int hbx_store_paths_zcb(hbx_ctx *ctx, uint64_t n_files, const char *const *paths, const uint64_t *lens,
                         uint64_t *cut_ends, uint8_t *ids, const uint64_t *out_base, const uint64_t *caps,
