@@ -189,8 +189,7 @@ struct hbx_ctx {
   // 1255 GiB/s spread, 100 steps); 0 spreads them one per CU first
   uint32_t k3_dense = 1;
   uint32_t k1_run = 64;       // K1 bytes per thread per iteration: 64 (1024 threads) or 128 (512, K1b)
-  uint32_t k3_threads = 256;
-  bool k3_sets3 = false;      // A/B: hbx_k3_block_md5_s3 (HBX_K3_SETS=3)  // K3 workgroup: 256 = one wave per SIMD (hbx_k3_block_md5), 512 = two (_w2)
+  uint32_t k3_threads = 256;  // K3 workgroup: 256 = one wave per SIMD (hbx_k3_block_md5), 512 = two (_w2)
   uint32_t md5_slice = 16384; // K3 time slice: full MD5 blocks per chain per launch (0 = unlimited)
   // K1 gate (hbx_k1_gate): a batch's K1 waits until every workgroup of the K3
   // launch of the same submit has been dispatched.  k3_started counts K3
@@ -533,9 +532,7 @@ int md5_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
     c->k3_open.push_back(L);
   }
   const uint32_t waves = c->md5_wgs * (c->k3_threads / 64);
-  hipLaunchKernelGGL(c->k3_threads == (uint32_t)kK3Threads2 ? hbx_k3_block_md5_w2
-                     : c->k3_sets3                      ? hbx_k3_block_md5_s3
-                                                        : hbx_k3_block_md5,
+  hipLaunchKernelGGL(c->k3_threads == (uint32_t)kK3Threads2 ? hbx_k3_block_md5_w2 : hbx_k3_block_md5,
                      dim3(c->md5_wgs), dim3(c->k3_threads), 0, s,
                      c->d_order[slot].as<OrderEntry>(), static_cast<const uint32_t*>(c->d_octl[slot].as<uint32_t>()),
                      budget, c->k3_dense, c->d_gate.as<uint32_t>(), c->k3_dispatched, c->k3_waves + waves - 1u, tslot,
@@ -1075,7 +1072,6 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = std::getenv("HBX_MD5_WGS")) c->md5_wgs = (uint32_t)std::max(1, std::atoi(v));
   if (const char* v = std::getenv("HBX_K3_DENSE")) c->k3_dense = std::atoi(v) ? 1u : 0u;
   if (const char* v = std::getenv("HBX_K1_RUN")) c->k1_run = std::atoi(v) == 128 ? 128u : 64u;
-  if (const char* v = std::getenv("HBX_K3_SETS")) c->k3_sets3 = std::atoi(v) == 3;
   if (const char* v = std::getenv("HBX_K3_WAVES")) c->k3_threads = std::atoi(v) == 2 ? kK3Threads2 : kK3Threads;
   if (const char* v = std::getenv("HBX_TILE_ITERS")) c->tile_iters = (uint32_t)std::min(1024, std::max(0, std::atoi(v)));
   if (const char* v = std::getenv("HBX_JOIN_LAG")) c->join_lag = (uint32_t)std::min(4, std::max(1, std::atoi(v)));

@@ -1530,18 +1530,6 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
                                            tslot, probe);
 }
 
-// A/B (HBX_K3_SETS=3): one wave per SIMD with three register sets of
-// cooperative loads in flight (12 blocks of look-ahead instead of 8).
-extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5_s3(
-    const OrderEntry* __restrict__ order, const uint32_t* __restrict__ n_order, uint32_t budget,
-    uint32_t dense, uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last,
-    uint64_t* __restrict__ tslot, uint64_t* __restrict__ probe) {
-  __shared__ __attribute__((aligned(16))) uint8_t k3_lds[kK3Threads / 64][Coop<16>::WaveLds];
-  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  k3_body<kK3Threads, 16, 3, HBX_MD5_RING>(k3_lds[wave], order, n_order, budget, dense, started, t_first, t_last,
-                                           tslot, probe);
-}
-
 // Two waves per SIMD (the MD5 chain runs at one wave's issue rate, and two
 // waves of a SIMD each keep that rate: tools/ubench/valu_latency), so the
 // same chains fill half the CUs and leave the rest to the next batch's K1:
