@@ -168,10 +168,10 @@ struct hbx_ctx {
   std::mutex mu;
   std::string err;
   // K1 tile length in 64 KiB iterations; 0 = per batch (k1_tile_iters):
-  // about two tiles per CU, 16..256.  At 8 GiB batches that is 256 (fewer
-  // halo primes and, beside K3, fewer, longer K1 workgroups: 2,139-2,146 vs
-  // 2,088-2,108 GiB/s for 64); a 1 GiB batch gets 32 so that its K1 still
-  // spreads over every CU K3 leaves
+  // about two tiles per CU (four up to 4 GiB), 16..256.  At 8 GiB batches
+  // that is 256 (fewer halo primes and, beside K3, fewer, longer K1
+  // workgroups: 2,139-2,146 vs 2,088-2,108 GiB/s for 64); a 1 GiB batch gets
+  // 16 so that its K1 spreads evenly over the CUs K3 leaves
   uint32_t tile_iters = 0;
   uint32_t join_lag = 1;      // hbx_set_join_lag
   // where and when K2c plans run (plan_mode_of): 0 on the scan stream, by
@@ -678,10 +678,16 @@ void k1_tiles(hbx_ctx* c, uint32_t f, uint32_t iters, uint32_t tile) {
 constexpr uint32_t kTileItersMin = 16, kTileItersMax = 256;
 
 // K1 tile length for a batch of `total` iterations (c->tile_iters, or about
-// two tiles per CU when that is 0)
+// two or four tiles per CU when that is 0)
 uint32_t k1_tile_iters(const hbx_ctx* c, uint64_t total) {
   if (c->tile_iters) return c->tile_iters;
-  const uint64_t t = (total + 2ull * c->md5_wgs - 1) / (2ull * c->md5_wgs);
+  // about two tiles per CU for large batches, four up to 4 GiB (65,536
+  // iterations): the strong-scaling shares of configs[2] (tools/gpu_tile_sweep.sh,
+  // profiles/r02n_tiles: 1 GiB 1,825 -> 1,948 GiB/s with 16 instead of 32
+  // iterations, 2 GiB 2,068 -> 2,147 with 32 instead of 64; 4 GiB equal; 8 GiB
+  // 2,231 at 256 vs 2,205 at 128)
+  const uint64_t per_cu = total <= 65536ull ? 4ull : 2ull;
+  const uint64_t t = (total + per_cu * c->md5_wgs - 1) / (per_cu * c->md5_wgs);
   return (uint32_t)std::min<uint64_t>(kTileItersMax, std::max<uint64_t>(kTileItersMin, t));
 }
 
