@@ -110,13 +110,18 @@ def pipelined(eng, nf, fb, steps=200, lead=2):
         lists.append((co, cl, ex))
     B = -(-131073 // (R - lead))
     pe = Engine(0, md5_slice=B)
+    # a batch's chains join the K3 launch of the next submit (join lag 1) and
+    # need ceil(131073 / B) launches: collect only once that many submits
+    # have followed, or hbx_wait forces a drain launch (R - lead + 1 deep;
+    # the arena of batch j is reused at submit j + R, after its collect)
+    depth = -(-131073 // B) + 1
     bad = 0
     nbytes = 0
 
     def run(k):
         nonlocal bad, nbytes
         for j in range(k):
-            if pe.pending() >= R - lead:
+            if pe.pending() >= depth:
                 bad += pe.wait()[2]
             co, cl, ex = lists[j % R]
             pe.verify_submit_device(arenas[j % R].data_ptr(), co, cl, expect=ex)
