@@ -488,239 +488,266 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
   for (uint32_t k = t; k < 32u; k += kThreads) hd[k] = 0u;
   __syncthreads();
 
-  // 1. candidates in position order + Adler partials
+  // 0. incompressible segments: the order-0 entropy of the bytes.  At >= 7.97
+  //    bits per byte no Huffman code beats a stored block, and the parse
+  //    (steps 1-2) is skipped: the segment is stored.  Every stream stays
+  //    valid zlib; only a segment of random bytes that repeats itself within
+  //    32 KiB compresses less than a full parse would make it.
   uint32_t A = 0u, J = 0u;  // sum x, sum j*x over this thread's positions (j < 32768: J < 2^32)
-  for (uint32_t r = 0; r < kSeg / kThreads; r++) {
-    const uint32_t p = kThreads * r + t;
-    const uint32_t x = seg4(data, p + sh);
-    const bool live = p + 4u <= n;
-    const uint32_t h = zhash(x);
-    uint32_t best = 0u, bl = 0u;
-    if (live) {
-      const uint4 c = *reinterpret_cast<const uint4*>(&tab[h * kWays]);
-      const uint32_t lim = min(258u, n - p);
-      const uint32_t cs[4] = {c.x, c.y, c.z, c.w};
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        // a slot may already hold a later position of this round (no barrier
-        // between reads and inserts): only earlier positions are candidates
-        if (cs[k] != 0u && cs[k] - 1u < p && seg4(data, cs[k] - 1u + sh) == x) {
-          const uint32_t q = cs[k] - 1u;
-          const uint32_t L = 4u + match_len(data, sh, p + 4u, q + 4u, lim - 4u);
-          if (L > bl || (L == bl && p - q < best)) {
-            bl = L;
-            best = p - q;
+  uint32_t fbits = 0u, fincl = 0u, ftot = 0u, fixed_bytes = 0xFFFFFFFFu;
+  const uint32_t stored_bytes = 5u + n;
+  bool incompressible = false;
+  if (n >= 4096u) {
+    for (uint32_t k = t; k < 256u; k += kThreads) llc[k] = 0u;
+    __syncthreads();
+    for (uint32_t p = t; p < n; p += kThreads) atomicAdd(&llc[seg4(data, p + sh) & 0xFFu], 1u);
+    __syncthreads();
+    const uint32_t cnt = t < 256u ? llc[t] : 0u;
+    const uint32_t bits = cnt ? (uint32_t)((float)cnt * (__log2f((float)n) - __log2f((float)cnt))) : 0u;
+    uint32_t hsum;
+    (void)wg_incl_sum(bits, wsum, hsum);
+    incompressible = (float)hsum >= 7.97f * (float)n;  // wave-uniform (a workgroup total)
+  }
+  if (incompressible) {
+    for (uint32_t p = t; p < n; p += kThreads) {
+      const uint32_t x = seg4(data, p + sh) & 0xFFu;
+      A += x;
+      J += p * x;
+    }
+    if (t == 0) zpar[0] = 0u;
+  } else {
+    // 1. candidates in position order + Adler partials
+    for (uint32_t r = 0; r < kSeg / kThreads; r++) {
+      const uint32_t p = kThreads * r + t;
+      const uint32_t x = seg4(data, p + sh);
+      const bool live = p + 4u <= n;
+      const uint32_t h = zhash(x);
+      uint32_t best = 0u, bl = 0u;
+      if (live) {
+        const uint4 c = *reinterpret_cast<const uint4*>(&tab[h * kWays]);
+        const uint32_t lim = min(258u, n - p);
+        const uint32_t cs[4] = {c.x, c.y, c.z, c.w};
+  #pragma unroll
+        for (int k = 0; k < 4; k++) {
+          // a slot may already hold a later position of this round (no barrier
+          // between reads and inserts): only earlier positions are candidates
+          if (cs[k] != 0u && cs[k] - 1u < p && seg4(data, cs[k] - 1u + sh) == x) {
+            const uint32_t q = cs[k] - 1u;
+            const uint32_t L = 4u + match_len(data, sh, p + 4u, q + 4u, lim - 4u);
+            if (L > bl || (L == bl && p - q < best)) {
+              bl = L;
+              best = p - q;
+            }
           }
         }
       }
+      cd[cphys(p)] = (uint16_t)best;
+      if (p < n) {
+        A += x & 0xFFu;
+        J += p * (x & 0xFFu);
+      }
+      if (live) atomicMax(&tab[h * kWays + (p & (kWays - 1u))], p + 1u);
+      __syncthreads();
     }
-    cd[cphys(p)] = (uint16_t)best;
-    if (p < n) {
-      A += x & 0xFFu;
-      J += p * (x & 0xFFu);
-    }
-    if (live) atomicMax(&tab[h * kWays + (p & (kWays - 1u))], p + 1u);
-    __syncthreads();
-  }
 
-  // 2. tokens, symbol frequencies, fixed-code size
-  uint32_t extra;
-  const uint32_t fbits = tokenize(data, cd, hll, hd, sh, n, extra);
-  uint32_t ftot, etot, ntok;
-  const uint32_t fincl = wg_incl_sum(fbits, wsum, ftot);
-  (void)wg_incl_sum(extra, wsum, etot);
-  const uint32_t fixed_bytes = ((3u + ftot + 7u + 3u + 7u) >> 3) + 4u;  // header, tokens, EOB, sync flush
-  const uint32_t stored_bytes = 5u + n;
-  // entropy estimate of a dynamic code: build one only if it can win
-  const uint32_t f_t = t < 286u ? hll[t] : (t >= 288u && t < 318u ? hd[t - 288u] : 0u);
-  (void)wg_incl_sum(t < 286u ? f_t : 0u, wsum, ntok);
-  uint32_t ndist;
-  (void)wg_incl_sum(t >= 288u ? f_t : 0u, wsum, ndist);
-  const float nn = t < 286u ? (float)ntok : (float)max(ndist, 1u);
-  const uint32_t h_t = f_t ? (uint32_t)((float)f_t * (__log2f(nn) - __log2f((float)f_t))) : 0u;
-  uint32_t htot;
-  (void)wg_incl_sum(h_t, wsum, htot);
-  const uint32_t best_other = min(fixed_bytes, stored_bytes) * 8u;
-  const bool try_dyn = htot + etot + 600u < best_other;
-  if (try_dyn) {
-    // scratch in the (idle) hash table
-    uint32_t* keys = tab;                                      // 512 litlen keys, sorted
-    uint32_t* keysd = tab + 512;                               // 32 distance keys, sorted
-    uint32_t* keys2 = tab + 544;                               // 32 code-length keys
-    uint32_t* hw = tab + 576;                                  // weights: litlen 572, distance 60 at +576
-    uint32_t* npar = tab + 1792;                               // tree parents, distance nodes at +576
-    uint32_t* nanc = tab + 2816;                               // pointer-jumping ancestors
-    uint32_t* ndep = tab + 3840;                               // depths
-    uint32_t* blc = tab + 4864;                                // 2 x 16 length counts
-    uint32_t* cw = tab + 4896;                                 // code-length code: weights (38)
-    uint16_t* cpar = reinterpret_cast<uint16_t*>(tab + 4960);  // 38
-    uint8_t* cdep = reinterpret_cast<uint8_t*>(tab + 4992);    // 38
-    for (uint32_t k = t; k < 512u; k += kThreads) keys[k] = (k < 286u && hll[k]) ? (hll[k] << 9) | k : 0xFFFFFFFFu;
-    for (uint32_t k = t; k < 320u; k += kThreads) zl[k] = 0u;
-    if (t < 32u) blc[t] = 0u;
-    if (t < 19u) clf[t] = 0u;
-    if (t < 8u) zctl[t] = 0u;
-    __syncthreads();
-    if (t < 64u) {  // bitonic sort of the litlen keys, ascending, one wave
-      for (uint32_t k = 2; k <= 512u; k <<= 1)
-        for (uint32_t j = k >> 1; j > 0u; j >>= 1)
-          for (uint32_t i = t; i < 512u; i += 64u) {
-            const uint32_t ixj = i ^ j;
-            if (ixj > i) {
-              const uint32_t a = keys[i], b = keys[ixj];
-              if ((a > b) == ((i & k) == 0u)) {
-                keys[i] = b;
-                keys[ixj] = a;
+    // 2. tokens, symbol frequencies, fixed-code size
+    uint32_t extra;
+    fbits = tokenize(data, cd, hll, hd, sh, n, extra);
+    uint32_t etot, ntok;
+    fincl = wg_incl_sum(fbits, wsum, ftot);
+    (void)wg_incl_sum(extra, wsum, etot);
+    fixed_bytes = ((3u + ftot + 7u + 3u + 7u) >> 3) + 4u;  // header, tokens, EOB, sync flush
+    // entropy estimate of a dynamic code: build one only if it can win
+    const uint32_t f_t = t < 286u ? hll[t] : (t >= 288u && t < 318u ? hd[t - 288u] : 0u);
+    (void)wg_incl_sum(t < 286u ? f_t : 0u, wsum, ntok);
+    uint32_t ndist;
+    (void)wg_incl_sum(t >= 288u ? f_t : 0u, wsum, ndist);
+    const float nn = t < 286u ? (float)ntok : (float)max(ndist, 1u);
+    const uint32_t h_t = f_t ? (uint32_t)((float)f_t * (__log2f(nn) - __log2f((float)f_t))) : 0u;
+    uint32_t htot;
+    (void)wg_incl_sum(h_t, wsum, htot);
+    const uint32_t best_other = min(fixed_bytes, stored_bytes) * 8u;
+    const bool try_dyn = htot + etot + 600u < best_other;
+    if (try_dyn) {
+      // scratch in the (idle) hash table
+      uint32_t* keys = tab;                                      // 512 litlen keys, sorted
+      uint32_t* keysd = tab + 512;                               // 32 distance keys, sorted
+      uint32_t* keys2 = tab + 544;                               // 32 code-length keys
+      uint32_t* hw = tab + 576;                                  // weights: litlen 572, distance 60 at +576
+      uint32_t* npar = tab + 1792;                               // tree parents, distance nodes at +576
+      uint32_t* nanc = tab + 2816;                               // pointer-jumping ancestors
+      uint32_t* ndep = tab + 3840;                               // depths
+      uint32_t* blc = tab + 4864;                                // 2 x 16 length counts
+      uint32_t* cw = tab + 4896;                                 // code-length code: weights (38)
+      uint16_t* cpar = reinterpret_cast<uint16_t*>(tab + 4960);  // 38
+      uint8_t* cdep = reinterpret_cast<uint8_t*>(tab + 4992);    // 38
+      for (uint32_t k = t; k < 512u; k += kThreads) keys[k] = (k < 286u && hll[k]) ? (hll[k] << 9) | k : 0xFFFFFFFFu;
+      for (uint32_t k = t; k < 320u; k += kThreads) zl[k] = 0u;
+      if (t < 32u) blc[t] = 0u;
+      if (t < 19u) clf[t] = 0u;
+      if (t < 8u) zctl[t] = 0u;
+      __syncthreads();
+      if (t < 64u) {  // bitonic sort of the litlen keys, ascending, one wave
+        for (uint32_t k = 2; k <= 512u; k <<= 1)
+          for (uint32_t j = k >> 1; j > 0u; j >>= 1)
+            for (uint32_t i = t; i < 512u; i += 64u) {
+              const uint32_t ixj = i ^ j;
+              if (ixj > i) {
+                const uint32_t a = keys[i], b = keys[ixj];
+                if ((a > b) == ((i & k) == 0u)) {
+                  keys[i] = b;
+                  keys[ixj] = a;
+                }
               }
             }
-          }
-    } else if (t < 96u) {  // rank sort of the distance keys, a second wave
-      const uint32_t k = t - 64u;
-      const uint32_t key = (k < 30u && hd[k]) ? (hd[k] << 9) | k : 0xFFFFFFFFu;
-      if (key != 0xFFFFFFFFu) {
-        uint32_t r = 0u;
-        for (uint32_t q = 0; q < 30u; q++) r += hd[q] && ((hd[q] << 9) | q) < key;
-        keysd[r] = key;
+      } else if (t < 96u) {  // rank sort of the distance keys, a second wave
+        const uint32_t k = t - 64u;
+        const uint32_t key = (k < 30u && hd[k]) ? (hd[k] << 9) | k : 0xFFFFFFFFu;
+        if (key != 0xFFFFFFFFu) {
+          uint32_t r = 0u;
+          for (uint32_t q = 0; q < 30u; q++) r += hd[q] && ((hd[q] << 9) | q) < key;
+          keysd[r] = key;
+        }
       }
-    }
-    const uint32_t ml = (uint32_t)__syncthreads_count(t < 286u && hll[t] != 0u);  // >= 1 (EOB)
-    const uint32_t md = (uint32_t)__syncthreads_count(t < 30u && hd[t] != 0u);
-    // Huffman trees of both codes at once: the serial merges on two waves,
-    // then depths by pointer jumping over every node; halve and rebuild a
-    // code whose longest length exceeds 15.
-    bool need_l = ml >= 2u, need_d = md >= 2u;
-    for (uint32_t shift = 0; need_l || need_d; shift++) {
-      if (t == 0u && need_l) huff_merge(keys, ml, shift, hw, npar, 0u);
-      if (t == 64u && need_d) huff_merge(keysd, md, shift, hw + 576, npar + 576, 576u);
-      if (t < 2u) zctl[t] = 0u;
-      __syncthreads();
-      uint32_t x0 = t, x1 = t + kThreads, a0, a1, d0, d1;
-      auto init = [&](uint32_t x, uint32_t& a, uint32_t& d) {
-        const bool dist = x >= 576u;
-        const uint32_t m = dist ? md : ml, root = (dist ? 576u : 0u) + 2u * m - 2u;
-        const bool live = m >= 2u && x <= root && x >= (dist ? 576u : 0u);
-        a = live && x != root ? npar[x] : x;
-        d = live && x != root ? 1u : 0u;
-      };
-      init(x0, a0, d0);
-      init(x1, a1, d1);
-      nanc[x0] = a0;
-      nanc[x1] = a1;
-      ndep[x0] = d0;
-      ndep[x1] = d1;
-      __syncthreads();
-      for (int r = 0; r < 10; r++) {  // depth <= 571 < 2^10
-        const uint32_t e0 = ndep[a0], e1 = ndep[a1], b0 = nanc[a0], b1 = nanc[a1];
+      const uint32_t ml = (uint32_t)__syncthreads_count(t < 286u && hll[t] != 0u);  // >= 1 (EOB)
+      const uint32_t md = (uint32_t)__syncthreads_count(t < 30u && hd[t] != 0u);
+      // Huffman trees of both codes at once: the serial merges on two waves,
+      // then depths by pointer jumping over every node; halve and rebuild a
+      // code whose longest length exceeds 15.
+      bool need_l = ml >= 2u, need_d = md >= 2u;
+      for (uint32_t shift = 0; need_l || need_d; shift++) {
+        if (t == 0u && need_l) huff_merge(keys, ml, shift, hw, npar, 0u);
+        if (t == 64u && need_d) huff_merge(keysd, md, shift, hw + 576, npar + 576, 576u);
+        if (t < 2u) zctl[t] = 0u;
         __syncthreads();
-        d0 += e0;
-        d1 += e1;
-        a0 = b0;
-        a1 = b1;
-        ndep[x0] = d0;
-        ndep[x1] = d1;
+        uint32_t x0 = t, x1 = t + kThreads, a0, a1, d0, d1;
+        auto init = [&](uint32_t x, uint32_t& a, uint32_t& d) {
+          const bool dist = x >= 576u;
+          const uint32_t m = dist ? md : ml, root = (dist ? 576u : 0u) + 2u * m - 2u;
+          const bool live = m >= 2u && x <= root && x >= (dist ? 576u : 0u);
+          a = live && x != root ? npar[x] : x;
+          d = live && x != root ? 1u : 0u;
+        };
+        init(x0, a0, d0);
+        init(x1, a1, d1);
         nanc[x0] = a0;
         nanc[x1] = a1;
+        ndep[x0] = d0;
+        ndep[x1] = d1;
+        __syncthreads();
+        for (int r = 0; r < 10; r++) {  // depth <= 571 < 2^10
+          const uint32_t e0 = ndep[a0], e1 = ndep[a1], b0 = nanc[a0], b1 = nanc[a1];
+          __syncthreads();
+          d0 += e0;
+          d1 += e1;
+          a0 = b0;
+          a1 = b1;
+          ndep[x0] = d0;
+          ndep[x1] = d1;
+          nanc[x0] = a0;
+          nanc[x1] = a1;
+          __syncthreads();
+        }
+        if (x0 < ml) atomicMax(&zctl[0], d0);
+        if (x0 >= 576u && x0 < 576u + md) atomicMax(&zctl[1], d0);
+        if (x1 >= 576u && x1 < 576u + md) atomicMax(&zctl[1], d1);
+        __syncthreads();
+        need_l = need_l && zctl[0] > 15u;
+        need_d = need_d && zctl[1] > 15u;
         __syncthreads();
       }
-      if (x0 < ml) atomicMax(&zctl[0], d0);
-      if (x0 >= 576u && x0 < 576u + md) atomicMax(&zctl[1], d0);
-      if (x1 >= 576u && x1 < 576u + md) atomicMax(&zctl[1], d1);
-      __syncthreads();
-      need_l = need_l && zctl[0] > 15u;
-      need_d = need_d && zctl[1] > 15u;
-      __syncthreads();
-    }
-    // code lengths (one distance symbol gets a second: RFC 1951 §3.2.7)
-    if (t < ml) zl[keys[t] & 511u] = ml >= 2u ? (uint8_t)ndep[t] : 1u;
-    if (md >= 2u && t < md) zl[288u + (keysd[t] & 511u)] = (uint8_t)ndep[576u + t];
-    if (md == 0u && t < 2u) zl[288u + t] = 1u;
-    if (md == 1u && t < 2u) {
-      const uint32_t x = keysd[0] & 511u;
-      zl[288u + (t ? (x ? 0u : 1u) : x)] = 1u;
-    }
-    __syncthreads();
-    // HLIT, HDIST, per-length counts
-    const uint32_t zt = t < 286u ? zl[t] : (t >= 288u && t < 318u ? zl[t] : 0u);
-    if (zt) atomicAdd(&blc[(t >= 288u ? 16u : 0u) + zt], 1u);
-    if (zt && t >= 257u && t < 286u) atomicMax(&zctl[2], t + 1u);
-    if (zt && t >= 288u) atomicMax(&zctl[3], t - 288u + 1u);
-    __syncthreads();
-    const uint32_t hlit = max(zctl[2], 257u), hdist = max(zctl[3], 1u);
-    // canonical codes (RFC 1951 §3.2.2): first code of the length + the rank
-    // among the symbols of that length before this one
-    if (zt) {
-      const uint32_t cb = t >= 288u ? 16u : 0u, s0 = t >= 288u ? 288u : 0u;
-      uint32_t code = 0u;
-      for (uint32_t b = 1; b <= zt; b++) code = (code + (b > 1u ? blc[cb + b - 1u] : 0u)) << 1;
-      const uint32_t* zw = reinterpret_cast<const uint32_t*>(zl);
-      const uint32_t pat = zt * 0x01010101u;
-      uint32_t rank = 0u;
-      for (uint32_t q = s0; q < t; q += 4u) {
-        uint32_t v = zw[q >> 2] ^ pat;
-        if (t - q < 4u) v |= 0xFFFFFFFFu << (8u * (t - q));  // bytes at or past t never count
-        const uint32_t y = ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v | 0x7F7F7F7Fu);
-        rank += __builtin_popcount(y);
+      // code lengths (one distance symbol gets a second: RFC 1951 §3.2.7)
+      if (t < ml) zl[keys[t] & 511u] = ml >= 2u ? (uint8_t)ndep[t] : 1u;
+      if (md >= 2u && t < md) zl[288u + (keysd[t] & 511u)] = (uint8_t)ndep[576u + t];
+      if (md == 0u && t < 2u) zl[288u + t] = 1u;
+      if (md == 1u && t < 2u) {
+        const uint32_t x = keysd[0] & 511u;
+        zl[288u + (t ? (x ? 0u : 1u) : x)] = 1u;
       }
-      const uint32_t c = rev(code + rank, zt) | (zt << 16);
-      if (t >= 288u) dcc[t - 288u] = c; else llc[t] = c;
-    } else if (t < 286u) {
-      llc[t] = 0u;
-    } else if (t >= 288u && t < 318u) {
-      dcc[t - 288u] = 0u;
-    }
-    // code-length sequence, run-length coded (16/17/18): one thread per run
-    const uint32_t nl = hlit + hdist;
-    auto zv = [&](uint32_t i) -> uint32_t { return i < hlit ? zl[i] : zl[288u + i - hlit]; };
-    uint32_t cur = 0u, run = 0u, cnt = 0u;
-    if (t < nl && (t == 0u || zv(t - 1u) != zv(t))) {
-      cur = zv(t);
-      run = 1u;
-      while (t + run < nl && zv(t + run) == cur) run++;
-      cnt = rle_runs<false>(cur, run, nullptr, nullptr);
-    }
-    uint32_t nr;
-    const uint32_t at = wg_incl_sum(cnt, wsum, nr) - cnt;
-    if (cnt) rle_runs<true>(cur, run, rle + at, clf);
-    __syncthreads();
-    if (t == 0) {  // the code-length code: <= 19 symbols, serial
-      for (uint32_t k = 0; k < 19u; k++) cll[k] = 0u;
-      const uint32_t mc = sort_small(clf, 19u, keys2);
-      if (mc == 1u) {
-        const uint32_t x = keys2[0] & 511u;
-        cll[x] = 1u;
-        cll[x ? 0u : 1u] = 1u;
-      } else {
-        huff_lengths(keys2, mc, 7u, cll, cw, cpar, cdep);
+      __syncthreads();
+      // HLIT, HDIST, per-length counts
+      const uint32_t zt = t < 286u ? zl[t] : (t >= 288u && t < 318u ? zl[t] : 0u);
+      if (zt) atomicAdd(&blc[(t >= 288u ? 16u : 0u) + zt], 1u);
+      if (zt && t >= 257u && t < 286u) atomicMax(&zctl[2], t + 1u);
+      if (zt && t >= 288u) atomicMax(&zctl[3], t - 288u + 1u);
+      __syncthreads();
+      const uint32_t hlit = max(zctl[2], 257u), hdist = max(zctl[3], 1u);
+      // canonical codes (RFC 1951 §3.2.2): first code of the length + the rank
+      // among the symbols of that length before this one
+      if (zt) {
+        const uint32_t cb = t >= 288u ? 16u : 0u, s0 = t >= 288u ? 288u : 0u;
+        uint32_t code = 0u;
+        for (uint32_t b = 1; b <= zt; b++) code = (code + (b > 1u ? blc[cb + b - 1u] : 0u)) << 1;
+        const uint32_t* zw = reinterpret_cast<const uint32_t*>(zl);
+        const uint32_t pat = zt * 0x01010101u;
+        uint32_t rank = 0u;
+        for (uint32_t q = s0; q < t; q += 4u) {
+          uint32_t v = zw[q >> 2] ^ pat;
+          if (t - q < 4u) v |= 0xFFFFFFFFu << (8u * (t - q));  // bytes at or past t never count
+          const uint32_t y = ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v | 0x7F7F7F7Fu);
+          rank += __builtin_popcount(y);
+        }
+        const uint32_t c = rev(code + rank, zt) | (zt << 16);
+        if (t >= 288u) dcc[t - 288u] = c; else llc[t] = c;
+      } else if (t < 286u) {
+        llc[t] = 0u;
+      } else if (t >= 288u && t < 318u) {
+        dcc[t - 288u] = 0u;
       }
-      canon_codes(cll, 19u, clc, blc);
-      uint32_t hclen = 4u;
-      for (uint32_t k = 0; k < 19u; k++)
-        if (cll[kClOrder[k]]) hclen = max(hclen, k + 1u);
-      zctl[4] = hclen;
+      // code-length sequence, run-length coded (16/17/18): one thread per run
+      const uint32_t nl = hlit + hdist;
+      auto zv = [&](uint32_t i) -> uint32_t { return i < hlit ? zl[i] : zl[288u + i - hlit]; };
+      uint32_t cur = 0u, run = 0u, cnt = 0u;
+      if (t < nl && (t == 0u || zv(t - 1u) != zv(t))) {
+        cur = zv(t);
+        run = 1u;
+        while (t + run < nl && zv(t + run) == cur) run++;
+        cnt = rle_runs<false>(cur, run, nullptr, nullptr);
+      }
+      uint32_t nr;
+      const uint32_t at = wg_incl_sum(cnt, wsum, nr) - cnt;
+      if (cnt) rle_runs<true>(cur, run, rle + at, clf);
+      __syncthreads();
+      if (t == 0) {  // the code-length code: <= 19 symbols, serial
+        for (uint32_t k = 0; k < 19u; k++) cll[k] = 0u;
+        const uint32_t mc = sort_small(clf, 19u, keys2);
+        if (mc == 1u) {
+          const uint32_t x = keys2[0] & 511u;
+          cll[x] = 1u;
+          cll[x ? 0u : 1u] = 1u;
+        } else {
+          huff_lengths(keys2, mc, 7u, cll, cw, cpar, cdep);
+        }
+        canon_codes(cll, 19u, clc, blc);
+        uint32_t hclen = 4u;
+        for (uint32_t k = 0; k < 19u; k++)
+          if (cll[kClOrder[k]]) hclen = max(hclen, k + 1u);
+        zctl[4] = hclen;
+      }
+      __syncthreads();
+      const uint32_t hclen = zctl[4];
+      uint32_t hcost = 0u, tcost = 0u, hb_body, tok_body;
+      if (t < nr) {
+        const uint32_t sy = rle[t] & 31u;
+        hcost = (clc[sy] >> 16) + (sy == 16u ? 2u : sy == 17u ? 3u : sy == 18u ? 7u : 0u);
+      }
+      if (t < 286u) tcost = hll[t] * zl[t];  // EOB included (hll[256] = 1)
+      else if (t >= 288u && t < 318u) tcost = hd[t - 288u] * zl[t];
+      (void)wg_incl_sum(hcost, wsum, hb_body);
+      (void)wg_incl_sum(tcost, wsum, tok_body);
+      if (t == 0) {
+        const uint32_t hb = 3u + 5u + 5u + 4u + 3u * hclen + hb_body;
+        const uint32_t dyn_bytes = ((hb + etot + tok_body + 3u + 7u) >> 3) + 4u;
+        zpar[0] = dyn_bytes < min(fixed_bytes, stored_bytes) ? 2u : 0u;
+        zpar[1] = hb;
+        zpar[2] = dyn_bytes;
+        zpar[3] = hlit | (hdist << 16);
+        zpar[4] = hclen | (nr << 16);
+      }
+      __syncthreads();
+    } else if (t == 0) {
+      zpar[0] = 0u;
     }
-    __syncthreads();
-    const uint32_t hclen = zctl[4];
-    uint32_t hcost = 0u, tcost = 0u, hb_body, tok_body;
-    if (t < nr) {
-      const uint32_t sy = rle[t] & 31u;
-      hcost = (clc[sy] >> 16) + (sy == 16u ? 2u : sy == 17u ? 3u : sy == 18u ? 7u : 0u);
-    }
-    if (t < 286u) tcost = hll[t] * zl[t];  // EOB included (hll[256] = 1)
-    else if (t >= 288u && t < 318u) tcost = hd[t - 288u] * zl[t];
-    (void)wg_incl_sum(hcost, wsum, hb_body);
-    (void)wg_incl_sum(tcost, wsum, tok_body);
-    if (t == 0) {
-      const uint32_t hb = 3u + 5u + 5u + 4u + 3u * hclen + hb_body;
-      const uint32_t dyn_bytes = ((hb + etot + tok_body + 3u + 7u) >> 3) + 4u;
-      zpar[0] = dyn_bytes < min(fixed_bytes, stored_bytes) ? 2u : 0u;
-      zpar[1] = hb;
-      zpar[2] = dyn_bytes;
-      zpar[3] = hlit | (hdist << 16);
-      zpar[4] = hclen | (nr << 16);
-    }
-    __syncthreads();
-  } else if (t == 0) {
-    zpar[0] = 0u;
   }
   __syncthreads();
   uint32_t mode = zpar[0];  // 2 dynamic, 1 fixed, 0 stored
