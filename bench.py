@@ -389,7 +389,7 @@ def run_workload(a, name, eng, arenas, offs, lens, R, B, need, lanes, dist, gpu,
         # the whole path's bound: K1 + K3 VALU wave-instructions per step over
         # the chip's measured issue capacity at the spec clock (the box runs
         # power-capped at ~2.09 GHz while pipelined)
-        "valu_roofline": {"bound": "valu-issue", "unit": "wave-instr/s",
+        "valu_roofline": {"bound": "valu-issue", "unit": "wave-instr/s per GPU",
                           "achieved": round(rank_batch * (K1_WAVE_VALU_PER_BYTE + K3_WAVE_VALU_PER_BYTE)
                                             / (el / a.steps), 0),
                           "peak": round(VALU_PEAK_WAVE_INSTR, 0),
