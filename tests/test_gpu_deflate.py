@@ -164,3 +164,21 @@ def test_store_paths_on_batch_needs_compress(engine, tmp_path):
     p.write_bytes(b"abc")
     with pytest.raises(ValueError):
         engine.store_paths([p], on_batch=lambda a, c: None)
+
+
+def test_entropy_early_out_boundaries(engine):
+    """K7's incompressible early-out (order-0 entropy >= 7.97 bits per byte ->
+    stored, no parse): random bytes repeating within 32 KiB are stored but
+    valid; bytes over 200 symbols (7.64 bits) still get a Huffman code; a
+    block below 4 KiB takes the full parse (it finds the repeat); mixes of
+    both kinds in one block stay valid."""
+    rng = np.random.default_rng(33)
+    rep = rng.integers(0, 256, 8192, dtype=np.uint8).tobytes() * 8         # 64 KiB, entropy ~8 bits
+    few = rng.integers(0, 200, 1 << 17, dtype=np.uint8).tobytes()            # log2(200) = 7.64 bits
+    small = rng.integers(0, 256, 1500, dtype=np.uint8).tobytes() * 2         # 3000 B: below the early-out
+    mix = rng.integers(0, 256, 40000, dtype=np.uint8).tobytes() + _text(60000, 5)
+    zr, zf, zs, zm = _check(engine, [rep, few, small, mix])
+    assert len(zr) == len(rep) + 5 * (len(rep) // 32768) + 11  # stored segments
+    assert len(zf) < 0.98 * len(few), (len(zf), len(few))     # Huffman-coded, not stored
+    assert len(zs) < 0.7 * len(small), (len(zs), len(small))  # the full parse matched the repeat
+    assert len(zm) < len(mix), (len(zm), len(mix))            # the text half compresses
