@@ -485,6 +485,7 @@ def main():
     torch.cuda.synchronize(dev)
 
     if a.k3_probe:
+        os.environ["HBX_AB"] = "1"
         os.environ["HBX_K3_PROBE"] = "1"
     eng = Engine(dev_idx, md5_slice=B, join_lag=lag, k3_waves=a.k3_waves)
     # every batch slot, chain table and summary buffer of the pipeline is

@@ -1034,6 +1034,14 @@ int hbx_device_count(int* n) {
 
 uint64_t hbx_max_chunks(uint64_t len) { return max_chunks(len); }
 
+// A/B and diagnostic switches (HBX_*) are read only when HBX_AB=1 is set as
+// well: a caller's stray environment must not change the product path.  The
+// effective values are reported by hbx_knobs().
+static const char* ab_env(const char* name) {
+  const char* ab = std::getenv("HBX_AB");
+  return (ab && std::atoi(ab) != 0) ? std::getenv(name) : nullptr;
+}
+
 // HBX_SCAN_CUS / HBX_HASH_CUS / HBX_RES_CUS = "first:count[:stride]" restrict a
 // stream's dispatches to those CU indices (hipExtStreamCreateWithCUMask);
 // "off" or unset = an ordinary stream.  The scan stream defaults to a full
@@ -1042,7 +1050,7 @@ uint64_t hbx_max_chunks(uint64_t len) { return max_chunks(len); }
 // tools/gpu_ab_cumask3.sh).  Masking the hash or result stream, even with
 // all CUs, serializes K1 and K3 (1,510-1,540 GiB/s): leave them unmasked.
 static hipError_t make_stream(hipStream_t* s, const char* env, int ncu, const char* dflt = nullptr) {
-  const char* v = std::getenv(env);
+  const char* v = ab_env(env);
   if (!v) v = dflt;
   int first = 0, count = 0, stride = 1;
   if (!v || std::sscanf(v, "%d:%d:%d", &first, &count, &stride) < 2 || count <= 0 || ncu <= 0) {
@@ -1075,22 +1083,22 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   int ncu = 0;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->md5_wgs = (uint32_t)(ncu = prop.multiProcessorCount);
-  if (const char* v = std::getenv("HBX_MD5_WGS")) c->md5_wgs = (uint32_t)std::max(1, std::atoi(v));
-  if (const char* v = std::getenv("HBX_K3_DENSE")) c->k3_dense = std::atoi(v) ? 1u : 0u;
-  if (const char* v = std::getenv("HBX_K1_RUN")) c->k1_run = std::atoi(v) == 128 ? 128u : 64u;
-  if (const char* v = std::getenv("HBX_K3_WAVES")) c->k3_threads = std::atoi(v) == 2 ? kK3Threads2 : kK3Threads;
-  if (const char* v = std::getenv("HBX_TILE_ITERS")) c->tile_iters = (uint32_t)std::min(1024, std::max(0, std::atoi(v)));
-  if (const char* v = std::getenv("HBX_JOIN_LAG")) c->join_lag = (uint32_t)std::min(4, std::max(1, std::atoi(v)));
-  if (const char* v = std::getenv("HBX_K4_WINDOW")) c->k4_window = (uint32_t)std::min(1024, std::max(1, std::atoi(v)));
-  if (const char* v = std::getenv("HBX_PLAN_MODE")) c->plan_mode = std::min(2, std::max(0, std::atoi(v)));
-  if (const char* v = std::getenv("HBX_MD5_SLICE")) c->md5_slice = (uint32_t)std::max(0, std::atoi(v));
-  if (const char* v = std::getenv("HBX_K1_GATE")) c->k1_gate = std::atoi(v) ? 1u : 0u;
+  if (const char* v = ab_env("HBX_MD5_WGS")) c->md5_wgs = (uint32_t)std::max(1, std::atoi(v));
+  if (const char* v = ab_env("HBX_K3_DENSE")) c->k3_dense = std::atoi(v) ? 1u : 0u;
+  if (const char* v = ab_env("HBX_K1_RUN")) c->k1_run = std::atoi(v) == 128 ? 128u : 64u;
+  if (const char* v = ab_env("HBX_K3_WAVES")) c->k3_threads = std::atoi(v) == 2 ? kK3Threads2 : kK3Threads;
+  if (const char* v = ab_env("HBX_TILE_ITERS")) c->tile_iters = (uint32_t)std::min(1024, std::max(0, std::atoi(v)));
+  if (const char* v = ab_env("HBX_JOIN_LAG")) c->join_lag = (uint32_t)std::min(4, std::max(1, std::atoi(v)));
+  if (const char* v = ab_env("HBX_K4_WINDOW")) c->k4_window = (uint32_t)std::min(1024, std::max(1, std::atoi(v)));
+  if (const char* v = ab_env("HBX_PLAN_MODE")) c->plan_mode = std::min(2, std::max(0, std::atoi(v)));
+  if (const char* v = ab_env("HBX_MD5_SLICE")) c->md5_slice = (uint32_t)std::max(0, std::atoi(v));
+  if (const char* v = ab_env("HBX_K1_GATE")) c->k1_gate = std::atoi(v) ? 1u : 0u;
   if (hipSetDevice(device) != hipSuccess || make_stream(&c->stream, "HBX_SCAN_CUS", ncu, "0:4096") != hipSuccess) {
     delete c;
     return HBX_ERR_HIP;
   }
-  const char* one = std::getenv("HBX_ONE_STREAM");  // A/B: scan, hash and results on one stream
-  if (const char* v = std::getenv("HBX_K2_STREAM")) c->k2_own = std::atoi(v) ? 1 : 0;
+  const char* one = ab_env("HBX_ONE_STREAM");  // A/B: scan, hash and results on one stream
+  if (const char* v = ab_env("HBX_K2_STREAM")) c->k2_own = std::atoi(v) ? 1 : 0;
   c->cstream = c->stream;
   if (one && std::atoi(one)) {
     c->hstream = c->rstream = c->stream;
@@ -1100,7 +1108,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
     return HBX_ERR_HIP;
   }
   if (c->h_k3t.ensure(kK3TimeRing * 16) == hipSuccess) std::memset(c->h_k3t.p, 0, kK3TimeRing * 16);
-  if (const char* v = std::getenv("HBX_K3_PROBE"))
+  if (const char* v = ab_env("HBX_K3_PROBE"))
     if (std::atoi(v) && c->h_probe.ensure((size_t)c->md5_wgs * (kK3Threads2 / 64) * 32) == hipSuccess)
       std::memset(c->h_probe.p, 0, (size_t)c->md5_wgs * (kK3Threads2 / 64) * 32);
   if (c->d_gate.ensure(256) != hipSuccess || hipMemset(c->d_gate.p, 0, 256) != hipSuccess ||
@@ -1185,6 +1193,21 @@ int hbx_set_join_lag(hbx_ctx* c, uint32_t lag) {
   HBX_TRY(c, hipSetDevice(c->device));
   c->join_lag = lag;
   return ensure_cut_stream(c);
+}
+
+int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
+  if (!c || !out || cap == 0) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  const char* ab = std::getenv("HBX_AB");
+  const int n = std::snprintf(
+      out, (size_t)cap,
+      "{\"ab_env\": %d, \"md5_slice\": %u, \"join_lag\": %u, \"tile_iters\": %u, \"k1_run\": %u, "
+      "\"k3_waves\": %u, \"k3_dense\": %u, \"k1_gate\": %u, \"md5_wgs\": %u, \"plan_mode\": %d, "
+      "\"k2_own\": %d, \"k4_window\": %u, \"one_stream\": %d, \"k3_probe\": %d}",
+      (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_run,
+      c->k3_threads == kK3Threads2 ? 2u : 1u, c->k3_dense, c->k1_gate, c->md5_wgs, c->plan_mode, c->k2_own,
+      c->k4_window, c->hstream == c->stream ? 1 : 0, c->h_probe.p ? 1 : 0);
+  return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }
 
 int hbx_k3_wave_times(hbx_ctx* c, uint64_t* out, uint32_t max_waves, uint32_t* n_waves) {
@@ -1582,6 +1605,8 @@ struct ZPend {
   std::vector<uint64_t> dst;  // stream offset of each chunk in the stage
   std::shared_future<int> fin;  // its unpack (z_finish), on a worker thread
   double t_sync = 0.0;          // HBX_ZDIAG: time that unpack waited for the GPU
+  std::string err;              // the worker's error text: it never writes c->err,
+                                // which the main loop owns; zdrain_one copies it
 };
 
 int z_start(hbx_ctx* c, ZPend& zp, const uint64_t* cut_ends, const uint64_t* out_base,
@@ -1639,13 +1664,19 @@ int z_start(hbx_ctx* c, ZPend& zp, const uint64_t* cut_ends, const uint64_t* out
 }
 
 // Wait for a started job, place its streams and call the batch back.
-int z_finish(hbx_ctx* c, const ZPend& zp, const uint64_t* out_base, const hbx_file_summary* sums, const ZOut& z,
+// Runs on a worker thread: reports errors only through zp.err (never c->err,
+// c->hip or c->fail, which the caller's thread uses meanwhile).
+int z_finish(const hbx_ctx* c, ZPend& zp, const uint64_t* out_base, const hbx_file_summary* sums, const ZOut& z,
              uint32_t threads, double& t_sync) {
   const auto& Z = c->zs[zp.stage];
   const uint64_t nc = zp.dst.size();
   if (nc) {
     const auto t0 = std::chrono::steady_clock::now();
-    HBX_TRY(c, hipEventSynchronize(Z.done));
+    const hipError_t e = hipEventSynchronize(Z.done);
+    if (e != hipSuccess) {
+      zp.err = std::string("hipEventSynchronize(compression stage): ") + hipGetErrorString(e);
+      return HBX_ERR_HIP;
+    }
     t_sync += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     const uint8_t* h = Z.stage.as<uint8_t>();
     const uint64_t* ol = Z.lens.as<uint64_t>();
@@ -1794,10 +1825,17 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
   auto zdrain_one = [&]() -> int {
     const double t0 = now();
     const int r = zq.front().fin.get();
+    if (r && !zq.front().err.empty()) c->err = zq.front().err;  // the worker's text, on this thread
     zt[2] += now() - t0;
     zt[3] += zq.front().t_sync;
     zq.pop_front();
     return r;
+  };
+  // every compression stream idle: K7 of a failed job may still read an arena
+  // that the next call rewrites
+  auto zsync_all = [&]() {
+    for (auto& Z : c->zs)
+      if (Z.stream) (void)hipStreamSynchronize(Z.stream);
   };
   auto collect = [&]() -> int {
     const double t0 = now();
@@ -1896,8 +1934,9 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
       zq.pop_front();
     }
   }
+  if (rc != HBX_OK && z.zout) zsync_all();
   c->io_s[1] += now() - td;
-  if (z.zout && std::getenv("HBX_ZDIAG"))
+  if (z.zout && ab_env("HBX_ZDIAG"))
     std::fprintf(stderr, "zdiag: wait_oldest %.3f s, z_start %.3f s, z_finish %.3f s (event waits %.3f s), jobs %llu\n",
                  zt[0], zt[1], zt[2], zt[3], (unsigned long long)zjobs);
   return rc;
@@ -2277,7 +2316,7 @@ int hbx_inflate_blocks_device(hbx_ctx* c, const void* d_in, uint64_t n, const ui
     tcap += desc[k].cap;
   }
   bool lanes = n >= 8192 && tin * 10 < tcap * 7 && tcap / n <= (256u << 10);
-  if (const char* m = std::getenv("HBX_K8_MODE")) lanes = std::strcmp(m, "lane") == 0;
+  if (const char* m = ab_env("HBX_K8_MODE")) lanes = std::strcmp(m, "lane") == 0;
   if (lanes)
     hipLaunchKernelGGL(hbx_k8_inflate_lanes, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, s,
                        c->d_idesc.as<InflateDesc>(), (uint32_t)n, dres, dres + n);

@@ -310,6 +310,14 @@ class Engine:
         self._check(self._L.hbx_k3_wave_times(self._ctx, _p(out), n.value, ctypes.byref(n)), "hbx_k3_wave_times")
         return out[:n.value]
 
+    def knobs(self) -> dict:
+        """The context's effective pipeline knobs (hbx_knobs), including
+        whether HBX_* A/B switches were honoured (only with HBX_AB=1)."""
+        import json
+        buf = ctypes.create_string_buffer(1024)
+        self._check(self._L.hbx_knobs(self._ctx, buf, len(buf)), "hbx_knobs")
+        return json.loads(buf.value.decode())
+
     def reserve(self, batches: int, files: int, nbytes: int):
         """Pre-size the pipeline for ``batches`` batches in flight of up to
         ``files`` files / ``nbytes`` bytes each, so the steady state never

@@ -433,6 +433,12 @@ int hbx_after_stream(hbx_ctx *ctx, void *stream);
 int hbx_alloc_pinned(uint64_t bytes, void **out);
 int hbx_free_pinned(void *p);
 
+/* The context's effective pipeline knobs as one JSON object (NUL-terminated,
+ * at most cap bytes): slice, join lag, K1 tile and run, K3 waves and placement,
+ * and whether the HBX_* A/B environment switches were honoured (ab_env: they
+ * are read only when HBX_AB=1).  No reference counterpart: diagnostics. */
+int hbx_knobs(hbx_ctx *ctx, char *out, uint64_t cap);
+
 /* Device time (ms) of the last completed batch per stage:
  * [0] K1 window-digest scan, [1] K2 cut chain, [2] K2 end -> results ready
  * (the batch's share of the pipelined MD5 launches, K4 and the copy),

@@ -18,6 +18,7 @@ pytestmark = pytest.mark.gpu
 def k8_mode(request, monkeypatch):
     """Both decoders: a wave per stream (the default) and a lane per stream
     (picked for tens of thousands of short compressible streams)."""
+    monkeypatch.setenv("HBX_AB", "1")
     monkeypatch.setenv("HBX_K8_MODE", request.param)
     return request.param
 

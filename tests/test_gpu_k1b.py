@@ -14,6 +14,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture
 def k1b(monkeypatch):
+    monkeypatch.setenv("HBX_AB", "1")
     monkeypatch.setenv("HBX_K1_RUN", "128")
 
 

@@ -66,6 +66,7 @@ def test_content_id_windows(oracle, monkeypatch, window):
     with HBX_K4_WINDOW) and reads them twice, as ids and as links: files of
     many more chunks than the window restage it on both passes."""
     from hashbox_amd import Engine
+    monkeypatch.setenv("HBX_AB", "1")
     monkeypatch.setenv("HBX_K4_WINDOW", str(window))
     files = [oracle.random_bytes(n, 60 + i) for i, n in enumerate([9 * MAXB + 3, 40 * MAXB + 11, 3 * MIN])]
     with Engine(0) as e:
@@ -252,6 +253,7 @@ def test_pipelined_steady_state(oracle, monkeypatch, join_lag, plan_mode):
     the hash stream (HBX_PLAN_MODE 0/1: schedule only)."""
     from hashbox_amd import Engine
     if plan_mode is not None:
+        monkeypatch.setenv("HBX_AB", "1")
         monkeypatch.setenv("HBX_PLAN_MODE", plan_mode)
     batches = _device_batches(oracle, 3, 57)
     got = []
@@ -281,6 +283,7 @@ def test_reserved_pipeline_placements(oracle, monkeypatch, dense, k3_waves):
     wave placements (HBX_K3_DENSE) give the same bit-exact results through a
     pipeline that runs its scan stream two steps ahead."""
     from hashbox_amd import Engine
+    monkeypatch.setenv("HBX_AB", "1")
     monkeypatch.setenv("HBX_K3_DENSE", dense)
     batches = _device_batches(oracle, 2, 43)
     got, order = [], [i % 2 for i in range(12)]
@@ -308,8 +311,10 @@ def test_stream_cu_sets(oracle, monkeypatch, scan, hash_):
     A/B switches; the scan stream is masked to every CU by default) change
     only the schedule: the pipeline stays bit-exact."""
     from hashbox_amd import Engine
+    monkeypatch.setenv("HBX_AB", "1")
     monkeypatch.setenv("HBX_SCAN_CUS", scan)
     if hash_:
+        monkeypatch.setenv("HBX_AB", "1")
         monkeypatch.setenv("HBX_HASH_CUS", hash_)
     batches = _device_batches(oracle, 2, 47)
     got, order = [], [0, 1, 0, 1]

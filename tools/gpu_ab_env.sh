@@ -2,6 +2,7 @@
 # A/B of environment switches on one build, alternating so drift shows.
 # usage: ENVS="HBX_HASH_CUS=prio:hi;HBX_RES_CUS=prio:hi" BENCH_ARGS="--steps 20" tools/gpu_ab_env.sh
 set -o pipefail
+export HBX_AB=1  # the library honours HBX_* A/B switches only with this
 O=gpurun_out/abenv
 mkdir -p $O
 IFS=';' read -ra VS <<< "base;${ENVS}"

@@ -2,6 +2,7 @@
 # K1 tiles fitted to the CUs K3 leaves (default) vs two per CU (HBX_K1_FIT=0),
 # at 33-36 resident batches (64 files) and at strong-scaling batch sizes.
 set -o pipefail
+export HBX_AB=1  # the library honours HBX_* A/B switches only with this
 out=gpurun_out/k1fit; mkdir -p $out
 run() {  # tag fit args...
   local tag=$1 fit=$2; shift 2

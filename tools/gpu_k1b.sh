@@ -2,6 +2,7 @@
 # K1b (128-byte runs, 512 threads): parity, then the bench A/B against K1 at
 # the default residency (lead 2) and at lead 1 (hbx_input_after_oldest).
 set -o pipefail
+export HBX_AB=1  # the library honours HBX_* A/B switches only with this
 O=gpurun_out/${TAG:-k1b}
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_gpu_k1b.py -x -v --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }

@@ -2,6 +2,7 @@
 # K1 vs K1b under PMC (kernels serialized: each runs alone on the chip):
 # VALU instructions, wave cycles, issue activity.
 set -o pipefail
+export HBX_AB=1  # the library honours HBX_* A/B switches only with this
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-k1b_pmc}
 mkdir -p $O

@@ -2,6 +2,7 @@
 # K3 per-launch time with K1 serialized against it (CU-masked hash stream, every CU set):
 # separates K3's in-kernel fixed cost from K1's interference.  usage: bash tools/gpu_k3_alone.sh [files...]
 set -o pipefail
+export HBX_AB=1  # the library honours HBX_* A/B switches only with this
 for nf in ${@:-8 64}; do
   for m in "" "0:4096"; do
     HBX_HASH_CUS=$m timeout -k 10 200 python bench.py --no-cpu-baseline --no-check --workload random --steps 100 --files $nf \

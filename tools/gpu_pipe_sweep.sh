@@ -3,6 +3,7 @@
 # mode or lead "-" = the default).  Prints value, ms/step and kernel ms/step.
 # usage: bash tools/gpu_pipe_sweep.sh 8:2:-:- 8:3:-:6 ...
 set -o pipefail
+export HBX_AB=1  # the library honours HBX_* A/B switches only with this
 out=gpurun_out/pipe
 mkdir -p $out
 for cfg in "$@"; do

@@ -2,6 +2,7 @@
 # Strong-scaling batch (8 files per GPU, the N = 8 share): K1 vs K1b and the
 # K1 tile length, alternating.
 set -o pipefail
+export HBX_AB=1  # the library honours HBX_* A/B switches only with this
 O=gpurun_out/${TAG:-small_k1}; mkdir -p $O
 for i in 1 2; do for cfg in "64 0" "128 0" "64 16" "128 16"; do
   set -- $cfg

@@ -2,6 +2,7 @@
 # K1 tile length vs the scan lead: does a finer K1 tile (more, shorter
 # rounds over the CUs K3 leaves) remove the lead-1 cliff?
 set -o pipefail
+export HBX_AB=1  # the library honours HBX_* A/B switches only with this
 O=gpurun_out/${TAG:-tile_lead}
 mkdir -p $O
 for cfg in "64 1" "128 1" "32 1" "16 1" "128 -1"; do

@@ -2,6 +2,7 @@
 # K1 tile length per batch size (files per GPU = 64/N of strong scaling):
 # the automatic choice (two tiles per CU) vs shorter tiles, alternating.
 set -o pipefail
+export HBX_AB=1  # the library honours HBX_* A/B switches only with this
 O=gpurun_out/${TAG:-tile_sweep}; mkdir -p $O
 for cfg in ${CFGS:-"8 8" "8 16" "16 0" "16 16" "16 32" "32 0" "32 32" "32 64" "64 0" "64 128" "8 0"}; do
   set -- $cfg

@@ -2,6 +2,7 @@
 # Asynchronous compression in the disk path: the store_paths / deflate /
 # inflate / wire GPU tests, then config 5 with every chunk compressed.
 set -o pipefail
+export HBX_AB=1  # the library honours HBX_* A/B switches only with this
 O=gpurun_out/${TAG:-zpipe}; mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "store_paths or tree or deflate or wire or inflate" > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
