@@ -117,6 +117,15 @@ def parse():
                          "free).  Never the headline: the line is marked 'aliased'")
     ap.add_argument("--single-alloc", action="store_true",
                     help="the R arenas as views of one allocation instead of R allocations")
+    ap.add_argument("--dist-timeout", type=float, default=300.0,
+                    help="seconds a rank waits in torch.distributed setup and collectives before failing")
+    ap.add_argument("--plan-only", action="store_true",
+                    help="print each rank's residency plan (no GPU work) and exit; with --free-gib it runs "
+                         "on a CPU host (tests)")
+    ap.add_argument("--free-gib", type=float, default=0.0,
+                    help="--plan-only: free HBM per device to plan for (default: the device's)")
+    ap.add_argument("--fail-rank", type=int, default=-1,
+                    help="diagnostics: this rank raises during setup (every rank must then exit non-zero)")
     return ap.parse_args()
 
 
@@ -412,6 +421,66 @@ def run_workload(a, name, eng, arenas, offs, lens, R, B, need, lanes, dist, gpu,
     return out
 
 
+ARENA_SLACK = 64 << 20  # per resident batch beyond its packed bytes (allocator rounding)
+
+
+def residency_plan(files, file_mib, world, rank, scaling="strong", free_bytes=0, hbm_frac=0.95,
+                   ranks_per_device=1, arenas=0, md5_slice=-1, join_lag=0, lead=-1, e2e=False,
+                   alias_depth=0):
+    """The pipeline each rank runs, a pure function so the
+    CPU tests can check it for N = 1..8.  Files of the job: `files` x
+    `file_mib` MiB; strong scaling gives this rank its LPT share of each
+    step's files (independent files, store.go:84-199), weak a whole batch.
+    R batches stay resident (as many as `hbm_frac` of the free HBM holds),
+    each K3 launch advances every chain by B blocks, a batch needs `need`
+    launches and its chains join `lag` submits after its own:
+    need + lag <= R keeps the window free of forced drains."""
+    from hashbox_amd.shard import lpt_assign
+    import workloads as W
+    fbytes = file_mib << 20
+    job_lens = [fbytes] * files
+    mine = lpt_assign(job_lens, world)[rank] if scaling == "strong" else list(range(files))
+    lens = [job_lens[i] for i in mine]
+    if not lens:
+        raise ValueError(f"rank {rank} has no files: --files {files} < world {world}")
+    nf = len(lens)
+    # small per-GPU batches (strong scaling) are scan-latency-bound at lag 1:
+    # lag 3 plans each launch a step ahead (tools/gpu_pipe_sweep.sh: 8 files
+    # 1,576 -> 1,976 GiB/s, 16 files 1,752 -> 2,185); at 64 files lag 1 is best
+    lag = join_lag if join_lag > 0 else (3 if nf < 64 else 1)
+    ld = lead if lead >= 0 else lag + 1
+    offs, total = W.pack_layout(lens)
+    # launches a batch needs before its chains are all hashed
+    nfull = (min(fbytes, 8 << 20) + 8) >> 6
+    r_fit = max(ld + 1, int(free_bytes * hbm_frac / max(1, ranks_per_device)) // (total + ARENA_SLACK))
+    if e2e:
+        r_fit = min(r_fit, ld + 2)  # PCIe-bound: a shallow pipeline suffices
+    if md5_slice < 0:
+        R = arenas if arenas > 0 else r_fit
+        B = -(-nfull // max(1, R - ld))
+    else:
+        B = md5_slice
+        R = arenas if arenas > 0 else min((1 if B == 0 else -(-nfull // B)) + ld, r_fit)
+    physical = R
+    if alias_depth > 0:  # diagnostics: D in flight over the R physical arenas
+        R = alias_depth
+        if md5_slice < 0:
+            B = -(-nfull // max(1, R - ld))
+    need = 1 if B == 0 else -(-nfull // B)
+    if need + lag > R:
+        raise ValueError(f"pipeline depth {R} < launches per batch {need} + join lag {lag}: raise --arenas "
+                         "or the slice")
+    return {"mine": mine, "lens": lens, "files_per_gpu": nf, "join_lag": lag, "lead": ld, "offs": offs,
+            "arena_bytes": total, "R": R, "physical_arenas": physical, "B": B, "need": need,
+            "hbm_bytes": physical * (total + ARENA_SLACK), "file_bytes": fbytes}
+
+
+def check_host_bytes(plan, world_on_host=1):
+    """Host memory the oracle check legs take on one rank (a copy of one batch
+    plus the oracle's outputs), times the ranks sharing the host."""
+    return world_on_host * (int(plan["arena_bytes"]) + 64 * int(plan["files_per_gpu"]) * 1024)
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -420,80 +489,111 @@ def main():
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     if world != a.gpus and rank == 0:
         print(f"note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    ndev = torch.cuda.device_count()
+    ndev = torch.cuda.device_count()  # counts only; does not initialise the GPU
     dev_idx = local % max(ndev, 1)
-    torch.cuda.set_device(dev_idx)
     dev = torch.device("cuda", dev_idx)
     dist = None
     if world > 1:
+        import datetime
         import torch.distributed as dist
-        if a.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+        to = datetime.timedelta(seconds=a.dist_timeout)
+        if a.dist_backend == "nccl" and not a.plan_only:
+            torch.cuda.set_device(dev_idx)
+            dist.init_process_group("nccl", device_id=dev, timeout=to)
         else:
-            dist.init_process_group(a.dist_backend)
-    red_dev = dev if (dist and a.dist_backend == "nccl") else torch.device("cpu")
+            dist.init_process_group(a.dist_backend, timeout=to)
+    red_dev = dev if (dist and a.dist_backend == "nccl" and not a.plan_only) else torch.device("cpu")
 
-    from hashbox_amd import Engine, _lib
-    from hashbox_amd.shard import lpt_assign
-    import workloads as W
+    # Per-rank setup.  Any failure here (a bad plan, out of memory, a HIP
+    # error) is reported to every rank before the first barrier, so all exit
+    # non-zero instead of leaving the others waiting until the timeout.
+    err = None
+    try:
+        S = setup(a, rank, world, local_world, ndev, dev_idx, dev)
+    except Exception as e:  # noqa: BLE001  reported below, then every rank exits
+        import traceback
+        traceback.print_exc()
+        err = f"{type(e).__name__}: {e}"
+        S = None
+    ok = max_over_ranks(0.0 if err else 1.0, dist, red_dev, op="min") == 1.0
+    if not ok:
+        print(f"rank {rank}: setup failed ({err or 'on another rank'}); exiting", file=sys.stderr, flush=True)
+        if dist:
+            dist.destroy_process_group()
+        sys.exit(1)
+    if a.plan_only:
+        P = S["plan"]
+        mine = {"rank": rank, **{k: P[k] for k in ("files_per_gpu", "join_lag", "lead", "R", "physical_arenas",
+                                                   "B", "need", "hbm_bytes", "file_bytes", "arena_bytes")},
+                "mine": P["mine"], "check_host_bytes": check_host_bytes(P)}
+        plans = [mine]
+        if dist:
+            plans = [None] * world
+            dist.all_gather_object(plans, mine)
+            dist.destroy_process_group()
+        if rank == 0:
+            print(json.dumps({"plan_only": True, "world": world, "scaling": a.scaling, "plans": plans}), flush=True)
+        return
+    run(a, S, rank, world, local_world, dist, dev, red_dev)
 
-    fbytes = a.file_mib << 20
-    job_lens = [fbytes] * a.files
-    mine = lpt_assign(job_lens, world)[rank] if a.scaling == "strong" else list(range(a.files))
-    lens = [job_lens[i] for i in mine]
-    if not lens:
-        raise SystemExit(f"rank {rank} has no files: --files {a.files} < world {world}")
-    nf = len(lens)
-    # small per-GPU batches (strong scaling) are scan-latency-bound at lag 1:
-    # lag 3 plans each launch a step ahead (tools/gpu_pipe_sweep.sh: 8 files
-    # 1,576 -> 1,976 GiB/s, 16 files 1,752 -> 2,185); at 64 files lag 1 is best
-    lag = a.join_lag if a.join_lag > 0 else (3 if nf < 64 else 1)
-    lead = a.lead if a.lead >= 0 else lag + 1
-    offs, total = W.pack_layout(lens)
-    job_batch = (sum(job_lens) if a.scaling == "strong" else sum(job_lens) * world)
-    # launches a batch needs before its chains are all hashed
-    nfull = (min(fbytes, 8 << 20) + 8) >> 6
+
+def setup(a, rank, world, local_world, ndev, dev_idx, dev):
+    """Everything a rank prepares before the first barrier: its plan, arenas
+    and engine (with every pipeline buffer reserved)."""
+    if a.fail_rank == rank:
+        raise RuntimeError(f"--fail-rank {rank}: injected setup failure")
     # ranks sharing one device (tests) share its HBM
     share = max(1, -(-local_world // max(ndev, 1)))
-    free, _ = torch.cuda.mem_get_info(dev)
-    r_fit = max(lead + 1, int(free * a.hbm_frac / share) // (total + (64 << 20)))
-    if a.e2e:
-        r_fit = min(r_fit, lead + 2)  # PCIe-bound: a shallow pipeline suffices
-    if a.md5_slice < 0:
-        R = a.arenas if a.arenas > 0 else r_fit
-        B = -(-nfull // max(1, R - lead))
+    if a.plan_only and a.free_gib > 0:  # planning for one device per rank
+        free, share = int(a.free_gib * GIB), 1
     else:
-        B = a.md5_slice
-        R = a.arenas if a.arenas > 0 else min((1 if B == 0 else -(-nfull // B)) + lead, r_fit)
-    need = 1 if B == 0 else -(-nfull // B)
-    if need + lag > R:
-        raise SystemExit(f"pipeline depth {R} < launches per batch {need} + join lag {lag}: raise --arenas "
-                         "or the slice")
+        torch.cuda.set_device(dev_idx)
+        free, _ = torch.cuda.mem_get_info(dev)
+    P = residency_plan(a.files, a.file_mib, world, rank, a.scaling, free, a.hbm_frac, share, a.arenas,
+                       a.md5_slice, a.join_lag, a.lead, a.e2e, a.alias_depth)
+    if a.plan_only:
+        return {"plan": P}
+    from hashbox_amd import Engine
+    import workloads as W
+    lens, offs, total = P["lens"], P["offs"], P["arena_bytes"]
+    R, B, need, lag = P["R"], P["B"], P["need"], P["join_lag"]
     cores = cpu_info()
     threads = a.cpu_threads or cores["usable"]
-    if dist:  # ranks share the host's cores for the oracle check
+    if world > 1:  # ranks share the host's cores for the oracle check
         threads = max(1, threads // local_world)
-    arenas = W.random_arenas(R, total, a.seed + 7919 * rank, dev, single=a.single_alloc)
-    if a.alias_depth > 0:  # diagnostics: D in flight over the R physical arenas
-        n_phys = R
-        R = a.alias_depth
-        arenas = [arenas[i % n_phys] for i in range(R)]
-        if a.md5_slice < 0:
-            B = -(-nfull // max(1, R - lead))
-        need = 1 if B == 0 else -(-nfull // B)
+    # every rank generates its own share of the corpus from its own seed
+    # (seed + 7919 rank): strong scaling splits each step's file count, not
+    # one generated corpus
+    arenas = W.random_arenas(P["physical_arenas"], total, a.seed + 7919 * rank, dev, single=a.single_alloc)
+    if a.alias_depth > 0:  # diagnostics: D in flight over the physical arenas
+        arenas = [arenas[i % P["physical_arenas"]] for i in range(R)]
     ballast = torch.zeros(int(a.ballast_gib * GIB), dtype=torch.uint8, device=dev) if a.ballast_gib else None
     torch.cuda.synchronize(dev)
-
     if a.k3_probe:
         os.environ["HBX_AB"] = "1"
         os.environ["HBX_K3_PROBE"] = "1"
     eng = Engine(dev_idx, md5_slice=B, join_lag=lag, k3_waves=a.k3_waves)
     # every batch slot, chain table and summary buffer of the pipeline is
     # allocated now: an allocation inside the timed region would drain the streams
-    eng.reserve(R + 2, nf, sum(lens))
+    eng.reserve(R + 2, len(lens), sum(lens))
     for _ in range(2):  # single-batch latency (one batch alone, synchronous call), untimed
         eng.chunk_hash_device(arenas[0].data_ptr(), offs, lens)
     latency = eng.stage_times()
+    return {"plan": P, "arenas": arenas, "ballast": ballast, "eng": eng, "latency": latency, "cores": cores,
+            "threads": threads}
+
+
+def run(a, S, rank, world, local_world, dist, dev, red_dev):
+    """The measurement proper: steady-state windows, checks, the JSON line."""
+    from hashbox_amd import _lib
+    import workloads as W
+    P, eng, arenas, latency = S["plan"], S["eng"], S["arenas"], S["latency"]
+    lens, offs, total = P["lens"], P["offs"], P["arena_bytes"]
+    R, B, need, lag, lead, nf = P["R"], P["B"], P["need"], P["join_lag"], P["lead"], P["files_per_gpu"]
+    n_phys = P["physical_arenas"]
+    fbytes = P["file_bytes"]
+    cores, threads = S["cores"], S["threads"]
+    job_batch = a.files * fbytes if a.scaling == "strong" else a.files * fbytes * world
     lanes = torch.cuda.get_device_properties(dev).multi_processor_count * 4 * 64
 
     before = None
@@ -560,8 +660,13 @@ def main():
                                + (", sharded by file across GPUs: configs[2])" if world > 1 else ")"),
                    "files_per_step": a.files, "files_per_gpu": nf, "file_bytes": fbytes,
                    "md5_slice_blocks": B, "pipeline_depth": R, "launches_per_batch": need,
-                   "scan_lead": lead, "join_lag": lag, "k3_waves_per_simd": a.k3_waves, "parallelism": f"file-sharded x{world} ({a.scaling} scaling; "
-                                                       "independent HIP streams, no data-path collective)"},
+                   "scan_lead": lead, "join_lag": lag, "k3_waves_per_simd": a.k3_waves,
+                   "parallelism": f"file-sharded x{world} ({a.scaling} scaling; independent HIP streams, "
+                                  "no data-path collective)",
+                   "seeds": f"each rank generates its own share on its device: random arenas seed {a.seed} + "
+                            f"7919 x rank, Zipf corpus seed {a.seed + 4} + 7919 x rank"
+                            + (" (strong scaling splits each step's file count, not one corpus)"
+                               if world > 1 and a.scaling == "strong" else "")},
     }
     out.update({k: v for k, v in head.items() if k not in ("value", "ms_per_step")})
     out["single_batch"] = {"ms": round(float(latency[4]), 3),
@@ -574,7 +679,7 @@ def main():
     if a.alias_depth > 0:
         out["aliased"] = {"depth": R, "physical_arenas": n_phys,
                           "note": "diagnostic: in-flight batches share arenas; not a headline"}
-    out["lib"] = _lib.identity()
+    out["lib"] = dict(_lib.identity(), knobs=eng.knobs())
     if rank == 0:
         print(json.dumps(out), flush=True)
     if host_pin is not None:

@@ -72,3 +72,70 @@ def test_gloo_world2_sharded_matches_single():
         r = O.store_file(f, fast=True)
         assert res[i][0] == r.cut_ends.tolist()
         assert res[i][1] == [bytes(x).hex() for x in r.ids]
+
+
+# ---- bench.py's N>1 setup (the driver's 8-GPU run), on the CPU -------------
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FREE_GIB = 268.0  # free HBM one MI355X reports to a fresh process (~95 % of it is planned)
+
+
+@pytest.mark.parametrize("world", range(1, 9))
+@pytest.mark.parametrize("scaling", ["strong", "weak"])
+def test_residency_plan_per_world(world, scaling):
+    """Every rank's plan at N = 1..8: the files of a step are split exactly
+    (strong) or whole per rank (weak); need + lag <= R (no forced drain in the
+    window); B x need covers an 8 MiB chunk; the arenas fit 95 % of free HBM;
+    the check legs' host copies of all ranks fit the box's host memory."""
+    import bench
+    free = int(FREE_GIB * (1 << 30))
+    seen = []
+    host = 0
+    for rank in range(world):
+        P = bench.residency_plan(64, 128, world, rank, scaling, free)
+        nfull = ((8 << 20) + 8) >> 6
+        assert P["need"] + P["join_lag"] <= P["R"], P
+        assert P["B"] * P["need"] >= nfull
+        assert P["hbm_bytes"] <= 0.95 * free
+        assert P["join_lag"] == (3 if P["files_per_gpu"] < 64 else 1)
+        seen.extend(P["mine"])
+        host += bench.check_host_bytes(P)
+    if scaling == "strong":
+        assert sorted(seen) == list(range(64))
+        assert all(len(bench.residency_plan(64, 128, world, r, scaling, free)["mine"]) == 64 // world
+                   for r in range(world)) or 64 % world
+    else:
+        assert sorted(seen) == sorted(list(range(64)) * world)
+    assert host <= 64 << 30 if scaling == "strong" else host <= world * (9 << 30)
+
+
+def _bench_plan(world, extra, timeout=120):
+    import subprocess
+    import sys
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--plan-only",
+           "--free-gib", str(FREE_GIB), "--dist-backend", "gloo", "--gpus", str(world),
+           "--dist-timeout", "60"] + extra
+    return subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout,
+                          env=dict(os.environ, OMP_NUM_THREADS="1"))
+
+
+def test_bench_plan_world4_through_torchrun():
+    import json
+    r = _bench_plan(4, [])
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    plans = json.loads(line)["plans"]
+    assert [p["rank"] for p in plans] == [0, 1, 2, 3]
+    assert sorted(sum((p["mine"] for p in plans), [])) == list(range(64))
+    assert all(p["files_per_gpu"] == 16 and p["need"] + p["join_lag"] <= p["R"] for p in plans)
+
+
+def test_bench_failing_rank_exits_nonzero():
+    """A rank whose setup fails makes every rank exit non-zero before the
+    first barrier: torchrun returns an error quickly instead of hanging."""
+    import time
+    t0 = time.time()
+    r = _bench_plan(2, ["--fail-rank", "1"])
+    assert r.returncode != 0
+    assert time.time() - t0 < 60
+    assert "injected setup failure" in r.stderr and "setup failed (on another rank)" in r.stderr

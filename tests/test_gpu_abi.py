@@ -65,3 +65,19 @@ def test_state_rules(oracle):
         for a, r in zip(g, refs):
             assert np.array_equal(a.cut_ends, r.cut_ends) and np.array_equal(a.ids, r.ids)
             assert a.content_id == r.content_id
+
+
+def test_ab_switches_need_hbx_ab(monkeypatch):
+    """HBX_* A/B switches change nothing unless HBX_AB=1 (a caller's stray
+    environment must not swap kernels): HBX_K1_RUN=128 alone keeps K1."""
+    from hashbox_amd import Engine
+    monkeypatch.delenv("HBX_AB", raising=False)
+    monkeypatch.setenv("HBX_K1_RUN", "128")
+    monkeypatch.setenv("HBX_JOIN_LAG", "3")
+    with Engine(0) as e:
+        k = e.knobs()
+    assert k["ab_env"] == 0 and k["k1_run"] == 64 and k["join_lag"] == 1, k
+    monkeypatch.setenv("HBX_AB", "1")
+    with Engine(0) as e:
+        k = e.knobs()
+    assert k["ab_env"] == 1 and k["k1_run"] == 128 and k["join_lag"] == 3, k

@@ -1,0 +1,201 @@
+"""GPU: every BASELINE config that is a parity case, at its stated size,
+bit-exact against the oracle's literal storeFile loop (store.go:111-196) plus
+block.go:96-111 framing.
+
+* configs[0]: one 1 GiB uniform random file (PCG64 seed 1) — from disk through
+  hbx_store_paths and hbx_store_paths_z (every chunk's zlib stream strictly
+  inflated back to the chunk), from host memory through hbx_chunk_hash, and
+  device-resident through the pipelined submit/wait path.
+* configs[3]: the 32 GiB Zipf-duplicated corpus (256 x 128 MiB, ~50 % repeat
+  content) through the synchronous device call and the pipelined time-sliced
+  path (4 batches of 64 files in flight), every file against the oracle on
+  all host cores.
+* configs[4], scaled to 10,000 files: log-uniform 4 KiB-4 MiB sizes (seed 5),
+  a quarter of them compressible text, on disk, through hbx_store_paths and
+  hbx_store_paths_zcb: every file checked (not a sample), every compressed
+  stream inflated strictly (zlib, Adler-32, no trailing bytes) and equal to
+  its chunk, callbacks FIFO and each file reported exactly once.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GIB = 1 << 30
+
+
+def _threads():
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, int(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    return min(16, os.cpu_count() or 1)
+
+
+@pytest.fixture
+def big_tmp(tmp_path):
+    """A scratch directory for GiBs of files: /dev/shm when present (the box's
+    /tmp may be small), else pytest's tmp_path.  Removed afterwards."""
+    import shutil
+    import tempfile
+    d = tempfile.mkdtemp(prefix="hbx_cfg_", dir="/dev/shm") if os.path.isdir("/dev/shm") else str(tmp_path)
+    try:
+        yield d
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def _same(g, r):
+    assert np.array_equal(g.cut_ends, r.cut_ends), "cut ends differ"
+    assert np.array_equal(g.ids, r.ids), "block ids differ"
+
+
+def _chunks(data, cut_ends):
+    s = 0
+    for e in cut_ends:
+        yield data[s:int(e)]
+        s = int(e)
+
+
+def _check_streams(pairs, threads):
+    """pairs: [(data, FileChunks with zstreams)]; every chunk's stream must
+    inflate strictly to the chunk's bytes."""
+    from oracle import deflate as Z
+    from concurrent.futures import ThreadPoolExecutor
+    work = []
+    for data, res in pairs:
+        pieces = list(_chunks(data, res.cut_ends))
+        assert len(res.zstreams) == len(pieces)
+        work.extend(zip(res.zstreams, pieces))
+
+    def one(zp):
+        return Z.inflate_strict(bytes(zp[0])) == zp[1].tobytes()
+
+    with ThreadPoolExecutor(threads) as ex:
+        ok = list(ex.map(one, work))
+    assert all(ok), f"{ok.count(False)} zlib streams do not inflate to their chunks"
+
+
+def test_configs0_one_gib_file(engine, oracle, big_tmp):
+    import torch
+    n = 1 << 30
+    data = np.random.Generator(np.random.PCG64(1)).integers(0, 256, n, dtype=np.uint8)
+    ref = oracle.store_file(data)
+    assert ref.n_chunks > 100
+    # host memory, one call (hbx_chunk_hash)
+    got = engine.chunk_hash(data)
+    _same(got, ref)
+    assert got.content_type == ref.content_type == 3 and got.content_id == ref.content_id
+    # from disk (hbx_store_paths), then with every chunk compressed (hbx_store_paths_z)
+    p = os.path.join(big_tmp, "config0.bin")
+    data.tofile(p)
+    for compress in (False, True):
+        (r,) = engine.store_paths([p], compress=compress)
+        _same(r, ref)
+        assert r.content_id == ref.content_id
+        if compress:
+            _check_streams([(data, r)], _threads())
+    os.unlink(p)
+    # device-resident, pipelined (hbx_submit_device / hbx_wait, time-sliced K3)
+    from hashbox_amd import Engine
+    d = torch.empty(n + 65536, dtype=torch.uint8, device="cuda:0")
+    d[:n].copy_(torch.from_numpy(data))
+    torch.cuda.synchronize()
+    with Engine(0, md5_slice=4096) as e:
+        e.submit_device(d.data_ptr(), [0], [n])
+        (r,) = e.wait()
+    _same(r, ref)
+    assert r.content_id == ref.content_id
+    del d
+    torch.cuda.empty_cache()
+
+
+def test_configs3_zipf_32_gib(oracle):
+    import torch
+    import workloads as W
+    from hashbox_amd import Engine
+    files, fbytes = 256, 128 << 20
+    total = files * fbytes
+    arena = torch.empty(total + 65536, dtype=torch.uint8, device="cuda:0")
+    rep = W.zipf_fill([arena], total, seed=4)
+    assert 0.4 < rep < 0.6, rep
+    offs = np.arange(files, dtype=np.uint64) * np.uint64(fbytes)
+    lens = [fbytes] * files
+    with Engine(0) as e:  # synchronous: one call over all 256 files
+        sync = e.chunk_hash_device(arena.data_ptr(), offs, lens)
+    with Engine(0, md5_slice=2048) as e:  # pipelined: 4 batches of 64 in flight
+        for b0 in range(0, files, 64):
+            e.submit_device(arena.data_ptr(), offs[b0:b0 + 64], lens[b0:b0 + 64])
+        pipe = []
+        while e.pending():
+            pipe.extend(e.wait())
+    host = arena[:total].cpu().numpy()
+    del arena
+    torch.cuda.empty_cache()
+    refs = oracle.store_batch_mt([host[i * fbytes:(i + 1) * fbytes] for i in range(files)], _threads())
+    assert len(sync) == len(pipe) == files
+    chunks = 0
+    for s, p, r in zip(sync, pipe, refs):
+        _same(s, r)
+        _same(p, r)
+        assert s.content_id == p.content_id and s.content_type == p.content_type
+        assert s.content_type == (3 if r.n_chunks > 1 else 2)
+        chunks += r.n_chunks
+    assert chunks > 5000
+
+
+def _text_pool(g, n):
+    words = [bytes(g.integers(97, 123, int(k), dtype=np.uint8)) for k in g.integers(2, 10, 4096)]
+    ranks = np.minimum(g.zipf(1.2, n // 4), len(words)) - 1
+    return np.frombuffer(b" ".join(words[int(r)] for r in ranks), np.uint8)[:n]
+
+
+def test_configs4_ten_thousand_files_on_disk(engine, oracle, big_tmp):
+    g = np.random.Generator(np.random.PCG64(5))
+    n = 10_000
+    sizes = np.exp(g.uniform(np.log(4096), np.log(4 << 20), n)).astype(np.int64)
+    rand = g.integers(0, 256, 256 << 20, dtype=np.uint8)
+    text = _text_pool(g, 16 << 20)
+    offs = g.integers(0, 1 << 40, n)
+    datas, paths = [], []
+    for i in range(n):
+        pool = text if i % 4 == 0 else rand
+        o = int(offs[i]) % (pool.size - int(sizes[i]))
+        d = pool[o:o + int(sizes[i])]
+        p = os.path.join(big_tmp, f"{i // 1000:02d}_{i:05d}.bin")
+        d.tofile(p)
+        datas.append(d)
+        paths.append(p)
+    refs = oracle.store_batch_mt(datas, _threads())
+    plain = engine.store_paths(paths, sizes=sizes, batch_bytes=256 << 20)
+    seen = []
+
+    def on_batch(first, count):
+        seen.append((first, count))
+
+    comp = engine.store_paths(paths, sizes=sizes, compress=True, on_batch=on_batch, batch_bytes=256 << 20)
+    # the callbacks cover every file once, in order
+    nxt = 0
+    for first, count in seen:
+        assert first == nxt and count > 0
+        nxt += count
+    assert nxt == n and len(seen) > 4
+    single = 0
+    for d, r, a, b in zip(datas, refs, plain, comp):
+        _same(a, r)
+        _same(b, r)
+        assert a.content_id == b.content_id and a.content_type == b.content_type
+        single += r.n_chunks == 1
+    assert 0 < single < n
+    # every compressed stream: strict inflate back to its chunk; text compresses
+    threads = _threads()
+    zin = zout = 0
+    for i in range(0, n, 500):  # the streams of 500 files inflate in parallel
+        _check_streams(list(zip(datas[i:i + 500], comp[i:i + 500])), threads)
+    for i in range(0, n, 4):
+        zin += datas[i].size
+        zout += sum(int(z.size) for z in comp[i].zstreams)
+    assert zout < 0.6 * zin, (zout, zin)
