@@ -338,6 +338,83 @@ __global__ __launch_bounds__(256) void md5real(Rec* rec, uint32_t* sink, uint32_
   }
 }
 
+
+// Two independent chains per lane, step-interleaved (ILP inside one wave).
+#define MSTEP2(FN, a, b, c, d, x, t, s)                                    \
+  { MSTEP(FN, a##0, b##0, c##0, d##0, x##0, t, s); MSTEP(FN, a##1, b##1, c##1, d##1, x##1, t, s); }
+__device__ __forceinline__ void md5c2(uint32_t (&h0)[4], const uint32_t (&m0)[16], uint32_t (&h1)[4],
+                                      const uint32_t (&m1)[16]) {
+  uint32_t a0 = h0[0], b0 = h0[1], c0 = h0[2], d0 = h0[3];
+  uint32_t a1 = h1[0], b1 = h1[1], c1 = h1[2], d1 = h1[3];
+#define X(j) m##j
+  const uint32_t *mm0 = m0, *mm1 = m1;
+#define S2(FN, a, b, c, d, j, t, s) { MSTEP(FN, a##0, b##0, c##0, d##0, mm0[j], t, s); MSTEP(FN, a##1, b##1, c##1, d##1, mm1[j], t, s); }
+  S2(MF, a, b, c, d, 0, 0xd76aa478u, 7);  S2(MF, d, a, b, c, 1, 0xe8c7b756u, 12);
+  S2(MF, c, d, a, b, 2, 0x242070dbu, 17); S2(MF, b, c, d, a, 3, 0xc1bdceeeu, 22);
+  S2(MF, a, b, c, d, 4, 0xf57c0fafu, 7);  S2(MF, d, a, b, c, 5, 0x4787c62au, 12);
+  S2(MF, c, d, a, b, 6, 0xa8304613u, 17); S2(MF, b, c, d, a, 7, 0xfd469501u, 22);
+  S2(MF, a, b, c, d, 8, 0x698098d8u, 7);  S2(MF, d, a, b, c, 9, 0x8b44f7afu, 12);
+  S2(MF, c, d, a, b, 10, 0xffff5bb1u, 17); S2(MF, b, c, d, a, 11, 0x895cd7beu, 22);
+  S2(MF, a, b, c, d, 12, 0x6b901122u, 7); S2(MF, d, a, b, c, 13, 0xfd987193u, 12);
+  S2(MF, c, d, a, b, 14, 0xa679438eu, 17); S2(MF, b, c, d, a, 15, 0x49b40821u, 22);
+  S2(MG, a, b, c, d, 1, 0xf61e2562u, 5);  S2(MG, d, a, b, c, 6, 0xc040b340u, 9);
+  S2(MG, c, d, a, b, 11, 0x265e5a51u, 14); S2(MG, b, c, d, a, 0, 0xe9b6c7aau, 20);
+  S2(MG, a, b, c, d, 5, 0xd62f105du, 5);  S2(MG, d, a, b, c, 10, 0x02441453u, 9);
+  S2(MG, c, d, a, b, 15, 0xd8a1e681u, 14); S2(MG, b, c, d, a, 4, 0xe7d3fbc8u, 20);
+  S2(MG, a, b, c, d, 9, 0x21e1cde6u, 5);  S2(MG, d, a, b, c, 14, 0xc33707d6u, 9);
+  S2(MG, c, d, a, b, 3, 0xf4d50d87u, 14); S2(MG, b, c, d, a, 8, 0x455a14edu, 20);
+  S2(MG, a, b, c, d, 13, 0xa9e3e905u, 5); S2(MG, d, a, b, c, 2, 0xfcefa3f8u, 9);
+  S2(MG, c, d, a, b, 7, 0x676f02d9u, 14); S2(MG, b, c, d, a, 12, 0x8d2a4c8au, 20);
+  S2(MH, a, b, c, d, 5, 0xfffa3942u, 4);  S2(MH, d, a, b, c, 8, 0x8771f681u, 11);
+  S2(MH, c, d, a, b, 11, 0x6d9d6122u, 16); S2(MH, b, c, d, a, 14, 0xfde5380cu, 23);
+  S2(MH, a, b, c, d, 1, 0xa4beea44u, 4);  S2(MH, d, a, b, c, 4, 0x4bdecfa9u, 11);
+  S2(MH, c, d, a, b, 7, 0xf6bb4b60u, 16); S2(MH, b, c, d, a, 10, 0xbebfbc70u, 23);
+  S2(MH, a, b, c, d, 13, 0x289b7ec6u, 4); S2(MH, d, a, b, c, 0, 0xeaa127fau, 11);
+  S2(MH, c, d, a, b, 3, 0xd4ef3085u, 16); S2(MH, b, c, d, a, 6, 0x04881d05u, 23);
+  S2(MH, a, b, c, d, 9, 0xd9d4d039u, 4);  S2(MH, d, a, b, c, 12, 0xe6db99e5u, 11);
+  S2(MH, c, d, a, b, 15, 0x1fa27cf8u, 16); S2(MH, b, c, d, a, 2, 0xc4ac5665u, 23);
+  S2(MI, a, b, c, d, 0, 0xf4292244u, 6);  S2(MI, d, a, b, c, 7, 0x432aff97u, 10);
+  S2(MI, c, d, a, b, 14, 0xab9423a7u, 15); S2(MI, b, c, d, a, 5, 0xfc93a039u, 21);
+  S2(MI, a, b, c, d, 12, 0x655b59c3u, 6); S2(MI, d, a, b, c, 3, 0x8f0ccc92u, 10);
+  S2(MI, c, d, a, b, 10, 0xffeff47du, 15); S2(MI, b, c, d, a, 1, 0x85845dd1u, 21);
+  S2(MI, a, b, c, d, 8, 0x6fa87e4fu, 6);  S2(MI, d, a, b, c, 15, 0xfe2ce6e0u, 10);
+  S2(MI, c, d, a, b, 6, 0xa3014314u, 15); S2(MI, b, c, d, a, 13, 0x4e0811a1u, 21);
+  S2(MI, a, b, c, d, 4, 0xf7537e82u, 6);  S2(MI, d, a, b, c, 11, 0xbd3af235u, 10);
+  S2(MI, c, d, a, b, 2, 0x2ad7d2bbu, 15); S2(MI, b, c, d, a, 9, 0xeb86d391u, 21);
+#undef S2
+#undef X
+  h0[0] += a0; h0[1] += b0; h0[2] += c0; h0[3] += d0;
+  h1[0] += a1; h1[1] += b1; h1[2] += c1; h1[3] += d1;
+}
+template <int DUMMY>
+__global__ __launch_bounds__(256) void md5real2(Rec* rec, uint32_t* sink, uint32_t seed) {
+  extern __shared__ uint32_t lds[];
+  uint32_t m0[16], m1[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    m0[j] = seed * (j + 1) + threadIdx.x * 0x9e3779b9u;
+    m1[j] = seed * (j + 7) + threadIdx.x * 0x7f4a7c15u;
+  }
+  uint32_t h0[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+  uint32_t h1[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+  if (seed == 0xffffffffu) lds[threadIdx.x] = m0[0];
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < MD5_BLOCKS / 2; i++) {
+    md5c2(h0, m0, h1, m1);
+    m0[i & 15] ^= h0[0];
+    m1[i & 15] ^= h1[0];
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  sink[blockIdx.x * blockDim.x + threadIdx.x] = h0[0] ^ h0[1] ^ h1[2] ^ h1[3];
+  if ((threadIdx.x & 63) == 0) {
+    Rec r;
+    r.t0 = t0; r.t1 = t1;
+    r.hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+    r.xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11)) & 0xfu;
+    rec[blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = r;
+  }
+}
+
 typedef void (*KFn)(Rec*, uint32_t*, uint32_t);
 struct OpDesc { const char* name; KFn fn; int valu_per_unit; };
 
@@ -345,6 +422,7 @@ struct OpDesc { const char* name; KFn fn; int valu_per_unit; };
 static const OpDesc OPS[] = {
     { "md5_real_xad (per STEP)", md5real<1>, MD5_BLOCKS * 64 / (ITER * 16) },
     { "md5_real_bitop3 (per STEP)", md5real<0>, MD5_BLOCKS * 64 / (ITER * 16) },
+    { "md5_real_2chains (per chain-STEP)", md5real2<0>, MD5_BLOCKS * 64 / (ITER * 16) },
     OPD("v_add_u32", 0, 8),      OPD("v_add3_u32", 1, 8),    OPD("v_bitop3_b32", 2, 8),
     OPD("v_alignbit_b32", 3, 8), OPD("v_xor_b32", 4, 8),     OPD("v_lshl_add_u32", 5, 8),
     OPD("v_add_u16_sdwa", 6, 8), OPD("v_pk_add_u16", 7, 8),  OPD("v_max3_u32", 8, 8),
@@ -396,7 +474,9 @@ int main(int argc, char** argv) {
   printf("# %s, %d CUs; clock %d kHz (prop)\n", prop.gcnArchName, cus, prop.clockRate);
   printf("# op, waves/SIMD, SIMDs, median cycles per wave-VALU per SIMD (aggregate), p10, p90, "
          "per-wave cycles/VALU (median), kernel ms, implied GHz\n");
+  const char* only = argc > 2 ? argv[2] : nullptr;
   for (const OpDesc& op : OPS) {
+    if (only && !strstr(op.name, only)) continue;
     for (int k : {1, 2, 4, 8}) {
       const size_t lds = (k == 1) ? 96 * 1024 : (k == 2) ? 64 * 1024 : (k == 4) ? 36 * 1024 : 18 * 1024;
       (void)hipFuncSetAttribute((const void*)op.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
