@@ -46,18 +46,32 @@ import torch  # noqa: E402
 
 METRIC = "device-resident GiB/s chunked+hashed at 1/2/4/8 MI355X; % HBM roofline"
 K3_VALU_PER_BLOCK = 325
-# The path is VALU-issue-bound (DESIGN.md §6 "The bound"): PMC SQ_INSTS_VALU
-# per launch of the default workload (profiles/r02b_pmc_summary.txt) gives
-# the wave-instructions per input byte of K1 (6.825e8 / 8 GiB) and K3
-# (6.887e8 / 8 GiB); a SIMD retires at most one wave64 VALU instruction per
-# ~4.84 cycles on this integer mix (K3 one wave per SIMD: 1.21 quad-cycles
-# per VALU at 91 % issue-active; K1 alone, four waves per SIMD, the same
-# per-SIMD rate; K3 with two waves per SIMD, --k3-waves 2, takes 1.87x as
-# long per launch).  Peak = 1024 SIMDs x 2.4 GHz (spec clock) / 4.84.
+# VALU issue ceiling (DESIGN.md §6 "The bound"), measured by
+# tools/ubench/valu_issue.hip on every SIMD of the chip with every wave
+# stamped (profiles/r03b/valu_issue.txt, r03d, r03f):
+#  * half-rate ops (v_add3, v_alignbit, SDWA, DPP, v_max3, v_perm, v_dot4,
+#    v_lshl_add, v_lshlrev, v_max_u32, ...): 4.10 cycles per wave64
+#    instruction per SIMD at 8 waves per SIMD, never dual-issued;
+#  * full-rate ops (v_add_u32, v_xor/and/or, v_bitop3, v_lshrrev, 16-bit
+#    VOP2 adds, v_fma_f32): 2.2-2.5 cycles with >= 2 waves (two waves
+#    dual-issue, SQ_ACTIVE_INST_VALU2), 4.66 with one wave;
+#  * one wave alone issues at most one instruction per ~4.1 cycles whatever
+#    its class (the compiler's MD5 step chain: 21.1 cycles per 5.1 VALU).
+# K1's scan is all half-rate ops at four waves per SIMD, and K3 runs one wave
+# per SIMD (a chain's speed, not the SIMD's total rate, sets the pipeline's
+# throughput at fixed residency: DESIGN.md §6), so both are capped at one
+# wave64 VALU per 4.10 cycles per SIMD.  Per-byte instruction counts: PMC
+# SQ_INSTS_VALU per launch of the default workload (profiles/r03c).
 K1_WAVE_VALU_PER_BYTE = 6.825e8 / (8 << 30)
-K3_WAVE_VALU_PER_BYTE = 6.887e8 / (8 << 30)
-SIMD_CYCLES_PER_VALU = 4.84
+K3_WAVE_VALU_PER_BYTE = 6.901e8 / (8 << 30)
+SIMD_CYCLES_PER_VALU = 4.10
 VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / SIMD_CYCLES_PER_VALU
+VALU_SOURCE = "tools/ubench/valu_issue.hip (profiles/r03b/valu_issue.txt); SQ_INSTS_VALU profiles/r03c"
+# Achievable HBM read bandwidth (tools/ubench/roofline_probe, round 1), and
+# the path's two reads of every byte: K1 scans it, K3 hashes it once its cut
+# is known (the first MD5 block holds BE32(len)), so the algorithmic rate is
+# at most half of what HBM delivers.
+HBM_PROBE_GBS = 6580.0
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md), GB/s
 GIB = 1 << 30
 KNAMES = ["k1_digest_scan", "k2_cut_chain", "k2c_chain_plan", "k3_block_md5", "k4_content_id"]
@@ -209,6 +223,28 @@ def measured_traffic(kernel, per_launch_bytes, batch_bytes):
     if not k:
         return None, None
     return int(k["hbm_bytes"]), os.path.relpath(files[-1], ROOT)
+
+
+def path_roofline(alg_bps, batch_bytes):
+    """Every byte is read twice per step (K1, then K3), so the algorithmic
+    rate can reach at most half of the HBM read bandwidth: with the probe's
+    6.58 TB/s that is 3.29 TB/s, 41 % of the 8 TB/s spec, for any design that
+    hashes after cutting.  `read_bytes_per_step` is the measured traffic of
+    both kernels (PMC FETCH_SIZE, tools/pmc_traffic.py)."""
+    t1, src = measured_traffic(KERNEL_OF["k1_digest_scan"], batch_bytes, batch_bytes)
+    t3, _ = measured_traffic(KERNEL_OF["k3_block_md5"], batch_bytes, batch_bytes)
+    alg = alg_bps / 1e9
+    out = {"unit": "GB/s", "algorithmic": round(alg, 2), "peak": HBM_PEAK_GBS,
+           "reads_per_byte": 2, "two_read_ceiling": round(HBM_PROBE_GBS / 2, 1),
+           "frac_of_two_read_ceiling": round(alg / (HBM_PROBE_GBS / 2), 4),
+           "two_read_ceiling_frac_of_spec": round(HBM_PROBE_GBS / 2 / HBM_PEAK_GBS, 4)}
+    if t1 and t3:
+        step_s = batch_bytes / alg_bps
+        out.update({"read_bytes_per_step": int(t1 + t3), "read_gbs": round((t1 + t3) / step_s / 1e9, 2),
+                    "frac": round((t1 + t3) / step_s / 1e9 / HBM_PEAK_GBS, 4),
+                    "frac_of_probe": round((t1 + t3) / step_s / 1e9 / HBM_PROBE_GBS, 4),
+                    "traffic_source": src})
+    return out
 
 
 # -------------------------------------------------------------- pipeline --
@@ -385,19 +421,19 @@ def run_workload(a, name, eng, arenas, offs, lens, R, B, need, lanes, dist, gpu,
         "fill_drain_gibs": round(r["batches_total"] * job_batch_bytes / fill / GIB, 3),
         "chunks_per_gpu_step": n_chunks,
         "longest_chunk_bytes": longest,
+        # the contract's HBM roofline of the dominant kernel; what actually
+        # limits K3 is its VALU issue at one wave per SIMD ("limiter")
         "roofline": {"kernel": "k3_block_md5", "bound": "hbm", "achieved": round(achieved, 2),
+                     "limiter": "valu-issue: one MD5 wave per SIMD, a chain's 5 dependent VALU per step",
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": traffic, "traffic_source": traffic_src, "launches": k3_n,
                      "avg_launch_ms": round(float(avg_ms[3]), 4),
                      "algorithmic_bytes_per_launch": int(per_launch), "window_only": True},
         "k1_roofline": {"achieved": round(k1_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(k1_gbs / HBM_PEAK_GBS, 4), "avg_launch_ms": round(float(avg_ms[0]), 4)},
-        # K3 is VALU-issue work: ~325 VALU per 64-B block on the cooperative
-        # path (5 per MD5 step); chip peak 256 CU x 4 SIMD-32 x 32 lanes x
-        # 2.4 GHz; one wave issues at most one VALU per 4 cycles.
-        # the whole path's bound: K1 + K3 VALU wave-instructions per step over
-        # the chip's measured issue capacity at the spec clock (the box runs
-        # power-capped at ~2.09 GHz while pipelined)
+        # the whole path's issue bound: K1 + K3 VALU wave-instructions per
+        # step over the chip's measured issue ceiling for their classes at the
+        # spec clock (the box runs power-capped at ~2.09 GHz while pipelined)
         "valu_roofline": {"bound": "valu-issue", "unit": "wave-instr/s per GPU",
                           "achieved": round(rank_batch * (K1_WAVE_VALU_PER_BYTE + K3_WAVE_VALU_PER_BYTE)
                                             / (el / a.steps), 0),
@@ -407,7 +443,10 @@ def run_workload(a, name, eng, arenas, offs, lens, R, B, need, lanes, dist, gpu,
                           "k1_valu_per_byte": round(K1_WAVE_VALU_PER_BYTE * 64, 3),
                           "k3_valu_per_byte": round(K3_WAVE_VALU_PER_BYTE * 64, 3),
                           "simd_cycles_per_valu": SIMD_CYCLES_PER_VALU,
-                          "source": "profiles/r02b_pmc_summary.txt (SQ_INSTS_VALU), profiles/r02g_k3w2"},
+                          "source": VALU_SOURCE},
+        # bytes the step actually reads (K1 + K3, PMC FETCH_SIZE) against the
+        # spec peak, and the algorithmic rate against the two-read ceiling
+        "path_roofline": path_roofline(a.steps * rank_batch / el, rank_batch),
         "k3_lanes": lane_occupancy(r["arena_res"], R, B, need, lanes),
         "kernel_ms_per_step": {n: round(float(v) / a.steps, 4) for n, v in zip(KNAMES, tot_ms)},
         "window_launches": {n: int(v) for n, v in zip(KNAMES, tot_n)},

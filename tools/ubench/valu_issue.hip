@@ -415,14 +415,232 @@ __global__ __launch_bounds__(256) void md5real2(Rec* rec, uint32_t* sink, uint32
   }
 }
 
+
+// Operand-read test: the same ops with every source a DIFFERENT register
+// (16 live registers, op i reads r[i+5], r[i+9] (, r[i+13]) and writes r[i]),
+// to separate the ALU rate from register-file reads (the single-op streams
+// above read the same m/k registers every instruction).
+template <int OP>
+__global__ __launch_bounds__(256) void distinct(Rec* rec, uint32_t* sink, uint32_t seed) {
+  extern __shared__ uint32_t lds[];
+  uint32_t r[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) r[j] = seed * (j + 3) + threadIdx.x;
+  if (seed == 0xffffffffu) lds[threadIdx.x] = r[0];
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < ITER; it++) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+#pragma unroll
+      for (int i = 0; i < 16; i++) {
+        uint32_t& d = r[i];
+        const uint32_t a = r[(i + 5) & 15], b = r[(i + 9) & 15], c = r[(i + 13) & 15];
+        if constexpr (OP == 0) asm volatile("v_add_u32_e32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+        if constexpr (OP == 1) asm volatile("v_xor_b32_e32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+        if constexpr (OP == 2) asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+        if constexpr (OP == 3) asm volatile("v_add3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+        if constexpr (OP == 4) asm volatile("v_alignbit_b32 %0, %1, %1, 7" : "=v"(d) : "v"(a));
+        if constexpr (OP == 5) asm volatile("v_add_u32_e32 %0, 0x5a827999, %1" : "=v"(d) : "v"(a));
+        if constexpr (OP == 6) asm volatile("v_mov_b32_e32 %0, %1" : "=v"(d) : "v"(a));
+        if constexpr (OP == 7) asm volatile("v_add_u32_e32 %0, %1, %0" : "+v"(d) : "v"(a));
+        if constexpr (OP == 8) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xca" : "+v"(d) : "v"(a), "v"(b));
+        if constexpr (OP == 9) asm volatile("v_add3_u32 %0, %1, %2, 0x10" : "=v"(d) : "v"(a), "v"(b));
+        if constexpr (OP == 10) asm volatile("v_alignbit_b32 %0, %1, %2, 7" : "=v"(d) : "v"(a), "v"(b));
+      }
+    }
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  uint32_t x = 0;
+#pragma unroll
+  for (int j = 0; j < 16; j++) x ^= r[j];
+  sink[blockIdx.x * blockDim.x + threadIdx.x] = x;
+  if ((threadIdx.x & 63) == 0) {
+    Rec rr;
+    rr.t0 = t0; rr.t1 = t1;
+    rr.hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+    rr.xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11)) & 0xfu;
+    rec[blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = rr;
+  }
+}
+
+
+// MD5 steps in inline asm with the constant as a literal in its own
+// full-rate v_add (no SGPR constants, no s_mov per step): bitop3 F, add a+x,
+// add K, add F, alignbit, add b = four full-rate + one half-rate op.
+// IMM: F 0xca (b?c:d), G 0xe4 (d?b:c), H 0x96, I 0x39 (c^(b|~d)).
+#define ASTEP(IMM, a, b, c, d, x, K, S)                                                       \
+  {                                                                                           \
+    uint32_t f_, t_;                                                                          \
+    asm volatile("v_bitop3_b32 %1, %3, %4, %5 bitop3:" #IMM "\n\t"                            \
+                 "v_add_u32_e32 %2, %0, %6\n\t"                                               \
+                 "v_add_u32_e32 %2, " #K ", %2\n\t"                                           \
+                 "v_add_u32_e32 %2, %2, %1\n\t"                                               \
+                 "v_alignbit_b32 %2, %2, %2, 32-" #S "\n\t"                                   \
+                 "v_add_u32_e32 %0, %2, %3"                                                    \
+                 : "+v"(a), "=&v"(f_), "=&v"(t_)                                               \
+                 : "v"(b), "v"(c), "v"(d), "v"(x));                                            \
+  }
+#define AROUNDS(ST, m)                                                                                  \
+  ST(0xca, a, b, c, d, m[0], 0xd76aa478, 7) ST(0xca, d, a, b, c, m[1], 0xe8c7b756, 12)                  \
+  ST(0xca, c, d, a, b, m[2], 0x242070db, 17) ST(0xca, b, c, d, a, m[3], 0xc1bdceee, 22)                 \
+  ST(0xca, a, b, c, d, m[4], 0xf57c0faf, 7) ST(0xca, d, a, b, c, m[5], 0x4787c62a, 12)                  \
+  ST(0xca, c, d, a, b, m[6], 0xa8304613, 17) ST(0xca, b, c, d, a, m[7], 0xfd469501, 22)                 \
+  ST(0xca, a, b, c, d, m[8], 0x698098d8, 7) ST(0xca, d, a, b, c, m[9], 0x8b44f7af, 12)                  \
+  ST(0xca, c, d, a, b, m[10], 0xffff5bb1, 17) ST(0xca, b, c, d, a, m[11], 0x895cd7be, 22)               \
+  ST(0xca, a, b, c, d, m[12], 0x6b901122, 7) ST(0xca, d, a, b, c, m[13], 0xfd987193, 12)                \
+  ST(0xca, c, d, a, b, m[14], 0xa679438e, 17) ST(0xca, b, c, d, a, m[15], 0x49b40821, 22)               \
+  ST(0xe4, a, b, c, d, m[1], 0xf61e2562, 5) ST(0xe4, d, a, b, c, m[6], 0xc040b340, 9)                   \
+  ST(0xe4, c, d, a, b, m[11], 0x265e5a51, 14) ST(0xe4, b, c, d, a, m[0], 0xe9b6c7aa, 20)                \
+  ST(0xe4, a, b, c, d, m[5], 0xd62f105d, 5) ST(0xe4, d, a, b, c, m[10], 0x02441453, 9)                  \
+  ST(0xe4, c, d, a, b, m[15], 0xd8a1e681, 14) ST(0xe4, b, c, d, a, m[4], 0xe7d3fbc8, 20)                \
+  ST(0xe4, a, b, c, d, m[9], 0x21e1cde6, 5) ST(0xe4, d, a, b, c, m[14], 0xc33707d6, 9)                  \
+  ST(0xe4, c, d, a, b, m[3], 0xf4d50d87, 14) ST(0xe4, b, c, d, a, m[8], 0x455a14ed, 20)                 \
+  ST(0xe4, a, b, c, d, m[13], 0xa9e3e905, 5) ST(0xe4, d, a, b, c, m[2], 0xfcefa3f8, 9)                  \
+  ST(0xe4, c, d, a, b, m[7], 0x676f02d9, 14) ST(0xe4, b, c, d, a, m[12], 0x8d2a4c8a, 20)                \
+  ST(0x96, a, b, c, d, m[5], 0xfffa3942, 4) ST(0x96, d, a, b, c, m[8], 0x8771f681, 11)                  \
+  ST(0x96, c, d, a, b, m[11], 0x6d9d6122, 16) ST(0x96, b, c, d, a, m[14], 0xfde5380c, 23)               \
+  ST(0x96, a, b, c, d, m[1], 0xa4beea44, 4) ST(0x96, d, a, b, c, m[4], 0x4bdecfa9, 11)                  \
+  ST(0x96, c, d, a, b, m[7], 0xf6bb4b60, 16) ST(0x96, b, c, d, a, m[10], 0xbebfbc70, 23)                \
+  ST(0x96, a, b, c, d, m[13], 0x289b7ec6, 4) ST(0x96, d, a, b, c, m[0], 0xeaa127fa, 11)                 \
+  ST(0x96, c, d, a, b, m[3], 0xd4ef3085, 16) ST(0x96, b, c, d, a, m[6], 0x04881d05, 23)                 \
+  ST(0x96, a, b, c, d, m[9], 0xd9d4d039, 4) ST(0x96, d, a, b, c, m[12], 0xe6db99e5, 11)                 \
+  ST(0x96, c, d, a, b, m[15], 0x1fa27cf8, 16) ST(0x96, b, c, d, a, m[2], 0xc4ac5665, 23)                \
+  ST(0x39, a, b, c, d, m[0], 0xf4292244, 6) ST(0x39, d, a, b, c, m[7], 0x432aff97, 10)                  \
+  ST(0x39, c, d, a, b, m[14], 0xab9423a7, 15) ST(0x39, b, c, d, a, m[5], 0xfc93a039, 21)                \
+  ST(0x39, a, b, c, d, m[12], 0x655b59c3, 6) ST(0x39, d, a, b, c, m[3], 0x8f0ccc92, 10)                 \
+  ST(0x39, c, d, a, b, m[10], 0xffeff47d, 15) ST(0x39, b, c, d, a, m[1], 0x85845dd1, 21)                \
+  ST(0x39, a, b, c, d, m[8], 0x6fa87e4f, 6) ST(0x39, d, a, b, c, m[15], 0xfe2ce6e0, 10)                 \
+  ST(0x39, c, d, a, b, m[6], 0xa3014314, 15) ST(0x39, b, c, d, a, m[13], 0x4e0811a1, 21)                \
+  ST(0x39, a, b, c, d, m[4], 0xf7537e82, 6) ST(0x39, d, a, b, c, m[11], 0xbd3af235, 10)                 \
+  ST(0x39, c, d, a, b, m[2], 0x2ad7d2bb, 15) ST(0x39, b, c, d, a, m[9], 0xeb86d391, 21)
+__device__ __forceinline__ void md5_asm(uint32_t (&h)[4], const uint32_t (&m)[16]) {
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
+  AROUNDS(ASTEP, m)
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d;
+}
+// two chains, step-interleaved
+#define ASTEP2(IMM, a, b, c, d, x, K, S) ASTEP(IMM, a##0, b##0, c##0, d##0, x##0, K, S) ASTEP(IMM, a##1, b##1, c##1, d##1, x##1, K, S)
+#define AROUNDS2(ST)                                                                                   \
+  ST(0xca, a, b, c, d, m0[0]*0+mA[0], 0xd76aa478, 7)
+__device__ __forceinline__ void md5_asm2(uint32_t (&h0)[4], const uint32_t (&mA)[16], uint32_t (&h1)[4],
+                                         const uint32_t (&mB)[16]) {
+  uint32_t a0 = h0[0], b0 = h0[1], c0 = h0[2], d0 = h0[3];
+  uint32_t a1 = h1[0], b1 = h1[1], c1 = h1[2], d1 = h1[3];
+#define ST2(IMM, a, b, c, d, x, K, S) ASTEP(IMM, a##0, b##0, c##0, d##0, mA[x], K, S) ASTEP(IMM, a##1, b##1, c##1, d##1, mB[x], K, S)
+#define IDX(j) j
+  ST2(0xca, a, b, c, d, 0, 0xd76aa478, 7) ST2(0xca, d, a, b, c, 1, 0xe8c7b756, 12)
+  ST2(0xca, c, d, a, b, 2, 0x242070db, 17) ST2(0xca, b, c, d, a, 3, 0xc1bdceee, 22)
+  ST2(0xca, a, b, c, d, 4, 0xf57c0faf, 7) ST2(0xca, d, a, b, c, 5, 0x4787c62a, 12)
+  ST2(0xca, c, d, a, b, 6, 0xa8304613, 17) ST2(0xca, b, c, d, a, 7, 0xfd469501, 22)
+  ST2(0xca, a, b, c, d, 8, 0x698098d8, 7) ST2(0xca, d, a, b, c, 9, 0x8b44f7af, 12)
+  ST2(0xca, c, d, a, b, 10, 0xffff5bb1, 17) ST2(0xca, b, c, d, a, 11, 0x895cd7be, 22)
+  ST2(0xca, a, b, c, d, 12, 0x6b901122, 7) ST2(0xca, d, a, b, c, 13, 0xfd987193, 12)
+  ST2(0xca, c, d, a, b, 14, 0xa679438e, 17) ST2(0xca, b, c, d, a, 15, 0x49b40821, 22)
+  ST2(0xe4, a, b, c, d, 1, 0xf61e2562, 5) ST2(0xe4, d, a, b, c, 6, 0xc040b340, 9)
+  ST2(0xe4, c, d, a, b, 11, 0x265e5a51, 14) ST2(0xe4, b, c, d, a, 0, 0xe9b6c7aa, 20)
+  ST2(0xe4, a, b, c, d, 5, 0xd62f105d, 5) ST2(0xe4, d, a, b, c, 10, 0x02441453, 9)
+  ST2(0xe4, c, d, a, b, 15, 0xd8a1e681, 14) ST2(0xe4, b, c, d, a, 4, 0xe7d3fbc8, 20)
+  ST2(0xe4, a, b, c, d, 9, 0x21e1cde6, 5) ST2(0xe4, d, a, b, c, 14, 0xc33707d6, 9)
+  ST2(0xe4, c, d, a, b, 3, 0xf4d50d87, 14) ST2(0xe4, b, c, d, a, 8, 0x455a14ed, 20)
+  ST2(0xe4, a, b, c, d, 13, 0xa9e3e905, 5) ST2(0xe4, d, a, b, c, 2, 0xfcefa3f8, 9)
+  ST2(0xe4, c, d, a, b, 7, 0x676f02d9, 14) ST2(0xe4, b, c, d, a, 12, 0x8d2a4c8a, 20)
+  ST2(0x96, a, b, c, d, 5, 0xfffa3942, 4) ST2(0x96, d, a, b, c, 8, 0x8771f681, 11)
+  ST2(0x96, c, d, a, b, 11, 0x6d9d6122, 16) ST2(0x96, b, c, d, a, 14, 0xfde5380c, 23)
+  ST2(0x96, a, b, c, d, 1, 0xa4beea44, 4) ST2(0x96, d, a, b, c, 4, 0x4bdecfa9, 11)
+  ST2(0x96, c, d, a, b, 7, 0xf6bb4b60, 16) ST2(0x96, b, c, d, a, 10, 0xbebfbc70, 23)
+  ST2(0x96, a, b, c, d, 13, 0x289b7ec6, 4) ST2(0x96, d, a, b, c, 0, 0xeaa127fa, 11)
+  ST2(0x96, c, d, a, b, 3, 0xd4ef3085, 16) ST2(0x96, b, c, d, a, 6, 0x04881d05, 23)
+  ST2(0x96, a, b, c, d, 9, 0xd9d4d039, 4) ST2(0x96, d, a, b, c, 12, 0xe6db99e5, 11)
+  ST2(0x96, c, d, a, b, 15, 0x1fa27cf8, 16) ST2(0x96, b, c, d, a, 2, 0xc4ac5665, 23)
+  ST2(0x39, a, b, c, d, 0, 0xf4292244, 6) ST2(0x39, d, a, b, c, 7, 0x432aff97, 10)
+  ST2(0x39, c, d, a, b, 14, 0xab9423a7, 15) ST2(0x39, b, c, d, a, 5, 0xfc93a039, 21)
+  ST2(0x39, a, b, c, d, 12, 0x655b59c3, 6) ST2(0x39, d, a, b, c, 3, 0x8f0ccc92, 10)
+  ST2(0x39, c, d, a, b, 10, 0xffeff47d, 15) ST2(0x39, b, c, d, a, 1, 0x85845dd1, 21)
+  ST2(0x39, a, b, c, d, 8, 0x6fa87e4f, 6) ST2(0x39, d, a, b, c, 15, 0xfe2ce6e0, 10)
+  ST2(0x39, c, d, a, b, 6, 0xa3014314, 15) ST2(0x39, b, c, d, a, 13, 0x4e0811a1, 21)
+  ST2(0x39, a, b, c, d, 4, 0xf7537e82, 6) ST2(0x39, d, a, b, c, 11, 0xbd3af235, 10)
+  ST2(0x39, c, d, a, b, 2, 0x2ad7d2bb, 15) ST2(0x39, b, c, d, a, 9, 0xeb86d391, 21)
+  h0[0] += a0; h0[1] += b0; h0[2] += c0; h0[3] += d0;
+  h1[0] += a1; h1[1] += b1; h1[2] += c1; h1[3] += d1;
+}
+#include "md5_asm_variants.inc"
+template <int CH>
+__global__ __launch_bounds__(256) void md5asm(Rec* rec, uint32_t* sink, uint32_t seed) {
+  extern __shared__ uint32_t lds[];
+  uint32_t m0[16], m1[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    m0[j] = seed * (j + 1) + threadIdx.x * 0x9e3779b9u;
+    m1[j] = seed * (j + 7) + threadIdx.x * 0x7f4a7c15u;
+  }
+  uint32_t h0[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+  uint32_t h1[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+  if (seed == 0xffffffffu) lds[threadIdx.x] = m0[0];
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < MD5_BLOCKS / (CH >= 20 ? 2 : CH >= 10 ? 1 : CH); i++) {
+    if constexpr (CH == 1) {
+      md5_asm(h0, m0);
+    } else if constexpr (CH >= 10 && CH < 20) {
+      if constexpr (CH == 10) md5v_plain(h0, m0);
+      if constexpr (CH == 11) md5v_nop(h0, m0);
+      if constexpr (CH == 12) md5v_mov(h0, m0);
+      if constexpr (CH == 13) md5v_xkfirst(h0, m0);
+      if constexpr (CH == 14) md5v_xkfirst_nop(h0, m0);
+      if constexpr (CH == 15) md5v_nop_after_r(h0, m0);
+      if constexpr (CH == 16) md5v_nop2(h0, m0);
+    } else if constexpr (CH >= 20) {
+      if constexpr (CH == 20) md5v2_op(h0, m0, h1, m1);
+      if constexpr (CH == 21) md5v2_step(h0, m0, h1, m1);
+      if constexpr (CH == 22) md5v2_op_nop(h0, m0, h1, m1);
+      m1[i & 15] ^= h1[0];
+    } else {
+      md5_asm2(h0, m0, h1, m1);
+      m1[i & 15] ^= h1[0];
+    }
+    m0[i & 15] ^= h0[0];
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  sink[blockIdx.x * blockDim.x + threadIdx.x] = h0[0] ^ h0[1] ^ h1[2] ^ h1[3];
+  if ((threadIdx.x & 63) == 0) {
+    Rec r;
+    r.t0 = t0; r.t1 = t1;
+    r.hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+    r.xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11)) & 0xfu;
+    rec[blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = r;
+  }
+}
+
 typedef void (*KFn)(Rec*, uint32_t*, uint32_t);
 struct OpDesc { const char* name; KFn fn; int valu_per_unit; };
 
 #define OPD(n, i, v) { n, stream<i>, v }
 static const OpDesc OPS[] = {
+    { "distinct v_add_u32 (2 reads)", distinct<0>, 8 },
+    { "distinct v_xor_b32 (2 reads)", distinct<1>, 8 },
+    { "distinct v_bitop3 (3 reads)", distinct<2>, 8 },
+    { "distinct v_add3 (3 reads)", distinct<3>, 8 },
+    { "distinct v_alignbit (1 read)", distinct<4>, 8 },
+    { "distinct v_add_u32 literal (1 read)", distinct<5>, 8 },
+    { "distinct v_mov_b32 (1 read)", distinct<6>, 8 },
+    { "distinct v_add_u32 acc (2 reads, dst=src)", distinct<7>, 8 },
+    { "distinct v_bitop3 acc (3 reads, dst=src)", distinct<8>, 8 },
+    { "distinct v_add3 literal (2 reads)", distinct<9>, 8 },
+    { "distinct v_alignbit (2 reads)", distinct<10>, 8 },
     { "md5_real_xad (per STEP)", md5real<1>, MD5_BLOCKS * 64 / (ITER * 16) },
     { "md5_real_bitop3 (per STEP)", md5real<0>, MD5_BLOCKS * 64 / (ITER * 16) },
     { "md5_real_2chains (per chain-STEP)", md5real2<0>, MD5_BLOCKS * 64 / (ITER * 16) },
+    { "md5_asm_litK (per STEP)", md5asm<1>, MD5_BLOCKS * 64 / (ITER * 16) },
+    { "md5_asm_litK_2chains (per chain-STEP)", md5asm<2>, MD5_BLOCKS * 64 / (ITER * 16) },
+    { "md5v plain (per chain-STEP)", md5asm<10>, MD5_BLOCKS * 64 / (ITER * 16) },
+    { "md5v nop (per chain-STEP)", md5asm<11>, MD5_BLOCKS * 64 / (ITER * 16) },
+    { "md5v mov (per chain-STEP)", md5asm<12>, MD5_BLOCKS * 64 / (ITER * 16) },
+    { "md5v xkfirst (per chain-STEP)", md5asm<13>, MD5_BLOCKS * 64 / (ITER * 16) },
+    { "md5v xkfirst_nop (per chain-STEP)", md5asm<14>, MD5_BLOCKS * 64 / (ITER * 16) },
+    { "md5v nop_after_r (per chain-STEP)", md5asm<15>, MD5_BLOCKS * 64 / (ITER * 16) },
+    { "md5v nop2 (per chain-STEP)", md5asm<16>, MD5_BLOCKS * 64 / (ITER * 16) },
+    { "md5v 2ch_op (per chain-STEP)", md5asm<20>, MD5_BLOCKS * 64 / (ITER * 16) },
+    { "md5v 2ch_step (per chain-STEP)", md5asm<21>, MD5_BLOCKS * 64 / (ITER * 16) },
+    { "md5v 2ch_op_nop (per chain-STEP)", md5asm<22>, MD5_BLOCKS * 64 / (ITER * 16) },
     OPD("v_add_u32", 0, 8),      OPD("v_add3_u32", 1, 8),    OPD("v_bitop3_b32", 2, 8),
     OPD("v_alignbit_b32", 3, 8), OPD("v_xor_b32", 4, 8),     OPD("v_lshl_add_u32", 5, 8),
     OPD("v_add_u16_sdwa", 6, 8), OPD("v_pk_add_u16", 7, 8),  OPD("v_max3_u32", 8, 8),
