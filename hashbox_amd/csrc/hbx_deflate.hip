@@ -8,16 +8,17 @@
 // (block.go:101).  What must hold is that the stream is valid zlib (RFC 1950/
 // 1951) and inflates to the block's data; that is what the tests check.
 //
-// Layout of one block's stream (all segments independent, so one workgroup
-// per 32 KiB segment, no serial dependence between segments):
+// Layout of one block's stream (one workgroup per 32 KiB segment; segments
+// are coded independently, so there is no serial dependence between them):
 //
 //   78 9C | seg 0 | seg 1 | ... | 01 00 00 FF FF | adler32 (BE)
 //
-//   seg = one non-final fixed-Huffman block (BTYPE 01) of LZ77 tokens whose
-//         matches stay inside the segment, closed by an empty stored block
-//         (a sync flush: 3 zero bits, pad, 00 00 FF FF) so the segment ends on
-//         a byte boundary; or, if that is not smaller, one non-final stored
-//         block (00 | LEN | ~LEN | data).
+//   seg = one non-final fixed- or dynamic-Huffman block (BTYPE 01 / 10) of
+//         LZ77 tokens, closed by an empty stored block (a sync flush: 3 zero
+//         bits, pad, 00 00 FF FF) so the segment ends on a byte boundary; or,
+//         if that is not smaller, one non-final stored block (00 | LEN | ~LEN
+//         | data).  Matches may reach back into the 16 KiB of the block before
+//         the segment (its history; the inflater's window holds it).
 //
 // K7a hbx_k7_deflate_size   per segment: LZ77 parse, coded image into a
 //                           scratch slot, its size, mode and Adler partials
@@ -27,18 +28,33 @@
 //                           stream at its byte offset
 //
 // The LZ77 parse (one 512-thread workgroup per 32 KiB segment, all in LDS):
-//   1. candidates, in position order: round r covers positions 512r..512r+511
-//      (thread t: 512r+t).  A 2048 x 4 hash table of 4-byte prefixes holds,
-//      per hash and per position residue mod 4, the latest position inserted
-//      so far (ds_max, no lock; one barrier per round, so a slot may already
-//      hold a later position of the same round, which is skipped).  Each thread keeps the
-//      longest verified match among its <= 4 candidates (as a distance).
-//   2. thread t parses its own 64-byte range greedily with those distances,
-//      one-step lazy (a longer match at p+1 defers p as a literal, as zlib's
-//      lazy matching does), a match growing 4 bytes per compare up to 258 or
-//      the range end; it counts the fixed-Huffman bits;
-//   3. after a workgroup prefix sum of the bit counts, the same parse emits
-//      the bits (ds_or) into the image, if that is smaller than stored.
+//   1. candidates, in position order.  The history's positions are inserted
+//      first, then round r covers segment positions 512r..512r+511 (thread t:
+//      512r+t).  A 2048-bucket hash table of 4-byte prefixes keeps each
+//      bucket's 8 latest positions (a 16-bit counter per bucket picks the
+//      slot; one barrier per round, so a slot may already hold a later
+//      position of the same round, which is skipped).  Each position keeps
+//      the longest verified match among its <= 8 candidates within 32 KiB
+//      (as a distance).
+//   2. the parse, greedy with one-step lazy matching (a longer match at p+1
+//      defers p as a literal, as zlib's lazy matching does).  Thread t owns
+//      the 64-byte range [64t, 64t+64) but a match may run past its end (up
+//      to 258 bytes), and the next thread then starts where it ended: every
+//      thread first parses from its range start ("dry", no writes), the ends
+//      are handed on, and threads whose start moved parse again, until no
+//      start moves (greedy parses resynchronise within a few tokens, so this
+//      takes one or two rounds; after 8 the last starts are kept and each
+//      thread's final parse is clipped to its successor's start, which keeps
+//      the stream exact either way).  The final parse records the tokens,
+//      symbol frequencies and fixed-code bits;
+//   3. after a workgroup prefix sum of the bit counts, the tokens are emitted
+//      (ds_or) into the image, if that is smaller than stored.
+// Versus the round-2 parse (32 KiB window starting at the segment, 4 latest
+// positions per bucket residue, matches clipped at the 64-byte range end) the
+// Zipf-text corpus of tools/bench_deflate.py compresses to ~0.325 of its size
+// instead of 0.368 (zlib -6: 0.311); tools/k7model/k7model.c models both
+// (history 16 KiB: 0.329 modelled, 12 KiB 0.331, none 0.372 = round 2's
+// 0.368 measured).  LDS: 162.6 of the CU's 160 KiB = 163,840 bytes.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -52,8 +68,14 @@ constexpr uint32_t kThreads = 512;
 constexpr uint32_t kWaves = kThreads / 64;
 constexpr uint32_t kSub = kSeg / kThreads;  // 64 bytes per thread in the parse
 constexpr uint32_t kHashBits = 11;
-constexpr uint32_t kWays = 4;
-constexpr uint32_t kDataWords = kSeg / 4 + 4;        // + slack for 4-byte reads past the end
+constexpr uint32_t kWays = 8;                 // positions kept per bucket (16-bit entries)
+constexpr uint32_t kHist = 16384;             // history bytes before a segment (within its block)
+constexpr uint32_t kHistWords = kHist / 4;
+constexpr uint32_t kWindow = 32768;           // deflate's largest distance
+constexpr uint32_t kParseRounds = 8;          // bound on the start hand-off rounds
+constexpr uint32_t kNice = 128;               // stop looking for a longer match at this length (zlib -6)
+constexpr uint32_t kRepSet = 2048;            // slots of the early-out's repeat sample set
+constexpr uint32_t kDataWords = kSeg / 4 + 8;        // + slack for the 16-byte reads past the end
 // The segment and the candidate array live in LDS with one pad dword per
 // parse range (kSub/4 data dwords, kSub/2 candidate dwords): thread t's range
 // starts kSub bytes after thread t-1's, which without padding puts the 64
@@ -63,7 +85,9 @@ constexpr uint32_t kCdShift = 31 - __builtin_clz(kSub / 2);
 constexpr uint32_t kDataPhys = kDataWords + (kDataWords >> kDataShift) + 1;
 constexpr uint32_t kCdPhys = (kSeg / 2 + (kSeg / 2 >> kCdShift)) * 2;  // u16 slots
 constexpr uint32_t kImgWords = (kSeg + 16) / 4 + 4;  // stored image (5 + kSeg) or a smaller fixed one
-constexpr uint32_t kTabWords = (1u << kHashBits) * kWays;
+// hash table: 2048 x 8 u16 entries (window position + 1), then 2048 u16
+// counters, in the region later reused for the Huffman scratch and the image
+constexpr uint32_t kTabWords = (1u << kHashBits) * kWays / 2 + (1u << kHashBits) / 2;
 constexpr uint32_t kSlot = kImgWords * 4;  // scratch bytes per segment
 constexpr uint32_t kAdlerMod = 65521;
 constexpr uint32_t kLazy = 32;  // no look-ahead past a match this long
@@ -160,12 +184,61 @@ __device__ __forceinline__ void load_segment(uint32_t* data, const uint8_t* src,
   for (uint32_t k = threadIdx.x; k < kDataWords; k += kThreads) data[dphys(k)] = k < nw ? base[k] : 0u;
 }
 
-// Common prefix length of the strings at p and q (q < p), at most limit.
-__device__ __forceinline__ uint32_t match_len(const uint32_t* data, uint32_t sh, uint32_t p, uint32_t q,
-                                              uint32_t limit) {
-  uint32_t len = 0u;
+// Window word i: the history's words first (unpadded: the parse never walks
+// them), then the segment's (padded).  hw = history words present.  The two
+// are one LDS array (data == hist + kHistWords), so a word is one load
+// whichever part it is in.
+__device__ __forceinline__ uint32_t wword(const uint32_t* hist, const uint32_t* data, uint32_t hw, uint32_t i) {
+  (void)data;
+  return hist[i < hw ? i : kHistWords + dphys(i - hw)];
+}
+// 4 bytes at window byte b (window position + sh)
+__device__ __forceinline__ uint32_t win4(const uint32_t* hist, const uint32_t* data, uint32_t hw, uint32_t b) {
+  const uint32_t i = b >> 2;
+  return __builtin_amdgcn_alignbyte(wword(hist, data, hw, i + 1u), wword(hist, data, hw, i), b & 3u);
+}
+
+// 16 bytes at segment byte b (position + sh) / window byte b, as 4 dwords:
+// five independent LDS loads, so a thread's candidates overlap their latency
+__device__ __forceinline__ void seg16(const uint32_t* data, uint32_t b, uint32_t (&c)[4]) {
+  const uint32_t i = b >> 2, r = b & 3u;
+  uint32_t w[5];
+#pragma unroll
+  for (int j = 0; j < 5; j++) w[j] = data[dphys(i + (uint32_t)j)];
+#pragma unroll
+  for (int j = 0; j < 4; j++) c[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], r);
+}
+__device__ __forceinline__ void win16(const uint32_t* hist, const uint32_t* data, uint32_t hw, uint32_t b,
+                                      uint32_t (&c)[4]) {
+  const uint32_t i = b >> 2, r = b & 3u;
+  uint32_t w[5];
+#pragma unroll
+  for (int j = 0; j < 5; j++) w[j] = wword(hist, data, hw, i + (uint32_t)j);
+#pragma unroll
+  for (int j = 0; j < 4; j++) c[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], r);
+}
+// leading equal bytes of two 16-byte strings (0..16)
+__device__ __forceinline__ uint32_t eq16(const uint32_t (&a)[4], const uint32_t (&b)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const uint32_t d = a[j] ^ b[j];
+    if (d) return 4u * (uint32_t)j + ((uint32_t)__builtin_ctz(d) >> 3);
+  }
+  return 16u;
+}
+
+// Common prefix length of the segment string at p and the window string at
+// window position q (q < p + hl), at most limit: the first 16 bytes with
+// independent loads, then 4 bytes per compare (matches past 16 are rare).
+__device__ __forceinline__ uint32_t match_len(const uint32_t* hist, const uint32_t* data, uint32_t hw,
+                                              uint32_t sh, uint32_t p, uint32_t q, uint32_t limit) {
+  uint32_t a[4], b[4];
+  seg16(data, p + sh, a);
+  win16(hist, data, hw, q + sh, b);
+  uint32_t len = eq16(a, b);
+  if (len < 16u) return min(len, limit);
   while (len < limit) {
-    const uint32_t dlt = seg4(data, p + len + sh) ^ seg4(data, q + len + sh);
+    const uint32_t dlt = seg4(data, p + len + sh) ^ win4(hist, data, hw, q + len + sh);
     if (dlt) {
       len += (uint32_t)__builtin_ctz(dlt) >> 3;
       break;
@@ -204,49 +277,61 @@ __device__ __forceinline__ void dist_sym(uint32_t dist, uint32_t& sym, uint32_t&
   }
 }
 
-// Step 2: thread t's greedy parse of [64t, 64t+64) ∩ [0, n) with the
-// candidate distances in `cd`, one-step lazy.  The tokens overwrite the
-// candidate slots they cover (already consumed): a literal at p is
-// 0x8000 | byte in slot p; a match is len in slot p and dist in slot p+1.
-// Symbol frequencies go to hll/hd; returns the fixed-code bits, `extra` the
-// extra bits (the same under any code).
-__device__ __forceinline__ uint32_t tokenize(const uint32_t* data, uint16_t* cd, uint32_t* hll, uint32_t* hd,
-                                             uint32_t sh, uint32_t n, uint32_t& extra) {
-  const uint32_t r0 = threadIdx.x * kSub;
-  const uint32_t end = min(r0 + kSub, n);
-  uint32_t bits = 0u, p = r0, len = 0u, d = 0u;
+// Step 2: the greedy parse of one thread, one-step lazy, with the candidate
+// distances in `cd` (d = 0: none).  Dry (REC = false): from s while p < rend
+// (the thread's range end), matches up to min(258, n - p); returns where the
+// last token ends, which may be past rend.  Final (REC = true): from s while
+// p < send (the next thread's start), matches clipped to send; the tokens
+// overwrite the candidate slots they cover (already consumed): a literal at p
+// is 0x8000 | byte in slot p; a match is len in slot p and dist in slot p+1.
+// Symbol frequencies go to hll/hd; `bits` = fixed-code bits, `extra` = extra
+// bits (the same under any code).  Lookahead only while p + 1 < rend, in both
+// passes, so a converged final parse repeats the dry one token for token.
+template <bool REC>
+__device__ __forceinline__ uint32_t parse(const uint32_t* hist, const uint32_t* data, uint32_t hw, uint16_t* cd,
+                                          uint32_t* hll, uint32_t* hd, uint32_t sh, uint32_t hl, uint32_t n,
+                                          uint32_t s, uint32_t rend, uint32_t send, uint32_t& bits,
+                                          uint32_t& extra) {
+  const uint32_t stop = REC ? send : rend;
+  const uint32_t cap = REC ? send : n;
+  uint32_t p = s, len = 0u, d = 0u;
+  bits = 0u;
   extra = 0u;
   bool have = false;  // (len, d) already hold the match at p
-  while (p < end) {
+  while (p < stop) {
     if (!have) {
       d = cd[cphys(p)];
-      len = d ? match_len(data, sh, p, p - d, min(258u, end - p)) : 0u;
+      len = d ? match_len(hist, data, hw, sh, p, p + hl - d, min(258u, cap - p)) : 0u;
     }
     have = false;
     bool defer = false;
     uint32_t len1 = 0u, d1 = 0u;
-    if (len >= 4u && len < kLazy && p + 1u < end) {
+    if (len >= 4u && len < kLazy && p + 1u < rend) {
       d1 = cd[cphys(p + 1u)];
-      len1 = d1 ? match_len(data, sh, p + 1u, p + 1u - d1, min(258u, end - p - 1u)) : 0u;
+      len1 = d1 ? match_len(hist, data, hw, sh, p + 1u, p + 1u + hl - d1, min(258u, cap - p - 1u)) : 0u;
       defer = len1 > len;  // lazy: p becomes a literal, the longer match starts at p + 1
     }
     if (len >= 4u && !defer) {
-      uint32_t v, nb, sym, ne, ex, ds, dne, dex;
-      match_code(len, d, v, nb);
-      len_sym(len, sym, ne, ex);
-      dist_sym(d, ds, dne, dex);
-      atomicAdd(&hll[sym], 1u);
-      atomicAdd(&hd[ds], 1u);
-      extra += ne + dne;
-      bits += nb;
-      cd[cphys(p)] = (uint16_t)len;
-      cd[cphys(p + 1u)] = (uint16_t)d;
+      if (REC) {
+        uint32_t v, nb, sym, ne, ex, ds, dne, dex;
+        match_code(len, d, v, nb);
+        len_sym(len, sym, ne, ex);
+        dist_sym(d, ds, dne, dex);
+        atomicAdd(&hll[sym], 1u);
+        atomicAdd(&hd[ds], 1u);
+        extra += ne + dne;
+        bits += nb;
+        cd[cphys(p)] = (uint16_t)len;
+        cd[cphys(p + 1u)] = (uint16_t)d;
+      }
       p += len;
     } else {
-      const uint32_t b = seg4(data, p + sh) & 0xFFu;
-      atomicAdd(&hll[b], 1u);
-      bits += b < 144u ? 8u : 9u;
-      cd[cphys(p)] = (uint16_t)(0x8000u | b);
+      if (REC) {
+        const uint32_t b = seg4(data, p + sh) & 0xFFu;
+        atomicAdd(&hll[b], 1u);
+        bits += b < 144u ? 8u : 9u;
+        cd[cphys(p)] = (uint16_t)(0x8000u | b);
+      }
       p += 1u;
       if (defer) {
         len = len1;
@@ -255,7 +340,7 @@ __device__ __forceinline__ uint32_t tokenize(const uint32_t* data, uint16_t* cd,
       }
     }
   }
-  return bits;
+  return p;
 }
 
 __device__ __forceinline__ void emit_bits(uint32_t* img, uint32_t& o, uint32_t v, uint32_t nb) {
@@ -269,11 +354,9 @@ __device__ __forceinline__ void emit_bits(uint32_t* img, uint32_t& o, uint32_t v
 // | length << 16); EMIT = false returns their bits, EMIT = true writes them.
 template <bool EMIT>
 __device__ __forceinline__ uint32_t walk_tokens(const uint16_t* cd, const uint32_t* llc, const uint32_t* dcc,
-                                                uint32_t* img, uint32_t n, uint32_t o) {
-  const uint32_t r0 = threadIdx.x * kSub;
-  const uint32_t end = min(r0 + kSub, n);
+                                                uint32_t* img, uint32_t s, uint32_t send, uint32_t o) {
   uint32_t bits = 0u;
-  for (uint32_t p = r0; p < end;) {
+  for (uint32_t p = s; p < send;) {
     const uint32_t v = cd[cphys(p)];
     if (v & 0x8000u) {
       const uint32_t e = llc[v & 0xFFu];
@@ -448,6 +531,19 @@ __device__ __forceinline__ uint32_t wg_incl_sum(uint32_t x, uint32_t* wsum, uint
 
 }  // namespace hbxz
 
+// Diagnostics (tools/ubench/k7_phases.hip builds with HBX_K7_PROBE=1): thread
+// 0 of each workgroup stamps s_memtime at the phase boundaries.
+#ifndef HBX_K7_PROBE
+#define HBX_K7_PROBE 0
+#endif
+#if HBX_K7_PROBE
+__device__ unsigned long long hbx_k7_probe[1 << 20];
+#define K7P(i) \
+  if (threadIdx.x == 0 && blockIdx.x < (1u << 16)) hbx_k7_probe[16u * blockIdx.x + (i)] = __builtin_amdgcn_s_memtime()
+#else
+#define K7P(i)
+#endif
+
 // Global segment g -> its block (binary search over seg0).
 __device__ __forceinline__ uint32_t zblock_of(const hbxz::ZBlock* blocks, uint32_t nb, uint32_t g) {
   uint32_t lo = 0, hi = nb - 1u;
@@ -466,9 +562,12 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
                                                                        hbxz::SegInfo* __restrict__ info,
                                                                        uint32_t* __restrict__ scratch) {
   using namespace hbxz;
-  __shared__ uint32_t data[kDataPhys];
+  __shared__ uint32_t win[kHistWords + kDataPhys];  // history words, then the segment's
+  uint32_t* const hist = win;
+  uint32_t* const data = win + kHistWords;
   __shared__ uint32_t tab[kTabWords > kImgWords ? kTabWords : kImgWords];  // hash table, then the image
   __shared__ uint16_t cd[kCdPhys];
+  __shared__ uint32_t starts[kThreads + 1];  // each thread's parse start (step 2)
   __shared__ uint32_t wsum[kWaves];
   __shared__ unsigned long long wadler[2 * kWaves];
   __shared__ uint32_t hll[288], hd[32], llc[288], dcc[32], rle[320], clf[19], clc[19], zpar[8], zctl[8];
@@ -476,37 +575,79 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
   __shared__ uint8_t cll[20];
   const uint32_t g = blockIdx.x;
   if (g >= nseg) return;
+  K7P(0);
   const ZBlock bk = blocks[zblock_of(blocks, nb, g)];
   const uint32_t s = g - bk.seg0;
   const uint64_t off = (uint64_t)s * kSeg;
   const uint32_t n = (uint32_t)min((uint64_t)kSeg, bk.len - off);
   const uint32_t t = threadIdx.x;
   uint32_t sh;
-  load_segment(data, reinterpret_cast<const uint8_t*>(bk.src) + off, n, sh);
+  const uint8_t* seg_src = reinterpret_cast<const uint8_t*>(bk.src) + off;
+  load_segment(data, seg_src, n, sh);
+  // history: the kHist bytes of the block before this segment (word j holds
+  // window bytes [4j - sh, 4j - sh + 4), like the segment's words), loaded
+  // only for a segment that is parsed (after the early-out below)
+  const uint32_t hl = s ? kHist : 0u, hw = hl / 4u;
   for (uint32_t k = t; k < kTabWords; k += kThreads) tab[k] = 0u;
   for (uint32_t k = t; k < 288u; k += kThreads) hll[k] = k == 256u ? 1u : 0u;  // EOB once
   for (uint32_t k = t; k < 32u; k += kThreads) hd[k] = 0u;
   __syncthreads();
 
+  K7P(1);
   // 0. incompressible segments: the order-0 entropy of the bytes.  At >= 7.97
-  //    bits per byte no Huffman code beats a stored block, and the parse
-  //    (steps 1-2) is skipped: the segment is stored.  Every stream stays
-  //    valid zlib; only a segment of random bytes that repeats itself within
-  //    32 KiB compresses less than a full parse would make it.
+  //    bits per byte no Huffman code beats a stored block, and unless the
+  //    window repeats itself the parse (steps 1-2) would find nothing either:
+  //    the segment is stored.  Repeats are detected by content-defined
+  //    sampling: every window position whose 4-byte prefix hashes to 0 mod 64
+  //    goes into a small set, and a second occurrence of the same 4 bytes
+  //    (random data repeating within the segment samples the same positions
+  //    of both copies) keeps the full parse.  Random data without repeats
+  //    puts ~510 samples into the set, colliding in 32 bits with probability
+  //    < 1e-4 (which only costs the parse).  Only the segment is sampled, not
+  //    its history: a repeat whose source lies only in the 16 KiB before the
+  //    segment is not seen (the segment is then stored, as in round 2).
   uint32_t A = 0u, J = 0u;  // sum x, sum j*x over this thread's positions (j < 32768: J < 2^32)
   uint32_t fbits = 0u, fincl = 0u, ftot = 0u, fixed_bytes = 0xFFFFFFFFu;
+  uint32_t p_s = 0u, p_e = 0u;  // this thread's tokens: positions [p_s, p_e)
   const uint32_t stored_bytes = 5u + n;
   bool incompressible = false;
   if (n >= 4096u) {
     for (uint32_t k = t; k < 256u; k += kThreads) llc[k] = 0u;
+    if (t == 0u) zctl[7] = 0u;
     __syncthreads();
-    for (uint32_t p = t; p < n; p += kThreads) atomicAdd(&llc[seg4(data, p + sh) & 0xFFu], 1u);
+    // tab[0 .. kRepSet): the sample set (zeroed at entry), keys x + 1
+    auto sample = [&](uint32_t x) -> bool {
+      if (zhash(x) & 63u) return false;
+      const uint32_t key = x + 1u ? x + 1u : 1u;
+      const uint32_t i0 = (x * 0x85EBCA6Bu) >> (32 - 11);
+      for (uint32_t r = 0; r < 8u; r++) {
+        const uint32_t old = atomicCAS(&tab[(i0 + r) & (kRepSet - 1u)], 0u, key);
+        if (old == 0u) return false;
+        if (old == key) return true;
+      }
+      return false;
+    };
+    bool rep = false;
+    for (uint32_t p = t; p < n; p += kThreads) {
+      const uint32_t x = seg4(data, p + sh);
+      atomicAdd(&llc[x & 0xFFu], 1u);
+      if (p + 4u <= n) rep |= sample(x);
+    }
+    if (rep) zctl[7] = 1u;
     __syncthreads();
     const uint32_t cnt = t < 256u ? llc[t] : 0u;
-    const uint32_t bits = cnt ? (uint32_t)((float)cnt * (__log2f((float)n) - __log2f((float)cnt))) : 0u;
+    // per-symbol bits rounded (truncating lost ~0.004 bits per byte)
+    const uint32_t bits = cnt ? (uint32_t)((float)cnt * (__log2f((float)n) - __log2f((float)cnt)) + 0.5f) : 0u;
     uint32_t hsum;
     (void)wg_incl_sum(bits, wsum, hsum);
-    incompressible = (float)hsum >= 7.97f * (float)n;  // wave-uniform (a workgroup total)
+    incompressible = (float)hsum >= 7.97f * (float)n && zctl[7] == 0u;  // workgroup-uniform
+    for (uint32_t k = t; k < kRepSet; k += kThreads) tab[k] = 0u;  // the candidate table starts empty
+    __syncthreads();
+  }
+  if (!incompressible && hl) {
+    const uint32_t* hb = reinterpret_cast<const uint32_t*>(seg_src - sh - hl);
+    for (uint32_t k = t; k < hw; k += kThreads) hist[k] = hb[k];
+    __syncthreads();
   }
   if (incompressible) {
     for (uint32_t p = t; p < n; p += kThreads) {
@@ -516,28 +657,59 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
     }
     if (t == 0) zpar[0] = 0u;
   } else {
-    // 1. candidates in position order + Adler partials
+    // 1. candidates in position order + Adler partials.  tab16[h*8 + k]:
+    //    window position + 1 of bucket h's k-th entry; cnt16[h]: inserts
+    //    so far (the slot of the next one, mod 8)
+    uint16_t* tab16 = reinterpret_cast<uint16_t*>(tab);
+    uint32_t* cnt = tab + (1u << kHashBits) * kWays / 2u;
+    auto insert = [&](uint32_t w, uint32_t h) {
+      const uint32_t sft = 16u * (h & 1u);
+      const uint32_t k = (atomicAdd(&cnt[h >> 1], 1u << sft) >> sft) & (kWays - 1u);
+      tab16[h * kWays + k] = (uint16_t)(w + 1u);
+    };
+    for (uint32_t r = 0; r < hl / kThreads; r++) {  // the history: inserts only
+      const uint32_t w = kThreads * r + t;
+      if (w + 4u <= hl + n) insert(w, zhash(win4(hist, data, hw, w + sh)));
+      __syncthreads();
+    }
+    K7P(2);
     for (uint32_t r = 0; r < kSeg / kThreads; r++) {
       const uint32_t p = kThreads * r + t;
+      const uint32_t w = p + hl;
       const uint32_t x = seg4(data, p + sh);
       const bool live = p + 4u <= n;
       const uint32_t h = zhash(x);
       uint32_t best = 0u, bl = 0u;
       if (live) {
-        const uint4 c = *reinterpret_cast<const uint4*>(&tab[h * kWays]);
+        const uint4 c = *reinterpret_cast<const uint4*>(&tab16[h * kWays]);
         const uint32_t lim = min(258u, n - p);
         const uint32_t cs[4] = {c.x, c.y, c.z, c.w};
+        // all 8 candidates' first 16 bytes at once (independent loads); a
+        // slot may already hold a later position of this round (no barrier
+        // between reads and inserts): only earlier positions within 32 KiB
+        // are candidates
+        uint32_t cur[4];
+        seg16(data, p + sh, cur);
+        uint32_t L[8], D[8];
   #pragma unroll
-        for (int k = 0; k < 4; k++) {
-          // a slot may already hold a later position of this round (no barrier
-          // between reads and inserts): only earlier positions are candidates
-          if (cs[k] != 0u && cs[k] - 1u < p && seg4(data, cs[k] - 1u + sh) == x) {
-            const uint32_t q = cs[k] - 1u;
-            const uint32_t L = 4u + match_len(data, sh, p + 4u, q + 4u, lim - 4u);
-            if (L > bl || (L == bl && p - q < best)) {
-              bl = L;
-              best = p - q;
-            }
+        for (int k = 0; k < 8; k++) {
+          const uint32_t e = (cs[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+          const uint32_t q = e - 1u;
+          const bool ok = e != 0u && q < w && w - q <= kWindow;
+          uint32_t wq[4];
+          win16(hist, data, hw, (ok ? q : 0u) + sh, wq);
+          L[k] = ok ? eq16(cur, wq) : 0u;
+          D[k] = w - q;
+        }
+  #pragma unroll
+        for (int k = 0; k < 8; k++) {
+          uint32_t Lk = L[k];
+          if (Lk == 16u && lim > 16u)  // rare: extend past 16 bytes
+            Lk = 16u + match_len(hist, data, hw, sh, p + 16u, w - D[k] + 16u, lim - 16u);
+          Lk = min(Lk, lim);
+          if (Lk >= 4u && (Lk > bl || (Lk == bl && D[k] < best))) {
+            bl = Lk;
+            best = D[k];
           }
         }
       }
@@ -546,13 +718,32 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
         A += x & 0xFFu;
         J += p * (x & 0xFFu);
       }
-      if (live) atomicMax(&tab[h * kWays + (p & (kWays - 1u))], p + 1u);
+      if (live) insert(w, h);
       __syncthreads();
     }
 
-    // 2. tokens, symbol frequencies, fixed-code size
-    uint32_t extra;
-    fbits = tokenize(data, cd, hll, hd, sh, n, extra);
+    K7P(3);
+    // 2. the parse: dry passes hand each thread's end on as the next
+    //    thread's start until no start moves, then the recording pass
+    const uint32_t r0 = min(t * kSub, n), rend = min(r0 + kSub, n);
+    uint32_t extra, my_s = r0;
+    uint32_t e_t = parse<false>(hist, data, hw, cd, hll, hd, sh, hl, n, my_s, rend, 0u, fbits, extra);
+    for (uint32_t it = 0; it < kParseRounds; it++) {
+      if (t + 1u < kThreads) starts[t + 1u] = e_t;
+      __syncthreads();
+      const uint32_t ns = t ? starts[t] : 0u;
+      const bool moved = ns != my_s;
+      if (!__syncthreads_or(moved)) break;
+      if (moved) {
+        my_s = ns;
+        e_t = parse<false>(hist, data, hw, cd, hll, hd, sh, hl, n, my_s, rend, 0u, fbits, extra);
+      }
+    }
+    K7P(4);
+    p_s = my_s;
+    p_e = t + 1u < kThreads ? starts[t + 1u] : n;
+    (void)parse<true>(hist, data, hw, cd, hll, hd, sh, hl, n, p_s, rend, p_e, fbits, extra);
+    K7P(5);
     uint32_t etot, ntok;
     fincl = wg_incl_sum(fbits, wsum, ftot);
     (void)wg_incl_sum(extra, wsum, etot);
@@ -587,22 +778,22 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
       if (t < 19u) clf[t] = 0u;
       if (t < 8u) zctl[t] = 0u;
       __syncthreads();
-      if (t < 64u) {  // bitonic sort of the litlen keys, ascending, one wave
-        for (uint32_t k = 2; k <= 512u; k <<= 1)
-          for (uint32_t j = k >> 1; j > 0u; j >>= 1)
-            for (uint32_t i = t; i < 512u; i += 64u) {
-              const uint32_t ixj = i ^ j;
-              if (ixj > i) {
-                const uint32_t a = keys[i], b = keys[ixj];
-                if ((a > b) == ((i & k) == 0u)) {
-                  keys[i] = b;
-                  keys[ixj] = a;
-                }
-              }
-            }
-      } else if (t < 96u) {  // rank sort of the distance keys, a second wave
-        const uint32_t k = t - 64u;
-        const uint32_t key = (k < 30u && hd[k]) ? (hd[k] << 9) | k : 0xFFFFFFFFu;
+      // rank sorts, ascending (keys are unique: the symbol is in the low
+      // bits): thread t < 286 places litlen symbol t, thread 288 + k distance
+      // symbol k; every thread reads the same frequency per step (an LDS
+      // broadcast).  (A one-wave bitonic sort of 512 keys took ~25 % of the
+      // segment's code construction.)
+      if (t < 286u && hll[t] != 0u) {
+        const uint32_t key = (hll[t] << 9) | t;
+        uint32_t r = 0u;
+        for (uint32_t q = 0; q < 286u; q++) {
+          const uint32_t f = hll[q];
+          r += f != 0u && ((f << 9) | q) < key;
+        }
+        keys[r] = key;
+      } else if (t >= 288u && t < 318u) {
+        const uint32_t k = t - 288u;
+        const uint32_t key = hd[k] ? (hd[k] << 9) | k : 0xFFFFFFFFu;
         if (key != 0xFFFFFFFFu) {
           uint32_t r = 0u;
           for (uint32_t q = 0; q < 30u; q++) r += hd[q] && ((hd[q] << 9) | q) < key;
@@ -750,6 +941,7 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
     }
   }
   __syncthreads();
+  K7P(6);
   uint32_t mode = zpar[0];  // 2 dynamic, 1 fixed, 0 stored
   if (mode == 0u && fixed_bytes < stored_bytes) mode = 1u;
   if (mode == 1u) {  // fixed code tables
@@ -769,7 +961,7 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
     // 3. emit: this thread's tokens at its prefix offset after the block header
     uint32_t mine = fbits, incl = fincl, tot = ftot;
     if (mode == 2u) {
-      mine = walk_tokens<false>(cd, llc, dcc, nullptr, n, 0u);
+      mine = walk_tokens<false>(cd, llc, dcc, nullptr, p_s, p_e, 0u);
       incl = wg_incl_sum(mine, wsum, tot);
     }
     const uint32_t base = mode == 2u ? zpar[1] : 3u;
@@ -792,7 +984,7 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
         }
       }
     }
-    walk_tokens<true>(cd, llc, dcc, img, n, base + incl - mine);
+    walk_tokens<true>(cd, llc, dcc, img, p_s, p_e, base + incl - mine);
     __syncthreads();
     if (t == 0) {
       uint32_t o = base + tot;
@@ -822,6 +1014,7 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
     }
   }
   __syncthreads();
+  K7P(7);
   uint32_t* slot = scratch + (uint64_t)g * kImgWords;
   for (uint32_t k = t; k < (nbytes + 3u) / 4u; k += kThreads) slot[k] = img[k];
 

@@ -167,18 +167,23 @@ def test_store_paths_on_batch_needs_compress(engine, tmp_path):
 
 
 def test_entropy_early_out_boundaries(engine):
-    """K7's incompressible early-out (order-0 entropy >= 7.97 bits per byte ->
-    stored, no parse): random bytes repeating within 32 KiB are stored but
-    valid; bytes over 200 symbols (7.64 bits) still get a Huffman code; a
-    block below 4 KiB takes the full parse (it finds the repeat); mixes of
-    both kinds in one block stay valid."""
+    """K7's incompressible early-out (order-0 entropy >= 7.97 bits per byte and
+    no sampled 4-byte repeat in the window -> stored, no parse): plain random
+    bytes are stored; random bytes that repeat within the window (periods of
+    8 KiB and 20 KiB) are parsed and compress; bytes over
+    200 symbols (7.64 bits) still get a Huffman code; a block below 4 KiB
+    takes the full parse; mixes of both kinds in one block stay valid."""
     rng = np.random.default_rng(33)
-    rep = rng.integers(0, 256, 8192, dtype=np.uint8).tobytes() * 8         # 64 KiB, entropy ~8 bits
+    rnd = rng.integers(0, 256, 1 << 16, dtype=np.uint8).tobytes()            # 64 KiB random: stored
+    rep = rng.integers(0, 256, 8192, dtype=np.uint8).tobytes() * 8         # 64 KiB, entropy ~8 bits, LZ-redundant
+    rep20 = rng.integers(0, 256, 20480, dtype=np.uint8).tobytes() * 4      # 80 KiB, period 20 KiB
     few = rng.integers(0, 200, 1 << 17, dtype=np.uint8).tobytes()            # log2(200) = 7.64 bits
     small = rng.integers(0, 256, 1500, dtype=np.uint8).tobytes() * 2         # 3000 B: below the early-out
     mix = rng.integers(0, 256, 40000, dtype=np.uint8).tobytes() + _text(60000, 5)
-    zr, zf, zs, zm = _check(engine, [rep, few, small, mix])
-    assert len(zr) == len(rep) + 5 * (len(rep) // 32768) + 11  # stored segments
+    zn, zr, z20, zf, zs, zm = _check(engine, [rnd, rep, rep20, few, small, mix])
+    assert len(zn) == len(rnd) + 5 * (len(rnd) // 32768) + 11  # stored segments
+    assert len(zr) < 0.25 * len(rep), (len(zr), len(rep))     # the parse found the repeats
+    assert len(z20) < 0.6 * len(rep20), (len(z20), len(rep20))
     assert len(zf) < 0.98 * len(few), (len(zf), len(few))     # Huffman-coded, not stored
     assert len(zs) < 0.7 * len(small), (len(zs), len(small))  # the full parse matched the repeat
     assert len(zm) < len(mix), (len(zm), len(mix))            # the text half compresses
