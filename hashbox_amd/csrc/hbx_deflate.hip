@@ -287,18 +287,23 @@ __device__ __forceinline__ void dist_sym(uint32_t dist, uint32_t& sym, uint32_t&
 // Symbol frequencies go to hll/hd; `bits` = fixed-code bits, `extra` = extra
 // bits (the same under any code).  Lookahead only while p + 1 < rend, in both
 // passes, so a converged final parse repeats the dry one token for token.
+// The dry pass also returns its token starts as a mask over the thread's
+// 64-byte range (bit i = a token starts at range start + i): a token of one
+// byte is a literal, a longer one the match of that length at distance cd[p].
 template <bool REC>
 __device__ __forceinline__ uint32_t parse(const uint32_t* hist, const uint32_t* data, uint32_t hw, uint16_t* cd,
                                           uint32_t* hll, uint32_t* hd, uint32_t sh, uint32_t hl, uint32_t n,
                                           uint32_t s, uint32_t rend, uint32_t send, uint32_t& bits,
-                                          uint32_t& extra) {
+                                          uint32_t& extra, uint64_t* starts_mask = nullptr, uint32_t r0 = 0u) {
   const uint32_t stop = REC ? send : rend;
   const uint32_t cap = REC ? send : n;
   uint32_t p = s, len = 0u, d = 0u;
   bits = 0u;
   extra = 0u;
   bool have = false;  // (len, d) already hold the match at p
+  uint64_t mask = 0ull;
   while (p < stop) {
+    if (!REC) mask |= 1ull << (p - r0);
     if (!have) {
       d = cd[cphys(p)];
       len = d ? match_len(hist, data, hw, sh, p, p + hl - d, min(258u, cap - p)) : 0u;
@@ -340,7 +345,42 @@ __device__ __forceinline__ uint32_t parse(const uint32_t* hist, const uint32_t* 
       }
     }
   }
+  if (!REC && starts_mask) *starts_mask = mask;
   return p;
+}
+
+// The recording pass from a dry pass's token starts (the converged case: the
+// tokens are the dry pass's, ending at `e`), without recomputing any match.
+__device__ __forceinline__ void record_tokens(const uint32_t* data, uint16_t* cd, uint32_t* hll, uint32_t* hd,
+                                              uint32_t sh, uint32_t r0, uint64_t mask, uint32_t e,
+                                              uint32_t& bits, uint32_t& extra) {
+  bits = 0u;
+  extra = 0u;
+  while (mask) {
+    const uint32_t i = (uint32_t)__builtin_ctzll(mask);
+    mask &= mask - 1ull;
+    const uint32_t p = r0 + i;
+    const uint32_t nx = mask ? r0 + (uint32_t)__builtin_ctzll(mask) : e;
+    const uint32_t len = nx - p;
+    if (len == 1u) {
+      const uint32_t b = seg4(data, p + sh) & 0xFFu;
+      atomicAdd(&hll[b], 1u);
+      bits += b < 144u ? 8u : 9u;
+      cd[cphys(p)] = (uint16_t)(0x8000u | b);
+    } else {
+      const uint32_t d = cd[cphys(p)];
+      uint32_t v, nb, sym, ne, ex, ds, dne, dex;
+      match_code(len, d, v, nb);
+      len_sym(len, sym, ne, ex);
+      dist_sym(d, ds, dne, dex);
+      atomicAdd(&hll[sym], 1u);
+      atomicAdd(&hd[ds], 1u);
+      extra += ne + dne;
+      bits += nb;
+      cd[cphys(p)] = (uint16_t)len;
+      cd[cphys(p + 1u)] = (uint16_t)d;
+    }
+  }
 }
 
 __device__ __forceinline__ void emit_bits(uint32_t* img, uint32_t& o, uint32_t v, uint32_t nb) {
@@ -727,7 +767,8 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
     //    thread's start until no start moves, then the recording pass
     const uint32_t r0 = min(t * kSub, n), rend = min(r0 + kSub, n);
     uint32_t extra, my_s = r0;
-    uint32_t e_t = parse<false>(hist, data, hw, cd, hll, hd, sh, hl, n, my_s, rend, 0u, fbits, extra);
+    uint64_t mask = 0ull;
+    uint32_t e_t = parse<false>(hist, data, hw, cd, hll, hd, sh, hl, n, my_s, rend, 0u, fbits, extra, &mask, r0);
     for (uint32_t it = 0; it < kParseRounds; it++) {
       if (t + 1u < kThreads) starts[t + 1u] = e_t;
       __syncthreads();
@@ -736,13 +777,17 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
       if (!__syncthreads_or(moved)) break;
       if (moved) {
         my_s = ns;
-        e_t = parse<false>(hist, data, hw, cd, hll, hd, sh, hl, n, my_s, rend, 0u, fbits, extra);
+        e_t = parse<false>(hist, data, hw, cd, hll, hd, sh, hl, n, my_s, rend, 0u, fbits, extra, &mask, r0);
       }
     }
     K7P(4);
     p_s = my_s;
     p_e = t + 1u < kThreads ? starts[t + 1u] : n;
-    (void)parse<true>(hist, data, hw, cd, hll, hd, sh, hl, n, p_s, rend, p_e, fbits, extra);
+    // converged: the last dry pass's tokens end exactly at the next start
+    if (e_t == p_e)
+      record_tokens(data, cd, hll, hd, sh, r0, mask, e_t, fbits, extra);
+    else
+      (void)parse<true>(hist, data, hw, cd, hll, hd, sh, hl, n, p_s, rend, p_e, fbits, extra);
     K7P(5);
     uint32_t etot, ntok;
     fincl = wg_incl_sum(fbits, wsum, ftot);

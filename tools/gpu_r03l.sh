@@ -4,6 +4,8 @@
 set -o pipefail
 O=gpurun_out/${TAG:-r03l}
 mkdir -p $O
+timeout -k 10 120 ./tools/ubench/k7_phases 256 > $O/k7_phases0.txt 2>&1 || { cat $O/k7_phases0.txt; exit 1; }
+cat $O/k7_phases0.txt
 timeout -k 10 400 python -u -m pytest tests/test_gpu_deflate.py tests/test_gpu_inflate.py tests/test_gpu_wire.py -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
 timeout -k 10 300 python tools/bench_deflate.py > $O/deflate.json 2> $O/deflate.err || { tail -20 $O/deflate.err; exit 1; }
