@@ -1,15 +1,11 @@
 #!/bin/bash
-# K7 with a 16 KiB history window, 8-way buckets and resolved thread ranges:
-# strict-inflate tests, the deflate bench; then K3 address translation: one
-# 2 MiB-aligned allocation for all arenas vs one allocation per arena.
+# K3 address translation: one 2 MiB-aligned allocation for all arenas
+# (--single-alloc) vs one allocation per arena; UTCL1 misses per launch and the
+# bench value for each.  Output: profiles/r03h.
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/${TAG:-r03h}
+O=gpurun_out/${TAG:-k3tlb}
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_gpu_deflate.py tests/test_gpu_inflate.py tests/test_gpu_wire.py tests/test_gpu_configs.py -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
-tail -2 $O/pytest.log
-timeout -k 10 300 python tools/bench_deflate.py > $O/deflate.json 2> $O/deflate.err || { tail -20 $O/deflate.err; exit 1; }
-cat $O/deflate.json
 for m in default single; do
   F=""; [ $m = single ] && F="--single-alloc"
   timeout -k 10 300 python bench.py --steps 100 --warmup 5 --workload random --no-cpu-baseline --no-check $F > $O/bench_$m.json 2> $O/bench_$m.err || { tail -5 $O/bench_$m.err; exit 1; }

@@ -2,7 +2,7 @@
 # K7 (history window, parallel candidates, repeat-aware early-out): strict
 # inflate tests, the deflate bench, phase times.
 set -o pipefail
-O=gpurun_out/${TAG:-r03l}
+O=gpurun_out/${TAG:-k7}
 mkdir -p $O
 timeout -k 10 120 ./tools/ubench/k7_phases 256 > $O/k7_phases0.txt 2>&1 || { cat $O/k7_phases0.txt; exit 1; }
 cat $O/k7_phases0.txt
