@@ -17,6 +17,7 @@
 //                          (type 3).
 // No MFMA anywhere: this is a byte scan plus an integer hash.
 #include <type_traits>
+#include <utility>
 
 #include "hbx_device.h"
 
@@ -1221,6 +1222,195 @@ __device__ void md5_coop(uint8_t* wl, const uint8_t* c, uint32_t (&h)[4], uint32
   }
 }
 
+// ---------------------------------------------- cooperative loads, LDS-DMA --
+// The same page-local streaming with the stage landing in LDS straight from
+// global memory (global_load_lds_dwordx4): no register staging, no
+// ds_write_b128 (the register-staged path's 16 back-to-back wide stores per
+// stage hold its wave ~100 cycles per block; one wave's wide LDS stores run at
+// half rate), and the freed registers hold the next block's words, read one
+// block ahead of its compression.
+//   SB blocks per stage (G = 4 SB granules of 16 B per chain), a ring of D
+//   stages per wave (D x 4 KiB x SB of LDS), DMAs D-1 stages ahead.
+//   DMA instruction q, lane i: chain C q + i / G (C = 64 / G chains per
+//   instruction, 16 G contiguous bytes each), LDS slot i % G of that chain's
+//   row.  A DMA writes its 64 x 16 B lane-linearly, so the rows cannot be
+//   padded; instead chain c's granule k sits in slot (k + rot(c)) mod G, the
+//   rotation chosen so that every 16-lane group of ds_read_b128 (lanes
+//   {0-3,12-15,20-27}, ...: MI355X_MICROARCH.md LDS) hits 16 distinct 16-B
+//   bank columns.  The swizzle goes on the DMA's source address.
+//   Four DMAs share one M0 (the instruction offset applies to both the global
+//   and the LDS address), and the ring is unrolled by D, so a DMA costs no
+//   address arithmetic: the per-instruction pointers advance once per ring.
+#ifndef HBX_K3_DMA
+#define HBX_K3_DMA 0
+#endif
+#ifndef HBX_K3_DMA_SB
+#define HBX_K3_DMA_SB 2
+#endif
+#ifndef HBX_K3_DMA_D
+#define HBX_K3_DMA_D 4
+#endif
+template <int SB, int D>
+struct CoopDma {
+  static_assert(SB == 1 || SB == 2 || SB == 4, "1, 2 or 4 blocks per stage");
+  static_assert(D >= 2 && (D * SB) % 2 == 0, "ring of >= 2 stages, an even number of blocks per ring");
+  static constexpr uint32_t G = 4u * SB;                         // granules per chain per stage
+  static constexpr uint32_t C = 64u / G;                         // chains per DMA instruction
+  static constexpr uint32_t Row = 16u * G;                       // one chain's stage
+  static constexpr uint32_t Stage = 64u * Row;                   // one stage of the wave's chains
+  static constexpr uint32_t WaveLds = (uint32_t)D * Stage;
+  static constexpr uint32_t RotShift = SB == 4 ? 0u : SB == 2 ? 1u : 2u;
+  static_assert(16u * G * (D - 1) + 3072u < 4096u, "instruction offsets fit 12 bits");
+};
+
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+typedef __attribute__((address_space(1))) void g_void;
+typedef __attribute__((address_space(3))) void l_void;
+template <int OFF>
+__device__ __forceinline__ void glds16(uint64_t g, uint32_t lds) {
+  __builtin_amdgcn_global_load_lds((g_void*)g, (l_void*)(uintptr_t)lds, 16, OFF, 0);
+}
+
+// Stage t into ring slot j, every source clamped to the chain's last granule
+// (prologue and the last rings).  P[q] + 1024 (q % 4) - 16 G pbase is chain
+// (C q + sub)'s stream address + 16 * its granule gq.
+template <int SB, int D, int J>
+__device__ __forceinline__ void dma_clamped(const uint64_t (&P)[CoopDma<SB, D>::G], uint32_t wbase, uint32_t t,
+                                            uint32_t pbase, uint32_t ngr, uint32_t pos, uint32_t sub) {
+  using K = CoopDma<SB, D>;
+#pragma unroll
+  for (int q = 0; q < (int)K::G; q++) {
+    const uint32_t ch = K::C * (uint32_t)q + sub;
+    const uint32_t gq = (pos - (ch >> K::RotShift)) & (K::G - 1u);
+    const uint32_t gi = min(K::G * t + gq, ngr - 1u);
+    const uint64_t a = P[q] + 1024ull * (uint32_t)(q % 4) - 16ull * K::G * pbase - 16ull * gq + 16ull * gi;
+    glds16<0>(a, wbase + (uint32_t)J * K::Stage + 1024u * (uint32_t)q);
+  }
+}
+
+// Stage pbase + J into ring slot J, no clamping: four DMAs per M0, the stage
+// and the instruction's place in its group in the immediate offset.
+template <int SB, int D, int J>
+__device__ __forceinline__ void dma_fast(const uint64_t (&P)[CoopDma<SB, D>::G], uint32_t wbase) {
+  using K = CoopDma<SB, D>;
+  constexpr int adv = (int)(16u * K::G) * J;
+  static_for<(int)K::G>([&](auto qc) {
+    constexpr int q = decltype(qc)::value;
+    glds16<1024 * (q % 4) + adv>(P[q], wbase + (uint32_t)J * K::Stage + 4096u * (uint32_t)(q / 4) - (uint32_t)adv);
+  });
+}
+
+typedef __attribute__((address_space(3))) const u32x4 l_u32x4;
+
+template <int SB, int D>
+__device__ __forceinline__ void md5_coop_dma(uint8_t* wl, const uint8_t* c, uint32_t (&h)[4], uint32_t b1,
+                                             uint32_t R) {
+  using K = CoopDma<SB, D>;
+  constexpr uint32_t G = K::G;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t S = reinterpret_cast<uint64_t>(c) + 64ull * b1 - 8ull;  // message block b1
+  const uint32_t ngr = 4u * R;                                           // granules of R blocks
+  const uint32_t pos = lane % G, sub = lane / G;
+  const uint32_t wbase = (uint32_t)(uintptr_t)wl;  // LDS byte address (low half of the flat address)
+  uint64_t P[G];
+#pragma unroll
+  for (int q = 0; q < (int)G; q++) {
+    const uint32_t ch = K::C * (uint32_t)q + sub;
+    const uint32_t gq = (pos - (ch >> K::RotShift)) & (G - 1u);
+    P[q] = shfl64(S, ch) + 16ull * gq - 1024ull * (uint32_t)(q % 4);
+  }
+  // this lane's row: granule k in slot (k + rot) mod G
+  const uint32_t rot = (lane >> K::RotShift) & (G - 1u);
+  uint32_t RA[G];
+#pragma unroll
+  for (int k = 0; k < (int)G; k++) RA[k] = wbase + K::Row * lane + 16u * (((uint32_t)k + rot) & (G - 1u));
+  // The block reads are issued by hand: with an LDS-DMA in flight the
+  // compiler waits lgkmcnt(0) before the first use of any LDS read, which
+  // would also wait for the next block's reads issued just before.  `rd`
+  // issues 4 ds_read_b128; `ready` waits until only the 4 issued after W are
+  // outstanding (LDS reads return in order) and ties W's uses behind it.
+  auto rd = [&](u32x4(&W)[4], auto jc, auto uc) {
+    constexpr uint32_t j = decltype(jc)::value, u = decltype(uc)::value;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint32_t a = RA[4u * u + (uint32_t)i];
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(W[i]) : "v"(a), "n"(j * K::Stage));
+    }
+  };
+  auto ready = [&](u32x4(&W)[4]) {
+    asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(W[0]), "+v"(W[1]), "+v"(W[2]), "+v"(W[3]));
+  };
+  // prologue: stages 0 .. D-1 into slots 0 .. D-1
+  static_for<D>([&](auto jc) { dma_clamped<SB, D, decltype(jc)::value>(P, wbase, (uint32_t)decltype(jc)::value, 0u, ngr, pos, sub); });
+#pragma unroll
+  for (int q = 0; q < (int)G; q++) P[q] += 16ull * G * D;
+  uint32_t pbase = D;
+  // stage 0 has landed once at most the D-1 later stages fly (in-order completion)
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * G) : "memory");
+  u32x4 WA[4], WB[4];
+  rd(WA, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+  // A ring = D stages.  Main rings hold no block past R and refill only
+  // stages whose granules all exist (no clamp, no per-block test); the last
+  // one or two rings test every block and clamp their refills.
+  uint32_t s0 = 0;
+  auto ring = [&](auto tail_c) -> bool {
+    constexpr bool TAIL = decltype(tail_c)::value;
+    bool go = true;
+    // block (j, u): its words are in Wc (read one block ahead), the next
+    // block's go to Wn
+    auto blk = [&](auto jc, auto uc, u32x4(&Wc)[4], u32x4(&Wn)[4]) {
+      constexpr int j = decltype(jc)::value, u = decltype(uc)::value;
+      if constexpr (TAIL) {
+        if (!go || SB * (s0 + (uint32_t)j) + (uint32_t)u >= R) {  // wave-uniform
+          go = false;
+          return;
+        }
+      }
+      if constexpr (u + 1 < SB) {
+        rd(Wn, jc, std::integral_constant<int, u + 1>{});
+        ready(Wc);
+      } else {
+        // the next stage (slot (j+1) mod D) has landed: the D-2 after it may fly
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * G) : "memory");
+        rd(Wn, std::integral_constant<int, (j + 1) % D>{}, std::integral_constant<int, 0>{});
+        ready(Wc);
+        // slot j is consumed (Wc's reads are back): refill it with stage s0 + j + D
+        if constexpr (TAIL) dma_clamped<SB, D, j>(P, wbase, s0 + (uint32_t)j + D, pbase, ngr, pos, sub);
+        else dma_fast<SB, D, j>(P, wbase);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // the reads above go out before this block's compression
+      const uint32_t m[16] = {Wc[0].x, Wc[0].y, Wc[0].z, Wc[0].w, Wc[1].x, Wc[1].y, Wc[1].z, Wc[1].w,
+                              Wc[2].x, Wc[2].y, Wc[2].z, Wc[2].w, Wc[3].x, Wc[3].y, Wc[3].z, Wc[3].w};
+      md5_compress(h, m);
+    };
+    // blocks alternate WA -> WB -> WA ...; D * SB is even, so every ring starts in WA
+    static_for<D * SB>([&](auto ic) {
+      constexpr int I = decltype(ic)::value;
+      if constexpr (I % 2 == 0) blk(std::integral_constant<int, I / SB>{}, std::integral_constant<int, I % SB>{}, WA, WB);
+      else blk(std::integral_constant<int, I / SB>{}, std::integral_constant<int, I % SB>{}, WB, WA);
+    });
+#pragma unroll
+    for (int q = 0; q < (int)G; q++) P[q] += 16ull * G * D;
+    pbase += D;
+    s0 += D;
+    return go;
+  };
+  for (; SB * (s0 + 2u * D) <= R;) ring(std::false_type{});
+  while (SB * s0 < R && ring(std::true_type{})) {
+  }
+  // no read may land in registers, and no DMA in the ring, after they are reused
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : "+v"(WA[0]), "+v"(WA[1]), "+v"(WA[2]), "+v"(WA[3]), "+v"(WB[0]),
+               "+v"(WB[1]), "+v"(WB[2]), "+v"(WB[3])::"memory");
+}
+
 }  // namespace
 
 // ------------------------------------------------------ MD5 chain table --
@@ -1393,6 +1583,16 @@ constexpr uint32_t kCoopMinBudget = 8u;
 constexpr int kK3Threads = 256;    // hbx_k3_block_md5: one wave per SIMD
 constexpr int kK3Threads2 = 512;   // hbx_k3_block_md5_w2: two waves per SIMD
 
+// The cooperative path of a K3 variant: LDS-DMA stages (HBX_K3_DMA) for one
+// wave per SIMD, else register-staged.
+template <int THREADS, int G, int SETS>
+__device__ __forceinline__ void coop(uint8_t* wl, const uint8_t* c, uint32_t (&h)[4], uint32_t b1, uint32_t R) {
+  if constexpr (THREADS == kK3Threads && HBX_K3_DMA) md5_coop_dma<HBX_K3_DMA_SB, HBX_K3_DMA_D>(wl, c, h, b1, R);
+  else md5_coop<G, SETS>(wl, c, h, b1, R);
+}
+constexpr uint32_t kK3WaveLds =
+    HBX_K3_DMA ? CoopDma<HBX_K3_DMA_SB, HBX_K3_DMA_D>::WaveLds : Coop<16>::WaveLds;
+
 // The body of both K3 variants: THREADS per workgroup (one per CU), the
 // cooperative stage of G granules with SETS register sets in flight, the
 // lane path's prefetch ring of RING blocks.  `wl` = this wave's LDS.
@@ -1458,7 +1658,7 @@ __device__ __forceinline__ void k3_body(
         pR = R;
         pmax = wave_max_all(cnt);
       }
-      md5_coop<G, SETS>(wl, src, h, ch.next + 1u, R - 1u);
+      coop<THREADS, G, SETS>(wl, src, h, ch.next + 1u, R - 1u);
       // A group that straddles two order bins mixes counts (e.g. 4,229 and
       // 4,093 blocks): the lanes still holding blocks go on cooperatively
       // while the others shadow the first of them and discard (the lane-mode
@@ -1475,7 +1675,7 @@ __device__ __forceinline__ void k3_body(
                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)reinterpret_cast<uint64_t>(src), L);
         const uint32_t p_sh = (uint32_t)__builtin_amdgcn_readlane((int)pos, L);
         uint32_t hk[4] = {h[0], h[1], h[2], h[3]};
-        md5_coop<G, SETS>(wl, part ? src : reinterpret_cast<const uint8_t*>(s_sh), hk, part ? pos : p_sh, R2);
+        coop<THREADS, G, SETS>(wl, part ? src : reinterpret_cast<const uint8_t*>(s_sh), hk, part ? pos : p_sh, R2);
         if (part) {
           h[0] = hk[0];
           h[1] = hk[1];
@@ -1524,7 +1724,7 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
     const OrderEntry* __restrict__ order, const uint32_t* __restrict__ n_order, uint32_t budget,
     uint32_t dense, uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last,
     uint64_t* __restrict__ tslot, uint64_t* __restrict__ probe) {
-  __shared__ __attribute__((aligned(16))) uint8_t k3_lds[kK3Threads / 64][Coop<16>::WaveLds];
+  __shared__ __attribute__((aligned(16))) uint8_t k3_lds[kK3Threads / 64][kK3WaveLds];
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   k3_body<kK3Threads, 16, 2, HBX_MD5_RING>(k3_lds[wave], order, n_order, budget, dense, started, t_first, t_last,
                                            tslot, probe);
