@@ -18,12 +18,14 @@ the engine's own launch counts).  The drain that empties the pipeline runs
 after the timer and is reported beside `value` (`drain_ms`,
 `fill_drain_gibs` = the whole run from an empty pipeline to a drained one).
 
-Multi-GPU (--scaling strong, the default; BASELINE configs[2]): every step's
-64 files are split across the ranks by LPT on bytes (hashbox_amd.shard), each
-rank pipelines its shard on its own GPU and streams; value = 8 GiB x K / the
-slowest rank's time.  --scaling weak: every rank takes a whole 8 GiB batch
-per step.  No collective touches the data: torch.distributed carries only
-the barriers, the max-time reduction and the check flags.
+Multi-GPU (--scaling weak, the default): files are independent objects, so
+every rank takes a whole batch of its own files per step (configs[1] per
+GPU) and pipelines it on its own GPU and streams; value = N x 8 GiB x K / the
+slowest rank's time.  --scaling strong (BASELINE configs[2], a parity case):
+every step's 64 files are split across the ranks by LPT on bytes
+(hashbox_amd.shard); value = 8 GiB x K / the slowest rank's time.  No
+collective touches the data: torch.distributed carries only the barriers,
+the max-time reduction and the check flags.
 
 Prints ONE JSON line on rank 0.  Multi-GPU:
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -88,9 +90,9 @@ def parse():
     ap.add_argument("--files", type=int, default=64, help="files per step (whole job)")
     ap.add_argument("--file-mib", type=int, default=128)
     ap.add_argument("--seed", type=int, default=1000)
-    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
-                    help="strong: each step's files are split across the ranks (configs[2]); "
-                         "weak: every rank takes a whole batch per step")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="weak",
+                    help="weak: every rank takes a whole batch of its own files per step (per-GPU work "
+                         "fixed); strong: each step's files are split across the ranks (configs[2])")
     ap.add_argument("--workload", choices=["both", "random", "zipf"], default="both",
                     help="both: the random headline plus a Zipf-duplicate line under key 'zipf'")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -696,7 +698,8 @@ def run(a, S, rank, world, local_world, dist, dev, red_dev):
                 f"resident batches per GPU, resident in HBM before timing",
         "config": {"workload": f"{a.files} x {a.file_mib} MiB random buffers per step, rollsum split + MD5 "
                                "block IDs + file content ids, device-resident (configs[1]"
-                               + (", sharded by file across GPUs: configs[2])" if world > 1 else ")"),
+                               + ((", sharded by file across GPUs: configs[2])" if a.scaling == "strong"
+                                   else " on every GPU, each rank its own files)") if world > 1 else ")"),
                    "files_per_step": a.files, "files_per_gpu": nf, "file_bytes": fbytes,
                    "md5_slice_blocks": B, "pipeline_depth": R, "launches_per_batch": need,
                    "scan_lead": lead, "join_lag": lag, "k3_waves_per_simd": a.k3_waves,

@@ -120,14 +120,29 @@ def _bench_plan(world, extra, timeout=120):
 
 
 def test_bench_plan_world4_through_torchrun():
+    """configs[2] (--scaling strong): the 64 files of a step split across 4 ranks."""
     import json
-    r = _bench_plan(4, [])
+    r = _bench_plan(4, ["--scaling", "strong"])
     assert r.returncode == 0, r.stderr[-2000:]
     (line,) = [x for x in r.stdout.splitlines() if x.startswith("{")]
-    plans = json.loads(line)["plans"]
+    d = json.loads(line)
+    plans = d["plans"]
+    assert d["scaling"] == "strong"
     assert [p["rank"] for p in plans] == [0, 1, 2, 3]
     assert sorted(sum((p["mine"] for p in plans), [])) == list(range(64))
     assert all(p["files_per_gpu"] == 16 and p["need"] + p["join_lag"] <= p["R"] for p in plans)
+
+
+def test_bench_plan_default_is_weak():
+    """The default multi-GPU mode: every rank a whole batch of its own files."""
+    import json
+    r = _bench_plan(2, [])
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    d = json.loads(line)
+    assert d["scaling"] == "weak"
+    assert all(p["mine"] == list(range(64)) and p["files_per_gpu"] == 64 for p in d["plans"])
+    assert all(p["need"] + p["join_lag"] <= p["R"] for p in d["plans"])
 
 
 def test_bench_failing_rank_exits_nonzero():
