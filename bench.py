@@ -121,6 +121,9 @@ def parse():
     ap.add_argument("--no-check", action="store_true",
                     help="skip the oracle check of the last collected and the last drained batch")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPUs; gloo for tests")
+    ap.add_argument("--dist-always", action="store_true",
+                    help="join a process group even at world 1 (exercises the RCCL barriers and reductions "
+                         "on a one-GPU box)")
     ap.add_argument("--ballast-gib", type=float, default=0.0,
                     help="diagnostics: hold this much extra device memory (written once, never read)")
     ap.add_argument("--k3-probe", action="store_true",
@@ -534,7 +537,7 @@ def main():
     dev_idx = local % max(ndev, 1)
     dev = torch.device("cuda", dev_idx)
     dist = None
-    if world > 1:
+    if world > 1 or a.dist_always:
         import datetime
         import torch.distributed as dist
         to = datetime.timedelta(seconds=a.dist_timeout)

@@ -6,6 +6,7 @@ on cuda:0 of the one-GPU box.
   the ranks) and --scaling weak, world 2, and strong at world 1: the window
   holds exactly K K1/K3 launches per rank and every rank's checked batches
   are bit-exact (check_vs_oracle, min over ranks).
+* bench.py over RCCL (the nccl backend the driver uses) at world 1.
 * hashbox_amd.multi.run_sharded driving the pipelined Engine on each rank:
   the gathered per-file results equal the oracle's for every file."""
 import json
@@ -51,6 +52,16 @@ def test_bench_through_torchrun(nproc, scaling):
     assert d["window_launches"]["k1_digest_scan"] == 6 and d["window_launches"]["k3_block_md5"] == 6
     assert d["config"]["files_per_gpu"] == (4 // nproc if scaling == "strong" else 4)
     assert d["value"] > 0
+
+
+def test_bench_rccl_world1_through_torchrun():
+    """The driver's backend: bench.py joins an RCCL (nccl) process group with
+    a device-bound init and a timeout, and its barriers and max/min reductions
+    run on device tensors (world 1: RCCL cannot put two ranks on one GPU)."""
+    args = [x for x in BENCH if x not in ("--dist-backend", "gloo")]
+    d = _torchrun(1, args + ["--gpus", "1", "--dist-backend", "nccl", "--dist-always"])
+    assert d["n_gpus"] == 1 and d["check_vs_oracle"] is True and d["zipf"]["check_vs_oracle"] is True
+    assert d["window_launches"]["k3_block_md5"] == 6 and d["value"] > 0
 
 
 def test_run_sharded_engine_world2():
