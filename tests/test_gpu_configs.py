@@ -10,6 +10,8 @@ block.go:96-111 framing.
   content) through the synchronous device call and the pipelined time-sliced
   path (4 batches of 64 files in flight), every file against the oracle on
   all host cores.
+* one file past 2^32 bytes (4 GiB + 1 MiB + 12,345): device-resident
+  (synchronous and pipelined) and from disk.
 * configs[4], scaled to 10,000 files: log-uniform 4 KiB-4 MiB sizes (seed 5),
   a quarter of them compressible text, on disk, through hbx_store_paths and
   hbx_store_paths_zcb: every file checked (not a sample), every compressed
@@ -111,6 +113,37 @@ def test_configs0_one_gib_file(engine, oracle, big_tmp):
     assert r.content_id == ref.content_id
     del d
     torch.cuda.empty_cache()
+
+
+def test_one_file_past_4_gib(engine, oracle, big_tmp):
+    """A single file longer than 2^32 bytes (odd length): 64-bit positions in
+    K1's tiles, K2's chain walk, the chains and the file reader, device-resident
+    (synchronous and pipelined) and from disk, against the oracle."""
+    import torch
+    from hashbox_amd import Engine
+    n = (4 << 30) + (1 << 20) + 12345
+    d = torch.empty(n + 65536, dtype=torch.uint8, device="cuda:0")
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(44)
+    d[:n].random_(0, 256, generator=g)
+    data = d[:n].cpu().numpy()
+    ref = oracle.store_file(data)
+    assert ref.n_chunks > 400 and int(ref.cut_ends[-1]) == n
+    (sync,) = engine.chunk_hash_device(d.data_ptr(), [0], [n])
+    _same(sync, ref)
+    with Engine(0, md5_slice=8192) as e:
+        e.submit_device(d.data_ptr(), [0], [n])
+        (pipe,) = e.wait()
+    _same(pipe, ref)
+    assert sync.content_id == pipe.content_id == ref.content_id and sync.content_type == 3
+    del d
+    torch.cuda.empty_cache()
+    p = os.path.join(big_tmp, "past4g.bin")
+    data.tofile(p)
+    (r,) = engine.store_paths([p])
+    os.unlink(p)
+    _same(r, ref)
+    assert r.content_id == ref.content_id
 
 
 def test_configs3_zipf_32_gib(oracle):
