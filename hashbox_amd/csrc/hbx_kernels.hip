@@ -30,6 +30,9 @@ constexpr int kK1Threads = 1024;
 #ifndef HBX_K1_SDWA
 #define HBX_K1_SDWA 1
 #endif
+#ifndef HBX_K1_DIAG_NODIGEST
+#define HBX_K1_DIAG_NODIGEST 0
+#endif
 #ifndef HBX_K1_COALESCED
 #define HBX_K1_COALESCED 1
 #endif  // 16 waves; 16 x 4096 B = one MIN window per iteration
@@ -217,7 +220,14 @@ __device__ __forceinline__ void k1_iteration(const uint32_t (&cur)[16], const ui
   sprev = readlane((s2_t << 16) | (S1_t & 0xffffu), 0);
 
   uint32_t M;
-#if HBX_K1_SDWA
+#if HBX_K1_DIAG_NODIGEST
+  // diagnostic build only (tools/gpu_k1_intensity.sh): K1 without its digest
+  // loop (~70 % of its VALU; the maxima are wrong), to measure how much K1's
+  // VALU work, as opposed to its memory traffic, slows K3 beside it
+  M = (s2_t << 16) ^ S1_t ^ s2_b ^ S1_b ^ cur[l & 15u] ^ out[(l + 1u) & 15u];
+  (void)S1p;
+  (void)S2p;
+#elif HBX_K1_SDWA
   const uint32_t XA = (s2_t << 16) | (S1_t & 0xffffu), XB = (s2_b << 16) | (S1_b & 0xffffu);
   if (qs + kMinBlock <= N) {
     M = digest_pass_sdwa<false>(cur, out, XA, XB, e_l, 0u);
