@@ -22,6 +22,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <iterator>
 #include <random>
 #include <unistd.h>
 #include <vector>
@@ -175,9 +176,17 @@ int main(int argc, char** argv) {
       {"coop_regs2_rand", 2, false, 0, 32768u}, {"coop_lds3_rand", 3, true, 0, 16384u},
       {"coop_lds3_rand", 3, true, 0, 32768u},  {"coop_lds2_local", 2, true, 1, 16384u},
       {"coop_lds2_local", 2, true, 1, 32768u},  {"coop_lds3_local", 3, true, 1, 32768u},
+      {"coop_lds2_page", 2, true, 2, 32768u},   {"coop_lds2_rand128", 2, true, 0, 32768u},
   };
-  (void)cases_full;  // the round-3 table (profiles/r03hbms/hbm_streams_sets_local.txt); swap in to rerun
-  for (const Case& k : cases) {
+  // cases_full: the round-3 table (profiles/r03hbms/hbm_streams_sets_local.txt), run by name (argv[2])
+  // argv[2] (optional): run only the cases named exactly so, argv[3] only that
+  // chain count, without the streamer (for rocprofv3 --pmc passes)
+  const char* only = argc > 2 ? argv[2] : nullptr;
+  const uint32_t only_s = argc > 3 ? (uint32_t)strtoul(argv[3], nullptr, 10) : 0u;
+  const std::vector<Case> run = only ? std::vector<Case>(std::begin(cases_full), std::end(cases_full))
+                                     : std::vector<Case>(std::begin(cases), std::end(cases));
+  for (const Case& k : run) {
+    if (only && (std::strcmp(k.name, only) != 0 || (only_s && k.S != only_s))) continue;
     const uint32_t S = k.S;
     const bool local = k.place == 1;
     const uint32_t stages = (k.place == 2 || std::strstr(k.name, "128"))
@@ -200,7 +209,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(d_addr, h.data(), S * 8ull, hipMemcpyHostToDevice));
     const uint32_t wgs = S / 256u;
     const double bytes = 256.0 * stages * S;
-    for (int beside = 0; beside < 2; beside++) {
+    for (int beside = 0; beside < (only ? 1 : 2); beside++) {
       float best = 1e30f, sms = 0.f;
       for (int rep = 0; rep < 3; rep++) {
         // coop first (its workgroups take their CUs), then the streamer on
