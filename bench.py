@@ -428,11 +428,11 @@ def run_workload(a, name, eng, arenas, offs, lens, R, B, need, lanes, dist, gpu,
         "longest_chunk_bytes": longest,
         # the contract's HBM roofline of the dominant kernel; what actually
         # limits K3 ("limiter"): its instruction stream at one
-        # wave per SIMD and, meeting it, the address translation of its loads
-        # (32k chains, each in its own page), pushed out by K1's HBM traffic
+        # wave per SIMD and, meeting it, its loads from 32k chains scattered
+        # over the arenas, pushed out by K1's HBM traffic
         "roofline": {"kernel": "k3_block_md5", "bound": "hbm", "achieved": round(achieved, 2),
                      "limiter": "valu-issue of one MD5 wave per SIMD (5 dependent VALU per step) meeting the "
-                                "translation-bound loads of 32k chains in distinct pages (tools/ubench/hbm_streams: "
+                                "loads of 32k chains scattered over the arenas (tools/ubench/hbm_streams: "
                                 "2.65-2.80 ms per 8 GiB without the MD5), plus K1's HBM traffic beside it",
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": traffic, "traffic_source": traffic_src, "launches": k3_n,

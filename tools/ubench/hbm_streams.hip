@@ -115,6 +115,54 @@ __global__ __launch_bounds__(256, 1) void coop(const uint64_t* __restrict__ addr
   if (r == 0x9e3779b9u) out[0] = r;
 }
 
+// Eight-block stages: 2 chains x 512 B per load instruction, one LDS stage
+// (33 KiB) per wave and the next two in registers, each written right after
+// the stage before it is read (hbx_kernels.hip's round-3 STAGE8 experiment).
+constexpr int kG8 = 32;
+constexpr uint32_t kRow8 = 16u * kG8 + 16u;
+__global__ __launch_bounds__(256, 1) void coop8(const uint64_t* __restrict__ addr, uint32_t stages,
+                                                uint32_t* __restrict__ out, uint32_t stride) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4][64u * kRow8];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  uint8_t* wl = lds[wave];
+  const uint64_t S = addr[(blockIdx.x * 4u + wave) * 64u + lane];
+  const uint32_t t = lane % kG8, sub = lane / kG8;
+  uint64_t Q[kG8];
+#pragma unroll
+  for (int q = 0; q < kG8; q++) Q[q] = shfl64(S, 2u * (uint32_t)q + sub) + 16ull * t;
+  const uint32_t wr = sub * kRow8 + 16u * t, rd = lane * kRow8;
+  u32x4 acc = {0u, 0u, 0u, 0u};
+  // stage units of 512 B per chain: stage st covers the 256-B stages 2st, 2st+1
+  auto load = [&](u32x4(&G)[kG8], uint32_t st) {
+#pragma unroll
+    for (int q = 0; q < kG8; q++) G[q] = *(g_u32x4*)(Q[q] + 16ull * kG8 * stride * st);
+  };
+  auto write = [&](const u32x4(&G)[kG8]) {
+#pragma unroll
+    for (int q = 0; q < kG8; q++) *reinterpret_cast<u32x4*>(wl + wr + 2u * kRow8 * (uint32_t)q) = G[q];
+  };
+  auto use = [&]() {
+#pragma unroll
+    for (int k = 0; k < kG8; k++) acc ^= *reinterpret_cast<const u32x4*>(wl + rd + 16u * k);
+  };
+  u32x4 GA[kG8], GB[kG8];
+  const uint32_t st8 = stages / 2u;
+  load(GA, 0u);
+  load(GB, 1u);
+  write(GA);
+  load(GA, 2u);
+  for (uint32_t s = 0; s + 2u < st8; s += 2u) {
+    use();
+    write(GB);
+    load(GB, s + 3u);
+    use();
+    write(GA);
+    load(GA, s + 4u);
+  }
+  const uint32_t r = acc.x ^ acc.y ^ acc.z ^ acc.w;
+  if (r == 0x9e3779b9u) out[0] = r;
+}
+
 // 1024-thread workgroups holding 128 KiB of (unused) dynamic LDS, like K1: they
 // cannot share a CU with a coop workgroup, so the two split the CUs as K1 and
 // K3 do.
@@ -177,6 +225,7 @@ int main(int argc, char** argv) {
       {"coop_lds3_rand", 3, true, 0, 32768u},  {"coop_lds2_local", 2, true, 1, 16384u},
       {"coop_lds2_local", 2, true, 1, 32768u},  {"coop_lds3_local", 3, true, 1, 32768u},
       {"coop_lds2_page", 2, true, 2, 32768u},   {"coop_lds2_rand128", 2, true, 0, 32768u},
+      {"coop8_rand", 8, true, 0, 32768u},        {"coop8_rand", 8, true, 0, 16384u},
   };
   // cases_full: the round-3 table (profiles/r03hbms/hbm_streams_sets_local.txt), run by name (argv[2])
   // argv[2] (optional): run only the cases named exactly so, argv[3] only that
@@ -216,7 +265,9 @@ int main(int argc, char** argv) {
         // the CUs left; the streamer outlasts the coop launch
         CK(hipEventRecord(c0, sc));
         const uint32_t stride = local ? 64u : 1u;  // local: stage stride 64 x 256 B = 16 KiB
-        if (!k.lds)
+        if (k.sets == 8)
+          hipLaunchKernelGGL(coop8, dim3(wgs), dim3(256), 0, sc, d_addr, stages, d_out, stride);
+        else if (!k.lds)
           hipLaunchKernelGGL((coop<false, 2>), dim3(wgs), dim3(256), 0, sc, d_addr, stages, d_out, stride);
         else if (k.sets == 3)
           hipLaunchKernelGGL((coop<true, 3>), dim3(wgs), dim3(256), 0, sc, d_addr, stages, d_out, stride);
