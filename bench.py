@@ -214,13 +214,21 @@ def oracle_check(arena, offs, lens, res, threads):
     return bool(ok)
 
 
+TRAFFIC_FILE = "profiles/r03f_traffic.json"  # PMC FETCH_SIZE pass of the final tree (tools/profile_round.sh)
+
+
 def measured_traffic(kernel, per_launch_bytes, batch_bytes):
     """HBM bytes per launch of `kernel` from the newest committed PMC pass of
     the default workload (profiles/*_traffic.json, tools/pmc_traffic.py from a
     separate rocprofv3 --pmc FETCH_SIZE run: PMC counters cannot be read
     inside this timed run), scaled to this launch's bytes."""
     import glob
+    # the round's final profile by name (round tags do not sort by date:
+    # r03f is round 3's final tree, after r03z), else the last by name
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
+    pick = os.path.join(ROOT, TRAFFIC_FILE)
+    if os.path.exists(pick):
+        files.append(pick)
     if not files or batch_bytes != 64 * (128 << 20):
         return None, None
     d = json.load(open(files[-1]))
