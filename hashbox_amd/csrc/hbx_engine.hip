@@ -93,10 +93,13 @@ struct PinBuf {
 };
 
 // Per-kernel cumulative timing: one event pair per launch, harvested once the
-// end event has completed (hbx_stage_totals).
+// end event has completed (hbx_stage_totals).  `owned`: the pair came from
+// the context's pool (returned there once harvested); a pair of a batch's own
+// events (lean marks) stays with the batch.
 struct TimedLaunch {
   hipEvent_t a, b;
   int stage;
+  bool owned = true;
 };
 
 // Layout of a batch's results, the same on the device (d_res) and in the
@@ -144,7 +147,8 @@ struct Batch {
   const uint8_t* v_expect = nullptr;
   uint8_t* v_ok = nullptr;
   uint64_t* v_nbad = nullptr;
-  hipEvent_t ev[5] = {};  // K1 start | K1 end | K2 end | plan+K3 end (first) | results ready
+  // K1 start | K1 end | K2r end | plan+K3 end (first) | results ready | K2 end (lean marks)
+  hipEvent_t ev[6] = {};
   void release() {
     for (DevBuf* d : {&d_meta, &d_res, &d_run, &d_fresh, &d_fcnt}) d->release();
     h_meta.release();
@@ -195,6 +199,18 @@ struct hbx_ctx {
   // launch of the same submit has been dispatched.  k3_started counts K3
   // workgroups on the device; k3_dispatched is the host's running total.
   uint32_t k1_gate = 1;
+  // Lean marks (HBX_LEAN_MARKS=0 for A/B): every event record or zero-fill
+  // between two kernels of one stream costs ~5 us of dispatch, and the scan
+  // stream's gate -> K1 -> K2 -> K2r -> plan is one of the step's two
+  // equal-length loops.  With them K1 and K2 are timed by the
+  // batch's own ev[0] | ev[1] | ev[5], K2 zeroes K2r's counter, the plan's
+  // timing end event is what K3 waits on, and the plan bins are zeroed
+  // after each plan (off the loop) instead of before it.
+  uint32_t lean_marks = 1;
+  hipStream_t plan_zeroed_on = nullptr;  // stream whose last op leaves d_plan zeroed (lean)
+  TimedLaunch plan_timer[3];             // lean: the plan's timing pair, queued once K3 waits on it
+  bool plan_timer_set[3] = {false, false, false};
+  hipEvent_t plan_wait[3] = {nullptr, nullptr, nullptr};  // what K3 of launch j%3 waits on
   DevBuf d_gate;
   uint32_t k3_dispatched = 0;
   // K3 launch times measured on the device (no timing events on the hash
@@ -314,13 +330,15 @@ struct StageTimer {
   hbx_ctx* c;
   hipStream_t s;
   TimedLaunch t;
-  StageTimer(hbx_ctx* ctx, hipStream_t st, int stage) : c(ctx), s(st) {
+  // on = false: a no-op (the caller times the launch with events it records anyway)
+  StageTimer(hbx_ctx* ctx, hipStream_t st, int stage, bool on = true) : c(ctx), s(st) {
     t.stage = stage;
-    t.a = c->event();
-    t.b = c->event();
+    t.a = on ? c->event() : nullptr;
+    t.b = on ? c->event() : nullptr;
     if (t.a) (void)hipEventRecord(t.a, s);
   }
   ~StageTimer() {
+    if (!t.a && !t.b) return;
     if (t.a && t.b && hipEventRecord(t.b, s) == hipSuccess) {
       c->open_t.push_back(t);
     } else {
@@ -347,8 +365,10 @@ void harvest_timings(hbx_ctx* c) {
     if (done) {
       c->tot_ms[t.stage] += ms;
       c->tot_n[t.stage] += 1;
-      c->ev_pool.push_back(t.a);
-      c->ev_pool.push_back(t.b);
+      if (t.owned) {
+        c->ev_pool.push_back(t.a);
+        c->ev_pool.push_back(t.b);
+      }
     } else {
       c->open_t[keep++] = t;
     }
@@ -480,8 +500,10 @@ int plan_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
   const int slot = (int)(c->launches % 3), ps = (int)((c->launches + 2) % 3);
   int rc = ensure_plan_buffers(c, 0);  // nb (if any) is already in pending
   if (rc) return rc;
-  // the K3 launch that read this slot three launches ago must be done
-  if (c->order_used[slot] && c->hstream != s) HBX_TRY(c, hipStreamWaitEvent(s, c->order_free[slot], 0));
+  // the K3 launch that read this slot three launches ago must be done (lean:
+  // no wait enqueued once the host has seen it complete, the usual case)
+  if (c->order_used[slot] && c->hstream != s && !(c->lean_marks && hipEventQuery(c->order_free[slot]) == hipSuccess))
+    HBX_TRY(c, hipStreamWaitEvent(s, c->order_free[slot], 0));
   // carried chains exist only while an older batch is unfinalized (a batch
   // is finalized once every chain of it is hashed); without one the previous
   // list is not read at all (hbx_reserve may have reallocated it)
@@ -492,6 +514,41 @@ int plan_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
   const bool fresh = nb && nb->n;
   // the joining batch's chains come from K2r (cut stream) or K6p (scan stream)
   if (fresh && !(s == c->stream && c->cstream == s)) HBX_TRY(c, hipStreamWaitEvent(s, nb->ev[2], 0));
+  if (c->lean_marks) {
+    TimedLaunch t;
+    t.stage = 2;
+    t.a = c->event();
+    t.b = c->event();
+    if (t.a && t.b) {
+      HBX_TRY(c, hipEventRecord(t.a, s));
+      if (c->plan_zeroed_on != s) HBX_TRY(c, hipMemsetAsync(c->d_plan.p, 0, 2 * kPlanBins * sizeof(uint32_t), s));
+      for (uint32_t phase = 0; phase < 2; phase++)
+        hipLaunchKernelGGL(hbx_k2c_plan, dim3(kPlanGroups), dim3(kPlanThreads), 0, s,
+                           has_prev ? c->d_order[ps].as<OrderEntry>() : nullptr,
+                           has_prev ? c->d_octl[ps].as<uint32_t>() : nullptr, c->last_budget,
+                           fresh ? nb->d_fresh.as<OrderEntry>() : nullptr,
+                           fresh ? nb->d_fcnt.as<uint32_t>() : nullptr, budget,
+                           c->d_order[slot].as<OrderEntry>(), c->d_octl[slot].as<uint32_t>(),
+                           c->d_plan.as<uint32_t>(), phase);
+      HBX_TRY(c, hipGetLastError());
+      HBX_TRY(c, hipEventRecord(t.b, s));
+      // K3 waits on the timing end itself; the pair is queued for harvest
+      // only once that wait is enqueued (md5_launch), so the pool cannot hand
+      // t.b out again before
+      if (c->plan_timer_set[slot]) c->open_t.push_back(c->plan_timer[slot]);  // (not reached: K3 took it)
+      c->plan_timer[slot] = t;
+      c->plan_timer_set[slot] = true;
+      c->plan_wait[slot] = t.b;
+      // the bins for the next plan, while K3 is being dispatched
+      c->plan_zeroed_on = nullptr;
+      HBX_TRY(c, hipMemsetAsync(c->d_plan.p, 0, 2 * kPlanBins * sizeof(uint32_t), s));
+      c->plan_zeroed_on = s;
+      return HBX_OK;
+    }
+    if (t.a) c->ev_pool.push_back(t.a);
+    if (t.b) c->ev_pool.push_back(t.b);
+  }
+  c->plan_zeroed_on = nullptr;
   {
     StageTimer t(c, s, 2);
     HBX_TRY(c, hipMemsetAsync(c->d_plan.p, 0, 2 * kPlanBins * sizeof(uint32_t), s));
@@ -506,6 +563,7 @@ int plan_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
   }
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(c->plan_done[slot], s));
+  c->plan_wait[slot] = c->plan_done[slot];
   return HBX_OK;
 }
 
@@ -516,7 +574,11 @@ int plan_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
 int md5_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
   hipStream_t s = c->hstream;
   const int slot = (int)(c->launches % 3);
-  if (s != plan_stream(c)) HBX_TRY(c, hipStreamWaitEvent(s, c->plan_done[slot], 0));
+  if (s != plan_stream(c)) HBX_TRY(c, hipStreamWaitEvent(s, c->plan_wait[slot], 0));
+  if (c->plan_timer_set[slot]) {  // lean marks: the wait is enqueued, the pair may be harvested
+    c->open_t.push_back(c->plan_timer[slot]);
+    c->plan_timer_set[slot] = false;
+  }
   // the device-timing slot of this launch (its previous user, kK3TimeRing
   // launches back, must have been harvested)
   const uint64_t L = c->launches;
@@ -808,9 +870,15 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
                        c->k3_dispatched, 1000000u);
     HBX_TRY(c, hipGetLastError());
   }
+  // lean marks with K2 on this stream: ev[0] | K1 | ev[1] | K2 | ev[5] | K2r
+  // | ev[2], one record between kernels, the batch's events doubling as K1's
+  // and K2's timers (the batch outlives their harvest: it is reused only
+  // after its collect, long after both completed)
+  hipStream_t s2 = c->cstream;
+  const bool lean = c->lean_marks && s2 == s;
   HBX_TRY(c, hipEventRecord(b->ev[0], s));
   if (nt) {
-    StageTimer t(c, s, 0);
+    StageTimer t(c, s, 0, !lean);
     if (c->k1_run == 128u)
       hipLaunchKernelGGL(hbx_k1_digest_scan_dma2, dim3((uint32_t)nt), dim3(kK1bThreads), 0, s, arena, d_off, d_len,
                          d_sb, d_tiles, ssum.as<uint2>(), slices);
@@ -820,20 +888,26 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   }
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(b->ev[1], s));
+  if (lean && nt) c->open_t.push_back(TimedLaunch{b->ev[0], b->ev[1], 0, false});
   // K2 on the cut stream: the scan stream goes straight on with the next
   // batch's K1 (into the other summary slot)
-  hipStream_t s2 = c->cstream;
   if (s2 != s) HBX_TRY(c, hipStreamWaitEvent(s2, b->ev[1], 0));
   {
-    StageTimer t(c, s2, 1);
+    StageTimer t(c, s2, 1, !lean);
     hipLaunchKernelGGL(hbx_k2_cut_chain, dim3((uint32_t)n), dim3(64), 0, s2, arena, d_off, d_len,
-                       d_sb, ssum.as<uint2>(), d_cb, b->cuts_d(), b->count_d());
+                       d_sb, ssum.as<uint2>(), d_cb, b->cuts_d(), b->count_d(),
+                       lean ? b->d_fcnt.as<uint32_t>() : nullptr);
   }
   HBX_TRY(c, hipGetLastError());
-  HBX_TRY(c, hipEventRecord(c->ssum_free[slot], s2));
+  if (lean) {  // the summary slot's next writer (K1, this stream) follows in order: no ssum_free
+    HBX_TRY(c, hipEventRecord(b->ev[5], s2));
+    c->open_t.push_back(TimedLaunch{b->ev[1], b->ev[5], 1, false});
+  } else {
+    HBX_TRY(c, hipEventRecord(c->ssum_free[slot], s2));
+  }
   c->ssum_used[slot] = true;
-  // K2r: the batch's chains and their order entries
-  HBX_TRY(c, hipMemsetAsync(b->d_fcnt.p, 0, 4, s2));
+  // K2r: the batch's chains and their order entries (lean: K2 zeroed the count)
+  if (!lean) HBX_TRY(c, hipMemsetAsync(b->d_fcnt.p, 0, 4, s2));
   hipLaunchKernelGGL(hbx_k2r_new_chains, dim3((uint32_t)((n * kPlanLanesPerFile + 255) / 256)), dim3(256), 0, s2,
                      (uint32_t)n, arena, d_off, d_cb, b->cuts_d(), b->count_d(), b->ids_d(), b->d_run.as<Chain>(), b->d_fresh.as<OrderEntry>(),
                      b->d_fcnt.as<uint32_t>());
@@ -1093,6 +1167,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = ab_env("HBX_PLAN_MODE")) c->plan_mode = std::min(2, std::max(0, std::atoi(v)));
   if (const char* v = ab_env("HBX_MD5_SLICE")) c->md5_slice = (uint32_t)std::max(0, std::atoi(v));
   if (const char* v = ab_env("HBX_K1_GATE")) c->k1_gate = std::atoi(v) ? 1u : 0u;
+  if (const char* v = ab_env("HBX_LEAN_MARKS")) c->lean_marks = std::atoi(v) ? 1u : 0u;
   if (hipSetDevice(device) != hipSuccess || make_stream(&c->stream, "HBX_SCAN_CUS", ncu, "0:4096") != hipSuccess) {
     delete c;
     return HBX_ERR_HIP;
@@ -1165,7 +1240,10 @@ void hbx_ctx_destroy(hbx_ctx* c) {
     b->release();
     delete b;
   }
+  for (int i = 0; i < 3; i++)
+    if (c->plan_timer_set[i]) c->open_t.push_back(c->plan_timer[i]);
   for (TimedLaunch& t : c->open_t) {
+    if (!t.owned) continue;  // a batch's own events (released with the batch)
     (void)hipEventDestroy(t.a);
     (void)hipEventDestroy(t.b);
   }
@@ -1203,10 +1281,10 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
       out, (size_t)cap,
       "{\"ab_env\": %d, \"md5_slice\": %u, \"join_lag\": %u, \"tile_iters\": %u, \"k1_run\": %u, "
       "\"k3_waves\": %u, \"k3_dense\": %u, \"k1_gate\": %u, \"md5_wgs\": %u, \"plan_mode\": %d, "
-      "\"k2_own\": %d, \"k4_window\": %u, \"one_stream\": %d, \"k3_probe\": %d}",
+      "\"k2_own\": %d, \"k4_window\": %u, \"one_stream\": %d, \"k3_probe\": %d, \"lean_marks\": %u}",
       (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_run,
       c->k3_threads == kK3Threads2 ? 2u : 1u, c->k3_dense, c->k1_gate, c->md5_wgs, c->plan_mode, c->k2_own,
-      c->k4_window, c->hstream == c->stream ? 1 : 0, c->h_probe.p ? 1 : 0);
+      c->k4_window, c->hstream == c->stream ? 1 : 0, c->h_probe.p ? 1 : 0, c->lean_marks);
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }
 
@@ -1980,6 +2058,9 @@ int hbx_input_after_oldest(hbx_ctx* c) {
   // the completion event of the launch that finished it (or of a later one,
   // if that slot has been recorded again since)
   const uint64_t L = c->launches - x->final_launch <= 3 ? x->final_launch : c->launches - 1;
+  // (lean marks: nothing to enqueue once the host has seen it complete -- in
+  // the steady state it finished two launches ago)
+  if (c->lean_marks && hipEventQuery(c->order_free[L % 3]) == hipSuccess) return HBX_OK;
   HBX_TRY(c, hipStreamWaitEvent(c->stream, c->order_free[L % 3], 0));
   return HBX_OK;
 }

@@ -679,9 +679,12 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k2_cut_chain(
     const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ slice_base,
     const uint2* __restrict__ ssum,
     const uint64_t* __restrict__ cut_base, uint64_t* __restrict__ cut_ends,
-    uint32_t* __restrict__ cut_count) {
+    uint32_t* __restrict__ cut_count, uint32_t* __restrict__ zero_word) {
   const uint32_t f = blockIdx.x;
   const uint32_t l = threadIdx.x;
+  // K2r's chain counter (which follows on the same stream), zeroed here
+  // instead of by a fill dispatch of its own (hbx_engine.hip, lean marks)
+  if (zero_word && f == 0u && l == 0u) *zero_word = 0u;
   const uint64_t N = file_len[f];
   const uint8_t* fb = arena + file_off[f];
   const uint64_t sb = slice_base[f];

@@ -1,12 +1,13 @@
 #!/bin/bash
 # A/B of environment switches on one build, alternating so drift shows.
 # usage: ENVS="HBX_HASH_CUS=prio:hi;HBX_RES_CUS=prio:hi" BENCH_ARGS="--steps 20" tools/gpu_ab_env.sh
+#        REPS=3 (default 2) alternations
 set -o pipefail
 export HBX_AB=1  # the library honours HBX_* A/B switches only with this
 O=gpurun_out/abenv
 mkdir -p $O
 IFS=';' read -ra VS <<< "base;${ENVS}"
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
   for v in "${VS[@]}"; do
     tag=$(echo "$v" | tr -c 'A-Za-z0-9' '_')
     if [ "$v" = base ]; then E=""; else E="$v"; fi
