@@ -514,6 +514,12 @@ int plan_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
   const bool fresh = nb && nb->n;
   // the joining batch's chains come from K2r (cut stream) or K6p (scan stream)
   if (fresh && !(s == c->stream && c->cstream == s)) HBX_TRY(c, hipStreamWaitEvent(s, nb->ev[2], 0));
+  // the plan stream changed (hbx_set_join_lag): the trailing bin fill queued on
+  // the old one must not land inside this plan
+  if (c->plan_zeroed_on && c->plan_zeroed_on != s) {
+    HBX_TRY(c, hipStreamSynchronize(c->plan_zeroed_on));
+    c->plan_zeroed_on = nullptr;
+  }
   if (c->lean_marks) {
     TimedLaunch t;
     t.stage = 2;

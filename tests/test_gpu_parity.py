@@ -277,6 +277,42 @@ def test_pipelined_steady_state(oracle, monkeypatch, join_lag, plan_mode):
             _check(a, r)
 
 
+@pytest.mark.parametrize("lean", ["1", "0"])
+def test_plan_stream_changes_in_one_context(oracle, monkeypatch, lean):
+    """One context through join lags 1 -> 2 -> 3 -> 1: the plan moves from
+    the scan stream (mode 0) to the hash stream (mode 1) to a preplan on the
+    scan stream (mode 2) and back.  With lean marks (hbx_engine.hip) the plan
+    bins are zeroed after each plan on the plan's stream, so every move must
+    order the new stream after the old one's fill; the stage totals still count
+    one K1, K2 and plan per batch.  HBX_LEAN_MARKS=0 runs the old schedule."""
+    from hashbox_amd import Engine
+    monkeypatch.setenv("HBX_AB", "1")
+    monkeypatch.setenv("HBX_LEAN_MARKS", lean)
+    batches = _device_batches(oracle, 2, 61)
+    with Engine(0, md5_slice=4096) as e:
+        assert e.knobs()["lean_marks"] == int(lean)
+        e.stage_totals(reset=True)
+        n_batches = 0
+        for lag in (1, 2, 3, 1):
+            e.set_join_lag(lag)
+            got, order = [], [i % 2 for i in range(6)]
+            for i in order:
+                dev, offs, sizes, _ = batches[i]
+                e.submit_device(dev.data_ptr(), offs, sizes)
+                if e.pending() >= 3:
+                    got.append(e.wait())
+            while e.pending():
+                got.append(e.wait())
+            n_batches += len(order)
+            assert len(got) == len(order)
+            for i, g in zip(order, got):
+                for a, r in zip(g, batches[i][3]):
+                    _check(a, r)
+        ms, n = e.stage_totals()
+        assert n[0] == n_batches and n[1] == n_batches and n[2] >= n_batches
+        assert all(m > 0 for m in ms[:4])
+
+
 @pytest.mark.parametrize("dense,k3_waves", [("0", 1), ("1", 1), ("0", 2), ("1", 2)])
 def test_reserved_pipeline_placements(oracle, monkeypatch, dense, k3_waves):
     """hbx_reserve pre-sizes the pool, chain tables and summaries; both K3
