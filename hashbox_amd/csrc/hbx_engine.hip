@@ -139,6 +139,7 @@ struct Batch {
   uint32_t need = 1, done = 0;  // K3 launches its chains need / have had
   bool joined = false;          // its chains are in the carried order lists (a plan took them)
   bool ev3 = false;             // ev[3] recorded (synchronous batches only)
+  bool k2_ev5 = false;          // lean marks: K2's end is ev[5] and ev[2] is not recorded
   uint64_t final_launch = 0;    // index of the K3 launch after which it was finalized
   bool finalized = false;
   // a VerifyBlock batch (hbx_verify_submit_device) instead of files
@@ -211,6 +212,11 @@ struct hbx_ctx {
   TimedLaunch plan_timer[3];             // lean: the plan's timing pair, queued once K3 waits on it
   bool plan_timer_set[3] = {false, false, false};
   hipEvent_t plan_wait[3] = {nullptr, nullptr, nullptr};  // what K3 of launch j%3 waits on
+  // lean: hbx_input_after_oldest's wait (for K3 launch input_wait_L), enqueued
+  // on the scan stream only just before the next thing that could touch the
+  // old input (flush_input_wait), i.e. after the plan instead of before it
+  bool input_wait_pending = false;
+  uint64_t input_wait_L = 0;
   DevBuf d_gate;
   uint32_t k3_dispatched = 0;
   // K3 launch times measured on the device (no timing events on the hash
@@ -411,6 +417,7 @@ Batch* acquire_batch(hbx_ctx* c) {
   b->rl = ResLayout{};  // a verify batch keeps its ids at offset 0 of d_res
   b->joined = false;
   b->ev3 = false;
+  b->k2_ev5 = false;
   b->final_launch = 0;
   b->finalized = false;
   b->cut_ends = nullptr;
@@ -495,6 +502,19 @@ int ensure_cut_stream(hbx_ctx* c) {
   return HBX_OK;
 }
 
+// Enqueue a deferred hbx_input_after_oldest wait on the scan stream (nothing
+// once the host has seen that launch complete).  Called before anything that
+// may read or write a caller's input on the scan stream, and before any K3
+// launch could record the launch's completion slot again.
+int flush_input_wait(hbx_ctx* c) {
+  if (!c->input_wait_pending) return HBX_OK;
+  c->input_wait_pending = false;
+  hipEvent_t e = c->order_free[c->input_wait_L % 3];
+  if (hipEventQuery(e) == hipSuccess) return HBX_OK;
+  HBX_TRY(c, hipStreamWaitEvent(c->stream, e, 0));
+  return HBX_OK;
+}
+
 int plan_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
   hipStream_t s = plan_stream(c);
   const int slot = (int)(c->launches % 3), ps = (int)((c->launches + 2) % 3);
@@ -549,7 +569,7 @@ int plan_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
       c->plan_zeroed_on = nullptr;
       HBX_TRY(c, hipMemsetAsync(c->d_plan.p, 0, 2 * kPlanBins * sizeof(uint32_t), s));
       c->plan_zeroed_on = s;
-      return HBX_OK;
+      return flush_input_wait(c);
     }
     if (t.a) c->ev_pool.push_back(t.a);
     if (t.b) c->ev_pool.push_back(t.b);
@@ -570,7 +590,7 @@ int plan_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(c->plan_done[slot], s));
   c->plan_wait[slot] = c->plan_done[slot];
-  return HBX_OK;
+  return flush_input_wait(c);
 }
 
 // One MD5 launch (planned by plan_launch just before): K3 with `budget`
@@ -578,6 +598,7 @@ int plan_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
 // those whose chains are now guaranteed complete are finalized.  A budget of
 // kBudgetAll completes every chain in flight.
 int md5_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
+  if (int frc = flush_input_wait(c)) return frc;  // (a preplanned launch comes without a plan_launch)
   hipStream_t s = c->hstream;
   const int slot = (int)(c->launches % 3);
   if (s != plan_stream(c)) HBX_TRY(c, hipStreamWaitEvent(s, c->plan_wait[slot], 0));
@@ -861,6 +882,7 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   c->ssum_slot ^= 1;
   DevBuf& ssum = c->d_ssum[slot];
 
+  if (int frc = flush_input_wait(c)) return frc;  // (no launch this submit: nothing flushed it yet)
   HBX_TRY(c, hipMemcpyAsync(b->d_meta.p, hm, meta_bytes, hipMemcpyHostToDevice, s));
   const uint64_t* d_off = b->d_meta.as<uint64_t>();
   const uint64_t* d_len = d_off + n;
@@ -877,7 +899,8 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
     HBX_TRY(c, hipGetLastError());
   }
   // lean marks with K2 on this stream: ev[0] | K1 | ev[1] | K2 | ev[5] | K2r
-  // | ev[2], one record between kernels, the batch's events doubling as K1's
+  // (| ev[2] unless the plan follows on this stream), one record between
+  // kernels, the batch's events doubling as K1's
   // and K2's timers (the batch outlives their harvest: it is reused only
   // after its collect, long after both completed)
   hipStream_t s2 = c->cstream;
@@ -919,8 +942,13 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
                      b->d_fcnt.as<uint32_t>());
   HBX_TRY(c, hipGetLastError());
   // the plan this batch joins waits for ev[2] (plan_launch), so with a join
-  // lag of 2 the scan stream never waits for this K2
-  HBX_TRY(c, hipEventRecord(b->ev[2], s2));
+  // lag of 2 the scan stream never waits for this K2.  Lean marks with the
+  // plan on this same stream: no one waits, and ev[5] already marks K2's end
+  if (lean && plan_stream(c) == s2) {
+    b->k2_ev5 = true;
+  } else {
+    HBX_TRY(c, hipEventRecord(b->ev[2], s2));
+  }
   c->unjoined.push_back(b);
   return HBX_OK;
 }
@@ -978,6 +1006,7 @@ int submit_verify_launch(hbx_ctx* c, Batch* b, const uint8_t* arena, uint64_t n,
   hipStream_t s = c->stream;
   int rc = md5_step(c, budget);  // launch j first, as in submit_batch_launch
   if (!rc) rc = preplan(c, budget);
+  if (!rc) rc = flush_input_wait(c);
   if (rc) return rc;
   if (n == 0) {
     for (int i = 0; i < 4; i++) HBX_TRY(c, hipEventRecord(b->ev[i], s));
@@ -1050,11 +1079,14 @@ int collect_batch(hbx_ctx* c, Batch* b) {
     if (b->ids) std::memcpy(b->ids + 16 * b->out_base[f], hid + 16 * ib, k * 16);
   }
   float ms = 0.f;
+  // stage boundaries: K1 start | K1 end | K2 end | plan+K3 end | results
+  // ready (K2's end is ev[5] where lean marks left ev[2] unrecorded)
+  const hipEvent_t bd[5] = {b->ev[0], b->ev[1], b->k2_ev5 ? b->ev[5] : b->ev[2], b->ev[3], b->ev[4]};
   for (int i = 0; i < 4; i++) {
     c->stage_ms[i] = 0.f;
     // a pipelined batch has no ev[3]: [2] then spans K2 end -> results ready
     const int e = (i == 2 && !b->ev3) ? 4 : i + 1;
-    if ((i != 3 || b->ev3) && hipEventElapsedTime(&ms, b->ev[i], b->ev[e]) == hipSuccess) c->stage_ms[i] = ms;
+    if ((i != 3 || b->ev3) && hipEventElapsedTime(&ms, bd[i], bd[e]) == hipSuccess) c->stage_ms[i] = ms;
   }
   if (hipEventElapsedTime(&ms, b->ev[0], b->ev[4]) == hipSuccess) c->stage_ms[4] = ms;
   return rc;
@@ -1610,6 +1642,7 @@ int hbx_memcpy_h2d(hbx_ctx* c, void* d, const void* h, uint64_t n) {
   if (!c || (n && (!d || !h))) return HBX_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   HBX_TRY(c, hipSetDevice(c->device));
+  if (int frc = flush_input_wait(c)) return frc;
   HBX_TRY(c, hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, c->stream));
   HBX_TRY(c, hipStreamSynchronize(c->stream));
   return HBX_OK;
@@ -2041,6 +2074,7 @@ int hbx_memcpy_h2d_async(hbx_ctx* c, void* d, const void* h, uint64_t n) {
   if (!c || (n && (!d || !h))) return HBX_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   HBX_TRY(c, hipSetDevice(c->device));
+  if (int frc = flush_input_wait(c)) return frc;
   HBX_TRY(c, hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, c->stream));
   return HBX_OK;
 }
@@ -2067,6 +2101,12 @@ int hbx_input_after_oldest(hbx_ctx* c) {
   // (lean marks: nothing to enqueue once the host has seen it complete -- in
   // the steady state it finished two launches ago)
   if (c->lean_marks && hipEventQuery(c->order_free[L % 3]) == hipSuccess) return HBX_OK;
+  if (c->lean_marks) {  // enqueued after the next plan (flush_input_wait), off the scan loop
+    if (int frc = flush_input_wait(c)) return frc;  // (an earlier one not yet flushed goes first)
+    c->input_wait_pending = true;
+    c->input_wait_L = L;
+    return HBX_OK;
+  }
   HBX_TRY(c, hipStreamWaitEvent(c->stream, c->order_free[L % 3], 0));
   return HBX_OK;
 }
