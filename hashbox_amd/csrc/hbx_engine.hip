@@ -11,6 +11,7 @@
 // Reference seams: hashback/store.go:111-199 (storeFile), pkg/core/client.go:
 // 556-560 + block.go:96-111 (StoreData -> HashData).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <fcntl.h>
 #include <unistd.h>
@@ -207,7 +208,7 @@ struct hbx_ctx {
   // batch's own ev[0] | ev[1] | ev[5], K2 zeroes K2r's counter, the plan's
   // timing end event is what K3 waits on, and the plan bins are zeroed
   // after each plan (off the loop) instead of before it.
-  uint32_t lean_marks = 1;
+  uint32_t lean_marks = 1;  // 0 off, 1 records, 2 records riding on K1/K2 (hipExtLaunchKernel)
   hipStream_t plan_zeroed_on = nullptr;  // stream whose last op leaves d_plan zeroed (lean)
   TimedLaunch plan_timer[3];             // lean: the plan's timing pair, queued once K3 waits on it
   bool plan_timer_set[3] = {false, false, false};
@@ -905,10 +906,19 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   // after its collect, long after both completed)
   hipStream_t s2 = c->cstream;
   const bool lean = c->lean_marks && s2 == s;
-  HBX_TRY(c, hipEventRecord(b->ev[0], s));
+  // lean_marks 2: ev[0], ev[1] and ev[5] ride on the K1 and K2 dispatches
+  // themselves (hipExtLaunchKernel's start/stop events), no packet between
+  const bool ext = lean && c->lean_marks >= 2;
+  if (!(ext && nt)) HBX_TRY(c, hipEventRecord(b->ev[0], s));
   if (nt) {
     StageTimer t(c, s, 0, !lean);
-    if (c->k1_run == 128u)
+    if (ext && c->k1_run == 128u)
+      hipExtLaunchKernelGGL(hbx_k1_digest_scan_dma2, dim3((uint32_t)nt), dim3(kK1bThreads), 0, s, b->ev[0], b->ev[1],
+                            0u, arena, d_off, d_len, d_sb, d_tiles, ssum.as<uint2>(), slices);
+    else if (ext)
+      hipExtLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3((uint32_t)nt), dim3(kK1Threads), 0, s, b->ev[0], b->ev[1],
+                            0u, arena, d_off, d_len, d_sb, d_tiles, ssum.as<uint2>(), slices);
+    else if (c->k1_run == 128u)
       hipLaunchKernelGGL(hbx_k1_digest_scan_dma2, dim3((uint32_t)nt), dim3(kK1bThreads), 0, s, arena, d_off, d_len,
                          d_sb, d_tiles, ssum.as<uint2>(), slices);
     else
@@ -916,20 +926,24 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
                          d_sb, d_tiles, ssum.as<uint2>(), slices);
   }
   HBX_TRY(c, hipGetLastError());
-  HBX_TRY(c, hipEventRecord(b->ev[1], s));
+  if (!(ext && nt)) HBX_TRY(c, hipEventRecord(b->ev[1], s));
   if (lean && nt) c->open_t.push_back(TimedLaunch{b->ev[0], b->ev[1], 0, false});
   // K2 on the cut stream: the scan stream goes straight on with the next
   // batch's K1 (into the other summary slot)
   if (s2 != s) HBX_TRY(c, hipStreamWaitEvent(s2, b->ev[1], 0));
   {
     StageTimer t(c, s2, 1, !lean);
-    hipLaunchKernelGGL(hbx_k2_cut_chain, dim3((uint32_t)n), dim3(64), 0, s2, arena, d_off, d_len,
-                       d_sb, ssum.as<uint2>(), d_cb, b->cuts_d(), b->count_d(),
-                       lean ? b->d_fcnt.as<uint32_t>() : nullptr);
+    if (ext)
+      hipExtLaunchKernelGGL(hbx_k2_cut_chain, dim3((uint32_t)n), dim3(64), 0, s2, nullptr, b->ev[5], 0u, arena, d_off,
+                            d_len, d_sb, ssum.as<const uint2>(), d_cb, b->cuts_d(), b->count_d(), b->d_fcnt.as<uint32_t>());
+    else
+      hipLaunchKernelGGL(hbx_k2_cut_chain, dim3((uint32_t)n), dim3(64), 0, s2, arena, d_off, d_len,
+                         d_sb, ssum.as<uint2>(), d_cb, b->cuts_d(), b->count_d(),
+                         lean ? b->d_fcnt.as<uint32_t>() : nullptr);
   }
   HBX_TRY(c, hipGetLastError());
   if (lean) {  // the summary slot's next writer (K1, this stream) follows in order: no ssum_free
-    HBX_TRY(c, hipEventRecord(b->ev[5], s2));
+    if (!ext) HBX_TRY(c, hipEventRecord(b->ev[5], s2));
     c->open_t.push_back(TimedLaunch{b->ev[1], b->ev[5], 1, false});
   } else {
     HBX_TRY(c, hipEventRecord(c->ssum_free[slot], s2));
@@ -1205,7 +1219,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = ab_env("HBX_PLAN_MODE")) c->plan_mode = std::min(2, std::max(0, std::atoi(v)));
   if (const char* v = ab_env("HBX_MD5_SLICE")) c->md5_slice = (uint32_t)std::max(0, std::atoi(v));
   if (const char* v = ab_env("HBX_K1_GATE")) c->k1_gate = std::atoi(v) ? 1u : 0u;
-  if (const char* v = ab_env("HBX_LEAN_MARKS")) c->lean_marks = std::atoi(v) ? 1u : 0u;
+  if (const char* v = ab_env("HBX_LEAN_MARKS")) c->lean_marks = (uint32_t)std::min(2, std::max(0, std::atoi(v)));
   if (hipSetDevice(device) != hipSuccess || make_stream(&c->stream, "HBX_SCAN_CUS", ncu, "0:4096") != hipSuccess) {
     delete c;
     return HBX_ERR_HIP;
