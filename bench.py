@@ -18,14 +18,21 @@ the engine's own launch counts).  The drain that empties the pipeline runs
 after the timer and is reported beside `value` (`drain_ms`,
 `fill_drain_gibs` = the whole run from an empty pipeline to a drained one).
 
-Multi-GPU (--scaling weak, the default): files are independent objects, so
-every rank takes a whole batch of its own files per step (configs[1] per
-GPU) and pipelines it on its own GPU and streams; value = N x 8 GiB x K / the
-slowest rank's time.  --scaling strong (BASELINE configs[2], a parity case):
-every step's 64 files are split across the ranks by LPT on bytes
-(hashbox_amd.shard); value = 8 GiB x K / the slowest rank's time.  No
-collective touches the data: torch.distributed carries only the barriers,
-the max-time reduction and the check flags.
+Multi-GPU (--scaling strong, the default: BASELINE configs[2]): every step's
+64 x 128 MiB files are split across the ranks by LPT on bytes
+(hashbox_amd.shard), each rank pipelines its share on its own GPU and
+streams; value = 8 GiB x K / the slowest rank's time.  --scaling weak (opt
+in): every rank takes a whole batch of its own files per step (configs[1] per
+GPU); value = N x 8 GiB x K / the slowest rank's time.  No collective touches
+the data: torch.distributed carries only the barriers, the max-time reduction
+and the check flags.
+
+End to end (key `e2e`, on by default, --e2e-steps 0 turns it off): after the
+device-resident lines, the same pipeline with every step's batch copied from
+pinned host memory (hbx_alloc_pinned + hbx_memcpy_h2d_async on the scan
+stream, overlapped with the previous batches' kernels), results back in host
+memory: the PCIe-inclusive rate north_star asks for (store.go:125 fill,
+client.go:249-258 send).
 
 Prints ONE JSON line on rank 0.  Multi-GPU:
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -90,9 +97,9 @@ def parse():
     ap.add_argument("--files", type=int, default=64, help="files per step (whole job)")
     ap.add_argument("--file-mib", type=int, default=128)
     ap.add_argument("--seed", type=int, default=1000)
-    ap.add_argument("--scaling", choices=["strong", "weak"], default="weak",
-                    help="weak: every rank takes a whole batch of its own files per step (per-GPU work "
-                         "fixed); strong: each step's files are split across the ranks (configs[2])")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="strong (default, configs[2]): each step's files are split across the ranks; "
+                         "weak: every rank takes a whole batch of its own files per step (per-GPU work fixed)")
     ap.add_argument("--workload", choices=["both", "random", "zipf"], default="both",
                     help="both: the random headline plus a Zipf-duplicate line under key 'zipf'")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -116,8 +123,11 @@ def parse():
                          "batch's scan overlap the launch finishing the old one (hbx_input_after_oldest), but at "
                          "the auto residency it puts 32 batches' chains in flight, past K3's 128-CU cliff")
     ap.add_argument("--e2e", action="store_true",
-                    help="host-inclusive mode: each step's batch is copied from pinned host memory "
-                         "(H2D on the engine's scan stream, overlapped with the pipeline)")
+                    help="host-inclusive mode as the headline: each step's batch is copied from pinned host "
+                         "memory (H2D on the engine's scan stream, overlapped with the pipeline)")
+    ap.add_argument("--e2e-steps", type=int, default=20,
+                    help="steps of the pinned-host leg reported under key 'e2e' after the device-resident "
+                         "lines (0 = skip)")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the oracle check of the last collected and the last drained batch")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPUs; gloo for tests")
@@ -339,7 +349,7 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
     if dist:
         dist.barrier()
     tot_ms, tot_n = eng.stage_totals()
-    probe = k3_probe_stats(eng.k3_wave_times()) if os.environ.get("HBX_K3_PROBE") == "1" else None
+    probe = k3_probe_stats(eng.k3_wave_times()) if eng.knobs().get("k3_probe") else None
     t_d = time.perf_counter()
     drained = None
     while order:
@@ -625,10 +635,9 @@ def setup(a, rank, world, local_world, ndev, dev_idx, dev):
         arenas = [arenas[i % P["physical_arenas"]] for i in range(R)]
     ballast = torch.zeros(int(a.ballast_gib * GIB), dtype=torch.uint8, device=dev) if a.ballast_gib else None
     torch.cuda.synchronize(dev)
-    if a.k3_probe:
-        os.environ["HBX_AB"] = "1"
-        os.environ["HBX_K3_PROBE"] = "1"
     eng = Engine(dev_idx, md5_slice=B, join_lag=lag, k3_waves=a.k3_waves)
+    if a.k3_probe:  # the probe alone (hbx_set_k3_probe), no other HBX_* switch
+        eng.set_k3_probe(True)
     # every batch slot, chain table and summary buffer of the pipeline is
     # allocated now: an allocation inside the timed region would drain the streams
     eng.reserve(R + 2, len(lens), sum(lens))
@@ -637,6 +646,59 @@ def setup(a, rank, world, local_world, ndev, dev_idx, dev):
     latency = eng.stage_times()
     return {"plan": P, "arenas": arenas, "ballast": ballast, "eng": eng, "latency": latency, "cores": cores,
             "threads": threads}
+
+
+def e2e_leg(a, eng, arenas, offs, lens, P, lanes, dist, dev, red_dev, world, rank, job_batch, threads):
+    """The PCIe-inclusive rate (north_star: "the end-to-end rate including
+    pinned hipMemcpyAsync H2D/D2H overlapped on a side stream must also be
+    measured"): the same pipeline, but every step's batch starts in pinned
+    host memory (hbx_alloc_pinned) and is copied into its arena by
+    hbx_memcpy_h2d_async on the engine's scan stream, overlapped with the
+    kernels of the batches before it; the cut lists, block IDs and content ids
+    come back by the result stream's D2H copy (hbx_wait).  H2D-bound, so a
+    shallow pipeline: R = lead + 2 resident arenas, two K3 launches per batch.
+    Runs after the device-resident lines; the random batch is regenerated."""
+    import copy
+    import ctypes
+    used = int(offs[-1]) + int(lens[-1])
+    ld, lag = P["lead"], P["join_lag"]
+    R_e = min(ld + 2, len(arenas))
+    nfull = (min(P["file_bytes"], 8 << 20) + 8) >> 6
+    B_e = -(-nfull // max(1, R_e - ld))
+    need_e = -(-nfull // B_e)
+    if need_e + lag > R_e:
+        return None
+    g = torch.Generator(device=dev)
+    g.manual_seed(a.seed + 7919 * rank)
+    arenas[0].random_(0, 256, generator=g)
+    hp = ctypes.c_void_p()
+    if eng._L.hbx_alloc_pinned(used, ctypes.byref(hp)) != 0:
+        raise RuntimeError("hbx_alloc_pinned failed")
+    try:
+        host = np.ctypeslib.as_array((ctypes.c_uint8 * used).from_address(hp.value))
+        torch.from_numpy(host).copy_(arenas[0][:used])
+        torch.cuda.synchronize(dev)
+        eng.set_md5_slice(B_e)
+
+        def before(i):
+            eng.memcpy_h2d_async(arenas[i].data_ptr(), hp.value, used)
+
+        ae = copy.copy(a)
+        ae.steps, ae.warmup = a.e2e_steps, min(a.warmup, 3)
+        r = run_workload(ae, "e2e", eng, arenas[:R_e], offs, lens, R_e, B_e, need_e, lanes, dist, dev, red_dev,
+                         world, rank, job_batch, threads, before)
+    finally:
+        eng._L.hbx_free_pinned(hp)
+    keep = ("value", "ms_per_step", "drain_ms", "fill_drain_gibs", "kernel_ms_per_step", "window_launches",
+            "host_ms_per_step", "check_vs_oracle")
+    out = {k: r[k] for k in keep if k in r}
+    out.update({"unit": "GiB/s", "steps": ae.steps, "warmup": ae.warmup,
+                "what": "pinned host memory (hbx_alloc_pinned) -> hbx_memcpy_h2d_async on the scan stream -> "
+                        "K1/K2/K3/K4 -> D2H of cut lists + block IDs + content ids into host memory; "
+                        "every step copies its whole batch over PCIe",
+                "h2d_bytes_per_step_per_gpu": used, "pipeline_depth": R_e, "md5_slice_blocks": B_e,
+                "launches_per_batch": need_e})
+    return out
 
 
 def run(a, S, rank, world, local_world, dist, dev, red_dev):
@@ -679,6 +741,10 @@ def run(a, S, rank, world, local_world, dist, dev, red_dev):
                                  world, rank, job_batch, threads, before)
         if zipf_repeat is not None and wl == "zipf":
             lines[wl]["repeat_fraction"] = round(zipf_repeat, 4)
+
+    e2e = None
+    if a.e2e_steps > 0 and not a.e2e and a.alias_depth == 0:
+        e2e = e2e_leg(a, eng, arenas, offs, lens, P, lanes, dist, dev, red_dev, world, rank, job_batch, threads)
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.e2e:
@@ -730,6 +796,8 @@ def run(a, S, rank, world, local_world, dist, dev, red_dev):
                            "gibs": round(sum(lens) / GIB / (float(latency[4]) * 1e-3), 3),
                            "stages_ms": [round(float(x), 3) for x in latency]}
     out["cpu_baseline"] = cpu
+    if e2e is not None:
+        out["e2e"] = e2e
     if "zipf" in lines and workloads[0] != "zipf":
         out["zipf"] = dict(lines["zipf"], workload=f"{a.files} x {a.file_mib} MiB Zipf-duplicated buffers "
                                                    "(configs[3] scheme), device-resident")

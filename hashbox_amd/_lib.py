@@ -34,6 +34,7 @@ EXPORTS = [
     "hbx_wire_encode_id", "hbx_wire_encode_block_header", "hbx_wire_parse",
     "hbx_verify_submit_device", "hbx_inflate_blocks_device", "hbx_store_paths_zcb", "hbx_after_stream",
     "hbx_set_join_lag", "hbx_k3_wave_times", "hbx_input_after_oldest", "hbx_knobs",
+    "hbx_input_fence", "hbx_set_k3_probe",
 ]
 # Functions returning something other than an int status.
 _NON_STATUS = ("hbx_ctx_destroy", "hbx_last_error", "hbx_max_chunks", "hbx_file_entry_size",
@@ -126,6 +127,8 @@ def load() -> ctypes.CDLL:
     L.hbx_set_k3_waves.argtypes = [P, ctypes.c_uint32]
     L.hbx_set_join_lag.argtypes = [P, ctypes.c_uint32]
     L.hbx_input_after_oldest.argtypes = [P]
+    L.hbx_input_fence.argtypes = [P, P]
+    L.hbx_set_k3_probe.argtypes = [P, I]
     L.hbx_k3_wave_times.argtypes = [P, P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
     L.hbx_knobs.argtypes = [P, ctypes.c_char_p, U64]
     L.hbx_stage_totals.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64), I]

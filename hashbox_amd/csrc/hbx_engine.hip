@@ -218,6 +218,10 @@ struct hbx_ctx {
   // old input (flush_input_wait), i.e. after the plan instead of before it
   bool input_wait_pending = false;
   uint64_t input_wait_L = 0;
+  // the launch the latest hbx_input_after_oldest ordered input behind
+  // (hbx_input_fence hands it to a caller's stream); unset once known complete
+  bool input_fence_set = false;
+  uint64_t input_fence_L = 0;
   DevBuf d_gate;
   uint32_t k3_dispatched = 0;
   // K3 launch times measured on the device (no timing events on the hash
@@ -1340,11 +1344,28 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }
 
+int hbx_set_k3_probe(hbx_ctx* c, int on) {
+  if (!c) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  // the launch in flight may still write the records
+  if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
+  HBX_TRY(c, hipSetDevice(c->device));
+  HBX_TRY(c, hipStreamSynchronize(c->hstream));
+  if (!on) {
+    c->h_probe.release();
+    return HBX_OK;
+  }
+  const size_t n = (size_t)c->md5_wgs * (kK3Threads2 / 64) * 32;
+  HBX_TRY(c, c->h_probe.ensure(n));
+  std::memset(c->h_probe.p, 0, n);
+  return HBX_OK;
+}
+
 int hbx_k3_wave_times(hbx_ctx* c, uint64_t* out, uint32_t max_waves, uint32_t* n_waves) {
   if (!c || !n_waves) return HBX_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   *n_waves = 0;
-  if (!c->h_probe.p) return c->fail(HBX_ERR_STATE, "K3 probe not enabled (HBX_K3_PROBE=1 at context creation)");
+  if (!c->h_probe.p) return c->fail(HBX_ERR_STATE, "K3 probe not enabled (hbx_set_k3_probe)");
   HBX_TRY(c, hipSetDevice(c->device));
   HBX_TRY(c, hipStreamSynchronize(c->hstream));
   const uint32_t n = c->md5_wgs * (c->k3_threads / 64);
@@ -2097,6 +2118,7 @@ int hbx_input_after_oldest(hbx_ctx* c) {
   if (!c) return HBX_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   if (c->broken) return c->fail(HBX_ERR_STATE, "context is unusable after a failed submit; destroy it");
+  c->input_fence_set = false;
   if (c->pending.empty()) return HBX_OK;
   HBX_TRY(c, hipSetDevice(c->device));
   Batch* x = c->pending.front();
@@ -2115,6 +2137,8 @@ int hbx_input_after_oldest(hbx_ctx* c) {
   // (lean marks: nothing to enqueue once the host has seen it complete -- in
   // the steady state it finished two launches ago)
   if (c->lean_marks && hipEventQuery(c->order_free[L % 3]) == hipSuccess) return HBX_OK;
+  c->input_fence_set = true;
+  c->input_fence_L = L;
   if (c->lean_marks) {  // enqueued after the next plan (flush_input_wait), off the scan loop
     if (int frc = flush_input_wait(c)) return frc;  // (an earlier one not yet flushed goes first)
     c->input_wait_pending = true;
@@ -2122,6 +2146,16 @@ int hbx_input_after_oldest(hbx_ctx* c) {
     return HBX_OK;
   }
   HBX_TRY(c, hipStreamWaitEvent(c->stream, c->order_free[L % 3], 0));
+  return HBX_OK;
+}
+
+int hbx_input_fence(hbx_ctx* c, void* stream) {
+  if (!c) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  HBX_TRY(c, hipSetDevice(c->device));
+  if (int frc = flush_input_wait(c)) return frc;
+  if (stream && c->input_fence_set)
+    HBX_TRY(c, hipStreamWaitEvent(static_cast<hipStream_t>(stream), c->order_free[c->input_fence_L % 3], 0));
   return HBX_OK;
 }
 

@@ -295,13 +295,24 @@ class Engine:
         (hbx_input_after_oldest)."""
         self._check(self._L.hbx_input_after_oldest(self._ctx), "hbx_input_after_oldest")
 
+    def input_fence(self, stream: Optional[int] = None):
+        """Enqueue the pending wait of :meth:`input_after_oldest` now, and on
+        ``stream`` (a raw hipStream_t handle) too: needed before the caller
+        writes the old batch's memory with its own work (hbx_input_fence)."""
+        self._check(self._L.hbx_input_fence(self._ctx, ctypes.c_void_p(int(stream) if stream else 0)),
+                    "hbx_input_fence")
+
+    def set_k3_probe(self, on: bool = True):
+        """Diagnostics: per-wave records of every K3 launch (hbx_set_k3_probe)."""
+        self._check(self._L.hbx_set_k3_probe(self._ctx, int(bool(on))), "hbx_set_k3_probe")
+
     def set_join_lag(self, lag: int):
         """Submits between a batch's own and the MD5 launch its chains join
         (1..4; 2 gives a small batch's scan a whole extra step)."""
         self._check(self._L.hbx_set_join_lag(self._ctx, int(lag)), "hbx_set_join_lag")
 
     def k3_wave_times(self) -> np.ndarray:
-        """Diagnostics (HBX_K3_PROBE=1 at creation): per-wave records of the
+        """Diagnostics (:meth:`set_k3_probe`): per-wave records of the
         latest K3 launch, shape (waves, 4): start, start-up end | XCC << 56,
         end (100 MHz ticks), R | max count << 16 | HW_ID << 32."""
         n = ctypes.c_uint32(0)

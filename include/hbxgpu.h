@@ -146,15 +146,26 @@ int hbx_set_md5_slice(hbx_ctx *ctx, uint32_t blocks);
  * Results are identical; HBX_K3_WAVES sets the initial value.  Fails with
  * HBX_ERR_STATE while batches are pending. */
 int hbx_set_k3_waves(hbx_ctx *ctx, uint32_t waves_per_simd);
-/* Reuse the input memory of the OLDEST pending batch: enqueue on the
- * engine's input (scan) stream a GPU-side wait for the MD5 launch that
- * finishes that batch, so input copies (hbx_memcpy_h2d_async) and batches
- * submitted afterwards read it only once the batch's last chain is hashed —
+/* Reuse the input memory of the OLDEST pending batch: order the engine's
+ * next input copies (hbx_memcpy_h2d_async) and submitted batches (chunking
+ * and verify) after the MD5 launch that finishes that batch, with a GPU-side
+ * wait, so they touch the memory only once the batch's last chain is hashed —
  * before the batch is collected with hbx_wait, and without blocking the
  * host.  A ring of device arenas then needs no slot for results still on
  * their way to the host.  If that batch's last launch has not been issued
- * yet, the chains in flight are drained first (correct, only slower). */
+ * yet, the chains in flight are drained first (correct, only slower).
+ * The wait is enqueued lazily, just before the next engine-issued copy or
+ * submit (it then sits after the next MD5 plan, off the scan loop), so ONLY
+ * engine-issued work is ordered by this call.  A caller that writes the
+ * memory itself (its own stream, kernel or copy) calls hbx_input_fence
+ * first. */
 int hbx_input_after_oldest(hbx_ctx *ctx);
+/* Enqueue the wait of the latest hbx_input_after_oldest now: on the engine's
+ * scan stream and, if `stream` (a hipStream_t) is not NULL, on that stream
+ * too, so the caller's own writes into the old batch's memory are ordered
+ * after the MD5 launch that finishes it.  Nothing is enqueued once the host
+ * has seen that launch complete.  Never blocks the host. */
+int hbx_input_fence(hbx_ctx *ctx, void *stream);
 /* Optional: pre-size the pipeline for `batches` batches in flight of up to
  * `files` files and `bytes` bytes each.  The batch pool, the MD5 chain tables
  * and the slice summaries are allocated now, so the steady state never
@@ -452,7 +463,11 @@ int hbx_stage_times(hbx_ctx *ctx, float ms[5]);
  * [0] K1 scan, [1] K2 cut chain, [2] K2c chain plan, [3] K3 block MD5,
  * [4] K4 content id.  reset != 0 zeroes the totals after reading. */
 int hbx_stage_totals(hbx_ctx *ctx, double ms[5], uint64_t launches[5], int reset);
-/* Diagnostics: with HBX_K3_PROBE=1 in the environment at context creation,
+/* Diagnostics: turn the per-wave K3 records below on (on != 0) or off.
+ * Changes no result and no other knob.  Fails with HBX_ERR_STATE while
+ * batches are pending. */
+int hbx_set_k3_probe(hbx_ctx *ctx, int on);
+/* Diagnostics: with the probe on (hbx_set_k3_probe),
  * every K3 launch records per wave {start, end of its start-up (first
  * group's loads and prologue block) | XCC id << 56, end, R | max count << 16
  * | HW_ID << 32} (times in s_memrealtime ticks, 100 MHz; R and the count

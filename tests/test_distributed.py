@@ -133,10 +133,29 @@ def test_bench_plan_world4_through_torchrun():
     assert all(p["files_per_gpu"] == 16 and p["need"] + p["join_lag"] <= p["R"] for p in plans)
 
 
-def test_bench_plan_default_is_weak():
-    """The default multi-GPU mode: every rank a whole batch of its own files."""
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_plan_default_is_strong(world):
+    """The default multi-GPU mode is BASELINE configs[2]: each step's 64 files
+    split across the ranks by LPT (strong scaling), the N = 8 operating point
+    the driver's scaling run hits (8 files per rank, join lag 3)."""
     import json
-    r = _bench_plan(2, [])
+    r = _bench_plan(world, [])
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    d = json.loads(line)
+    assert d["scaling"] == "strong"
+    plans = d["plans"]
+    assert sorted(sum((p["mine"] for p in plans), [])) == list(range(64))
+    assert all(p["files_per_gpu"] == 64 // world for p in plans)
+    assert all(p["need"] + p["join_lag"] <= p["R"] for p in plans)
+    if world == 8:
+        assert all(p["join_lag"] == 3 and p["lead"] == 4 for p in plans)
+
+
+def test_bench_plan_weak_opt_in():
+    """--scaling weak: every rank a whole batch of its own files."""
+    import json
+    r = _bench_plan(2, ["--scaling", "weak"])
     assert r.returncode == 0, r.stderr[-2000:]
     (line,) = [x for x in r.stdout.splitlines() if x.startswith("{")]
     d = json.loads(line)

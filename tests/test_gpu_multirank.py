@@ -2,8 +2,9 @@
 (torch.distributed.run, one process per rank), here with gloo and every rank
 on cuda:0 of the one-GPU box.
 
-* bench.py --scaling strong (configs[2]: each step's files LPT-split across
-  the ranks) and --scaling weak, world 2, and strong at world 1: the window
+* bench.py at its default (strong scaling, configs[2]: each step's files
+  LPT-split across the ranks) and --scaling weak, world 2, and strong at
+  world 1, each with its pinned-host e2e leg: the window
   holds exactly K K1/K3 launches per rank and every rank's checked batches
   are bit-exact (check_vs_oracle, min over ranks).
 * bench.py over RCCL (the nccl backend the driver uses) at world 1.
@@ -44,14 +45,20 @@ BENCH = ["bench.py", "--files", "4", "--file-mib", "16", "--steps", "6", "--warm
          "--md5-slice", "32768", "--no-cpu-baseline", "--dist-backend", "gloo", "--cpu-threads", "4"]
 
 
-@pytest.mark.parametrize("nproc,scaling", [(2, "strong"), (2, "weak"), (1, "strong")])
+@pytest.mark.parametrize("nproc,scaling", [(2, None), (2, "weak"), (1, "strong")])
 def test_bench_through_torchrun(nproc, scaling):
-    d = _torchrun(nproc, BENCH + ["--gpus", str(nproc), "--scaling", scaling])
+    """scaling None = bench.py's default, which must be strong (configs[2]).
+    Every line carries the pinned-host e2e leg, checked against the oracle."""
+    d = _torchrun(nproc, BENCH + ["--gpus", str(nproc)] + (["--scaling", scaling] if scaling else []))
+    scaling = scaling or "strong"
     assert d["n_gpus"] == nproc and d["scaling"] == scaling
     assert d["check_vs_oracle"] is True and d["zipf"]["check_vs_oracle"] is True
     assert d["window_launches"]["k1_digest_scan"] == 6 and d["window_launches"]["k3_block_md5"] == 6
     assert d["config"]["files_per_gpu"] == (4 // nproc if scaling == "strong" else 4)
     assert d["value"] > 0
+    e = d["e2e"]
+    assert e["check_vs_oracle"] is True and e["value"] > 0
+    assert e["window_launches"]["k3_block_md5"] == e["steps"]
 
 
 def test_bench_rccl_world1_through_torchrun():
