@@ -769,22 +769,42 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
     uint32_t extra, my_s = r0;
     uint64_t mask = 0ull;
     uint32_t e_t = parse<false>(hist, data, hw, cd, hll, hd, sh, hl, n, my_s, rend, 0u, fbits, extra, &mask, r0);
+    bool converged = false;  // workgroup-uniform
     for (uint32_t it = 0; it < kParseRounds; it++) {
       if (t + 1u < kThreads) starts[t + 1u] = e_t;
       __syncthreads();
       const uint32_t ns = t ? starts[t] : 0u;
       const bool moved = ns != my_s;
-      if (!__syncthreads_or(moved)) break;
+      if (!__syncthreads_or(moved)) {
+        converged = true;
+        break;
+      }
       if (moved) {
         my_s = ns;
         e_t = parse<false>(hist, data, hw, cd, hll, hd, sh, hl, n, my_s, rend, 0u, fbits, extra, &mask, r0);
       }
     }
     K7P(4);
-    p_s = my_s;
+    if (!converged) {
+      // The hand-off did not settle (all-zero data cycles with period 4):
+      // starts[t] is thread t-1's latest end and starts[t+1] thread t's, and a
+      // re-parsed thread t-1 may now end past thread t's end.  The recording
+      // ranges [starts[t], starts[t+1]) must tile [0, n) exactly, so they are
+      // made ascending by a running maximum (an empty range records nothing;
+      // the final parse clips its matches to the range end).
+      if (t == 0u) {
+        uint32_t m = 0u;
+        for (uint32_t k = 1u; k < kThreads; k++) {
+          m = max(m, starts[k]);
+          starts[k] = m;
+        }
+      }
+      __syncthreads();
+    }
+    p_s = t ? starts[t] : 0u;
     p_e = t + 1u < kThreads ? starts[t + 1u] : n;
     // converged: the last dry pass's tokens end exactly at the next start
-    if (e_t == p_e)
+    if (converged && p_s == my_s && e_t == p_e)
       record_tokens(data, cd, hll, hd, sh, r0, mask, e_t, fbits, extra);
     else
       (void)parse<true>(hist, data, hw, cd, hll, hd, sh, hl, n, p_s, rend, p_e, fbits, extra);

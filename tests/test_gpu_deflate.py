@@ -187,3 +187,35 @@ def test_entropy_early_out_boundaries(engine):
     assert len(zf) < 0.98 * len(few), (len(zf), len(few))     # Huffman-coded, not stored
     assert len(zs) < 0.7 * len(small), (len(zs), len(small))  # the full parse matched the repeat
     assert len(zm) < len(mix), (len(zm), len(mix))            # the text half compresses
+
+
+def test_parse_handoff_that_does_not_settle(engine):
+    """K7's parse hands each thread's end on as the next thread's start for at
+    most 8 rounds.  Zero runs never settle (the hand-off cycles with period 4);
+    long matches of repeated phrases at shifting alignments make a re-parsed
+    thread end past its successor's end.  The recording ranges must still tile
+    the segment exactly (hbx_deflate.hip: a running maximum over the starts
+    when the hand-off did not settle), else bytes are coded twice and the
+    stream inflates to the wrong data.  Every block is strictly inflated."""
+    rng = np.random.default_rng(4242)
+    blocks = []
+    for i in range(160):
+        out = bytearray(bytes(1024 + 37 * i))  # a zero run of >= 1 KiB
+        phrase = _text(int(rng.integers(259, 900)), 1000 + i)
+        while len(out) < 70_000:
+            kind = int(rng.integers(0, 4))
+            if kind == 0:
+                out += bytes(int(rng.integers(1, 3000)))
+            elif kind == 1:
+                out += phrase[int(rng.integers(0, 64)):]
+            elif kind == 2:
+                out += bytes(rng.integers(0, 256, int(rng.integers(1, 70)), dtype=np.uint8))
+            else:
+                out += (phrase[:int(rng.integers(4, 300))]) * int(rng.integers(1, 6))
+        blocks.append(bytes(out[:int(rng.integers(40_000, 70_000))]))
+    for k in (1, 2, 3, 5, 7, 63, 65, 257, 259):  # zeros with a single byte every k*64 + j bytes
+        for j in (0, 1, 31):
+            b = bytearray(65_536)
+            b[j::64 * k + j + 1] = b"\x01" * len(b[j::64 * k + j + 1])
+            blocks.append(bytes(b))
+    _check(engine, blocks)
