@@ -137,9 +137,7 @@ def parse():
     ap.add_argument("--ballast-gib", type=float, default=0.0,
                     help="diagnostics: hold this much extra device memory (written once, never read)")
     ap.add_argument("--k3-probe", action="store_true",
-                    help="diagnostics: per-wave timeline of the window's last K3 launch (HBX_K3_PROBE)")
-    ap.add_argument("--k3-waves", type=int, default=1, choices=[1, 2],
-                    help="block-MD5 kernel waves per SIMD (hbx_set_k3_waves)")
+                    help="diagnostics: per-wave timeline of the window's last K3 launch (hbx_set_k3_probe)")
     ap.add_argument("--alias-depth", type=int, default=0,
                     help="diagnostics: D batches in flight over the physical arenas (batch j reads arena "
                          "j %% R; inputs are read-only, so aliasing emulates the residency a paged arena would "
@@ -635,7 +633,7 @@ def setup(a, rank, world, local_world, ndev, dev_idx, dev):
         arenas = [arenas[i % P["physical_arenas"]] for i in range(R)]
     ballast = torch.zeros(int(a.ballast_gib * GIB), dtype=torch.uint8, device=dev) if a.ballast_gib else None
     torch.cuda.synchronize(dev)
-    eng = Engine(dev_idx, md5_slice=B, join_lag=lag, k3_waves=a.k3_waves)
+    eng = Engine(dev_idx, md5_slice=B, join_lag=lag)
     if a.k3_probe:  # the probe alone (hbx_set_k3_probe), no other HBX_* switch
         eng.set_k3_probe(True)
     # every batch slot, chain table and summary buffer of the pipeline is
@@ -783,7 +781,7 @@ def run(a, S, rank, world, local_world, dist, dev, red_dev):
                                    else " on every GPU, each rank its own files)") if world > 1 else ")"),
                    "files_per_step": a.files, "files_per_gpu": nf, "file_bytes": fbytes,
                    "md5_slice_blocks": B, "pipeline_depth": R, "launches_per_batch": need,
-                   "scan_lead": lead, "join_lag": lag, "k3_waves_per_simd": a.k3_waves,
+                   "scan_lead": lead, "join_lag": lag,
                    "parallelism": f"file-sharded x{world} ({a.scaling} scaling; independent HIP streams, "
                                   "no data-path collective)",
                    "seeds": f"each rank generates its own share on its device: random arenas seed {a.seed} + "

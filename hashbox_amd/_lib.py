@@ -24,7 +24,7 @@ EXPORTS = [
     "hbx_last_error", "hbx_chunk_hash", "hbx_chunk_hash_batch", "hbx_chunk_hash_device",
     "hbx_submit_device", "hbx_wait", "hbx_store_paths", "hbx_block_id", "hbx_arena_alloc", "hbx_arena_free",
     "hbx_memcpy_h2d", "hbx_memcpy_h2d_async", "hbx_alloc_pinned", "hbx_free_pinned", "hbx_stage_times",
-    "hbx_set_tile_iters", "hbx_pending", "hbx_set_md5_slice", "hbx_set_k3_waves", "hbx_stage_totals", "hbx_io_times",
+    "hbx_set_tile_iters", "hbx_pending", "hbx_set_md5_slice", "hbx_stage_totals", "hbx_io_times",
     "hbx_reserve", "hbx_verify_blocks", "hbx_verify_blocks_device",
     "hbx_file_entry_size", "hbx_file_entry_serialize", "hbx_file_entry_parse",
     "hbx_chain_block_serialize", "hbx_chain_block_parse", "hbx_directory_block_size",
@@ -124,7 +124,6 @@ def load() -> ctypes.CDLL:
     L.hbx_set_tile_iters.argtypes = [P, ctypes.c_uint32]
     L.hbx_pending.argtypes = [P]
     L.hbx_set_md5_slice.argtypes = [P, ctypes.c_uint32]
-    L.hbx_set_k3_waves.argtypes = [P, ctypes.c_uint32]
     L.hbx_set_join_lag.argtypes = [P, ctypes.c_uint32]
     L.hbx_input_after_oldest.argtypes = [P]
     L.hbx_input_fence.argtypes = [P, P]

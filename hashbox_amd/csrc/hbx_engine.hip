@@ -180,22 +180,12 @@ struct hbx_ctx {
   // 16 so that its K1 spreads evenly over the CUs K3 leaves
   uint32_t tile_iters = 0;
   uint32_t join_lag = 1;      // hbx_set_join_lag
-  // where and when K2c plans run (plan_mode_of): 0 on the scan stream, by
-  // the submit that launches; 1 the same on the hash stream; 2 on the scan
-  // stream one launch ahead (preplan).  -1 = 2 at join lag >= 2, else 0
-  // (HBX_PLAN_MODE for A/B).
-  int plan_mode = -1;
+  // where and when K2c plans run follows from the join lag (plan_mode_of)
   bool preplanned = false;    // the plan of launch `launches` is enqueued (mode 2)
   Batch* pre_nb = nullptr;    // the batch whose chains that plan adds
   uint32_t k4_window = 1024;  // K4's LDS window of ids (HBX_K4_WINDOW, 1..1024: tests)
   int k2_own = -1;            // ensure_cut_stream: -1 = by join lag (HBX_K2_STREAM for A/B)
   uint32_t md5_wgs = 256;     // K3 grid: one 256-thread workgroup per CU (set from the device)
-  // K3 wave placement: 1 packs the busy waves into the fewest CUs (4 per CU,
-  // one per SIMD), leaving whole CUs to the next batch's K1 (measured 1510 vs
-  // 1255 GiB/s spread, 100 steps); 0 spreads them one per CU first
-  uint32_t k3_dense = 1;
-  uint32_t k1_run = 64;       // K1 bytes per thread per iteration: 64 (1024 threads) or 128 (512, K1b)
-  uint32_t k3_threads = 256;  // K3 workgroup: 256 = one wave per SIMD (hbx_k3_block_md5), 512 = two (_w2)
   uint32_t md5_slice = 16384; // K3 time slice: full MD5 blocks per chain per launch (0 = unlimited)
   // K1 gate (hbx_k1_gate): a batch's K1 waits until every workgroup of the K3
   // launch of the same submit has been dispatched.  k3_started counts K3
@@ -208,7 +198,7 @@ struct hbx_ctx {
   // batch's own ev[0] | ev[1] | ev[5], K2 zeroes K2r's counter, the plan's
   // timing end event is what K3 waits on, and the plan bins are zeroed
   // after each plan (off the loop) instead of before it.
-  uint32_t lean_marks = 1;  // 0 off, 1 records, 2 records riding on K1/K2 (hipExtLaunchKernel)
+  uint32_t lean_marks = 1;  // 0 off (the old schedule, A/B), 1 on
   hipStream_t plan_zeroed_on = nullptr;  // stream whose last op leaves d_plan zeroed (lean)
   TimedLaunch plan_timer[3];             // lean: the plan's timing pair, queued once K3 waits on it
   bool plan_timer_set[3] = {false, false, false};
@@ -231,7 +221,7 @@ struct hbx_ctx {
   // started) and d_gate[1] (waves ended).  Harvested once a launch is known
   // complete (k3_done_upto: launches [0, k3_done_upto) are).
   PinBuf h_k3t;
-  PinBuf h_probe;  // HBX_K3_PROBE: per-wave times of the latest K3 launch (hbx_k3_wave_times)
+  PinBuf h_probe;  // hbx_set_k3_probe: per-wave times of the latest K3 launch (hbx_k3_wave_times)
   uint32_t k3_waves = 0;
   std::deque<uint64_t> k3_open;
   uint64_t k3_done_upto = 0;
@@ -487,7 +477,6 @@ int ensure_plan_buffers(hbx_ctx* c, uint64_t extra);
 //   schedule would make K1 j wait for K2 of batch j-1 (measured 1,575 GiB/s at
 //   8 files per GPU, vs 1,890 for mode 1).
 int plan_mode_of(const hbx_ctx* c) {
-  if (c->plan_mode >= 0) return c->plan_mode;
   return c->join_lag >= 3 ? 2 : c->join_lag == 2 ? 1 : 0;
 }
 hipStream_t plan_stream(const hbx_ctx* c) { return plan_mode_of(c) == 1 ? c->hstream : c->stream; }
@@ -625,11 +614,10 @@ int md5_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
     tslot[0] = tslot[1] = 0;
     c->k3_open.push_back(L);
   }
-  const uint32_t waves = c->md5_wgs * (c->k3_threads / 64);
-  hipLaunchKernelGGL(c->k3_threads == (uint32_t)kK3Threads2 ? hbx_k3_block_md5_w2 : hbx_k3_block_md5,
-                     dim3(c->md5_wgs), dim3(c->k3_threads), 0, s,
+  const uint32_t waves = c->md5_wgs * (kK3Threads / 64);
+  hipLaunchKernelGGL(hbx_k3_block_md5, dim3(c->md5_wgs), dim3(kK3Threads), 0, s,
                      c->d_order[slot].as<OrderEntry>(), static_cast<const uint32_t*>(c->d_octl[slot].as<uint32_t>()),
-                     budget, c->k3_dense, c->d_gate.as<uint32_t>(), c->k3_dispatched, c->k3_waves + waves - 1u, tslot,
+                     budget, c->d_gate.as<uint32_t>(), c->k3_dispatched, c->k3_waves + waves - 1u, tslot,
                      c->h_probe.p ? c->h_probe.as<uint64_t>() : nullptr);
   HBX_TRY(c, hipGetLastError());
   c->k3_dispatched += c->md5_wgs;
@@ -910,44 +898,27 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   // after its collect, long after both completed)
   hipStream_t s2 = c->cstream;
   const bool lean = c->lean_marks && s2 == s;
-  // lean_marks 2: ev[0], ev[1] and ev[5] ride on the K1 and K2 dispatches
-  // themselves (hipExtLaunchKernel's start/stop events), no packet between
-  const bool ext = lean && c->lean_marks >= 2;
-  if (!(ext && nt)) HBX_TRY(c, hipEventRecord(b->ev[0], s));
+  HBX_TRY(c, hipEventRecord(b->ev[0], s));
   if (nt) {
     StageTimer t(c, s, 0, !lean);
-    if (ext && c->k1_run == 128u)
-      hipExtLaunchKernelGGL(hbx_k1_digest_scan_dma2, dim3((uint32_t)nt), dim3(kK1bThreads), 0, s, b->ev[0], b->ev[1],
-                            0u, arena, d_off, d_len, d_sb, d_tiles, ssum.as<uint2>(), slices);
-    else if (ext)
-      hipExtLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3((uint32_t)nt), dim3(kK1Threads), 0, s, b->ev[0], b->ev[1],
-                            0u, arena, d_off, d_len, d_sb, d_tiles, ssum.as<uint2>(), slices);
-    else if (c->k1_run == 128u)
-      hipLaunchKernelGGL(hbx_k1_digest_scan_dma2, dim3((uint32_t)nt), dim3(kK1bThreads), 0, s, arena, d_off, d_len,
-                         d_sb, d_tiles, ssum.as<uint2>(), slices);
-    else
-      hipLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3((uint32_t)nt), dim3(kK1Threads), 0, s, arena, d_off, d_len,
-                         d_sb, d_tiles, ssum.as<uint2>(), slices);
+    hipLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3((uint32_t)nt), dim3(kK1Threads), 0, s, arena, d_off, d_len,
+                       d_sb, d_tiles, ssum.as<uint2>(), slices);
   }
   HBX_TRY(c, hipGetLastError());
-  if (!(ext && nt)) HBX_TRY(c, hipEventRecord(b->ev[1], s));
+  HBX_TRY(c, hipEventRecord(b->ev[1], s));
   if (lean && nt) c->open_t.push_back(TimedLaunch{b->ev[0], b->ev[1], 0, false});
   // K2 on the cut stream: the scan stream goes straight on with the next
   // batch's K1 (into the other summary slot)
   if (s2 != s) HBX_TRY(c, hipStreamWaitEvent(s2, b->ev[1], 0));
   {
     StageTimer t(c, s2, 1, !lean);
-    if (ext)
-      hipExtLaunchKernelGGL(hbx_k2_cut_chain, dim3((uint32_t)n), dim3(64), 0, s2, nullptr, b->ev[5], 0u, arena, d_off,
-                            d_len, d_sb, ssum.as<const uint2>(), d_cb, b->cuts_d(), b->count_d(), b->d_fcnt.as<uint32_t>());
-    else
-      hipLaunchKernelGGL(hbx_k2_cut_chain, dim3((uint32_t)n), dim3(64), 0, s2, arena, d_off, d_len,
-                         d_sb, ssum.as<uint2>(), d_cb, b->cuts_d(), b->count_d(),
-                         lean ? b->d_fcnt.as<uint32_t>() : nullptr);
+    hipLaunchKernelGGL(hbx_k2_cut_chain, dim3((uint32_t)n), dim3(64), 0, s2, arena, d_off, d_len,
+                       d_sb, ssum.as<uint2>(), d_cb, b->cuts_d(), b->count_d(),
+                       lean ? b->d_fcnt.as<uint32_t>() : nullptr);
   }
   HBX_TRY(c, hipGetLastError());
   if (lean) {  // the summary slot's next writer (K1, this stream) follows in order: no ssum_free
-    if (!ext) HBX_TRY(c, hipEventRecord(b->ev[5], s2));
+    HBX_TRY(c, hipEventRecord(b->ev[5], s2));
     c->open_t.push_back(TimedLaunch{b->ev[1], b->ev[5], 1, false});
   } else {
     HBX_TRY(c, hipEventRecord(c->ssum_free[slot], s2));
@@ -1213,35 +1184,24 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   int ncu = 0;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->md5_wgs = (uint32_t)(ncu = prop.multiProcessorCount);
-  if (const char* v = ab_env("HBX_MD5_WGS")) c->md5_wgs = (uint32_t)std::max(1, std::atoi(v));
-  if (const char* v = ab_env("HBX_K3_DENSE")) c->k3_dense = std::atoi(v) ? 1u : 0u;
-  if (const char* v = ab_env("HBX_K1_RUN")) c->k1_run = std::atoi(v) == 128 ? 128u : 64u;
-  if (const char* v = ab_env("HBX_K3_WAVES")) c->k3_threads = std::atoi(v) == 2 ? kK3Threads2 : kK3Threads;
   if (const char* v = ab_env("HBX_TILE_ITERS")) c->tile_iters = (uint32_t)std::min(1024, std::max(0, std::atoi(v)));
   if (const char* v = ab_env("HBX_JOIN_LAG")) c->join_lag = (uint32_t)std::min(4, std::max(1, std::atoi(v)));
   if (const char* v = ab_env("HBX_K4_WINDOW")) c->k4_window = (uint32_t)std::min(1024, std::max(1, std::atoi(v)));
-  if (const char* v = ab_env("HBX_PLAN_MODE")) c->plan_mode = std::min(2, std::max(0, std::atoi(v)));
   if (const char* v = ab_env("HBX_MD5_SLICE")) c->md5_slice = (uint32_t)std::max(0, std::atoi(v));
   if (const char* v = ab_env("HBX_K1_GATE")) c->k1_gate = std::atoi(v) ? 1u : 0u;
-  if (const char* v = ab_env("HBX_LEAN_MARKS")) c->lean_marks = (uint32_t)std::min(2, std::max(0, std::atoi(v)));
+  if (const char* v = ab_env("HBX_LEAN_MARKS")) c->lean_marks = std::atoi(v) ? 1u : 0u;
   if (hipSetDevice(device) != hipSuccess || make_stream(&c->stream, "HBX_SCAN_CUS", ncu, "0:4096") != hipSuccess) {
     delete c;
     return HBX_ERR_HIP;
   }
-  const char* one = ab_env("HBX_ONE_STREAM");  // A/B: scan, hash and results on one stream
   if (const char* v = ab_env("HBX_K2_STREAM")) c->k2_own = std::atoi(v) ? 1 : 0;
   c->cstream = c->stream;
-  if (one && std::atoi(one)) {
-    c->hstream = c->rstream = c->stream;
-  } else if (make_stream(&c->hstream, "HBX_HASH_CUS", ncu) != hipSuccess ||
+  if (make_stream(&c->hstream, "HBX_HASH_CUS", ncu) != hipSuccess ||
              make_stream(&c->rstream, "HBX_RES_CUS", ncu) != hipSuccess || ensure_cut_stream(c) != HBX_OK) {
     hbx_ctx_destroy(c);
     return HBX_ERR_HIP;
   }
   if (c->h_k3t.ensure(kK3TimeRing * 16) == hipSuccess) std::memset(c->h_k3t.p, 0, kK3TimeRing * 16);
-  if (const char* v = ab_env("HBX_K3_PROBE"))
-    if (std::atoi(v) && c->h_probe.ensure((size_t)c->md5_wgs * (kK3Threads2 / 64) * 32) == hipSuccess)
-      std::memset(c->h_probe.p, 0, (size_t)c->md5_wgs * (kK3Threads2 / 64) * 32);
   if (c->d_gate.ensure(256) != hipSuccess || hipMemset(c->d_gate.p, 0, 256) != hipSuccess ||
       hipEventCreateWithFlags(&c->ssum_free[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ssum_free[1], hipEventDisableTiming) != hipSuccess) {
@@ -1335,12 +1295,11 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
   const char* ab = std::getenv("HBX_AB");
   const int n = std::snprintf(
       out, (size_t)cap,
-      "{\"ab_env\": %d, \"md5_slice\": %u, \"join_lag\": %u, \"tile_iters\": %u, \"k1_run\": %u, "
-      "\"k3_waves\": %u, \"k3_dense\": %u, \"k1_gate\": %u, \"md5_wgs\": %u, \"plan_mode\": %d, "
-      "\"k2_own\": %d, \"k4_window\": %u, \"one_stream\": %d, \"k3_probe\": %d, \"lean_marks\": %u}",
-      (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_run,
-      c->k3_threads == kK3Threads2 ? 2u : 1u, c->k3_dense, c->k1_gate, c->md5_wgs, c->plan_mode, c->k2_own,
-      c->k4_window, c->hstream == c->stream ? 1 : 0, c->h_probe.p ? 1 : 0, c->lean_marks);
+      "{\"ab_env\": %d, \"md5_slice\": %u, \"join_lag\": %u, \"tile_iters\": %u, \"k1_gate\": %u, "
+      "\"md5_wgs\": %u, \"plan_mode\": %d, \"k2_own\": %d, \"k4_window\": %u, \"k3_probe\": %d, "
+      "\"lean_marks\": %u}",
+      (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_gate, c->md5_wgs,
+      plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks);
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }
 
@@ -1355,7 +1314,7 @@ int hbx_set_k3_probe(hbx_ctx* c, int on) {
     c->h_probe.release();
     return HBX_OK;
   }
-  const size_t n = (size_t)c->md5_wgs * (kK3Threads2 / 64) * 32;
+  const size_t n = (size_t)c->md5_wgs * (kK3Threads / 64) * 32;
   HBX_TRY(c, c->h_probe.ensure(n));
   std::memset(c->h_probe.p, 0, n);
   return HBX_OK;
@@ -1368,7 +1327,7 @@ int hbx_k3_wave_times(hbx_ctx* c, uint64_t* out, uint32_t max_waves, uint32_t* n
   if (!c->h_probe.p) return c->fail(HBX_ERR_STATE, "K3 probe not enabled (hbx_set_k3_probe)");
   HBX_TRY(c, hipSetDevice(c->device));
   HBX_TRY(c, hipStreamSynchronize(c->hstream));
-  const uint32_t n = c->md5_wgs * (c->k3_threads / 64);
+  const uint32_t n = c->md5_wgs * (kK3Threads / 64);
   if (out) std::memcpy(out, c->h_probe.p, (size_t)std::min(n, max_waves) * 32);
   *n_waves = n;
   return HBX_OK;
@@ -1389,16 +1348,6 @@ int hbx_set_md5_slice(hbx_ctx* c, uint32_t blocks) {
   // not all hashed
   if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
   c->md5_slice = blocks;
-  return HBX_OK;
-}
-
-int hbx_set_k3_waves(hbx_ctx* c, uint32_t waves_per_simd) {
-  if (!c || (waves_per_simd != 1u && waves_per_simd != 2u)) return HBX_ERR_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
-  // the K1 gate of a pending batch counts the workgroups and waves of the
-  // K3 launch it follows
-  if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
-  c->k3_threads = waves_per_simd == 2u ? kK3Threads2 : kK3Threads;
   return HBX_OK;
 }
 

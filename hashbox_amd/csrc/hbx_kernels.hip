@@ -26,16 +26,7 @@ using namespace hbx;
 namespace {
 
 // ------------------------------------------------------------------ K1 --
-constexpr int kK1Threads = 1024;
-#ifndef HBX_K1_SDWA
-#define HBX_K1_SDWA 1
-#endif
-#ifndef HBX_K1_DIAG_NODIGEST
-#define HBX_K1_DIAG_NODIGEST 0
-#endif
-#ifndef HBX_K1_COALESCED
-#define HBX_K1_COALESCED 1
-#endif  // 16 waves; 16 x 4096 B = one MIN window per iteration
+constexpr int kK1Threads = 1024;  // 16 waves; 16 x 4096 B = one MIN window per iteration
 
 // Per-lane in-aggregates of a 64-byte run: half (positions 0..31) and full.
 struct RunAgg {
@@ -61,37 +52,8 @@ __device__ __forceinline__ RunAgg run_aggregates(const uint32_t (&v)[16]) {
   return r;
 }
 
-// Per-position digest pass over one lane's 64 positions, as two packed u16
-// streams: low half = positions 0..31, high half = positions 32..63.
-//   S1 += in - out; s2 += S1; D = s2<<16 | S1; M = max(M, D)
-// TAIL masks positions >= lim (iteration-relative) out of the max.
-template <bool TAIL>
-__device__ __forceinline__ uint32_t digest_pass(const uint32_t (&in)[16], const uint32_t (&out)[16],
-                                                uint32_t S1p, uint32_t S2p, uint32_t e_l,
-                                                uint32_t lim) {
-  u16x2 s1 = as_u16x2(S1p), s2 = as_u16x2(S2p);
-  uint32_t M = 0;
-#pragma unroll
-  for (int j = 0; j < 32; j++) {
-    const int k = j >> 2, b = j & 3;
-    const uint32_t sel = (uint32_t)(4 + b) | (0x0cu << 8) | ((uint32_t)b << 16) | (0x0cu << 24);
-    const u16x2 pin = as_u16x2(__builtin_amdgcn_perm(in[k], in[8 + k], sel));
-    const u16x2 pout = as_u16x2(__builtin_amdgcn_perm(out[k], out[8 + k], sel));
-    s1 = s1 + pin;
-    s1 = s1 - pout;
-    s2 = s2 + s1;
-    uint32_t DA = __builtin_amdgcn_perm(as_u32(s2), as_u32(s1), 0x05040100u);
-    uint32_t DB = __builtin_amdgcn_perm(as_u32(s2), as_u32(s1), 0x07060302u);
-    if (TAIL) {
-      DA = (e_l + (uint32_t)j < lim) ? DA : 0u;
-      DB = (e_l + 32u + (uint32_t)j < lim) ? DB : 0u;
-    }
-    M = max(M, max(DA, DB));
-  }
-  return M;
-}
-
-// Same pass with the digest kept as ONE register per stream, X = s2<<16 | s1:
+// The digest pass over one lane's 64 positions, with the digest kept as ONE
+// register per stream, X = s2<<16 | s1:
 //   X.lo += in_byte; X.lo -= out_byte   (SDWA: 16-bit result, high half kept)
 //   X += X << 16                        (s2 += s1, mod 2^16, low half kept)
 // so X IS the digest — 3 VALU per position instead of ~4.25 + hazard nops.
@@ -215,34 +177,15 @@ __device__ __forceinline__ void k1_iteration(const uint32_t (&cur)[16], const ui
   const uint32_t A_pre2 = A_pre + A_hA, C_pre2 = C_pre + e_l * A_hA + J_hA;
   const uint32_t S1_b = st.S1c + A_pre2;
   const uint32_t s2_b = st.s2c + (e_l + 32u) * S1_b - C_pre2;
-  const uint32_t S1p = (S1_t & 0xffffu) | (S1_b << 16);
-  const uint32_t S2p = (s2_t & 0xffffu) | (s2_b << 16);
   sprev = readlane((s2_t << 16) | (S1_t & 0xffffu), 0);
 
   uint32_t M;
-#if HBX_K1_DIAG_NODIGEST
-  // diagnostic build only (tools/gpu_k1_intensity.sh): K1 without its digest
-  // loop (~70 % of its VALU; the maxima are wrong), to measure how much K1's
-  // VALU work, as opposed to its memory traffic, slows K3 beside it
-  M = (s2_t << 16) ^ S1_t ^ s2_b ^ S1_b ^ cur[l & 15u] ^ out[(l + 1u) & 15u];
-  (void)S1p;
-  (void)S2p;
-#elif HBX_K1_SDWA
   const uint32_t XA = (s2_t << 16) | (S1_t & 0xffffu), XB = (s2_b << 16) | (S1_b & 0xffffu);
   if (qs + kMinBlock <= N) {
     M = digest_pass_sdwa<false>(cur, out, XA, XB, e_l, 0u);
   } else {
     M = digest_pass_sdwa<true>(cur, out, XA, XB, e_l, (uint32_t)(N - qs));
   }
-  (void)S1p;
-  (void)S2p;
-#else
-  if (qs + kMinBlock <= N) {
-    M = digest_pass<false>(cur, out, S1p, S2p, e_l, 0u);
-  } else {
-    M = digest_pass<true>(cur, out, S1p, S2p, e_l, (uint32_t)(N - qs));
-  }
-#endif
   smax = readlane(wave_max_to_lane63(M), 63);
 
   st.S1c += totA;
@@ -334,15 +277,14 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_d
   const s32x4 srd = make_srd(fb + q0, nbytes);
   const uint32_t lds0 = (uint32_t)(uintptr_t)&land[w][0][0];
   const uint32_t lds1 = (uint32_t)(uintptr_t)&land[w][1][0];
-  // HBX_K1_COALESCED: each DMA instruction reads 1 KiB contiguous (lane l:
-  // bytes 16l..16l+15 of the piece) so the LDS slot holds the wave's 4 KiB in
-  // file order; the per-lane 64-byte reads then take a 4-way bank conflict.
-  // Otherwise lane l of piece k reads bytes 16k.. of its own run (strided
-  // global access, conflict-free LDS reads).
+  // Each DMA instruction reads 1 KiB contiguous (lane l: bytes 16l..16l+15
+  // of the piece), so the LDS slot holds the wave's 4 KiB in file order; the
+  // per-lane 64-byte reads then take a 4-way bank conflict (a lane reading
+  // bytes 16k.. of its own run instead makes the global access strided).
   auto issue = [&](uint32_t it, uint32_t lds) {  // 4 DMA ops, always issued
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      const uint32_t voff = HBX_K1_COALESCED ? (w * kSlice + 1024u * k + 16u * l) : (e_l + 16u * k);
+      const uint32_t voff = w * kSlice + 1024u * k + 16u * l;
       dma16(srd, voff, it * kMinBlock, lds + 1024u * k);
     }
   };
@@ -350,7 +292,7 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_d
     const u32x4* p = reinterpret_cast<const u32x4*>(&land[w][slot][0]);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      const u32x4 t = HBX_K1_COALESCED ? p[4 * l + k] : p[64 * k + l];
+      const u32x4 t = p[4 * l + k];
       v[4 * k + 0] = t.x;
       v[4 * k + 1] = t.y;
       v[4 * k + 2] = t.z;
@@ -386,241 +328,6 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_d
     k1_iteration(cur, prev, st, wtot, it, w, l, e_l, qs, N, smax, sprev);
     const bool ok = qs + (uint64_t)w * kSlice < N;
     k1_store_slice(ssum, ok ? sb + ((qs >> kSliceShift) + w) : dummy, l, smax, sprev);
-  };
-  for (uint32_t it = 0; it < n_it; it += 2u) {
-    step(it, run_b, out);
-    if (it + 1u < n_it) step(it + 1u, out, run_b);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup exits
-}
-
-// ------------------------------------------- K1b (128-byte runs, LDS-DMA) --
-// The same scan with half the per-byte overhead: 512 threads (8 waves, two
-// per SIMD), each owning 128 contiguous positions of a 64 KiB iteration, so
-// the run aggregates, the two wave scans, the cross-wave exchange, the
-// barrier and the slice maxima are paid once per 128 positions instead of 64
-// (K1's digest loop is 3.5 VALU per position, the rest was ~1.6 per byte;
-// the path is VALU-issue-bound, DESIGN.md §6 "The bound").  A wave covers two
-// slices (lanes 0-31, 32-63).  Four digest streams per lane (positions 0-31,
-// 32-63, 64-95, 96-127).  The wave's 8 KiB land in LDS by DMA in a swizzled
-// image: DMA op k fetches lane rows 8k..8k+7 (1 KiB contiguous in the file),
-// and row r's granule g sits at column g ^ ((r >> 1) & 7), so each lane's
-// ds_read_b128 of its own row is bank-conflict-free (every 16-lane group of
-// ds_read_b128 hits 16 distinct 4-bank columns; MI355X_MICROARCH.md LDS).
-constexpr int kK1bThreads = 512;
-constexpr uint32_t kK1bSlot = 8192;  // bytes per wave per iteration
-
-struct RunAgg4 {
-  uint32_t a[4], j[4];  // in-aggregates of positions [0, 32(s+1)) of the run
-};
-__device__ __forceinline__ RunAgg4 run_aggregates128(const uint32_t (&v)[32]) {
-  RunAgg4 r;
-  uint32_t a = 0, j = 0;
-#pragma unroll
-  for (int s = 0; s < 4; s++) {
-#pragma unroll
-    for (int k = 8 * s; k < 8 * s + 8; k++) {
-      a = dot4(v[k], 0x01010101u, a);
-      j = dot4(v[k], jw(k), j);
-    }
-    r.a[s] = a;
-    r.j[s] = j;
-  }
-  return r;
-}
-
-template <bool TAIL>
-__device__ __forceinline__ uint32_t digest_pass128(const uint32_t (&in)[32], const uint32_t (&out)[32],
-                                                   uint32_t (&X)[4], uint32_t e_l, uint32_t lim) {
-  uint32_t M = 0;
-  if (!TAIL) {
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      HBX_SDWA_DWORD(X[0], X[1], M, in[k], out[k], in[8 + k], out[8 + k]);
-      HBX_SDWA_DWORD(X[2], X[3], M, in[16 + k], out[16 + k], in[24 + k], out[24 + k]);
-    }
-    return M;
-  }
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-#define HBX_SDWA_PAIR4(B)                                                            \
-    {                                                                                \
-      HBX_SDWA_STEP(X[0], in[k], out[k], B);                                         \
-      HBX_SDWA_STEP(X[1], in[8 + k], out[8 + k], B);                                 \
-      HBX_SDWA_STEP(X[2], in[16 + k], out[16 + k], B);                               \
-      HBX_SDWA_STEP(X[3], in[24 + k], out[24 + k], B);                               \
-      const uint32_t p = e_l + 4u * k + B;                                           \
-      const uint32_t D0 = p < lim ? X[0] : 0u, D1 = p + 32u < lim ? X[1] : 0u;       \
-      const uint32_t D2 = p + 64u < lim ? X[2] : 0u, D3 = p + 96u < lim ? X[3] : 0u; \
-      asm("v_max3_u32 %0, %0, %1, %2" : "+v"(M) : "v"(D0), "v"(D1));                \
-      asm("v_max3_u32 %0, %0, %1, %2" : "+v"(M) : "v"(D2), "v"(D3));                \
-    }
-    HBX_SDWA_PAIR4(0) HBX_SDWA_PAIR4(1) HBX_SDWA_PAIR4(2) HBX_SDWA_PAIR4(3)
-#undef HBX_SDWA_PAIR4
-  }
-  return M;
-}
-
-struct K1bState {
-  uint32_t S1c, s2c;  // state before the iteration's first position
-  RunAgg4 pa;         // in-aggregates of the previous run (= this run's "out")
-};
-
-// Half-wave max: lane 31 = max of lanes 0-31, lane 63 = max of lanes 32-63.
-__device__ __forceinline__ uint32_t half_max_to_31_63(uint32_t x) {
-  x = max(x, dpp<kRowShr1>(x));
-  x = max(x, dpp<kRowShr2>(x));
-  x = max(x, dpp<kRowShr4>(x));
-  x = max(x, dpp<kRowShr8>(x));
-  x = max(x, dpp<kRowBcast15, 0xa>(x));
-  return x;
-}
-
-extern "C" __global__ __launch_bounds__(kK1bThreads, 2) void hbx_k1_digest_scan_dma2(
-    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
-    const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ slice_base,
-    const uint4* __restrict__ tiles, uint2* __restrict__ ssum, uint64_t dummy) {
-  constexpr uint32_t W = kK1bThreads / 64;
-  __shared__ uint2 wtot[2][W];
-  __shared__ __attribute__((aligned(1024))) uint8_t land[W][2][kK1bSlot];
-  const uint4 td = tiles[blockIdx.x];
-  const uint32_t f = td.x;
-  const uint64_t N = file_len[f];
-  const uint64_t q0 = (uint64_t)td.y * kMinBlock;
-  const uint32_t tile_iters = td.z;
-  const uint8_t* fb = arena + file_off[f];
-  const uint64_t sb = slice_base[f];
-
-  const uint32_t tid = threadIdx.x;
-  const uint32_t l = tid & 63u;
-  const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
-  const uint32_t e_l = w * kK1bSlot + l * 128u;
-
-  const uint64_t rem = N - q0;
-  const uint32_t n_it = (uint32_t)umin64(tile_iters, (rem + kMinBlock - 1) / kMinBlock);
-  const uint32_t nbytes = (uint32_t)((umin64(rem, (uint64_t)n_it * kMinBlock) + 15ull) & ~15ull);
-  const s32x4 srd = make_srd(fb + q0, nbytes);
-  const uint32_t lds0 = (uint32_t)(uintptr_t)&land[w][0][0];
-  const uint32_t lds1 = (uint32_t)(uintptr_t)&land[w][1][0];
-  // DMA op k, lane i: row r = 8k + i/8 of the wave, column i%8 holds granule
-  // (i%8) ^ ((r>>1)&7); the offsets do not depend on the iteration
-  uint32_t voff[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const uint32_t r = 8u * (uint32_t)k + (l >> 3);
-    voff[k] = w * kK1bSlot + r * 128u + 16u * ((l & 7u) ^ ((r >> 1) & 7u));
-  }
-  auto issue = [&](uint32_t it, uint32_t lds) {  // 8 DMA ops, always issued
-#pragma unroll
-    for (int k = 0; k < 8; k++) dma16(srd, voff[k], it * kMinBlock, lds + 1024u * k);
-  };
-  const uint32_t xr = (l >> 1) & 7u;  // this lane's row swizzle
-  auto land_read = [&](uint32_t slot, uint32_t (&v)[32]) {
-    const uint8_t* row = &land[w][slot][l * 128u];
-#pragma unroll
-    for (int g = 0; g < 8; g++) {
-      const u32x4 t = *reinterpret_cast<const u32x4*>(row + 16u * ((uint32_t)g ^ xr));
-      v[4 * g + 0] = t.x;
-      v[4 * g + 1] = t.y;
-      v[4 * g + 2] = t.z;
-      v[4 * g + 3] = t.w;
-    }
-  };
-
-  uint32_t out[32];
-#pragma unroll
-  for (int k = 0; k < 32; k++) out[k] = 0u;
-  K1bState st;
-  if (q0 != 0) {  // prime: the state at q0-1 from the MIN bytes before q0
-    const __amdgpu_buffer_rsrc_t rh = make_rsrc_u(fb + q0 - kMinBlock, kMinBlock);
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const u32x4 t = bload16(rh, e_l + 16u * k, 0u);
-      out[4 * k + 0] = t.x;
-      out[4 * k + 1] = t.y;
-      out[4 * k + 2] = t.z;
-      out[4 * k + 3] = t.w;
-    }
-    st.pa = run_aggregates128(out);
-    const uint32_t iA = wave_incl_sum(st.pa.a[3]);
-    const uint32_t iC = wave_incl_sum(e_l * st.pa.a[3] + st.pa.j[3]);
-    if (l == 63u) wtot[1][w] = make_uint2(iA, iC);
-    __syncthreads();
-    const uint2 t = (l < W) ? wtot[1][l] : make_uint2(0u, 0u);
-    const uint32_t sA = row_incl_sum(t.x), sC = row_incl_sum(t.y);
-    st.S1c = readlane(sA, 15);
-    st.s2c = 0x8000u - readlane(sC, 15);  // virtual-zero start: s2 = 2^15 - sum k*x_k
-  } else {
-#pragma unroll
-    for (int s = 0; s < 4; s++) st.pa.a[s] = st.pa.j[s] = 0u;
-    st.S1c = 0u;
-    st.s2c = 0x8000u;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-  issue(0u, lds0);
-  issue(1u, lds1);  // past the tile end: out-of-range reads land zeros, never read
-  uint32_t run_b[32];
-  auto step = [&](uint32_t it, uint32_t (&cur)[32], const uint32_t (&prev)[32]) {
-    // outstanding, oldest first: DMA(it) x8, store(it-2), DMA(it+1) x8, store(it-1)
-    if (it == 0)
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (it == 1)
-      asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-    land_read(it & 1u, cur);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot consumed before it is refilled
-    issue(it + 2u, (it & 1u) ? lds1 : lds0);
-    const uint64_t qs = q0 + (uint64_t)it * kMinBlock;
-    // --- one iteration (k1_iteration with four streams per lane)
-    const RunAgg4 ca = run_aggregates128(cur);
-    uint32_t Ac[4], Jc[4];
-#pragma unroll
-    for (int s = 0; s < 4; s++) {
-      Ac[s] = ca.a[s] - st.pa.a[s];
-      Jc[s] = ca.j[s] - st.pa.j[s];
-    }
-    const uint32_t A_l = Ac[3], C_l = e_l * Ac[3] + Jc[3];
-    const uint32_t iA = wave_incl_sum(A_l);
-    const uint32_t iC = wave_incl_sum(C_l);
-    if (l == 63u) wtot[it & 1u][w] = make_uint2(iA, iC);
-    __syncthreads();
-    const uint2 t = (l < W) ? wtot[it & 1u][l] : make_uint2(0u, 0u);
-    const uint32_t sA = row_incl_sum(t.x), sC = row_incl_sum(t.y);
-    const uint32_t WA = w ? readlane(sA, (int)w - 1) : 0u;
-    const uint32_t WC = w ? readlane(sC, (int)w - 1) : 0u;
-    const uint32_t totA = readlane(sA, 15), totC = readlane(sC, 15);
-    const uint32_t A_pre = WA + (iA - A_l), C_pre = WC + (iC - C_l);
-    uint32_t X[4];
-#pragma unroll
-    for (int s = 0; s < 4; s++) {
-      const uint32_t Ap = A_pre + (s ? Ac[s - 1] : 0u);
-      const uint32_t Cp = C_pre + (s ? e_l * Ac[s - 1] + Jc[s - 1] : 0u);
-      const uint32_t S1 = st.S1c + Ap;
-      const uint32_t s2 = st.s2c + (e_l + 32u * (uint32_t)s) * S1 - Cp;
-      X[s] = (s2 << 16) | (S1 & 0xffffu);
-    }
-    const uint32_t sprev0 = readlane(X[0], 0), sprev1 = readlane(X[0], 32);
-    uint32_t M;
-    if (qs + kMinBlock <= N) {
-      M = digest_pass128<false>(cur, prev, X, e_l, 0u);
-    } else {
-      M = digest_pass128<true>(cur, prev, X, e_l, (uint32_t)(N - qs));
-    }
-    const uint32_t hm = half_max_to_31_63(M);
-    const uint32_t smax0 = readlane(hm, 31), smax1 = readlane(hm, 63);
-    st.S1c += totA;
-    st.s2c -= totC;  // 65536*(...) vanishes mod 2^16
-    st.pa = ca;
-    // slice summaries of the wave's two slices: ONE store instruction (lanes
-    // 0-3), always issued (slices past the file end go to the dummy slot)
-    const uint64_t sl = (qs >> kSliceShift) + 2u * w + (l >> 1);
-    const bool ok = (sl << kSliceShift) < N;
-    if (l < 4u) {
-      const uint32_t v = (l == 0u) ? smax0 : (l == 1u) ? sprev0 : (l == 2u) ? smax1 : sprev1;
-      reinterpret_cast<uint32_t*>(ssum + (ok ? sb + sl : dummy))[l & 1u] = v;
-    }
   };
   for (uint32_t it = 0; it < n_it; it += 2u) {
     step(it, run_b, out);
@@ -775,9 +482,6 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k2_cut_chain(
 }
 
 // -------------------------------------------------------------- MD5 -----
-#ifndef HBX_MD5_XAD
-#define HBX_MD5_XAD 1
-#endif
 namespace {
 
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int s) {
@@ -785,7 +489,6 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, int s) {
 }
 #define HBX_F(b, c, d) ((((c) ^ (d)) & (b)) ^ (d))
 #define HBX_G(b, c, d) ((((b) ^ (c)) & (d)) ^ (c))
-#define HBX_H(b, c, d) __builtin_amdgcn_bitop3_b32((b), (c), (d), 0x96)  // b ^ c ^ d in one op
 #define HBX_I(b, c, d) ((c) ^ ((b) | ~(d)))
 #define HBX_STEP(FN, a, b, c, d, x, t, s) a = (b) + rotl((a) + (FN(b, c, d)) + (x) + (t), s)
 // A step's critical path is the chain through b (the previous step's result):
@@ -804,15 +507,11 @@ __device__ __forceinline__ uint32_t xad(uint32_t b, uint32_t cd, uint32_t t1) { 
   asm("v_xad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(cd), "v"(t1));
   return r;
 }
-#if HBX_MD5_XAD
 #define HBX_STEP_H(a, b, c, d, x, t, s)                    \
   {                                                        \
     const uint32_t cd_ = xor_offpath(c, d);                \
     a = (b) + rotl(xad((b), cd_, (a) + (x) + (t)), s);     \
   }
-#else
-#define HBX_STEP_H(a, b, c, d, x, t, s) HBX_STEP(HBX_H, a, b, c, d, x, t, s)
-#endif
 
 __device__ __forceinline__ void md5_compress(uint32_t (&h)[4], const uint32_t (&m)[16]) {
   uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
@@ -924,15 +623,6 @@ __device__ void md5_tail(const uint8_t* c, uint32_t len, uint32_t (&h)[4], bool 
 #ifndef HBX_MD5_RING
 #define HBX_MD5_RING 8
 #endif
-// 1: load each block's 16 message words straight from their (unaligned) byte
-// address instead of aligned dwords + 16 v_alignbyte per block
-#ifndef HBX_MD5_UNALIGNED
-#define HBX_MD5_UNALIGNED 0
-#endif
-// 1: chunk bytes are loaded nontemporal (measured slower: 99 vs 88 ms per batch)
-#ifndef HBX_MD5_NT
-#define HBX_MD5_NT 0
-#endif
 // Chunk bytes are read through explicit global (address space 1) pointers.
 // A pointer rebuilt from an integer address is generic to the compiler, and a
 // generic (flat) load counts against lgkmcnt as well as vmcnt: every wait for
@@ -942,13 +632,8 @@ typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
 __device__ __forceinline__ g_u32* gptr32(const void* p) { return (g_u32*)(uintptr_t)p; }
 __device__ __forceinline__ g_u32x4* gptr128(uint64_t a) { return (g_u32x4*)a; }
 
-__device__ __forceinline__ u32x4 md5_load(g_u32x4* p) {
-#if HBX_MD5_NT
-  return __builtin_nontemporal_load(p);
-#else
-  return *p;
-#endif
-}
+// (Nontemporal loads measured slower: 99 vs 88 ms per batch.)
+__device__ __forceinline__ u32x4 md5_load(g_u32x4* p) { return *p; }
 template <int RING = HBX_MD5_RING>  // blocks of prefetch (16 VGPRs each)
 __device__ void md5_run(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32_t b0, uint32_t cnt,
                         bool finish) {
@@ -971,15 +656,7 @@ __device__ void md5_run(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32
     c0 = va[16u * b0 - 2u];
     c1 = va[16u * b0 - 1u];
   }
-#if HBX_MD5_UNALIGNED
-  // message block b >= 1 = data bytes [64b-8, 64b+56); block 0 loads data
-  // bytes [0, 64) and shifts by two words (its first two are the framing)
-  auto blk_src = [&](uint32_t b) {
-    return gptr128(reinterpret_cast<uint64_t>(b ? c + 64u * b - 8u : c));
-  };
-#else
   auto blk_src = [&](uint32_t b) { return reinterpret_cast<g_u32x4*>(va + 16u * b); };
-#endif
   u32x4 ring[RING][4];
 #pragma unroll
   for (int r = 0; r < RING; r++) {
@@ -997,17 +674,6 @@ __device__ void md5_run(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32
       R[4 * q + 3] = ring[r][q].w;
     }
     uint32_t m[16];
-#if HBX_MD5_UNALIGNED
-#pragma unroll
-    for (int j = 0; j < 16; j++) m[j] = R[j];
-    if (i == 0u && any_first) {  // wave-uniform; block 0 carries the framing
-      const bool f = b0 == 0u;
-#pragma unroll
-      for (int j = 15; j >= 2; j--) m[j] = f ? R[j - 2] : R[j];
-      m[0] = f ? 0u : R[0];
-      m[1] = f ? bswap32(len) : R[1];
-    }
-#else
     // message word j = data word 16b+j-2 = bytes of R[16b+j-2], R[16b+j-1]
     m[0] = alignbyte(c1, c0, sh);
     m[1] = alignbyte(R[0], c1, sh);
@@ -1019,19 +685,11 @@ __device__ void md5_run(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32
     }
     c0 = R[14];
     c1 = R[15];
-#endif
     auto do_refill = [&]() {
       g_u32x4* src = blk_src(min(b0 + i + (uint32_t)RING, last));
 #pragma unroll
       for (int q = 0; q < 4; q++) ring[r][q] = md5_load(src + q);
     };
-#if HBX_MD5_UNALIGNED
-    // the message words ARE the slot's registers: refill once compressed
-    uint32_t t[4] = {h[0], h[1], h[2], h[3]};
-    md5_compress(t, m);
-    __builtin_amdgcn_sched_barrier(0);
-    if (refill) do_refill();
-#else
     // refill only after the slot's registers are consumed (the aligned
     // words feed v_alignbyte): the load then reuses them and the ring needs
     // no copies at the loop back-edge
@@ -1039,7 +697,6 @@ __device__ void md5_run(const uint8_t* c, uint32_t len, uint32_t (&h)[4], uint32
     __builtin_amdgcn_sched_barrier(0);  // keep the refill ahead of this block's compression
     uint32_t t[4] = {h[0], h[1], h[2], h[3]};
     md5_compress(t, m);
-#endif
     const bool live = i < cnt;
 #pragma unroll
     for (int q = 0; q < 4; q++) h[q] = live ? t[q] : h[q];
@@ -1120,9 +777,9 @@ __device__ void md5_block_at(const uint8_t* c, uint32_t len, uint32_t (&h)[4], u
 // staged through registers into LDS rows of 16*G + 16 bytes (conflict-free
 // ds_read_b128 of a lane's own row), two stages resident (the current one and
 // the next); each lane reads its row with 4 aligned ds_read_b128 per block.
-//   G = 16: 4-block stages, 272-B rows, 34 KiB per wave (one wave per SIMD);
-//   G = 8:  2-block stages, 144-B rows, 18 KiB per wave (two waves per SIMD
-//           fit the CU's 160 KiB of LDS).
+//   G = 16: 4-block stages, 272-B rows, 34 KiB per wave (one wave per SIMD).
+// (G = 8, 2-block stages for two waves per SIMD, measured 1.9x slower per
+// launch at the contract's residency: DESIGN.md §5 K3.)
 template <int G>
 struct Coop {
   static constexpr uint32_t C = 64u / G;          // chains per load instruction
@@ -1179,12 +836,11 @@ __device__ __forceinline__ void coop_hash(const uint8_t* wl, uint32_t rd, uint32
   }
 }
 
-// SETS register sets of loads in flight: stages s+1 .. s+SETS while stage s
-// is hashed (2 or 3).
-template <int G, int SETS>
+// Two register sets of loads in flight: stages s+1 and s+2 while stage s is
+// hashed (a third measured no faster).
+template <int G>
 __device__ void md5_coop(uint8_t* wl, const uint8_t* c, uint32_t (&h)[4], uint32_t b1, uint32_t R) {
-  static_assert(G == 8 || G == 16, "stage of 2 or 4 blocks");
-  static_assert(SETS == 2 || SETS == 3, "2 or 3 register sets");
+  static_assert(G == 16, "stage of 4 blocks");
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t S = reinterpret_cast<uint64_t>(c) + 64ull * b1 - 8ull;  // message block b1
   const uint32_t ngr = 4u * R;                                           // granules of R blocks
@@ -1203,225 +859,18 @@ __device__ void md5_coop(uint8_t* wl, const uint8_t* c, uint32_t (&h)[4], uint32
   coop_load<G>(GB, Q, 1u, t, ngr);
   coop_write<G>(wl, wr, 0u, GA);
   coop_load<G>(GA, Q, 2u, t, ngr);
-  if constexpr (SETS == 2) {
-    // start of stage s: stage s+1 (in Gn) into the other half, then Gn's
-    // registers take the loads of stage s+3
-    auto stage = [&](auto half_c, uint32_t s, u32x4(&Gn)[G]) {
-      constexpr uint32_t HALF = decltype(half_c)::value;
-      coop_write<G>(wl, wr, HALF ^ 1u, Gn);
-      coop_load<G>(Gn, Q, min(s + 3u, nst - 1u), t, ngr);
-      coop_hash<G>(wl, rd, HALF, s, R, h);
-    };
-    for (uint32_t s = 0; BPS * s < R; s += 2u) {
-      stage(std::integral_constant<uint32_t, 0>{}, s, GB);
-      stage(std::integral_constant<uint32_t, 1>{}, s + 1u, GA);  // hashes nothing past block R
-    }
-  } else {
-    // the sets rotate statically (unrolled by 3), the LDS half alternates at
-    // run time
-    u32x4 GC[G];
-    coop_load<G>(GC, Q, 3u, t, ngr);  // GA holds stage 2, GB stage 1, stage 0 is in half 0
-    auto stage = [&](uint32_t s, u32x4(&Gn)[G]) {
-      const uint32_t half = s & 1u;
-      coop_write<G>(wl, wr, half ^ 1u, Gn);  // stage s+1
-      coop_load<G>(Gn, Q, min(s + 4u, nst - 1u), t, ngr);
-      coop_hash<G>(wl, rd, half, s, R, h);
-    };
-    for (uint32_t s = 0; BPS * s < R; s += 3u) {
-      stage(s, GB);       // GB: stage s+1
-      stage(s + 1u, GA);  // GA: stage s+2
-      stage(s + 2u, GC);  // GC: stage s+3 (hashes nothing past block R)
-    }
-  }
-}
-
-// ---------------------------------------------- cooperative loads, LDS-DMA --
-// The same page-local streaming with the stage landing in LDS straight from
-// global memory (global_load_lds_dwordx4): no register staging, no
-// ds_write_b128 (the register-staged path's 16 back-to-back wide stores per
-// stage hold its wave ~100 cycles per block; one wave's wide LDS stores run at
-// half rate), and the freed registers hold the next block's words, read one
-// block ahead of its compression.
-//   SB blocks per stage (G = 4 SB granules of 16 B per chain), a ring of D
-//   stages per wave (D x 4 KiB x SB of LDS), DMAs D-1 stages ahead.
-//   DMA instruction q, lane i: chain C q + i / G (C = 64 / G chains per
-//   instruction, 16 G contiguous bytes each), LDS slot i % G of that chain's
-//   row.  A DMA writes its 64 x 16 B lane-linearly, so the rows cannot be
-//   padded; instead chain c's granule k sits in slot (k + rot(c)) mod G, the
-//   rotation chosen so that every 16-lane group of ds_read_b128 (lanes
-//   {0-3,12-15,20-27}, ...: MI355X_MICROARCH.md LDS) hits 16 distinct 16-B
-//   bank columns.  The swizzle goes on the DMA's source address.
-//   Four DMAs share one M0 (the instruction offset applies to both the global
-//   and the LDS address), and the ring is unrolled by D, so a DMA costs no
-//   address arithmetic: the per-instruction pointers advance once per ring.
-#ifndef HBX_K3_DMA
-#define HBX_K3_DMA 0
-#endif
-#ifndef HBX_K3_DMA_SB
-#define HBX_K3_DMA_SB 2
-#endif
-#ifndef HBX_K3_DMA_D
-#define HBX_K3_DMA_D 4
-#endif
-template <int SB, int D>
-struct CoopDma {
-  static_assert(SB == 1 || SB == 2 || SB == 4, "1, 2 or 4 blocks per stage");
-  static_assert(D >= 2 && (D * SB) % 2 == 0, "ring of >= 2 stages, an even number of blocks per ring");
-  static constexpr uint32_t G = 4u * SB;                         // granules per chain per stage
-  static constexpr uint32_t C = 64u / G;                         // chains per DMA instruction
-  static constexpr uint32_t Row = 16u * G;                       // one chain's stage
-  static constexpr uint32_t Stage = 64u * Row;                   // one stage of the wave's chains
-  static constexpr uint32_t WaveLds = (uint32_t)D * Stage;
-  static constexpr uint32_t RotShift = SB == 4 ? 0u : SB == 2 ? 1u : 2u;
-  static_assert(16u * G * (D - 1) + 3072u < 4096u, "instruction offsets fit 12 bits");
-};
-
-template <class F, int... I>
-__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  static_for_impl(f, std::make_integer_sequence<int, N>{});
-}
-
-typedef __attribute__((address_space(1))) void g_void;
-typedef __attribute__((address_space(3))) void l_void;
-template <int OFF>
-__device__ __forceinline__ void glds16(uint64_t g, uint32_t lds) {
-  __builtin_amdgcn_global_load_lds((g_void*)g, (l_void*)(uintptr_t)lds, 16, OFF, 0);
-}
-
-// Stage t into ring slot j, every source clamped to the chain's last granule
-// (prologue and the last rings).  P[q] + 1024 (q % 4) - 16 G pbase is chain
-// (C q + sub)'s stream address + 16 * its granule gq.
-template <int SB, int D, int J>
-__device__ __forceinline__ void dma_clamped(const uint64_t (&P)[CoopDma<SB, D>::G], uint32_t wbase, uint32_t t,
-                                            uint32_t pbase, uint32_t ngr, uint32_t pos, uint32_t sub) {
-  using K = CoopDma<SB, D>;
-#pragma unroll
-  for (int q = 0; q < (int)K::G; q++) {
-    const uint32_t ch = K::C * (uint32_t)q + sub;
-    const uint32_t gq = (pos - (ch >> K::RotShift)) & (K::G - 1u);
-    const uint32_t gi = min(K::G * t + gq, ngr - 1u);
-    const uint64_t a = P[q] + 1024ull * (uint32_t)(q % 4) - 16ull * K::G * pbase - 16ull * gq + 16ull * gi;
-    glds16<0>(a, wbase + (uint32_t)J * K::Stage + 1024u * (uint32_t)q);
-  }
-}
-
-// Stage pbase + J into ring slot J, no clamping: four DMAs per M0, the stage
-// and the instruction's place in its group in the immediate offset.
-template <int SB, int D, int J>
-__device__ __forceinline__ void dma_fast(const uint64_t (&P)[CoopDma<SB, D>::G], uint32_t wbase) {
-  using K = CoopDma<SB, D>;
-  constexpr int adv = (int)(16u * K::G) * J;
-  static_for<(int)K::G>([&](auto qc) {
-    constexpr int q = decltype(qc)::value;
-    glds16<1024 * (q % 4) + adv>(P[q], wbase + (uint32_t)J * K::Stage + 4096u * (uint32_t)(q / 4) - (uint32_t)adv);
-  });
-}
-
-typedef __attribute__((address_space(3))) const u32x4 l_u32x4;
-
-template <int SB, int D>
-__device__ __forceinline__ void md5_coop_dma(uint8_t* wl, const uint8_t* c, uint32_t (&h)[4], uint32_t b1,
-                                             uint32_t R) {
-  using K = CoopDma<SB, D>;
-  constexpr uint32_t G = K::G;
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t S = reinterpret_cast<uint64_t>(c) + 64ull * b1 - 8ull;  // message block b1
-  const uint32_t ngr = 4u * R;                                           // granules of R blocks
-  const uint32_t pos = lane % G, sub = lane / G;
-  const uint32_t wbase = (uint32_t)(uintptr_t)wl;  // LDS byte address (low half of the flat address)
-  uint64_t P[G];
-#pragma unroll
-  for (int q = 0; q < (int)G; q++) {
-    const uint32_t ch = K::C * (uint32_t)q + sub;
-    const uint32_t gq = (pos - (ch >> K::RotShift)) & (G - 1u);
-    P[q] = shfl64(S, ch) + 16ull * gq - 1024ull * (uint32_t)(q % 4);
-  }
-  // this lane's row: granule k in slot (k + rot) mod G
-  const uint32_t rot = (lane >> K::RotShift) & (G - 1u);
-  uint32_t RA[G];
-#pragma unroll
-  for (int k = 0; k < (int)G; k++) RA[k] = wbase + K::Row * lane + 16u * (((uint32_t)k + rot) & (G - 1u));
-  // The block reads are issued by hand: with an LDS-DMA in flight the
-  // compiler waits lgkmcnt(0) before the first use of any LDS read, which
-  // would also wait for the next block's reads issued just before.  `rd`
-  // issues 4 ds_read_b128; `ready` waits until only the 4 issued after W are
-  // outstanding (LDS reads return in order) and ties W's uses behind it.
-  auto rd = [&](u32x4(&W)[4], auto jc, auto uc) {
-    constexpr uint32_t j = decltype(jc)::value, u = decltype(uc)::value;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const uint32_t a = RA[4u * u + (uint32_t)i];
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(W[i]) : "v"(a), "n"(j * K::Stage));
-    }
+  // start of stage s: stage s+1 (in Gn) into the other half, then Gn's
+  // registers take the loads of stage s+3
+  auto stage = [&](auto half_c, uint32_t s, u32x4(&Gn)[G]) {
+    constexpr uint32_t HALF = decltype(half_c)::value;
+    coop_write<G>(wl, wr, HALF ^ 1u, Gn);
+    coop_load<G>(Gn, Q, min(s + 3u, nst - 1u), t, ngr);
+    coop_hash<G>(wl, rd, HALF, s, R, h);
   };
-  auto ready = [&](u32x4(&W)[4]) {
-    asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(W[0]), "+v"(W[1]), "+v"(W[2]), "+v"(W[3]));
-  };
-  // prologue: stages 0 .. D-1 into slots 0 .. D-1
-  static_for<D>([&](auto jc) { dma_clamped<SB, D, decltype(jc)::value>(P, wbase, (uint32_t)decltype(jc)::value, 0u, ngr, pos, sub); });
-#pragma unroll
-  for (int q = 0; q < (int)G; q++) P[q] += 16ull * G * D;
-  uint32_t pbase = D;
-  // stage 0 has landed once at most the D-1 later stages fly (in-order completion)
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * G) : "memory");
-  u32x4 WA[4], WB[4];
-  rd(WA, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
-  // A ring = D stages.  Main rings hold no block past R and refill only
-  // stages whose granules all exist (no clamp, no per-block test); the last
-  // one or two rings test every block and clamp their refills.
-  uint32_t s0 = 0;
-  auto ring = [&](auto tail_c) -> bool {
-    constexpr bool TAIL = decltype(tail_c)::value;
-    bool go = true;
-    // block (j, u): its words are in Wc (read one block ahead), the next
-    // block's go to Wn
-    auto blk = [&](auto jc, auto uc, u32x4(&Wc)[4], u32x4(&Wn)[4]) {
-      constexpr int j = decltype(jc)::value, u = decltype(uc)::value;
-      if constexpr (TAIL) {
-        if (!go || SB * (s0 + (uint32_t)j) + (uint32_t)u >= R) {  // wave-uniform
-          go = false;
-          return;
-        }
-      }
-      if constexpr (u + 1 < SB) {
-        rd(Wn, jc, std::integral_constant<int, u + 1>{});
-        ready(Wc);
-      } else {
-        // the next stage (slot (j+1) mod D) has landed: the D-2 after it may fly
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * G) : "memory");
-        rd(Wn, std::integral_constant<int, (j + 1) % D>{}, std::integral_constant<int, 0>{});
-        ready(Wc);
-        // slot j is consumed (Wc's reads are back): refill it with stage s0 + j + D
-        if constexpr (TAIL) dma_clamped<SB, D, j>(P, wbase, s0 + (uint32_t)j + D, pbase, ngr, pos, sub);
-        else dma_fast<SB, D, j>(P, wbase);
-      }
-      __builtin_amdgcn_sched_barrier(0);  // the reads above go out before this block's compression
-      const uint32_t m[16] = {Wc[0].x, Wc[0].y, Wc[0].z, Wc[0].w, Wc[1].x, Wc[1].y, Wc[1].z, Wc[1].w,
-                              Wc[2].x, Wc[2].y, Wc[2].z, Wc[2].w, Wc[3].x, Wc[3].y, Wc[3].z, Wc[3].w};
-      md5_compress(h, m);
-    };
-    // blocks alternate WA -> WB -> WA ...; D * SB is even, so every ring starts in WA
-    static_for<D * SB>([&](auto ic) {
-      constexpr int I = decltype(ic)::value;
-      if constexpr (I % 2 == 0) blk(std::integral_constant<int, I / SB>{}, std::integral_constant<int, I % SB>{}, WA, WB);
-      else blk(std::integral_constant<int, I / SB>{}, std::integral_constant<int, I % SB>{}, WB, WA);
-    });
-#pragma unroll
-    for (int q = 0; q < (int)G; q++) P[q] += 16ull * G * D;
-    pbase += D;
-    s0 += D;
-    return go;
-  };
-  for (; SB * (s0 + 2u * D) <= R;) ring(std::false_type{});
-  while (SB * s0 < R && ring(std::true_type{})) {
+  for (uint32_t s = 0; BPS * s < R; s += 2u) {
+    stage(std::integral_constant<uint32_t, 0>{}, s, GB);
+    stage(std::integral_constant<uint32_t, 1>{}, s + 1u, GA);  // hashes nothing past block R
   }
-  // no read may land in registers, and no DMA in the ring, after they are reused
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : "+v"(WA[0]), "+v"(WA[1]), "+v"(WA[2]), "+v"(WA[3]), "+v"(WB[0]),
-               "+v"(WB[1]), "+v"(WB[2]), "+v"(WB[3])::"memory");
 }
 
 }  // namespace
@@ -1584,36 +1033,21 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
 // in the planner's order).  Each lane resumes its chain at `next`,
 // compresses up to `budget` full blocks and either finishes (tail blocks,
 // BlockID stored at `out`, entry marked done) or saves the state for the
-// next launch.  grid = one workgroup per CU (256 threads = one wave per SIMD,
-// or 512 = two); placement of groups on waves: see `dense`.  The MD5 chain
-// is bound by the issue rate of one wave (DESIGN.md "K3").
-//
-// cooperative (page-local) loads for waves of full-slice chains
-#ifndef HBX_K3_COOP
-#define HBX_K3_COOP 1
-#endif
+// next launch.  grid = one 256-thread workgroup per CU (one wave per SIMD);
+// group g runs on wave g % 4 of workgroup g / 4 (dense placement, below).
+// The MD5 chain is bound by the issue rate of one wave (DESIGN.md "K3").
+// Waves whose 64 chains all hold >= kCoopMinBudget blocks stream them with
+// cooperative (page-local) loads.
 constexpr uint32_t kCoopMinBudget = 8u;
-constexpr int kK3Threads = 256;    // hbx_k3_block_md5: one wave per SIMD
-constexpr int kK3Threads2 = 512;   // hbx_k3_block_md5_w2: two waves per SIMD
+constexpr int kK3Threads = 256;  // one wave per SIMD
+constexpr uint32_t kK3WaveLds = Coop<16>::WaveLds;
 
-// The cooperative path of a K3 variant: LDS-DMA stages (HBX_K3_DMA) for one
-// wave per SIMD, else register-staged.
-template <int THREADS, int G, int SETS>
-__device__ __forceinline__ void coop(uint8_t* wl, const uint8_t* c, uint32_t (&h)[4], uint32_t b1, uint32_t R) {
-  if constexpr (THREADS == kK3Threads && HBX_K3_DMA) md5_coop_dma<HBX_K3_DMA_SB, HBX_K3_DMA_D>(wl, c, h, b1, R);
-  else md5_coop<G, SETS>(wl, c, h, b1, R);
-}
-constexpr uint32_t kK3WaveLds =
-    HBX_K3_DMA ? CoopDma<HBX_K3_DMA_SB, HBX_K3_DMA_D>::WaveLds : Coop<16>::WaveLds;
-
-// The body of both K3 variants: THREADS per workgroup (one per CU), the
-// cooperative stage of G granules with SETS register sets in flight, the
-// lane path's prefetch ring of RING blocks.  `wl` = this wave's LDS.
-template <int THREADS, int G, int SETS, int RING>
+// One wave's share of a K3 launch (VGPR + AGPR, no scratch).  `wl` = this
+// wave's LDS.
 __device__ __forceinline__ void k3_body(
     uint8_t* wl, const OrderEntry* __restrict__ order, const uint32_t* __restrict__ n_order, uint32_t budget,
-    uint32_t dense, uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last,
-    uint64_t* __restrict__ tslot, uint64_t* __restrict__ probe) {
+    uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last, uint64_t* __restrict__ tslot,
+    uint64_t* __restrict__ probe) {
   // the MD5 chains are issue-bound: win the SIMD's issue arbitration against
   // co-resident waves of other kernels
   __builtin_amdgcn_s_setprio(3);
@@ -1630,18 +1064,17 @@ __device__ __forceinline__ void k3_body(
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t n_total = *n_order;
   const uint32_t groups = (n_total + 63u) / 64u;
-  const uint32_t nwaves = gridDim.x * (THREADS / 64);
-  // spread: group g on wave (g / grid) % W of workgroup g % grid (one busy
-  // wave per CU first); dense: group g on wave g % W of workgroup g / W, so
-  // the busy waves fill the fewest CUs and whole CUs stay free for the scan
-  // stream's K1/K2.  The groups are in descending block count, so a CU's four
+  const uint32_t nwaves = gridDim.x * (kK3Threads / 64);
+  // dense: group g on wave g % 4 of workgroup g / 4, so the busy waves fill
+  // the fewest CUs and whole CUs stay free for the scan stream's K1/K2
+  // (spreading one busy wave per CU first measured 1,255 vs 1,510 GiB/s).  The groups are in descending block count, so a CU's four
   // waves end together and the CUs of the short ones free up early for K1.
   // (Dealing the groups round-robin over ceil(groups / 4) workgroups rounded
   // to a multiple of the 8 XCDs, to even out K3's CUs per XCD, mixed long and
   // short waves on every CU: K3 3.52 -> 3.41 ms but K1 3.25 -> 3.54 ms beside
   // it, 2,235 -> 2,091 GiB/s at 33 resident batches.)
-  const uint32_t g0 = dense ? blockIdx.x * (THREADS / 64) + wave : wave * gridDim.x + blockIdx.x;
-  // diagnostics (HBX_K3_PROBE): per wave its start, the end of its first
+  const uint32_t g0 = blockIdx.x * (kK3Threads / 64) + wave;
+  // diagnostics (hbx_set_k3_probe): per wave its start, the end of its first
   // group's start-up (loads + prologue), its end, R and the largest count
   const uint64_t pt0 = probe ? __builtin_amdgcn_s_memrealtime() : 0ull;
   uint64_t pt1 = 0ull;
@@ -1659,7 +1092,6 @@ __device__ __forceinline__ void k3_body(
     const bool finish = active && b0 + cnt == ((len + 8u) >> 6);
     uint32_t h[4] = {ch.h[0], ch.h[1], ch.h[2], ch.h[3]};
     const uint8_t* src = reinterpret_cast<const uint8_t*>(ch.src);
-#if HBX_K3_COOP
     // R = the wave's smallest count: all 64 chains advance R blocks together
     // through page-local cooperative loads (idle lanes shadow the group's
     // first chain, whose count is >= R), then each lane its own remainder
@@ -1671,7 +1103,7 @@ __device__ __forceinline__ void k3_body(
         pR = R;
         pmax = wave_max_all(cnt);
       }
-      coop<THREADS, G, SETS>(wl, src, h, ch.next + 1u, R - 1u);
+      md5_coop<16>(wl, src, h, ch.next + 1u, R - 1u);
       // A group that straddles two order bins mixes counts (e.g. 4,229 and
       // 4,093 blocks): the lanes still holding blocks go on cooperatively
       // while the others shadow the first of them and discard (the lane-mode
@@ -1688,7 +1120,7 @@ __device__ __forceinline__ void k3_body(
                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)reinterpret_cast<uint64_t>(src), L);
         const uint32_t p_sh = (uint32_t)__builtin_amdgcn_readlane((int)pos, L);
         uint32_t hk[4] = {h[0], h[1], h[2], h[3]};
-        coop<THREADS, G, SETS>(wl, part ? src : reinterpret_cast<const uint8_t*>(s_sh), hk, part ? pos : p_sh, R2);
+        md5_coop<16>(wl, part ? src : reinterpret_cast<const uint8_t*>(s_sh), hk, part ? pos : p_sh, R2);
         if (part) {
           h[0] = hk[0];
           h[1] = hk[1];
@@ -1698,14 +1130,10 @@ __device__ __forceinline__ void k3_body(
           rem -= R2;
         }
       }
-      md5_run<RING>(src, len, h, pos, rem, finish);
+      md5_run<>(src, len, h, pos, rem, finish);
     } else {
-      md5_run<RING>(src, len, h, b0, cnt, finish);
+      md5_run<>(src, len, h, b0, cnt, finish);
     }
-#else
-    (void)wl;
-    md5_run<RING>(src, len, h, b0, cnt, finish);
-#endif
     if (finish) {
       *(__attribute__((address_space(1))) u32x4*)ch.out = u32x4{h[0], h[1], h[2], h[3]};
       chp->next = kChainDone;
@@ -1715,7 +1143,7 @@ __device__ __forceinline__ void k3_body(
     }
   }
   if (probe && (threadIdx.x & 63u) == 0u) {
-    uint64_t* p = probe + 4u * (blockIdx.x * (THREADS / 64) + wave);
+    uint64_t* p = probe + 4u * (blockIdx.x * (kK3Threads / 64) + wave);
     // hardware placement: HW_ID (wave, SIMD, CU, SH, SE) and XCC_ID
     const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));
     const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11)) & 0xfu;
@@ -1735,27 +1163,11 @@ __device__ __forceinline__ void k3_body(
 // (VGPR + AGPR, 346 registers, no scratch).
 extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
     const OrderEntry* __restrict__ order, const uint32_t* __restrict__ n_order, uint32_t budget,
-    uint32_t dense, uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last,
-    uint64_t* __restrict__ tslot, uint64_t* __restrict__ probe) {
+    uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last, uint64_t* __restrict__ tslot,
+    uint64_t* __restrict__ probe) {
   __shared__ __attribute__((aligned(16))) uint8_t k3_lds[kK3Threads / 64][kK3WaveLds];
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  k3_body<kK3Threads, 16, 2, HBX_MD5_RING>(k3_lds[wave], order, n_order, budget, dense, started, t_first, t_last,
-                                           tslot, probe);
-}
-
-// Two waves per SIMD (the MD5 chain runs at one wave's issue rate, and two
-// waves of a SIMD each keep that rate: tools/ubench/valu_latency), so the
-// same chains fill half the CUs and leave the rest to the next batch's K1:
-// 2-block stages (18 KiB of LDS per wave), three register sets, a 4-block
-// lane ring, at most 256 registers.
-extern "C" __global__ __launch_bounds__(kK3Threads2, 2) void hbx_k3_block_md5_w2(
-    const OrderEntry* __restrict__ order, const uint32_t* __restrict__ n_order, uint32_t budget,
-    uint32_t dense, uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last,
-    uint64_t* __restrict__ tslot, uint64_t* __restrict__ probe) {
-  __shared__ __attribute__((aligned(16))) uint8_t k3_lds[kK3Threads2 / 64][Coop<8>::WaveLds];
-  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  k3_body<kK3Threads2, 8, 3, 4>(k3_lds[wave], order, n_order, budget, dense, started, t_first, t_last, tslot,
-                                probe);
+  k3_body(k3_lds[wave], order, n_order, budget, started, t_first, t_last, tslot, probe);
 }
 
 // K1 gate (scan stream, just before a batch's K1): holds the K1 back until
@@ -1977,7 +1389,7 @@ extern "C" __global__ __launch_bounds__(64, 1) void hbx_k6_hash_blocks(
   // the longest), the per-lane remainder through the lane path
   const uint32_t R = ~wave_max_all(active ? ~cnt : 0u);
   const uint32_t Rc = R >= kCoopMinBudget ? R : 0u;  // wave-uniform
-  if (Rc) md5_coop<16, 2>(k6_lds, vs, h, hb, Rc);
+  if (Rc) md5_coop<16>(k6_lds, vs, h, hb, Rc);
   const uint32_t rest = cnt - Rc;
   md5_run<>(rest ? vs : zeros + 64, rest ? len + p - 8u : 0u, h, rest ? hb + Rc : 1u, rest, false);
   if (fast) md5_tail(vs, len + p - 8u, h, true);

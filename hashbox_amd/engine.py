@@ -95,8 +95,7 @@ class Engine:
     """One MI355X (one HIP stream) running the chunk + block-ID path."""
 
     def __init__(self, device: int = 0, tile_iters: Optional[int] = None,
-                 md5_slice: Optional[int] = None, join_lag: Optional[int] = None,
-                 k3_waves: Optional[int] = None):
+                 md5_slice: Optional[int] = None, join_lag: Optional[int] = None):
         self._L = _lib.load()
         self._ctx = ctypes.c_void_p()
         rc = self._L.hbx_ctx_create(int(device), ctypes.byref(self._ctx))
@@ -112,8 +111,6 @@ class Engine:
             self.set_md5_slice(md5_slice)
         if join_lag is not None:
             self.set_join_lag(join_lag)
-        if k3_waves is not None:
-            self.set_k3_waves(k3_waves)
 
     # ----------------------------------------------------------- plumbing --
     def _after_producer(self):
@@ -284,10 +281,6 @@ class Engine:
     def set_md5_slice(self, blocks: int):
         """MD5 blocks per chain per K3 launch (0 = unlimited)."""
         self._check(self._L.hbx_set_md5_slice(self._ctx, int(blocks)), "hbx_set_md5_slice")
-
-    def set_k3_waves(self, waves_per_simd: int):
-        """Block-MD5 kernel with 1 or 2 waves per SIMD (hbx_set_k3_waves)."""
-        self._check(self._L.hbx_set_k3_waves(self._ctx, int(waves_per_simd)), "hbx_set_k3_waves")
 
     def input_after_oldest(self):
         """The next input copy / batch may reuse the oldest pending batch's

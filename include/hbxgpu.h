@@ -140,12 +140,6 @@ int hbx_pending(hbx_ctx *ctx);
  * + ceil(min(longest file, 8 MiB)/64 / blocks) - 1 further launches; results are
  * identical for every setting. */
 int hbx_set_md5_slice(hbx_ctx *ctx, uint32_t blocks);
-/* Waves per SIMD of the block-MD5 kernel: 1 (default; 4-block cooperative
- * stages, 346 registers) or 2 (2-block stages, at most 256 registers: the
- * same chains on half the CUs, leaving the rest to the next batch's scan).
- * Results are identical; HBX_K3_WAVES sets the initial value.  Fails with
- * HBX_ERR_STATE while batches are pending. */
-int hbx_set_k3_waves(hbx_ctx *ctx, uint32_t waves_per_simd);
 /* Reuse the input memory of the OLDEST pending batch: order the engine's
  * next input copies (hbx_memcpy_h2d_async) and submitted batches (chunking
  * and verify) after the MD5 launch that finishes that batch, with a GPU-side

@@ -47,8 +47,8 @@ def test_state_rules(oracle):
         e.submit_device(dev.data_ptr(), offs, sizes)
         with pytest.raises(HbxError):
             e.set_md5_slice(3)
-        with pytest.raises(HbxError):  # the K3 variant is fixed while batches are pending
-            e.set_k3_waves(2)
+        with pytest.raises(HbxError):  # the probe is fixed while batches are pending
+            e.set_k3_probe(True)
         with pytest.raises(HbxError):  # offset not 16-byte aligned
             e.submit_device(dev.data_ptr(), offs + np.uint64(4), sizes)
         assert e.pending() == 1
@@ -56,11 +56,13 @@ def test_state_rules(oracle):
         got = [e.wait(), e.wait()]
         assert e.pending() == 0
         e.set_md5_slice(3)  # allowed once drained
-        e.set_k3_waves(2)
-        with pytest.raises(HbxError):
-            e.set_k3_waves(3)
+        e.set_k3_probe(True)
         e.submit_device(dev.data_ptr(), offs, sizes)
         got.append(e.wait())
+        w = e.k3_wave_times()  # the probe's per-wave records of the latest K3 launch
+        assert w.shape[1] == 4 and (w[:, 2] >= w[:, 0]).all()
+        e.set_k3_probe(False)
+        assert e.knobs()["k3_probe"] == 0
     for g in got:
         for a, r in zip(g, refs):
             assert np.array_equal(a.cut_ends, r.cut_ends) and np.array_equal(a.ids, r.ids)
@@ -69,15 +71,16 @@ def test_state_rules(oracle):
 
 def test_ab_switches_need_hbx_ab(monkeypatch):
     """HBX_* A/B switches change nothing unless HBX_AB=1 (a caller's stray
-    environment must not swap kernels): HBX_K1_RUN=128 alone keeps K1."""
+    environment must not change the schedule): HBX_JOIN_LAG=3 and
+    HBX_LEAN_MARKS=0 alone keep join lag 1 and lean marks."""
     from hashbox_amd import Engine
     monkeypatch.delenv("HBX_AB", raising=False)
-    monkeypatch.setenv("HBX_K1_RUN", "128")
+    monkeypatch.setenv("HBX_LEAN_MARKS", "0")
     monkeypatch.setenv("HBX_JOIN_LAG", "3")
     with Engine(0) as e:
         k = e.knobs()
-    assert k["ab_env"] == 0 and k["k1_run"] == 64 and k["join_lag"] == 1, k
+    assert k["ab_env"] == 0 and k["lean_marks"] == 1 and k["join_lag"] == 1, k
     monkeypatch.setenv("HBX_AB", "1")
     with Engine(0) as e:
         k = e.knobs()
-    assert k["ab_env"] == 1 and k["k1_run"] == 128 and k["join_lag"] == 3, k
+    assert k["ab_env"] == 1 and k["lean_marks"] == 0 and k["join_lag"] == 3 and k["plan_mode"] == 2, k

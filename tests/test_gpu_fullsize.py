@@ -34,7 +34,7 @@ def _oracle_of(oracle, arena, offs, lens):
     return refs
 
 
-def _run_schedule(arenas, offs, lens, steps, R=33, lead=2, k3_waves=1):
+def _run_schedule(arenas, offs, lens, steps, R=33, lead=2):
     """bench.py's steady(): R submitted before any collect, then collect the
     oldest + submit one; drain at the end.  Returns [(arena index, results)]."""
     import torch
@@ -42,7 +42,7 @@ def _run_schedule(arenas, offs, lens, steps, R=33, lead=2, k3_waves=1):
     nfull = ((8 << 20) + 8) >> 6
     B = -(-nfull // (R - lead))
     out, order = [], deque()
-    with Engine(0, md5_slice=B, k3_waves=k3_waves) as e:
+    with Engine(0, md5_slice=B) as e:
         e.reserve(R + 1, len(lens), int(sum(lens)))
         for j in range(steps):
             if len(order) >= R:
@@ -72,15 +72,14 @@ def _check(results, refs):
             assert g.content_type == (3 if r.n_chunks > 1 else 2)
 
 
-@pytest.mark.parametrize("k3_waves", [1, 2])
-def test_configs1_full_size_steady_state(oracle, k3_waves):
+def test_configs1_full_size_steady_state(oracle):
     import torch
     import workloads as W
     lens = [128 << 20] * 64
     offs, total = W.pack_layout(lens)
     arenas = W.random_arenas(3, total, 1000, torch.device("cuda", 0))
     refs = [_oracle_of(oracle, a, offs, lens) for a in arenas]
-    results = _run_schedule(arenas, offs, lens, steps=40, k3_waves=k3_waves)
+    results = _run_schedule(arenas, offs, lens, steps=40)
     assert len(results) == 40
     _check(results, refs)
     del arenas

@@ -212,17 +212,16 @@ def _device_batches(oracle, nb, seed):
     return out
 
 
-@pytest.mark.parametrize("md5_slice,join_lag,k3_waves", [(1, 1, 1), (3, 1, 1), (64, 1, 1), (16384, 1, 1), (3, 2, 1),
-                                                         (64, 2, 1), (64, 3, 1), (16384, 4, 1), (1, 1, 2),
-                                                         (9, 1, 2), (64, 3, 2), (16384, 1, 2)])
-def test_pipelined_batches_time_sliced(oracle, md5_slice, join_lag, k3_waves):
+@pytest.mark.parametrize("md5_slice,join_lag", [(1, 1), (3, 1), (9, 1), (64, 1), (16384, 1), (3, 2), (64, 2), (64, 3),
+                                                (16384, 4)])
+def test_pipelined_batches_time_sliced(oracle, md5_slice, join_lag):
     """Several batches in flight on one context with the block-MD5 stage
     time-sliced: chains resume across many K3 launches, new batches' chunks
     join carried chains (join_lag submits later), results come back in FIFO
     order, bit-exact."""
     from hashbox_amd import Engine
     batches = _device_batches(oracle, 4, 31 + md5_slice % 7)
-    with Engine(0, md5_slice=md5_slice, join_lag=join_lag, k3_waves=k3_waves) as e:
+    with Engine(0, md5_slice=md5_slice, join_lag=join_lag) as e:
         for dev, offs, sizes, _ in batches[:3]:
             e.submit_device(dev.data_ptr(), offs, sizes)
         assert e.pending() == 3
@@ -244,17 +243,14 @@ def test_pipelined_batches_time_sliced(oracle, md5_slice, join_lag, k3_waves):
         assert n[3] >= 1 and ms[3] > 0
 
 
-@pytest.mark.parametrize("join_lag,plan_mode", [(1, None), (2, None), (3, None), (2, "0"), (2, "1"), (1, "1")])
-def test_pipelined_steady_state(oracle, monkeypatch, join_lag, plan_mode):
+@pytest.mark.parametrize("join_lag", [1, 2, 3, 4])
+def test_pipelined_steady_state(oracle, join_lag):
     """A deep pipeline as bench.py drives it: submit, and wait only once
     `depth` batches are pending, so batches complete through the slice
-    schedule rather than a forced drain.  Join lags 1-3, with the plans one
-    launch ahead (the default at lag >= 2), inline on the scan stream or on
-    the hash stream (HBX_PLAN_MODE 0/1: schedule only)."""
+    schedule rather than a forced drain.  Join lags 1-4: the plan inline on
+    the scan stream (lag 1), on the hash stream (lag 2), one launch ahead on
+    the scan stream (lag >= 3)."""
     from hashbox_amd import Engine
-    if plan_mode is not None:
-        monkeypatch.setenv("HBX_AB", "1")
-        monkeypatch.setenv("HBX_PLAN_MODE", plan_mode)
     batches = _device_batches(oracle, 3, 57)
     got = []
     with Engine(0, md5_slice=4096, join_lag=join_lag) as e:  # 256 KiB per chain per launch: 32 per 8 MiB
@@ -313,17 +309,13 @@ def test_plan_stream_changes_in_one_context(oracle, monkeypatch, lean):
         assert all(m > 0 for m in ms[:4])
 
 
-@pytest.mark.parametrize("dense,k3_waves", [("0", 1), ("1", 1), ("0", 2), ("1", 2)])
-def test_reserved_pipeline_placements(oracle, monkeypatch, dense, k3_waves):
-    """hbx_reserve pre-sizes the pool, chain tables and summaries; both K3
-    wave placements (HBX_K3_DENSE) give the same bit-exact results through a
-    pipeline that runs its scan stream two steps ahead."""
+def test_reserved_pipeline(oracle):
+    """hbx_reserve pre-sizes the pool, chain tables and summaries; a pipeline
+    that runs its scan stream two steps ahead stays bit-exact."""
     from hashbox_amd import Engine
-    monkeypatch.setenv("HBX_AB", "1")
-    monkeypatch.setenv("HBX_K3_DENSE", dense)
     batches = _device_batches(oracle, 2, 43)
     got, order = [], [i % 2 for i in range(12)]
-    with Engine(0, md5_slice=2048, k3_waves=k3_waves) as e:
+    with Engine(0, md5_slice=2048) as e:
         e.reserve(10, max(len(b[2]) for b in batches), max(int(sum(b[2])) for b in batches))
         for i in order:
             dev, offs, sizes, _ = batches[i]
@@ -410,6 +402,50 @@ def test_input_after_oldest_ring(oracle, md5_slice):
             got.append(e.wait())
     L.hbx_free_pinned(pin)
     assert len(got) == 12
+    for d, res in zip(order, got):
+        for g, r in zip(res, refs[d]):
+            _check(g, r)
+
+
+def test_input_fence_orders_caller_stream(oracle):
+    """The ring of test_input_after_oldest_ring refilled by the CALLER's own
+    work (a device-to-device copy on a torch stream of its own) instead of
+    hbx_memcpy_h2d_async: hbx_input_fence(ctx, stream) puts the wait for the
+    launch that finishes the oldest batch on that stream, so the refill never
+    overwrites bytes K3 is still hashing.  Every batch must match the oracle
+    on ITS data."""
+    import torch
+    from hashbox_amd import Engine, pack_arena_layout
+    rng = np.random.default_rng(73)
+    sizes = [9 * MAXB + 5, 3 * MIN + 7, 2 * MAXB + 99]
+    offs, total = pack_arena_layout(sizes)
+    datas = []
+    for j in range(4):
+        host = np.zeros(total, np.uint8)
+        for o, n in zip(offs, sizes):
+            host[int(o):int(o) + n] = rng.integers(0, 256, n, dtype=np.uint8)
+        datas.append(host)
+    refs = [[oracle.store_file(h[int(o):int(o) + n], fast=True) for o, n in zip(offs, sizes)] for h in datas]
+    src = [torch.from_numpy(h).to("cuda:0") for h in datas]
+    ring = [torch.empty(total, dtype=torch.uint8, device="cuda:0") for _ in range(3)]
+    side = torch.cuda.Stream(device=0)
+    torch.cuda.synchronize()
+    got, order = [], []
+    with Engine(0, md5_slice=4096) as e:
+        for j in range(10):
+            if e.pending() >= 3:
+                e.input_after_oldest()
+                e.input_fence(side.cuda_stream)
+            d = j % 4
+            with torch.cuda.stream(side):
+                ring[j % 3].copy_(src[d])
+                e.submit_device(ring[j % 3].data_ptr(), offs, sizes)  # ordered after `side` (hbx_after_stream)
+            order.append(d)
+            if e.pending() > 3:
+                got.append(e.wait())
+        while e.pending():
+            got.append(e.wait())
+    assert len(got) == 10
     for d, res in zip(order, got):
         for g, r in zip(res, refs[d]):
             _check(g, r)

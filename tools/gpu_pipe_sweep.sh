@@ -1,16 +1,15 @@
 #!/bin/bash
-# Per-GPU pipeline sweep: each argument is "files:lag:plan_mode:lead" (plan
-# mode or lead "-" = the default).  Prints value, ms/step and kernel ms/step.
-# usage: bash tools/gpu_pipe_sweep.sh 8:2:-:- 8:3:-:6 ...
+# Per-GPU pipeline sweep: each argument is "files:lag:lead" (lead "-" = the
+# default; the plan placement follows the lag).  Prints value, ms/step and
+# kernel ms/step.
+# usage: bash tools/gpu_pipe_sweep.sh 8:2:- 8:3:6 ...
 set -o pipefail
-export HBX_AB=1  # the library honours HBX_* A/B switches only with this
 out=gpurun_out/pipe
 mkdir -p $out
 for cfg in "$@"; do
-  IFS=: read nf lag mode lead <<< "$cfg"
-  if [ "$mode" = "-" ]; then unset HBX_PLAN_MODE; else export HBX_PLAN_MODE=$mode; fi
+  IFS=: read nf lag lead <<< "$cfg"
   la=""; [ "$lead" != "-" ] && la="--lead $lead"
-  tag=nf${nf}_lag${lag}_m${mode}_l${lead}
+  tag=nf${nf}_lag${lag}_l${lead}
   timeout -k 10 240 python bench.py --no-cpu-baseline --no-check --workload random --steps 200 \
     --files $nf --join-lag $lag $la > $out/$tag.json 2> $out/$tag.err || { tail -3 $out/$tag.err; exit 1; }
   python - $out/$tag.json $tag <<'PY'
