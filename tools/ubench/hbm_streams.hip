@@ -51,37 +51,44 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
   return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 
-template <bool LDS, int SETS = 2>
+// CPW chains per wave (64: K3's layout; 32: the same chains spread over twice
+// the waves, i.e. 256 CUs instead of 128, half the LDS rows and half the load
+// instructions per stage; lanes >= 32 only help with the loads).
+template <bool LDS, int SETS = 2, int CPW = 64>
 __global__ __launch_bounds__(256, 1) void coop(const uint64_t* __restrict__ addr, uint32_t stages,
                                                uint32_t* __restrict__ out, uint32_t stride) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[4][kWaveLds];
+  constexpr int NQ = CPW / (int)kC;  // load instructions per stage
+  constexpr uint32_t Half = (uint32_t)CPW * kRow;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4][2u * Half];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   uint8_t* wl = lds[wave];
-  const uint64_t S = addr[(blockIdx.x * 4u + wave) * 64u + lane];
+  const uint64_t S = addr[(blockIdx.x * 4u + wave) * (uint32_t)CPW + (lane % (uint32_t)CPW)];
   const uint32_t t = lane % kG, sub = lane / kG;
-  uint64_t Q[kG];
+  uint64_t Q[NQ];
 #pragma unroll
-  for (int q = 0; q < kG; q++) Q[q] = shfl64(S, kC * (uint32_t)q + sub) + 16ull * t;
+  for (int q = 0; q < NQ; q++) Q[q] = shfl64(S, kC * (uint32_t)q + sub) + 16ull * t;
   const uint32_t wr = sub * kRow + 16u * t, rd = lane * kRow;
   u32x4 acc = {0u, 0u, 0u, 0u};
-  auto load = [&](u32x4(&G)[kG], uint32_t st) {
+  auto load = [&](u32x4(&G)[NQ], uint32_t st) {
 #pragma unroll
-    for (int q = 0; q < kG; q++) G[q] = *(g_u32x4*)(Q[q] + 16ull * kG * stride * st);
+    for (int q = 0; q < NQ; q++) G[q] = *(g_u32x4*)(Q[q] + 16ull * kG * stride * st);
   };
-  auto write = [&](uint32_t half, const u32x4(&G)[kG]) {
+  auto write = [&](uint32_t half, const u32x4(&G)[NQ]) {
 #pragma unroll
-    for (int q = 0; q < kG; q++) *reinterpret_cast<u32x4*>(wl + wr + half * kHalf + kC * kRow * (uint32_t)q) = G[q];
+    for (int q = 0; q < NQ; q++) *reinterpret_cast<u32x4*>(wl + wr + half * Half + kC * kRow * (uint32_t)q) = G[q];
   };
-  auto use = [&](uint32_t half, const u32x4(&G)[kG]) {
+  auto use = [&](uint32_t half, const u32x4(&G)[NQ]) {
     if constexpr (LDS) {
+      if (CPW == 64 || lane < (uint32_t)CPW) {
 #pragma unroll
-      for (int k = 0; k < kG; k++) acc ^= *reinterpret_cast<const u32x4*>(wl + rd + half * kHalf + 16u * k);
+        for (int k = 0; k < kG; k++) acc ^= *reinterpret_cast<const u32x4*>(wl + rd + half * Half + 16u * k);
+      }
     } else {
 #pragma unroll
-      for (int q = 0; q < kG; q++) acc ^= G[q];
+      for (int q = 0; q < NQ; q++) acc ^= G[q];
     }
   };
-  u32x4 GA[kG], GB[kG];
+  u32x4 GA[NQ], GB[NQ];
   load(GA, 0u);
   load(GB, 1u);
   if constexpr (LDS) write(0u, GA);
@@ -97,7 +104,7 @@ __global__ __launch_bounds__(256, 1) void coop(const uint64_t* __restrict__ addr
       load(GA, s + 4u);
     }
   } else {  // three register sets: stages s+1..s+3 in flight while s is used
-    u32x4 GC[kG];
+    u32x4 GC[NQ];
     load(GC, 3u);
     for (uint32_t s = 0; s + 3u < stages; s += 3u) {
       write(1u, GB);
@@ -165,7 +172,8 @@ __global__ __launch_bounds__(256, 1) void coop8(const uint64_t* __restrict__ add
 
 // 1024-thread workgroups holding 128 KiB of (unused) dynamic LDS, like K1: they
 // cannot share a CU with a coop workgroup, so the two split the CUs as K1 and
-// K3 do.
+// K3 do.  With 64 KiB (the "_shared" cases) one fits beside a 32-chains-per-
+// wave coop workgroup (68 KiB) on every CU.
 __global__ __launch_bounds__(1024) void stream_read(const u32x4* __restrict__ p, uint64_t n16, uint32_t reps,
                                                     uint32_t* __restrict__ out) {
   extern __shared__ uint32_t pad_lds[];
@@ -213,10 +221,13 @@ int main(int argc, char** argv) {
   // stages each): few translations per wave like "local", but every chain's
   // 256 B in a DRAM row of its own like "rand" (TLB reach vs DRAM locality);
   // "rand128" is "rand" over the same 128 stages.
-  struct Case { const char* name; int sets; bool lds; int place; uint32_t S; };
+  struct Case { const char* name; int sets; bool lds; int place; uint32_t S; int cpw = 64; };
+  // default: round 4, K3's 32,768 chains at 64 per wave (128 CUs, the
+  // streamer on the other 128) vs 32 per wave (all 256 CUs, the streamer
+  // sharing them with 64 KiB of LDS)
   const Case cases[] = {
-      {"coop_lds2_page", 2, true, 2, 32768u},     {"coop_lds2_rand128", 2, true, 0, 32768u},
-      {"coop_lds2_page", 2, true, 2, 16384u},     {"coop_lds2_rand128", 2, true, 0, 16384u},
+      {"coop_lds2_rand", 2, true, 0, 32768u, 64},   {"coop32_lds2_rand", 2, true, 0, 32768u, 32},
+      {"coop_lds2_rand", 2, true, 0, 16384u, 64},   {"coop32_lds2_rand", 2, true, 0, 16384u, 32},
   };
   const Case cases_full[] = {
       {"coop_lds2_rand", 2, true, 0, 8192u},   {"coop_lds2_rand", 2, true, 0, 16384u},
@@ -256,7 +267,8 @@ int main(int argc, char** argv) {
     uint64_t* d_addr = nullptr;
     CK(hipMalloc(&d_addr, S * 8ull));
     CK(hipMemcpy(d_addr, h.data(), S * 8ull, hipMemcpyHostToDevice));
-    const uint32_t wgs = S / 256u;
+    const uint32_t wgs = S / (4u * (uint32_t)k.cpw);
+    const bool shared = k.cpw == 32;  // the streamer shares the coop's CUs
     const double bytes = 256.0 * stages * S;
     for (int beside = 0; beside < (only ? 1 : 2); beside++) {
       float best = 1e30f, sms = 0.f;
@@ -265,7 +277,9 @@ int main(int argc, char** argv) {
         // the CUs left; the streamer outlasts the coop launch
         CK(hipEventRecord(c0, sc));
         const uint32_t stride = local ? 64u : 1u;  // local: stage stride 64 x 256 B = 16 KiB
-        if (k.sets == 8)
+        if (k.cpw == 32)
+          hipLaunchKernelGGL((coop<true, 2, 32>), dim3(wgs), dim3(256), 0, sc, d_addr, stages, d_out, stride);
+        else if (k.sets == 8)
           hipLaunchKernelGGL(coop8, dim3(wgs), dim3(256), 0, sc, d_addr, stages, d_out, stride);
         else if (!k.lds)
           hipLaunchKernelGGL((coop<false, 2>), dim3(wgs), dim3(256), 0, sc, d_addr, stages, d_out, stride);
@@ -277,8 +291,12 @@ int main(int argc, char** argv) {
         if (beside) {
           usleep(300);
           CK(hipEventRecord(s0, ss));
-          hipLaunchKernelGGL(stream_read, dim3(256 - std::min(wgs, 255u)), dim3(1024), 128 * 1024, ss,
-                             (const u32x4*)d_s, sbytes / 16, 4u, d_out);
+          if (shared)  // one 64 KiB streamer workgroup beside every coop workgroup
+            hipLaunchKernelGGL(stream_read, dim3(256), dim3(1024), 64 * 1024, ss, (const u32x4*)d_s, sbytes / 16, 4u,
+                               d_out);
+          else
+            hipLaunchKernelGGL(stream_read, dim3(256 - std::min(wgs, 255u)), dim3(1024), 128 * 1024, ss,
+                               (const u32x4*)d_s, sbytes / 16, 4u, d_out);
           CK(hipEventRecord(s1, ss));
         }
         CK(hipDeviceSynchronize());
