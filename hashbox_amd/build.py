@@ -13,7 +13,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libhbxgpu.so")
-SOURCES = ["hbx_engine.hip", "hbx_kernels.hip", "hbx_device.h", "hbx_formats.h", "hbx_deflate.hip", "hbx_inflate.hip", "hbx_wire.h",
+SOURCES = ["hbx_engine.hip", "hbx_kernels.hip", "hbx_device.h", "hbx_formats.h", "hbx_deflate.hip", "hbx_inflate.hip", "hbx_inflate_split.hip", "hbx_wire.h",
            os.path.join("..", "..", "include", "hbxgpu.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"

@@ -33,6 +33,7 @@
 #include "hbx_kernels.hip"
 #include "hbx_deflate.hip"
 #include "hbx_inflate.hip"
+#include "hbx_inflate_split.hip"
 #include "hbx_formats.h"
 #include "hbx_wire.h"
 
@@ -251,6 +252,8 @@ struct hbx_ctx {
   DevBuf d_vdesc, d_vlinks, d_vout, d_vexp, d_zeros;  // hbx_verify_blocks*
   DevBuf d_zblk, d_zinfo, d_zoff, d_zlen, d_zout, d_zimg;  // hbx_deflate_blocks*
   DevBuf d_idesc, d_ires;                                  // hbx_inflate_blocks_device
+  DevBuf d_sreg, d_sstart, d_sres, d_sscratch, d_smeta;    // its split path (K8s)
+  uint64_t k8_split_streams = 0, k8_split_fallbacks = 0;   // (hbx_knobs: how often the split path resolved)
   PinBuf h_read[2];         // hbx_store_paths: pinned landing slots for file reads
   PinBuf h_zstage;          // hbx_store_paths_z: compressed streams of one batch (synchronous form)
   // hbx_store_paths_z: compression stages in flight, each on its own stream
@@ -1231,7 +1234,8 @@ void hbx_ctx_destroy(hbx_ctx* c) {
                     &c->d_octl[0], &c->d_octl[1], &c->d_octl[2], &c->d_gate,
                     &c->d_stage, &c->d_msg, &c->d_plan, &c->d_vdesc, &c->d_vlinks,
                     &c->d_vout, &c->d_vexp, &c->d_zeros, &c->d_zblk, &c->d_zinfo, &c->d_zoff,
-                    &c->d_zlen, &c->d_zout, &c->d_zimg, &c->d_idesc, &c->d_ires})
+                    &c->d_zlen, &c->d_zout, &c->d_zimg, &c->d_idesc, &c->d_ires, &c->d_sreg, &c->d_sstart,
+                    &c->d_sres, &c->d_sscratch, &c->d_smeta})
     b->release();
   for (PinBuf& h : c->h_read) h.release();
   c->h_zstage.release();
@@ -1297,9 +1301,10 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
       out, (size_t)cap,
       "{\"ab_env\": %d, \"md5_slice\": %u, \"join_lag\": %u, \"tile_iters\": %u, \"k1_gate\": %u, "
       "\"md5_wgs\": %u, \"plan_mode\": %d, \"k2_own\": %d, \"k4_window\": %u, \"k3_probe\": %d, "
-      "\"lean_marks\": %u}",
+      "\"lean_marks\": %u, \"k8_split_streams\": %llu, \"k8_split_fallbacks\": %llu}",
       (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_gate, c->md5_wgs,
-      plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks);
+      plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks,
+      (unsigned long long)c->k8_split_streams, (unsigned long long)c->k8_split_fallbacks);
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }
 
@@ -2418,6 +2423,35 @@ int hbx_inflate_blocks_device(hbx_ctx* c, const void* d_in, uint64_t n, const ui
     perm[i] = (uint32_t)i;
   }
   std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) { return in_lens[a] > in_lens[b]; });
+  // a wave per stream, except for tens of thousands of short compressible
+  // streams, where 64 streams per wave (one per lane) keep more streams in
+  // flight, and for long compressible streams when few of them fill the GPU:
+  // those are split into regions decoded in parallel (hbx_inflate_split.hip).
+  // HBX_K8_MODE=lane|wave|split forces one (tests; split then takes every
+  // stream of >= 2 regions, compressible or not).
+  uint64_t tin = 0, tcap = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    tin += in_lens[i];
+    tcap += out_caps[i];
+  }
+  bool lanes = n >= 8192 && tin * 10 < tcap * 7 && tcap / n <= (256u << 10);
+  const char* mode = ab_env("HBX_K8_MODE");
+  if (mode) lanes = std::strcmp(mode, "lane") == 0;
+  const bool force_split = mode && std::strcmp(mode, "split") == 0;
+  const bool no_split = lanes || (mode && std::strcmp(mode, "wave") == 0);
+  auto splits = [&](uint32_t i) {
+    if (no_split || in_lens[i] < 2ull * hbxs::kSplitRegion) return false;
+    return force_split || in_lens[i] * 10 < out_caps[i] * 8;
+  };
+  uint64_t long_streams = 0;
+  for (uint64_t i = 0; i < n; i++) long_streams += splits(perm[i]) ? 1 : 0;
+  // enough streams to fill the SIMDs on their own: no split (it costs a
+  // second pass over 2 bytes per output byte)
+  const bool split_any = long_streams > 0 && (force_split || long_streams < 2048);
+  // split streams last, so the wave kernel takes the prefix [0, nw)
+  if (split_any)
+    std::stable_partition(perm.begin(), perm.end(), [&](uint32_t i) { return !splits(i); });
+  const uint64_t nw = split_any ? n - long_streams : n;
   std::vector<InflateDesc> desc(n);
   for (uint64_t k = 0; k < n; k++) {
     const uint32_t i = perm[k];
@@ -2431,26 +2465,82 @@ int hbx_inflate_blocks_device(hbx_ctx* c, const void* d_in, uint64_t n, const ui
   HBX_TRY(c, c->d_ires.ensure(n * 8));
   HBX_TRY(c, hipMemcpyAsync(c->d_idesc.p, desc.data(), n * sizeof(InflateDesc), hipMemcpyHostToDevice, s));
   uint32_t* dres = c->d_ires.as<uint32_t>();
-  // a wave per stream, except for tens of thousands of short compressible
-  // streams, where 64 streams per wave (one per lane) keep more streams in
-  // flight (hbx_inflate.hip); HBX_K8_MODE=lane|wave forces one (tests)
-  uint64_t tin = 0, tcap = 0;
-  for (uint64_t k = 0; k < n; k++) {
-    tin += desc[k].len;
-    tcap += desc[k].cap;
-  }
-  bool lanes = n >= 8192 && tin * 10 < tcap * 7 && tcap / n <= (256u << 10);
-  if (const char* m = ab_env("HBX_K8_MODE")) lanes = std::strcmp(m, "lane") == 0;
-  if (lanes)
-    hipLaunchKernelGGL(hbx_k8_inflate_lanes, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, s,
-                       c->d_idesc.as<InflateDesc>(), (uint32_t)n, dres, dres + n);
-  else
-    hipLaunchKernelGGL(hbx_k8_inflate, dim3((uint32_t)n), dim3(64), 0, s, c->d_idesc.as<InflateDesc>(),
-                       (uint32_t)n, dres, dres + n);
+  const InflateDesc* ddesc = c->d_idesc.as<InflateDesc>();
+  if (nw && lanes)
+    hipLaunchKernelGGL(hbx_k8_inflate_lanes, dim3((uint32_t)((nw + 63) / 64)), dim3(64), 0, s, ddesc, (uint32_t)nw,
+                       dres, dres + n);
+  else if (nw)
+    hipLaunchKernelGGL(hbx_k8_inflate, dim3((uint32_t)nw), dim3(64), 0, s, ddesc, (uint32_t)nw, dres, dres + n);
   HBX_TRY(c, hipGetLastError());
+  if (split_any) {
+    // regions of kSplitRegion compressed bytes; each gets scratch for twice
+    // its share of the stream's output capacity (a region that needs more
+    // overflows and the stream is inflated again by the wave kernel)
+    std::vector<SplitRegion> reg;
+    std::vector<uint32_t> meta(3 * (n - nw));
+    uint64_t sym = 0;
+    for (uint64_t k = nw; k < n; k++) {
+      const uint32_t cnt = (uint32_t)((desc[k].len + hbxs::kSplitRegion - 1) / hbxs::kSplitRegion);
+      const uint64_t share = (2ull * desc[k].cap + cnt - 1) / cnt;
+      const uint32_t scap = (uint32_t)std::min<uint64_t>(((share + 63) & ~63ull) + 4096, 0x7FFFFFFFull);
+      meta[k - nw] = (uint32_t)k;
+      meta[(n - nw) + (k - nw)] = (uint32_t)reg.size();
+      meta[2 * (n - nw) + (k - nw)] = cnt;
+      const uint32_t first = (uint32_t)reg.size();
+      for (uint32_t r = 0; r < cnt; r++) {
+        reg.push_back(SplitRegion{(uint32_t)k, r, first, cnt, sym, scap, 0u});
+        sym += scap;
+      }
+    }
+    const uint64_t nreg = reg.size(), ns = n - nw;
+    if (nreg > 0x7FFFFFFFull) return c->fail(HBX_ERR_ARG, "too many inflate regions");
+    HBX_TRY(c, c->d_sreg.ensure(nreg * sizeof(SplitRegion)));
+    HBX_TRY(c, c->d_sstart.ensure(nreg * 8));
+    HBX_TRY(c, c->d_sres.ensure(nreg * sizeof(SplitResult)));
+    HBX_TRY(c, c->d_sscratch.ensure(sym * 2 + 64));
+    HBX_TRY(c, c->d_smeta.ensure(meta.size() * 4));
+    HBX_TRY(c, hipMemcpyAsync(c->d_sreg.p, reg.data(), nreg * sizeof(SplitRegion), hipMemcpyHostToDevice, s));
+    HBX_TRY(c, hipMemcpyAsync(c->d_smeta.p, meta.data(), meta.size() * 4, hipMemcpyHostToDevice, s));
+    const SplitRegion* dreg = c->d_sreg.as<SplitRegion>();
+    uint64_t* dstart = c->d_sstart.as<uint64_t>();
+    SplitResult* dsres = c->d_sres.as<SplitResult>();
+    const uint32_t* dmeta = c->d_smeta.as<uint32_t>();
+    hipLaunchKernelGGL(hbx_k8s_find, dim3((uint32_t)nreg), dim3(64), 0, s, ddesc, dreg, (uint32_t)nreg, dstart);
+    hipLaunchKernelGGL(hbx_k8s_decode, dim3((uint32_t)nreg), dim3(64), 0, s, ddesc, dreg, (uint32_t)nreg,
+                       static_cast<const uint64_t*>(dstart), c->d_sscratch.as<uint16_t>(), dsres);
+    hipLaunchKernelGGL(hbx_k8s_resolve, dim3((uint32_t)ns), dim3(256), 0, s, ddesc, dmeta, dmeta + ns, dmeta + 2 * ns,
+                       (uint32_t)ns, dreg, static_cast<const uint64_t*>(dstart),
+                       static_cast<const SplitResult*>(dsres), static_cast<const uint16_t*>(c->d_sscratch.as<uint16_t>()),
+                       dres, dres + n);
+    HBX_TRY(c, hipGetLastError());
+  }
   std::vector<uint32_t> res(2 * n);
   HBX_TRY(c, hipMemcpyAsync(res.data(), dres, n * 8, hipMemcpyDeviceToHost, s));
   HBX_TRY(c, hipStreamSynchronize(s));
+  if (split_any) {  // the streams the split path did not resolve: the wave kernel, from scratch
+    std::vector<InflateDesc> again;
+    std::vector<uint64_t> at;
+    for (uint64_t k = nw; k < n; k++)
+      if (res[n + k] != 0u) {
+        again.push_back(desc[k]);
+        at.push_back(k);
+      }
+    c->k8_split_fallbacks += again.size();
+    c->k8_split_streams += n - nw;
+    if (!again.empty()) {
+      const uint64_t m = again.size();
+      HBX_TRY(c, hipMemcpyAsync(c->d_idesc.p, again.data(), m * sizeof(InflateDesc), hipMemcpyHostToDevice, s));
+      hipLaunchKernelGGL(hbx_k8_inflate, dim3((uint32_t)m), dim3(64), 0, s, ddesc, (uint32_t)m, dres, dres + m);
+      HBX_TRY(c, hipGetLastError());
+      std::vector<uint32_t> r2(2 * m);
+      HBX_TRY(c, hipMemcpyAsync(r2.data(), dres, m * 8, hipMemcpyDeviceToHost, s));
+      HBX_TRY(c, hipStreamSynchronize(s));
+      for (uint64_t q = 0; q < m; q++) {
+        res[at[q]] = r2[q];
+        res[n + at[q]] = r2[m + q];
+      }
+    }
+  }
   for (uint64_t k = 0; k < n; k++) {
     out_lens[perm[k]] = res[k];
     status[perm[k]] = res[n + k];

@@ -14,10 +14,12 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["wave", "lane"])
+@pytest.fixture(autouse=True, params=["wave", "lane", "split"])
 def k8_mode(request, monkeypatch):
-    """Both decoders: a wave per stream (the default) and a lane per stream
-    (picked for tens of thousands of short compressible streams)."""
+    """Every decoder: a wave per stream, a lane per stream (picked for tens
+    of thousands of short compressible streams) and long streams split into
+    regions decoded in parallel (hbx_inflate_split.hip; forced here for every
+    stream of >= 2 regions, compressible or not)."""
     monkeypatch.setenv("HBX_AB", "1")
     monkeypatch.setenv("HBX_K8_MODE", request.param)
     return request.param
@@ -90,3 +92,76 @@ def test_verify_compressed_blocks(engine, oracle):
     assert st.tolist() == [0] * 50
     ids, ok, bad = engine.verify_blocks(outs, links, expect=want)
     assert bad == 0 and ok.all()
+
+
+def _long_streams():
+    """Long streams the split path must resolve or hand back: zlib at levels
+    1/6/9, with periodic sync flushes (byte-aligned block starts), the device
+    deflate's own streams (sync flush after every 32 KiB piece), a run of
+    zeros (a region's symbols overflow its scratch), and half random / half
+    text (stored and Huffman blocks in one stream)."""
+    import zlib as Z
+    rng = np.random.default_rng(21)
+    datas, streams = [], []
+    for i, n in enumerate([1 << 20, 3 << 20, (5 << 20) + 12345, 700_000]):
+        d = _text(n, 100 + i)
+        for level in (1, 6, 9):
+            datas.append(d)
+            streams.append(Z.compress(d, level))
+        co = Z.compressobj(6)
+        parts = [co.compress(d[k:k + 100_000]) + co.flush(Z.Z_SYNC_FLUSH) for k in range(0, len(d), 100_000)]
+        datas.append(d)
+        streams.append(b"".join(parts) + co.flush())
+    z = bytes(4 << 20)
+    mix = rng.integers(0, 256, 1 << 20, dtype=np.uint8).tobytes() + _text(2 << 20, 7)
+    for d in (z, mix):
+        datas.append(d)
+        streams.append(Z.compress(d, 6))
+    return datas, streams
+
+
+def test_inflate_long_streams(engine):
+    datas, streams = _long_streams()
+    k7 = [_text(4 << 20, 31), _text((2 << 20) + 777, 32)]
+    datas += k7
+    streams += engine.deflate_blocks(k7)
+    outs, st = engine.inflate_blocks(streams, [len(d) for d in datas])
+    assert st.tolist() == [0] * len(datas)
+    for d, o in zip(datas, outs):
+        assert o == d
+
+
+def test_split_resolves_text_streams(engine, k8_mode):
+    """The split path must decode long zlib -6 text streams itself (the
+    engine's counters: every stream split, none handed back to the wave
+    kernel), not merely fall back."""
+    import zlib as Z
+    if k8_mode != "split":
+        pytest.skip("split mode only")
+    datas = [_text((3 << 20) + 1000 * i, 200 + i) for i in range(6)]
+    streams = [Z.compress(d, 6) for d in datas] + engine.deflate_blocks(datas[:2])
+    datas = datas + datas[:2]
+    k0 = engine.knobs()
+    outs, st = engine.inflate_blocks(streams, [len(d) for d in datas])
+    k1 = engine.knobs()
+    assert st.tolist() == [0] * len(datas)
+    assert all(o == d for d, o in zip(datas, outs))
+    assert k1["k8_split_streams"] - k0["k8_split_streams"] == len(datas)
+    assert k1["k8_split_fallbacks"] - k0["k8_split_fallbacks"] == 0, (k0, k1)
+
+
+def test_inflate_corrupt_long_streams(engine):
+    """Corrupt long streams fail with a status in every mode (the split path
+    hands them to the wave kernel, whose status is the answer)."""
+    import zlib as Z
+    d = _text(2 << 20, 41)
+    z = Z.compress(d, 6)
+    rng = np.random.default_rng(5)
+    bad = [z[:len(z) // 2], z[:-4] + bytes(4), z[:-1]]
+    for at in rng.integers(100, len(z) - 100, 6):
+        bad.append(z[:int(at)] + bytes([z[int(at)] ^ 0x5A]) + z[int(at) + 1:])
+    outs, st = engine.inflate_blocks(bad + [z], [len(d)] * (len(bad) + 1))
+    assert st[-1] == 0 and outs[-1] == d
+    for b, s_, o in zip(bad, st[:-1], outs[:-1]):
+        assert s_ != 0 or o == d, "a corrupt stream inflated to different data with status 0"
+    assert all(s_ != 0 for s_ in st[:3])

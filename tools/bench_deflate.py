@@ -96,7 +96,8 @@ def run_corpus(eng, torch, name, host_or_dev, file_bytes, nfiles, sample, thread
     t0 = time.perf_counter()
     OD.inflate_mt([host_out[int(o_off[i]): int(o_off[i] + lens[i])].tobytes() for i in pick], threads)
     t_cinf = time.perf_counter() - t0
-    return {
+    zl = inflate_zlib6(eng, torch, host_in, c_off, c_len, threads) if name == "text" else None
+    out = {
         "inflate_device": {"seconds": round(t_inf, 4), "gbs_out": round(total_in / t_inf / 1e9, 2),
                            "streams": int(c_off.size), "failures_or_mismatches": ibad,
                            "cpu_zlib_inflate_gbs_out": round(s_in / t_cinf / 1e9, 3), "cpu_threads": threads},
@@ -108,6 +109,49 @@ def run_corpus(eng, torch, name, host_or_dev, file_bytes, nfiles, sample, thread
         "cpu_zlib6": {"threads": threads, "ratio": round(sum(map(len, ref)) / s_in, 4),
                       "gbs": round(s_in / t_cpu / 1e9, 3), "sample_bytes": s_in},
     }
+    if zl is not None:
+        out["inflate_zlib6_device"] = zl
+    return out
+
+
+def inflate_zlib6(eng, torch, host_in, c_off, c_len, threads):
+    """Every chunk of the corpus compressed by CPython zlib -6 (the stand-in
+    for Go's compress/zlib DefaultCompression, block.go:216), inflated on the
+    device in one call (K8: long streams split into regions, K8s) and by
+    CPython on `threads`; every stream checked."""
+    from oracle import deflate as OD
+    blocks = [host_in[int(o): int(o + n)].tobytes() for o, n in zip(c_off, c_len)]
+    zs = OD.compress_ref_mt(blocks, threads)
+    io = np.zeros(len(zs), np.uint64)
+    io[1:] = np.cumsum([(len(z) + 15) // 16 * 16 for z in zs[:-1]])
+    host = np.zeros(int(io[-1]) + len(zs[-1]) + 64, np.uint8)
+    for o, z in zip(io, zs):
+        host[int(o):int(o) + len(z)] = np.frombuffer(z, np.uint8)
+    d_in = torch.from_numpy(host).to("cuda:0")
+    caps = np.asarray(c_len, np.uint64)
+    oo = np.zeros_like(caps)
+    oo[1:] = np.cumsum(caps[:-1])
+    d_out = torch.empty(int(caps.sum()) + 64, dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()
+    k0 = eng.knobs()
+    times = []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        ol, st = eng.inflate_blocks_device(d_in.data_ptr(), io, [len(z) for z in zs], d_out.data_ptr(), oo, caps)
+        times.append(time.perf_counter() - t0)
+    k1 = eng.knobs()
+    back = d_out.cpu().numpy()
+    bad = int((st != 0).sum()) + sum(back[int(o):int(o) + len(b)].tobytes() != b for o, b in zip(oo, blocks))
+    t0 = time.perf_counter()
+    OD.inflate_mt(zs, threads)
+    t_cpu = time.perf_counter() - t0
+    total = int(caps.sum())
+    return {"streams": len(zs), "bytes_out": total, "compressed_bytes": int(sum(map(len, zs))),
+            "seconds": round(min(times), 4), "gbs_out": round(total / min(times) / 1e9, 2),
+            "failures_or_mismatches": bad,
+            "split_streams": (k1["k8_split_streams"] - k0["k8_split_streams"]) // 2,
+            "split_fallbacks": (k1["k8_split_fallbacks"] - k0["k8_split_fallbacks"]) // 2,
+            "cpu_zlib_inflate": {"threads": threads, "gbs_out": round(total / t_cpu / 1e9, 3)}}
 
 
 def main():
