@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round 4: K8s first (inflate tests in every mode, the deflate/inflate bench),
-# then the final-tree evidence (tools/gpu_r04_final.sh: suite, smoke, bench,
-# rocprof, configs).
+# then the final tree's suite, smoke and the driver's bench command.  The
+# rocprof evidence and the configs follow in tools/gpu_r04e.sh (the 1,200 s
+# limit per call).
 set -o pipefail
 O=gpurun_out/r04d
 mkdir -p $O
@@ -9,4 +10,4 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_inflate.py -x -v --timeout 
 tail -2 $O/pytest_inflate.log
 timeout -k 10 400 python tools/bench_deflate.py > $O/deflate.json 2> $O/deflate.err || { tail -5 $O/deflate.err; exit 1; }
 python3 -c "import json;d=json.load(open('$O/deflate.json'));print(d['text']['inflate_device'], d['text'].get('inflate_zlib6_device'))"
-TAG=r04z bash tools/gpu_r04_final.sh
+TAG=r04z bash tools/gpu_round_final.sh
