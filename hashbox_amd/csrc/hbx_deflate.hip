@@ -597,6 +597,112 @@ __device__ __forceinline__ uint32_t zblock_of(const hbxz::ZBlock* blocks, uint32
   return lo;
 }
 
+namespace hbxz {
+constexpr uint32_t kModeSrcStored = 3u;    // SegInfo.mode: stored, K7b copies the bytes from the source
+constexpr uint32_t kModeParse = 0xFFu;     // SegInfo.mode set by K7e: K7a decides
+constexpr uint32_t kEThreads = 256;
+}  // namespace hbxz
+
+// K7e, the incompressible early-out on its own (round 4): one 256-thread
+// workgroup per segment and 9 KiB of LDS (six per CU instead of K7a's one),
+// reading the segment straight from global memory.  The same rule as K7a's
+// step 0: a segment of >= 4096 bytes whose order-0 entropy is >= 7.97 bits
+// per byte and whose content-sampled 4-byte values never repeat is stored:
+// info[g] = {5 + n, kModeSrcStored, Adler partials}, and K7b copies its bytes
+// from the source (no image in the scratch).  Every other segment gets
+// kModeParse and goes through K7a.  (Random data: K7a's one 162 KB workgroup
+// per CU ran the early-out phases back to back, 241 GB/s.)
+extern "C" __global__ __launch_bounds__(256) void hbx_k7_deflate_entropy(const hbxz::ZBlock* __restrict__ blocks,
+                                                                         uint32_t nb, uint32_t nseg,
+                                                                         hbxz::SegInfo* __restrict__ info) {
+  using namespace hbxz;
+  __shared__ uint32_t cnt[256];
+  __shared__ uint32_t set[kRepSet];
+  __shared__ uint32_t wred[kEThreads / 64][3];
+  __shared__ uint32_t rep_any;
+  const uint32_t g = blockIdx.x;
+  if (g >= nseg) return;
+  const ZBlock bk = blocks[zblock_of(blocks, nb, g)];
+  const uint32_t s = g - bk.seg0;
+  const uint64_t off = (uint64_t)s * kSeg;
+  const uint32_t n = (uint32_t)min((uint64_t)kSeg, bk.len - off);
+  const uint32_t t = threadIdx.x;
+  if (n < 4096u) {
+    if (t == 0) info[g].mode = kModeParse;
+    return;
+  }
+  const uint64_t a = bk.src + off;
+  const uint32_t sh = (uint32_t)(a & 3u);
+  const uint32_t* base = reinterpret_cast<const uint32_t*>(a - sh);
+  const uint32_t nw = (n + sh + 3u) >> 2;  // words holding a byte of the segment
+  for (uint32_t k = t; k < 256u; k += kEThreads) cnt[k] = 0u;
+  for (uint32_t k = t; k < kRepSet; k += kEThreads) set[k] = 0u;
+  if (t == 0) rep_any = 0u;
+  __syncthreads();
+  auto sample = [&](uint32_t x) -> bool {  // (K7a's step 0)
+    if (zhash(x) & 63u) return false;
+    const uint32_t key = x + 1u ? x + 1u : 1u;
+    const uint32_t i0 = (x * 0x85EBCA6Bu) >> (32 - 11);
+    for (uint32_t r = 0; r < 8u; r++) {
+      const uint32_t old = atomicCAS(&set[(i0 + r) & (kRepSet - 1u)], 0u, key);
+      if (old == 0u) return false;
+      if (old == key) return true;
+    }
+    return false;
+  };
+  // thread t: aligned words k = t, t + 256, ...; positions p = 4k + j - sh
+  uint64_t A = 0ull, J = 0ull;
+  bool rep = false;
+  for (uint32_t k = t; k < nw; k += kEThreads) {
+    const uint32_t w0 = base[k], w1 = k + 1u < nw ? base[k + 1u] : 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < 4u; j++) {
+      const int64_t p = 4ll * k + j - sh;
+      if (p < 0 || p >= (int64_t)n) continue;
+      const uint32_t x = __builtin_amdgcn_alignbyte(w1, w0, j);
+      const uint32_t b = x & 0xFFu;
+      atomicAdd(&cnt[b], 1u);
+      A += b;
+      J += (uint64_t)p * b;
+      if ((uint32_t)p + 4u <= n) rep |= sample(x);
+    }
+  }
+  if (rep) rep_any = 1u;
+  __syncthreads();
+  // per-symbol bits rounded, summed over the workgroup (K7a's formula)
+  const uint32_t c = cnt[t];
+  uint32_t bits = c ? (uint32_t)((float)c * (__log2f((float)n) - __log2f((float)c)) + 0.5f) : 0u;
+  uint64_t A64 = A, J64 = J;
+  for (int d = 32; d >= 1; d >>= 1) {
+    bits += (uint32_t)__shfl_xor((int)bits, d);
+    A64 += (unsigned long long)__shfl_xor((long long)A64, d);
+    J64 += (unsigned long long)__shfl_xor((long long)J64, d);
+  }
+  __shared__ unsigned long long wad[kEThreads / 64][2];
+  if ((t & 63u) == 0u) {
+    wred[t >> 6][0] = bits;
+    wad[t >> 6][0] = A64;
+    wad[t >> 6][1] = J64;
+  }
+  __syncthreads();
+  if (t == 0) {
+    uint32_t hsum = 0u;
+    unsigned long long As = 0, Js = 0;
+    for (uint32_t w = 0; w < kEThreads / 64; w++) {
+      hsum += wred[w][0];
+      As += wad[w][0];
+      Js += wad[w][1];
+    }
+    const bool incompressible = (float)hsum >= 7.97f * (float)n && rep_any == 0u;
+    SegInfo si;
+    si.mode = incompressible ? kModeSrcStored : kModeParse;
+    si.bytes = 5u + n;
+    si.a = (uint32_t)(As % kAdlerMod);
+    si.b = (uint32_t)(((unsigned long long)n * As - Js) % kAdlerMod);
+    info[g] = si;
+  }
+}
+
 extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz::ZBlock* __restrict__ blocks,
                                                                        uint32_t nb, uint32_t nseg,
                                                                        hbxz::SegInfo* __restrict__ info,
@@ -614,7 +720,7 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
   __shared__ __attribute__((aligned(4))) uint8_t zl[320];
   __shared__ uint8_t cll[20];
   const uint32_t g = blockIdx.x;
-  if (g >= nseg) return;
+  if (g >= nseg || info[g].mode == kModeSrcStored) return;  // stored by K7e
   K7P(0);
   const ZBlock bk = blocks[zblock_of(blocks, nb, g)];
   const uint32_t s = g - bk.seg0;
@@ -1171,13 +1277,43 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k7_deflate_plan(const hbxz:
 extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_write(uint32_t nseg,
                                                                         const hbxz::SegInfo* __restrict__ info,
                                                                         const uint32_t* __restrict__ scratch,
-                                                                        const uint64_t* __restrict__ seg_off) {
+                                                                        const uint64_t* __restrict__ seg_off,
+                                                                        const hbxz::ZBlock* __restrict__ blocks,
+                                                                        uint32_t nb) {
   using namespace hbxz;
   __shared__ uint32_t img[kImgWords + 2];
   const uint32_t g = blockIdx.x;
   if (g >= nseg) return;
   const uint32_t t = threadIdx.x;
-  const uint32_t nbytes = info[g].bytes;
+  const SegInfo si = info[g];
+  const uint32_t nbytes = si.bytes;
+  if (si.mode == kModeSrcStored) {  // 00 | LEN | ~LEN | the segment's bytes, straight from the source
+    const ZBlock bk = blocks[zblock_of(blocks, nb, g)];
+    const uint32_t n = nbytes - 5u;
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(bk.src) + (uint64_t)(g - bk.seg0) * kSeg;
+    uint8_t* D = reinterpret_cast<uint8_t*>(seg_off[g]);
+    const uint8_t hdr[5] = {0u, (uint8_t)n, (uint8_t)(n >> 8), (uint8_t)~n, (uint8_t)(~n >> 8)};
+    auto byte_at = [&](uint32_t q) -> uint32_t { return q < 5u ? hdr[q] : src[q - 5u]; };
+    const uint32_t lead = (uint32_t)((4u - (reinterpret_cast<uint64_t>(D) & 3u)) & 3u);
+    const uint32_t head = min(lead, nbytes);
+    if (t < head) D[t] = (uint8_t)byte_at(t);
+    const uint32_t nw = (nbytes - head) >> 2;
+    uint32_t* Dw = reinterpret_cast<uint32_t*>(D + head);
+    for (uint32_t k = t; k < nw; k += kThreads) {
+      const uint32_t q = head + 4u * k;
+      uint32_t w;
+      if (q >= 5u) {  // four source bytes at any alignment (the hardware splits the load)
+        w = *reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(
+            reinterpret_cast<uintptr_t>(src + (q - 5u)));
+      } else {
+        w = byte_at(q) | (byte_at(q + 1u) << 8) | (byte_at(q + 2u) << 16) | (byte_at(q + 3u) << 24);
+      }
+      Dw[k] = w;
+    }
+    const uint32_t done = head + 4u * nw;
+    if (t < nbytes - done) D[done + t] = (uint8_t)byte_at(done + t);
+    return;
+  }
   const uint32_t* slot = scratch + (uint64_t)g * kImgWords;
   for (uint32_t k = t; k < kImgWords + 2u; k += kThreads) img[k] = k < (nbytes + 3u) / 4u ? slot[k] : 0u;
   __syncthreads();

@@ -1754,6 +1754,8 @@ int z_start(hbx_ctx* c, ZPend& zp, const uint64_t* cut_ends, const uint64_t* out
   hipStream_t s = Z.stream;
   HBX_TRY(c, hipMemcpyAsync(Z.blk.p, Z.desc.p, n * sizeof(hbxz::ZBlock), hipMemcpyHostToDevice, s));
   const hbxz::ZBlock* dz = Z.blk.as<hbxz::ZBlock>();
+  hipLaunchKernelGGL(hbx_k7_deflate_entropy, dim3((uint32_t)nseg), dim3(hbxz::kEThreads), 0, s, dz, (uint32_t)n,
+                     (uint32_t)nseg, Z.info.as<hbxz::SegInfo>());
   hipLaunchKernelGGL(hbx_k7_deflate_size, dim3((uint32_t)nseg), dim3(hbxz::kThreads), 0, s, dz, (uint32_t)n,
                      (uint32_t)nseg, Z.info.as<hbxz::SegInfo>(), Z.img.as<uint32_t>());
   HBX_TRY(c, hipGetLastError());
@@ -1761,7 +1763,7 @@ int z_start(hbx_ctx* c, ZPend& zp, const uint64_t* cut_ends, const uint64_t* out
                      Z.info.as<hbxz::SegInfo>(), Z.off.as<uint64_t>(), Z.len.as<uint64_t>());
   HBX_TRY(c, hipGetLastError());
   hipLaunchKernelGGL(hbx_k7_deflate_write, dim3((uint32_t)nseg), dim3(hbxz::kThreads), 0, s, (uint32_t)nseg,
-                     Z.info.as<hbxz::SegInfo>(), Z.img.as<uint32_t>(), Z.off.as<uint64_t>());
+                     Z.info.as<hbxz::SegInfo>(), Z.img.as<uint32_t>(), Z.off.as<uint64_t>(), dz, (uint32_t)n);
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipMemcpyAsync(Z.lens.p, Z.len.p, n * 8, hipMemcpyDeviceToHost, s));
   HBX_TRY(c, hipMemcpyAsync(Z.stage.p, Z.out.p, d, hipMemcpyDeviceToHost, s));
@@ -2288,6 +2290,8 @@ int deflate_device(hbx_ctx* c, uint64_t n, const uint64_t* src, const uint64_t* 
   HBX_TRY(c, hipMemcpyAsync(c->d_zblk.p, zb.data(), n * sizeof(hbxz::ZBlock), hipMemcpyHostToDevice, s));
   const hbxz::ZBlock* dz = c->d_zblk.as<hbxz::ZBlock>();
   if (nseg) {
+    hipLaunchKernelGGL(hbx_k7_deflate_entropy, dim3((uint32_t)nseg), dim3(hbxz::kEThreads), 0, s, dz, (uint32_t)n,
+                       (uint32_t)nseg, c->d_zinfo.as<hbxz::SegInfo>());
     hipLaunchKernelGGL(hbx_k7_deflate_size, dim3((uint32_t)nseg), dim3(hbxz::kThreads), 0, s, dz, (uint32_t)n,
                        (uint32_t)nseg, c->d_zinfo.as<hbxz::SegInfo>(), c->d_zimg.as<uint32_t>());
     HBX_TRY(c, hipGetLastError());
@@ -2297,7 +2301,8 @@ int deflate_device(hbx_ctx* c, uint64_t n, const uint64_t* src, const uint64_t* 
   HBX_TRY(c, hipGetLastError());
   if (nseg) {
     hipLaunchKernelGGL(hbx_k7_deflate_write, dim3((uint32_t)nseg), dim3(hbxz::kThreads), 0, s, (uint32_t)nseg,
-                       c->d_zinfo.as<hbxz::SegInfo>(), c->d_zimg.as<uint32_t>(), c->d_zoff.as<uint64_t>());
+                       c->d_zinfo.as<hbxz::SegInfo>(), c->d_zimg.as<uint32_t>(), c->d_zoff.as<uint64_t>(), dz,
+                       (uint32_t)n);
     HBX_TRY(c, hipGetLastError());
   }
   HBX_TRY(c, hipMemcpyAsync(out_lens, c->d_zlen.p, n * 8, hipMemcpyDeviceToHost, s));

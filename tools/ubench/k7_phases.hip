@@ -55,6 +55,7 @@ int main(int argc, char** argv) {
   (void)hipMalloc(&d_info, nseg * sizeof(hbxz::SegInfo));
   (void)hipMalloc(&d_img, (size_t)nseg * hbxz::kSlot);
   (void)hipMemcpy(d_zb, zb.data(), zb.size() * sizeof(hbxz::ZBlock), hipMemcpyHostToDevice);
+  (void)hipMemset(d_info, 0, nseg * sizeof(hbxz::SegInfo));  // no K7e pass: every segment through K7a
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
