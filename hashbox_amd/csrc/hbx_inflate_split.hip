@@ -253,7 +253,7 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k8s_find(const InflateDesc*
 
 namespace hbxs {
 
-struct SplitLds {
+struct alignas(16) SplitLds {
   uint16_t ring[kRing];
   uint8_t in[kInBuf + 16];
   Code lc, dc;
