@@ -27,34 +27,40 @@
 // K7b hbx_k7_deflate_write  per segment: its image from the slot to the
 //                           stream at its byte offset
 //
-// The LZ77 parse (one 512-thread workgroup per 32 KiB segment, all in LDS):
-//   1. candidates, in position order.  The history's positions are inserted
-//      first, then round r covers segment positions 512r..512r+511 (thread t:
-//      512r+t).  A 2048-bucket hash table of 4-byte prefixes keeps each
-//      bucket's 8 latest positions (a 16-bit counter per bucket picks the
-//      slot; one barrier per round, so a slot may already hold a later
-//      position of the same round, which is skipped).  Each position keeps
-//      the longest verified match among its <= 8 candidates within 32 KiB
-//      (as a distance).
-//   2. the parse, greedy with one-step lazy matching (a longer match at p+1
-//      defers p as a literal, as zlib's lazy matching does).  Thread t owns
-//      the 64-byte range [64t, 64t+64) but a match may run past its end (up
-//      to 258 bytes), and the next thread then starts where it ended: every
-//      thread first parses from its range start ("dry", no writes), the ends
-//      are handed on, and threads whose start moved parse again, until no
-//      start moves (greedy parses resynchronise within a few tokens, so this
-//      takes one or two rounds; after 8 the last starts are kept and each
-//      thread's final parse is clipped to its successor's start, which keeps
-//      the stream exact either way).  The final parse records the tokens,
-//      symbol frequencies and fixed-code bits;
+// The LZ77 parse (one 1024-thread workgroup per 32 KiB segment):
+//   1. candidates, in position order.  The 32 KiB of the block before the
+//      segment (its history) are inserted first, then round r covers
+//      segment positions 512r..512r+511, two adjacent threads per position
+//      (four bucket entries each, the better of the two kept).  A 4096-bucket
+//      hash table of 4-byte prefixes keeps each bucket's 8 latest positions
+//      (a 16-bit counter per bucket picks the slot; one barrier per round,
+//      so a slot may already hold a later position of the same round, which
+//      is skipped).  Each position keeps the longest verified match among its
+//      <= 8 candidates within 32 KiB, nearest first on a tie, and drops a
+//      4-byte one farther than kFar4: its distance (u16) and length (u8) go
+//      to the segment's scratch slot, because the table and 96 KiB of
+//      per-position results do not fit the LDS together; they come back into
+//      the table's and the history's LDS once the table is done.
+//   2. the parse, greedy with two-step lazy matching (a longer match at p+1,
+//      or one longer by 2 at p+2, defers p as a literal; zlib's lazy matching
+//      looks one step ahead), from the stored lengths alone (no byte
+//      compares).  Thread t < 512 owns the 64-byte range [64t, 64t+64) but a
+//      match may run past its end (up to 258 bytes), and the next thread then
+//      starts where it ended: every thread first parses from its range start
+//      ("dry", no writes), the ends are handed on, and threads whose start
+//      moved parse again, until no start moves (greedy parses resynchronise
+//      within a few tokens, so this takes one or two rounds; after 8 the
+//      starts are made ascending and each thread's final parse is clipped to
+//      its successor's start, which keeps the stream exact either way).  The
+//      final parse records the tokens, symbol frequencies and fixed-code bits;
 //   3. after a workgroup prefix sum of the bit counts, the tokens are emitted
-//      (ds_or) into the image, if that is smaller than stored.
-// Versus the round-2 parse (32 KiB window starting at the segment, 4 latest
-// positions per bucket residue, matches clipped at the 64-byte range end) the
-// Zipf-text corpus of tools/bench_deflate.py compresses to ~0.325 of its size
-// instead of 0.368 (zlib -6: 0.311); tools/k7model/k7model.c models both
-// (history 16 KiB: 0.329 modelled, 12 KiB 0.331, none 0.372 = round 2's
-// 0.368 measured).  LDS: 162.6 of the CU's 160 KiB = 163,840 bytes.
+//      (ds_or) into the image (over the window's LDS), if that is smaller than
+//      stored; a stored segment is copied by K7b from the source.
+// Zipf text of tools/bench_deflate.py: 0.3162 of its size at 20.9 GB/s (round
+// 3: 0.327 at 16.0 GB/s with 8 ways of 2,048 buckets, 16 KiB of history and
+// one-step lazy matching; zlib -6: 0.311).  tools/k7model/k7model.c models
+// the variants (32 ways of 1,024 buckets reach 0.3103 measured, at 7.6 GB/s).
+// LDS: 150.5 of the CU's 160 KiB.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -64,16 +70,19 @@
 namespace hbxz {
 
 constexpr uint32_t kSeg = 32768;  // bytes per segment (one workgroup)
-constexpr uint32_t kThreads = 512;
+constexpr uint32_t kThreads = 1024;  // K7a
 constexpr uint32_t kWaves = kThreads / 64;
-constexpr uint32_t kSub = kSeg / kThreads;  // 64 bytes per thread in the parse
-constexpr uint32_t kHashBits = 11;
+constexpr uint32_t kPair = 2;                // threads per position in the candidate rounds
+constexpr uint32_t kRound = kThreads / kPair;  // positions per candidate round
+constexpr uint32_t kParse = 512;            // parse ranges (threads t >= kParse have empty ones)
+constexpr uint32_t kSub = kSeg / kParse;    // 64 bytes per range
+constexpr uint32_t kWThreads = 512;         // K7b
+constexpr uint32_t kHashBits = 12;
 constexpr uint32_t kWays = 8;                 // positions kept per bucket (16-bit entries)
-constexpr uint32_t kHist = 16384;             // history bytes before a segment (within its block)
+constexpr uint32_t kHist = 32768;             // history bytes before a segment (within its block)
 constexpr uint32_t kHistWords = kHist / 4;
 constexpr uint32_t kWindow = 32768;           // deflate's largest distance
 constexpr uint32_t kParseRounds = 8;          // bound on the start hand-off rounds
-constexpr uint32_t kNice = 128;               // stop looking for a longer match at this length (zlib -6)
 constexpr uint32_t kRepSet = 2048;            // slots of the early-out's repeat sample set
 constexpr uint32_t kDataWords = kSeg / 4 + 8;        // + slack for the 16-byte reads past the end
 // The segment and the candidate array live in LDS with one pad dword per
@@ -85,12 +94,22 @@ constexpr uint32_t kCdShift = 31 - __builtin_clz(kSub / 2);
 constexpr uint32_t kDataPhys = kDataWords + (kDataWords >> kDataShift) + 1;
 constexpr uint32_t kCdPhys = (kSeg / 2 + (kSeg / 2 >> kCdShift)) * 2;  // u16 slots
 constexpr uint32_t kImgWords = (kSeg + 16) / 4 + 4;  // stored image (5 + kSeg) or a smaller fixed one
-// hash table: 2048 x 8 u16 entries (window position + 1), then 2048 u16
-// counters, in the region later reused for the Huffman scratch and the image
+// hash table: 4096 x 8 u16 entries (window position + 1), then 4096 u16
+// counters, in the region that holds the candidate distances after step 1
 constexpr uint32_t kTabWords = (1u << kHashBits) * kWays / 2 + (1u << kHashBits) / 2;
-constexpr uint32_t kSlot = kImgWords * 4;  // scratch bytes per segment
+// scratch bytes per segment: the candidate distances (u16 per position) and
+// their match lengths (u8 per position, length - 3, 0 = none) between steps 1
+// and 2, then the coded image
+constexpr uint32_t kSlot = 3u * kSeg;
+constexpr uint32_t kSlotLens = 2u * kSeg;  // byte offset of the lengths
+static_assert(kSlot >= kImgWords * 4u, "the image fits its slot");
+constexpr uint32_t kTabLds = kTabWords > kCdPhys / 2u ? kTabWords : kCdPhys / 2u;  // table, then distances
+// window positions + 1 are u16 entries, and a bucket's u16 insert counter
+// never carries into its neighbour's
+static_assert(kHist + kSeg <= 65536u, "window positions fit 16 bits");
 constexpr uint32_t kAdlerMod = 65521;
 constexpr uint32_t kLazy = 32;  // no look-ahead past a match this long
+constexpr uint32_t kFar4 = 1024;  // farthest 4-byte match kept
 
 struct SegInfo {
   uint32_t bytes;  // coded bytes of the segment (stored or fixed image)
@@ -121,7 +140,17 @@ __device__ __forceinline__ uint32_t cphys(uint32_t p) {
   return 2u * (wd + (wd >> kCdShift)) + (p & 1u);
 }
 
+// The match lengths in LDS (over the history's words once step 1 is done):
+// byte p of word (p / 4) XOR-swizzled within each 16-word group, so the 64
+// lanes of a wave, whose ranges start 64 bytes apart, hit different banks.
+__device__ __forceinline__ uint32_t lphys(uint32_t p) {
+  const uint32_t w = p >> 2;
+  return ((w ^ ((w >> 4) & 15u)) << 2) | (p & 3u);
+}
+
 __device__ __forceinline__ uint32_t zhash(uint32_t x) { return (x * 0x9E3779B1u) >> (32 - kHashBits); }
+// K7e's content-defined sample (1 in 64 four-byte values)
+__device__ __forceinline__ bool sampled(uint32_t x) { return ((x * 0x9E3779B1u) >> 21 & 63u) == 0u; }
 
 // Fixed-code tables (RFC 1951 §3.2.5-3.2.6), as (reversed code | extra << n, n).
 __device__ __forceinline__ uint32_t rev(uint32_t c, uint32_t n) { return __builtin_bitreverse32(c) >> (32u - n); }
@@ -277,7 +306,7 @@ __device__ __forceinline__ void dist_sym(uint32_t dist, uint32_t& sym, uint32_t&
   }
 }
 
-// Step 2: the greedy parse of one thread, one-step lazy, with the candidate
+// Step 2: the greedy parse of one thread, two-step lazy, with the candidate
 // distances in `cd` (d = 0: none).  Dry (REC = false): from s while p < rend
 // (the thread's range end), matches up to min(258, n - p); returns where the
 // last token ends, which may be past rend.  Final (REC = true): from s while
@@ -285,18 +314,26 @@ __device__ __forceinline__ void dist_sym(uint32_t dist, uint32_t& sym, uint32_t&
 // overwrite the candidate slots they cover (already consumed): a literal at p
 // is 0x8000 | byte in slot p; a match is len in slot p and dist in slot p+1.
 // Symbol frequencies go to hll/hd; `bits` = fixed-code bits, `extra` = extra
-// bits (the same under any code).  Lookahead only while p + 1 < rend, in both
-// passes, so a converged final parse repeats the dry one token for token.
+// bits (the same under any code).  Lookahead to p + 1 and p + 2 only while
+// that is < rend, in both passes, so a converged final parse repeats the dry
+// one token for token (and never reads a slot past the thread's own range,
+// since its tokens end at or past rend).
 // The dry pass also returns its token starts as a mask over the thread's
 // 64-byte range (bit i = a token starts at range start + i): a token of one
 // byte is a literal, a longer one the match of that length at distance cd[p].
 template <bool REC>
-__device__ __forceinline__ uint32_t parse(const uint32_t* hist, const uint32_t* data, uint32_t hw, uint16_t* cd,
-                                          uint32_t* hll, uint32_t* hd, uint32_t sh, uint32_t hl, uint32_t n,
-                                          uint32_t s, uint32_t rend, uint32_t send, uint32_t& bits,
-                                          uint32_t& extra, uint64_t* starts_mask = nullptr, uint32_t r0 = 0u) {
+__device__ __forceinline__ uint32_t parse(const uint32_t* data, const uint8_t* l8, uint16_t* cd, uint32_t* hll,
+                                          uint32_t* hd, uint32_t sh, uint32_t n, uint32_t s, uint32_t rend,
+                                          uint32_t send, uint32_t& bits, uint32_t& extra,
+                                          uint64_t* starts_mask = nullptr, uint32_t r0 = 0u) {
   const uint32_t stop = REC ? send : rend;
   const uint32_t cap = REC ? send : n;
+  // the match at q, at most cap - q long (step 1 measured it up to
+  // min(258, n - q); cap <= n, so the clip equals a compare up to the clip)
+  auto len_at = [&](uint32_t q) -> uint32_t {
+    const uint32_t v = l8[lphys(q)];
+    return v ? min(v + 3u, cap - q) : 0u;
+  };
   uint32_t p = s, len = 0u, d = 0u;
   bits = 0u;
   extra = 0u;
@@ -306,15 +343,20 @@ __device__ __forceinline__ uint32_t parse(const uint32_t* hist, const uint32_t* 
     if (!REC) mask |= 1ull << (p - r0);
     if (!have) {
       d = cd[cphys(p)];
-      len = d ? match_len(hist, data, hw, sh, p, p + hl - d, min(258u, cap - p)) : 0u;
+      len = d ? len_at(p) : 0u;
     }
     have = false;
     bool defer = false;
     uint32_t len1 = 0u, d1 = 0u;
     if (len >= 4u && len < kLazy && p + 1u < rend) {
       d1 = cd[cphys(p + 1u)];
-      len1 = d1 ? match_len(hist, data, hw, sh, p + 1u, p + 1u + hl - d1, min(258u, cap - p - 1u)) : 0u;
+      len1 = d1 ? len_at(p + 1u) : 0u;
       defer = len1 > len;  // lazy: p becomes a literal, the longer match starts at p + 1
+      if (!defer && p + 2u < rend) {
+        // second step: a match at p + 2 longer than len + 1 also defers p
+        // (p + 1 then defers to it in turn)
+        defer = len_at(p + 2u) > len + 1u;
+      }
     }
     if (len >= 4u && !defer) {
       if (REC) {
@@ -640,7 +682,7 @@ extern "C" __global__ __launch_bounds__(256) void hbx_k7_deflate_entropy(const h
   if (t == 0) rep_any = 0u;
   __syncthreads();
   auto sample = [&](uint32_t x) -> bool {  // (K7a's step 0)
-    if (zhash(x) & 63u) return false;
+    if (!sampled(x)) return false;
     const uint32_t key = x + 1u ? x + 1u : 1u;
     const uint32_t i0 = (x * 0x85EBCA6Bu) >> (32 - 11);
     for (uint32_t r = 0; r < 8u; r++) {
@@ -703,24 +745,30 @@ extern "C" __global__ __launch_bounds__(256) void hbx_k7_deflate_entropy(const h
   }
 }
 
-extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz::ZBlock* __restrict__ blocks,
+extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size(const hbxz::ZBlock* __restrict__ blocks,
                                                                        uint32_t nb, uint32_t nseg,
                                                                        hbxz::SegInfo* __restrict__ info,
                                                                        uint32_t* __restrict__ scratch) {
   using namespace hbxz;
-  __shared__ uint32_t win[kHistWords + kDataPhys];  // history words, then the segment's
+  // history words, then the segment's; after the parse, the Huffman scratch
+  // and then the coded image
+  __shared__ uint32_t win[kHistWords + kDataPhys];
   uint32_t* const hist = win;
   uint32_t* const data = win + kHistWords;
-  __shared__ uint32_t tab[kTabWords > kImgWords ? kTabWords : kImgWords];  // hash table, then the image
-  __shared__ uint16_t cd[kCdPhys];
+  // the hash table (step 1), then the candidate distances (steps 2-3)
+  __shared__ uint32_t tab[kTabLds];
+  uint16_t* const cd = reinterpret_cast<uint16_t*>(tab);
   __shared__ uint32_t starts[kThreads + 1];  // each thread's parse start (step 2)
   __shared__ uint32_t wsum[kWaves];
   __shared__ unsigned long long wadler[2 * kWaves];
   __shared__ uint32_t hll[288], hd[32], llc[288], dcc[32], rle[320], clf[19], clc[19], zpar[8], zctl[8];
   __shared__ __attribute__((aligned(4))) uint8_t zl[320];
   __shared__ uint8_t cll[20];
+  static_assert(kImgWords <= kHistWords + kDataPhys, "the image fits the window's LDS");
   const uint32_t g = blockIdx.x;
-  if (g >= nseg || info[g].mode == kModeSrcStored) return;  // stored by K7e
+  // K7e ran first: its stored segments are done (the early-out of step 0 in
+  // rounds 1-3 lives there now), every other segment is parsed
+  if (g >= nseg || info[g].mode == kModeSrcStored) return;
   K7P(0);
   const ZBlock bk = blocks[zblock_of(blocks, nb, g)];
   const uint32_t s = g - bk.seg0;
@@ -731,81 +779,36 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
   const uint8_t* seg_src = reinterpret_cast<const uint8_t*>(bk.src) + off;
   load_segment(data, seg_src, n, sh);
   // history: the kHist bytes of the block before this segment (word j holds
-  // window bytes [4j - sh, 4j - sh + 4), like the segment's words), loaded
-  // only for a segment that is parsed (after the early-out below)
+  // window bytes [4j - sh, 4j - sh + 4), like the segment's words); segment
+  // s >= 1 starts kSeg = kHist bytes into its block
+  static_assert(kHist <= kSeg, "a segment's history lies in its block");
   const uint32_t hl = s ? kHist : 0u, hw = hl / 4u;
+  if (hl) {
+    const uint32_t* hb = reinterpret_cast<const uint32_t*>(seg_src - sh - hl);
+    for (uint32_t k = t; k < hw; k += kThreads) hist[k] = hb[k];
+  }
   for (uint32_t k = t; k < kTabWords; k += kThreads) tab[k] = 0u;
   for (uint32_t k = t; k < 288u; k += kThreads) hll[k] = k == 256u ? 1u : 0u;  // EOB once
   for (uint32_t k = t; k < 32u; k += kThreads) hd[k] = 0u;
   __syncthreads();
 
   K7P(1);
-  // 0. incompressible segments: the order-0 entropy of the bytes.  At >= 7.97
-  //    bits per byte no Huffman code beats a stored block, and unless the
-  //    window repeats itself the parse (steps 1-2) would find nothing either:
-  //    the segment is stored.  Repeats are detected by content-defined
-  //    sampling: every window position whose 4-byte prefix hashes to 0 mod 64
-  //    goes into a small set, and a second occurrence of the same 4 bytes
-  //    (random data repeating within the segment samples the same positions
-  //    of both copies) keeps the full parse.  Random data without repeats
-  //    puts ~510 samples into the set, colliding in 32 bits with probability
-  //    < 1e-4 (which only costs the parse).  Only the segment is sampled, not
-  //    its history: a repeat whose source lies only in the 16 KiB before the
-  //    segment is not seen (the segment is then stored, as in round 2).
   uint32_t A = 0u, J = 0u;  // sum x, sum j*x over this thread's positions (j < 32768: J < 2^32)
   uint32_t fbits = 0u, fincl = 0u, ftot = 0u, fixed_bytes = 0xFFFFFFFFu;
   uint32_t p_s = 0u, p_e = 0u;  // this thread's tokens: positions [p_s, p_e)
   const uint32_t stored_bytes = 5u + n;
-  bool incompressible = false;
-  if (n >= 4096u) {
-    for (uint32_t k = t; k < 256u; k += kThreads) llc[k] = 0u;
-    if (t == 0u) zctl[7] = 0u;
-    __syncthreads();
-    // tab[0 .. kRepSet): the sample set (zeroed at entry), keys x + 1
-    auto sample = [&](uint32_t x) -> bool {
-      if (zhash(x) & 63u) return false;
-      const uint32_t key = x + 1u ? x + 1u : 1u;
-      const uint32_t i0 = (x * 0x85EBCA6Bu) >> (32 - 11);
-      for (uint32_t r = 0; r < 8u; r++) {
-        const uint32_t old = atomicCAS(&tab[(i0 + r) & (kRepSet - 1u)], 0u, key);
-        if (old == 0u) return false;
-        if (old == key) return true;
-      }
-      return false;
-    };
-    bool rep = false;
-    for (uint32_t p = t; p < n; p += kThreads) {
-      const uint32_t x = seg4(data, p + sh);
-      atomicAdd(&llc[x & 0xFFu], 1u);
-      if (p + 4u <= n) rep |= sample(x);
-    }
-    if (rep) zctl[7] = 1u;
-    __syncthreads();
-    const uint32_t cnt = t < 256u ? llc[t] : 0u;
-    // per-symbol bits rounded (truncating lost ~0.004 bits per byte)
-    const uint32_t bits = cnt ? (uint32_t)((float)cnt * (__log2f((float)n) - __log2f((float)cnt)) + 0.5f) : 0u;
-    uint32_t hsum;
-    (void)wg_incl_sum(bits, wsum, hsum);
-    incompressible = (float)hsum >= 7.97f * (float)n && zctl[7] == 0u;  // workgroup-uniform
-    for (uint32_t k = t; k < kRepSet; k += kThreads) tab[k] = 0u;  // the candidate table starts empty
-    __syncthreads();
-  }
-  if (!incompressible && hl) {
-    const uint32_t* hb = reinterpret_cast<const uint32_t*>(seg_src - sh - hl);
-    for (uint32_t k = t; k < hw; k += kThreads) hist[k] = hb[k];
-    __syncthreads();
-  }
-  if (incompressible) {
-    for (uint32_t p = t; p < n; p += kThreads) {
-      const uint32_t x = seg4(data, p + sh) & 0xFFu;
-      A += x;
-      J += p * x;
-    }
-    if (t == 0) zpar[0] = 0u;
-  } else {
+  // this segment's scratch slot: the candidate distances, later the image
+  uint32_t* const slot = scratch + (uint64_t)g * (kSlot / 4u);
+  uint16_t* const cdg = reinterpret_cast<uint16_t*>(slot);
+  uint8_t* const lg = reinterpret_cast<uint8_t*>(slot) + kSlotLens;
+  uint8_t* const l8 = reinterpret_cast<uint8_t*>(hist);  // the lengths, after step 1
+  {
     // 1. candidates in position order + Adler partials.  tab16[h*8 + k]:
     //    window position + 1 of bucket h's k-th entry; cnt16[h]: inserts
-    //    so far (the slot of the next one, mod 8)
+    //    so far (the slot of the next one, mod 8).  Each position's candidate
+    //    distance goes to the slot in global memory (the table and the 64 KiB
+    //    of distances do not fit the LDS together) and comes back into the
+    //    table's LDS once the table is done.
     uint16_t* tab16 = reinterpret_cast<uint16_t*>(tab);
     uint32_t* cnt = tab + (1u << kHashBits) * kWays / 2u;
     auto insert = [&](uint32_t w, uint32_t h) {
@@ -813,32 +816,48 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
       const uint32_t k = (atomicAdd(&cnt[h >> 1], 1u << sft) >> sft) & (kWays - 1u);
       tab16[h * kWays + k] = (uint16_t)(w + 1u);
     };
-    for (uint32_t r = 0; r < hl / kThreads; r++) {  // the history: inserts only
+    for (uint32_t r = 0; r < hl / kThreads; r++) {  // the history: inserts only, kThreads per round
       const uint32_t w = kThreads * r + t;
       if (w + 4u <= hl + n) insert(w, zhash(win4(hist, data, hw, w + sh)));
       __syncthreads();
     }
     K7P(2);
-    for (uint32_t r = 0; r < kSeg / kThreads; r++) {
-      const uint32_t p = kThreads * r + t;
+    // kPair threads per position (adjacent lanes), each over kWays / kPair
+    // of the bucket's entries; the best (longest, then nearest) is combined
+    // across the pair, the same choice as one thread over all of them
+    constexpr uint32_t kMine = kWays / kPair;
+    static_assert(kMine == 4u || kMine == 8u, "one 8- or 16-byte load of a thread's entries");
+    const uint32_t part = t % kPair;
+    for (uint32_t r = 0; r < kSeg / kRound; r++) {
+      const uint32_t p = kRound * r + t / kPair;
       const uint32_t w = p + hl;
       const uint32_t x = seg4(data, p + sh);
       const bool live = p + 4u <= n;
       const uint32_t h = zhash(x);
       uint32_t best = 0u, bl = 0u;
       if (live) {
-        const uint4 c = *reinterpret_cast<const uint4*>(&tab16[h * kWays]);
+        uint32_t cs[kMine / 2];
+        if constexpr (kMine == 8u) {
+          const uint4 c = *reinterpret_cast<const uint4*>(&tab16[h * kWays]);
+          cs[0] = c.x;
+          cs[1] = c.y;
+          cs[2] = c.z;
+          cs[3] = c.w;
+        } else {
+          const uint2 c = *reinterpret_cast<const uint2*>(&tab16[h * kWays + kMine * part]);
+          cs[0] = c.x;
+          cs[1] = c.y;
+        }
         const uint32_t lim = min(258u, n - p);
-        const uint32_t cs[4] = {c.x, c.y, c.z, c.w};
-        // all 8 candidates' first 16 bytes at once (independent loads); a
+        // the candidates' first 16 bytes at once (independent loads); a
         // slot may already hold a later position of this round (no barrier
         // between reads and inserts): only earlier positions within 32 KiB
         // are candidates
         uint32_t cur[4];
         seg16(data, p + sh, cur);
-        uint32_t L[8], D[8];
+        uint32_t L[kMine], D[kMine];
   #pragma unroll
-        for (int k = 0; k < 8; k++) {
+        for (uint32_t k = 0; k < kMine; k++) {
           const uint32_t e = (cs[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
           const uint32_t q = e - 1u;
           const bool ok = e != 0u && q < w && w - q <= kWindow;
@@ -848,25 +867,61 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
           D[k] = w - q;
         }
   #pragma unroll
-        for (int k = 0; k < 8; k++) {
+        for (uint32_t k = 0; k < kMine; k++) {
           uint32_t Lk = L[k];
           if (Lk == 16u && lim > 16u)  // rare: extend past 16 bytes
             Lk = 16u + match_len(hist, data, hw, sh, p + 16u, w - D[k] + 16u, lim - 16u);
           Lk = min(Lk, lim);
-          if (Lk >= 4u && (Lk > bl || (Lk == bl && D[k] < best))) {
+          // a 4-byte match farther than kFar4 costs more bits than its four
+          // literals (length and distance codes with >= 9 extra bits)
+          if (Lk >= 4u && !(Lk == 4u && D[k] > kFar4) && (Lk > bl || (Lk == bl && D[k] < best))) {
             bl = Lk;
             best = D[k];
           }
         }
       }
-      cd[cphys(p)] = (uint16_t)best;
-      if (p < n) {
-        A += x & 0xFFu;
-        J += p * (x & 0xFFu);
+      if constexpr (kPair == 2u) {
+        const uint32_t obl = (uint32_t)__shfl_xor((int)bl, 1), obest = (uint32_t)__shfl_xor((int)best, 1);
+        if (obl > bl || (obl == bl && obest < best)) {
+          bl = obl;
+          best = obest;
+        }
       }
-      if (live) insert(w, h);
+      if (part == 0u) {
+        cdg[p] = (uint16_t)best;
+        lg[p] = (uint8_t)(bl ? bl - 3u : 0u);
+        if (p < n) {
+          A += x & 0xFFu;
+          J += p * (x & 0xFFu);
+        }
+        if (live) insert(w, h);
+      }
       __syncthreads();
     }
+    // the distances back into LDS over the table (8 positions = 4 words per
+    // load, never split by a pad dword); the barrier above ordered the
+    // slot's stores before these loads within the workgroup
+    static_assert((kSub / 2) % 4u == 0u, "pad groups hold whole 4-word runs");
+    for (uint32_t k = t; k < kSeg / 8u; k += kThreads) {
+      const uint4 v = reinterpret_cast<const uint4*>(cdg)[k];
+      const uint32_t wd = 4u * k, ph = wd + (wd >> kCdShift);
+      tab[ph] = v.x;
+      tab[ph + 1u] = v.y;
+      tab[ph + 2u] = v.z;
+      tab[ph + 3u] = v.w;
+    }
+    // the lengths into the history's LDS (no longer read: the parse takes
+    // lengths from here, literals from the segment's words)
+    static_assert(kSeg <= 4u * kHistWords, "the lengths fit the history's LDS");
+    for (uint32_t k = t; k < kSeg / 16u; k += kThreads) {
+      const uint4 v = reinterpret_cast<const uint4*>(lg)[k];
+      const uint32_t w0 = 4u * k, sw = (w0 >> 4) & 15u;
+      hist[w0 ^ sw] = v.x;
+      hist[(w0 + 1u) ^ sw] = v.y;
+      hist[(w0 + 2u) ^ sw] = v.z;
+      hist[(w0 + 3u) ^ sw] = v.w;
+    }
+    __syncthreads();
 
     K7P(3);
     // 2. the parse: dry passes hand each thread's end on as the next
@@ -874,7 +929,7 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
     const uint32_t r0 = min(t * kSub, n), rend = min(r0 + kSub, n);
     uint32_t extra, my_s = r0;
     uint64_t mask = 0ull;
-    uint32_t e_t = parse<false>(hist, data, hw, cd, hll, hd, sh, hl, n, my_s, rend, 0u, fbits, extra, &mask, r0);
+    uint32_t e_t = parse<false>(data, l8, cd, hll, hd, sh, n, my_s, rend, 0u, fbits, extra, &mask, r0);
     bool converged = false;  // workgroup-uniform
     for (uint32_t it = 0; it < kParseRounds; it++) {
       if (t + 1u < kThreads) starts[t + 1u] = e_t;
@@ -887,7 +942,7 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
       }
       if (moved) {
         my_s = ns;
-        e_t = parse<false>(hist, data, hw, cd, hll, hd, sh, hl, n, my_s, rend, 0u, fbits, extra, &mask, r0);
+        e_t = parse<false>(data, l8, cd, hll, hd, sh, n, my_s, rend, 0u, fbits, extra, &mask, r0);
       }
     }
     K7P(4);
@@ -913,7 +968,7 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
     if (converged && p_s == my_s && e_t == p_e)
       record_tokens(data, cd, hll, hd, sh, r0, mask, e_t, fbits, extra);
     else
-      (void)parse<true>(hist, data, hw, cd, hll, hd, sh, hl, n, p_s, rend, p_e, fbits, extra);
+      (void)parse<true>(data, l8, cd, hll, hd, sh, n, p_s, rend, p_e, fbits, extra);
     K7P(5);
     uint32_t etot, ntok;
     fincl = wg_incl_sum(fbits, wsum, ftot);
@@ -931,18 +986,18 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
     const uint32_t best_other = min(fixed_bytes, stored_bytes) * 8u;
     const bool try_dyn = htot + etot + 600u < best_other;
     if (try_dyn) {
-      // scratch in the (idle) hash table
-      uint32_t* keys = tab;                                      // 512 litlen keys, sorted
-      uint32_t* keysd = tab + 512;                               // 32 distance keys, sorted
-      uint32_t* keys2 = tab + 544;                               // 32 code-length keys
-      uint32_t* hw = tab + 576;                                  // weights: litlen 572, distance 60 at +576
-      uint32_t* npar = tab + 1792;                               // tree parents, distance nodes at +576
-      uint32_t* nanc = tab + 2816;                               // pointer-jumping ancestors
-      uint32_t* ndep = tab + 3840;                               // depths
-      uint32_t* blc = tab + 4864;                                // 2 x 16 length counts
-      uint32_t* cw = tab + 4896;                                 // code-length code: weights (38)
-      uint16_t* cpar = reinterpret_cast<uint16_t*>(tab + 4960);  // 38
-      uint8_t* cdep = reinterpret_cast<uint8_t*>(tab + 4992);    // 38
+      // scratch in the window (idle since the recording pass)
+      uint32_t* keys = win;                                      // 512 litlen keys, sorted
+      uint32_t* keysd = win + 512;                               // 32 distance keys, sorted
+      uint32_t* keys2 = win + 544;                               // 32 code-length keys
+      uint32_t* hw = win + 576;                                  // weights: litlen 572, distance 60 at +576
+      uint32_t* npar = win + 1792;                               // tree parents, distance nodes at +576
+      uint32_t* nanc = win + 2816;                               // pointer-jumping ancestors
+      uint32_t* ndep = win + 3840;                               // depths
+      uint32_t* blc = win + 4864;                                // 2 x 16 length counts
+      uint32_t* cw = win + 4896;                                 // code-length code: weights (38)
+      uint16_t* cpar = reinterpret_cast<uint16_t*>(win + 4960);  // 38
+      uint8_t* cdep = reinterpret_cast<uint8_t*>(win + 4992);    // 38
       for (uint32_t k = t; k < 512u; k += kThreads) keys[k] = (k < 286u && hll[k]) ? (hll[k] << 9) | k : 0xFFFFFFFFu;
       for (uint32_t k = t; k < 320u; k += kThreads) zl[k] = 0u;
       if (t < 32u) blc[t] = 0u;
@@ -972,6 +1027,7 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
         }
       }
       const uint32_t ml = (uint32_t)__syncthreads_count(t < 286u && hll[t] != 0u);  // >= 1 (EOB)
+      K7P(8);
       const uint32_t md = (uint32_t)__syncthreads_count(t < 30u && hd[t] != 0u);
       // Huffman trees of both codes at once: the serial merges on two waves,
       // then depths by pointer jumping over every node; halve and rebuild a
@@ -982,7 +1038,10 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
         if (t == 64u && need_d) huff_merge(keysd, md, shift, hw + 576, npar + 576, 576u);
         if (t < 2u) zctl[t] = 0u;
         __syncthreads();
-        uint32_t x0 = t, x1 = t + kThreads, a0, a1, d0, d1;
+        // nodes 0 .. 576 + 59: x1 only while kThreads < 1024 (with 1024 threads
+        // x1 = x0 + 1024 would run past the scratch)
+        static_assert(kThreads == 512u || kThreads == 1024u, "node cover");
+        uint32_t x0 = t, x1 = kThreads < 1024u ? t + kThreads : t, a0, a1, d0, d1;
         auto init = [&](uint32_t x, uint32_t& a, uint32_t& d) {
           const bool dist = x >= 576u;
           const uint32_t m = dist ? md : ml, root = (dist ? 576u : 0u) + 2u * m - 2u;
@@ -1018,6 +1077,7 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
         need_d = need_d && zctl[1] > 15u;
         __syncthreads();
       }
+      K7P(9);
       // code lengths (one distance symbol gets a second: RFC 1951 §3.2.7)
       if (t < ml) zl[keys[t] & 511u] = ml >= 2u ? (uint8_t)ndep[t] : 1u;
       if (md >= 2u && t < md) zl[288u + (keysd[t] & 511u)] = (uint8_t)ndep[576u + t];
@@ -1056,6 +1116,7 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
       } else if (t >= 288u && t < 318u) {
         dcc[t - 288u] = 0u;
       }
+      K7P(10);
       // code-length sequence, run-length coded (16/17/18): one thread per run
       const uint32_t nl = hlit + hdist;
       auto zv = [&](uint32_t i) -> uint32_t { return i < hlit ? zl[i] : zl[288u + i - hlit]; };
@@ -1088,6 +1149,7 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
       }
       __syncthreads();
       const uint32_t hclen = zctl[4];
+      K7P(11);
       uint32_t hcost = 0u, tcost = 0u, hb_body, tok_body;
       if (t < nr) {
         const uint32_t sy = rle[t] & 31u;
@@ -1123,12 +1185,12 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
                         : rev(0xC0u + k - 280u, 8u) | (8u << 16);
     for (uint32_t k = t; k < 32u; k += kThreads) dcc[k] = rev(k, 5u) | (5u << 16);
   }
-  uint32_t* img = tab;
-  __syncthreads();
-  for (uint32_t k = t; k < kImgWords; k += kThreads) img[k] = 0u;
-  __syncthreads();
+  uint32_t* img = win;  // the window is idle (the tokens are in cd)
   uint32_t nbytes = stored_bytes;
   if (mode != 0u) {
+    __syncthreads();
+    for (uint32_t k = t; k < kImgWords; k += kThreads) img[k] = 0u;
+    __syncthreads();
     // 3. emit: this thread's tokens at its prefix offset after the block header
     uint32_t mine = fbits, incl = fincl, tot = ftot;
     if (mode == 2u) {
@@ -1171,23 +1233,11 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_size(const hbxz
     __syncthreads();
     nbytes = zpar[5];
   } else {
-    // stored image: 00 | LEN | ~LEN | data
-    for (uint32_t k = t; k < (n + 5u + 3u) / 4u; k += kThreads) {
-      uint32_t w;
-      if (k >= 2u) {
-        w = seg4(data, 4u * k - 5u + sh);
-      } else {
-        const uint32_t d0 = seg4(data, sh);
-        w = k == 0u ? ((n & 0xFFu) << 8) | (((n >> 8) & 0xFFu) << 16) | ((~n & 0xFFu) << 24)
-                    : ((~n >> 8) & 0xFFu) | (d0 << 8);
-      }
-      img[k] = w;
-    }
+    mode = kModeSrcStored;  // stored: K7b copies the bytes from the source
   }
-  __syncthreads();
   K7P(7);
-  uint32_t* slot = scratch + (uint64_t)g * kImgWords;
-  for (uint32_t k = t; k < (nbytes + 3u) / 4u; k += kThreads) slot[k] = img[k];
+  if (mode != kModeSrcStored)
+    for (uint32_t k = t; k < (nbytes + 3u) / 4u; k += kThreads) slot[k] = img[k];
 
   // Adler partials: B = sum (n - j) x_j = n*A - J  (64-bit, then mod)
   unsigned long long A64 = A, J64 = J;
@@ -1299,7 +1349,7 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_write(uint32_t 
     if (t < head) D[t] = (uint8_t)byte_at(t);
     const uint32_t nw = (nbytes - head) >> 2;
     uint32_t* Dw = reinterpret_cast<uint32_t*>(D + head);
-    for (uint32_t k = t; k < nw; k += kThreads) {
+    for (uint32_t k = t; k < nw; k += kWThreads) {
       const uint32_t q = head + 4u * k;
       uint32_t w;
       if (q >= 5u) {  // four source bytes at any alignment (the hardware splits the load)
@@ -1314,8 +1364,8 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_write(uint32_t 
     if (t < nbytes - done) D[done + t] = (uint8_t)byte_at(done + t);
     return;
   }
-  const uint32_t* slot = scratch + (uint64_t)g * kImgWords;
-  for (uint32_t k = t; k < kImgWords + 2u; k += kThreads) img[k] = k < (nbytes + 3u) / 4u ? slot[k] : 0u;
+  const uint32_t* slot = scratch + (uint64_t)g * (kSlot / 4u);
+  for (uint32_t k = t; k < kImgWords + 2u; k += kWThreads) img[k] = k < (nbytes + 3u) / 4u ? slot[k] : 0u;
   __syncthreads();
   // image [0, nbytes) -> the stream at byte address D
   uint8_t* D = reinterpret_cast<uint8_t*>(seg_off[g]);
@@ -1325,7 +1375,7 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_write(uint32_t 
   if (t < head) D[t] = ob[t];
   const uint32_t nw = (nbytes - head) >> 2;
   uint32_t* Dw = reinterpret_cast<uint32_t*>(D + head);
-  for (uint32_t k = t; k < nw; k += kThreads) Dw[k] = lds4(img, head + 4u * k);
+  for (uint32_t k = t; k < nw; k += kWThreads) Dw[k] = lds4(img, head + 4u * k);
   const uint32_t done = head + 4u * nw;
   if (t < nbytes - done) D[done + t] = ob[done + t];
 }

@@ -1762,7 +1762,7 @@ int z_start(hbx_ctx* c, ZPend& zp, const uint64_t* cut_ends, const uint64_t* out
   hipLaunchKernelGGL(hbx_k7_deflate_plan, dim3((uint32_t)n), dim3(64), 0, s, dz, (uint32_t)n,
                      Z.info.as<hbxz::SegInfo>(), Z.off.as<uint64_t>(), Z.len.as<uint64_t>());
   HBX_TRY(c, hipGetLastError());
-  hipLaunchKernelGGL(hbx_k7_deflate_write, dim3((uint32_t)nseg), dim3(hbxz::kThreads), 0, s, (uint32_t)nseg,
+  hipLaunchKernelGGL(hbx_k7_deflate_write, dim3((uint32_t)nseg), dim3(hbxz::kWThreads), 0, s, (uint32_t)nseg,
                      Z.info.as<hbxz::SegInfo>(), Z.img.as<uint32_t>(), Z.off.as<uint64_t>(), dz, (uint32_t)n);
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipMemcpyAsync(Z.lens.p, Z.len.p, n * 8, hipMemcpyDeviceToHost, s));
@@ -2300,7 +2300,7 @@ int deflate_device(hbx_ctx* c, uint64_t n, const uint64_t* src, const uint64_t* 
                      c->d_zinfo.as<hbxz::SegInfo>(), c->d_zoff.as<uint64_t>(), c->d_zlen.as<uint64_t>());
   HBX_TRY(c, hipGetLastError());
   if (nseg) {
-    hipLaunchKernelGGL(hbx_k7_deflate_write, dim3((uint32_t)nseg), dim3(hbxz::kThreads), 0, s, (uint32_t)nseg,
+    hipLaunchKernelGGL(hbx_k7_deflate_write, dim3((uint32_t)nseg), dim3(hbxz::kWThreads), 0, s, (uint32_t)nseg,
                        c->d_zinfo.as<hbxz::SegInfo>(), c->d_zimg.as<uint32_t>(), c->d_zoff.as<uint64_t>(), dz,
                        (uint32_t)n);
     HBX_TRY(c, hipGetLastError());

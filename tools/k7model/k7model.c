@@ -16,6 +16,9 @@
 //   -l LAZY     lazy look-ahead steps (1 in K7)
 //   -B BLOCK    block (chunk) bytes: segments of a block share history
 //   -F          FIFO buckets (the WAYS latest positions per hash)
+//   -f D4 / -g D5  length-4 / -5 matches farther than D4 / D5 are taken as literals
+//   -P 1        flexible parsing: a match is cut where the next one reaches farthest
+//   -x W2       a second FIFO table of W2 ways keyed by K2 bytes (-k K2, -y BITS2)
 //   cc -O2 -o k7model k7model.c -lm ; ./k7model [flags] < corpus
 #include <math.h>
 #include <stdint.h>
@@ -26,6 +29,7 @@
 
 static int WAYS = 4, HBITS = 11, RANGE = 64, SEG = 32768, HIST = 0, HLEN = 0, MINM = 4, LAZY = 1, ROUND = 512;
 static long BLOCK = 4 << 20;
+static int W2 = 0, K2 = 8, B2 = 11, FAR4 = 0, FAR5 = 0, FLEX = 0;
 static int FIFO = 0;  // -F: a bucket keeps its WAYS latest positions (a per-bucket counter) instead of one per residue
 static uint32_t* fcnt;
 static void ins(uint32_t* tab, uint32_t h, int rel) {
@@ -34,6 +38,13 @@ static void ins(uint32_t* tab, uint32_t h, int rel) {
 }
 
 static uint32_t rd4(const uint8_t* p) { uint32_t x; memcpy(&x, p, 4); return x; }
+static uint32_t* fcnt2;
+static uint32_t hsh2(const uint8_t* p) {
+  uint32_t a = rd4(p), b = rd4(p + 4);
+  if (K2 < 8) b &= (1u << (8 * (K2 - 4))) - 1u;
+  return ((a * 0x9E3779B1u) ^ (b * 0x85EBCA77u)) >> (32 - B2);
+}
+static void ins2(uint32_t* tab, uint32_t h, int rel) { tab[h * W2 + (fcnt2[h]++ % W2)] = (uint32_t)(rel + 1); }
 static uint32_t hsh(uint32_t x, int minm) {
   if (minm == 3) x &= 0xFFFFFFu;
   return (x * 0x9E3779B1u) >> (32 - HBITS);
@@ -99,7 +110,13 @@ static void dsym(int D, int* s, int* e) {
 
 int main(int argc, char** argv) {
   int c;
-  while ((c = getopt(argc, argv, "w:b:r:s:Hh:m:l:B:R:F")) != -1) {
+  while ((c = getopt(argc, argv, "w:b:r:s:Hh:m:l:B:R:Fx:k:y:f:g:P:")) != -1) {
+    if (c == 'P') FLEX = atoi(optarg);
+    if (c == 'f') FAR4 = atoi(optarg);
+    if (c == 'g') FAR5 = atoi(optarg);
+    if (c == 'x') W2 = atoi(optarg);
+    if (c == 'k') K2 = atoi(optarg);
+    if (c == 'y') B2 = atoi(optarg);
     if (c == 'h') { HIST = 1; HLEN = atoi(optarg); }
     if (c == 'F') FIFO = 1;
     if (c == 'w') WAYS = atoi(optarg);
@@ -120,6 +137,10 @@ int main(int argc, char** argv) {
   const int nh = 1 << HBITS;
   uint32_t* tab = malloc(sizeof(uint32_t) * nh * WAYS);
   fcnt = malloc(sizeof(uint32_t) * nh);
+  const int nh2 = 1 << B2;
+  uint32_t* tab2 = malloc(sizeof(uint32_t) * nh2 * (W2 ? W2 : 1));
+  uint32_t* snap2 = malloc(sizeof(uint32_t) * nh2 * (W2 ? W2 : 1));
+  fcnt2 = malloc(sizeof(uint32_t) * nh2);
   int* cd = malloc(sizeof(int) * (SEG + 8));
   double total_bits = 0;
   long nseg = 0;
@@ -134,16 +155,22 @@ int main(int argc, char** argv) {
       const int wlo = (HIST && s0 >= (size_t)hl) ? -hl : (HIST ? -(int)s0 : 0);
       memset(tab, 0, sizeof(uint32_t) * nh * WAYS);
       memset(fcnt, 0, sizeof(uint32_t) * nh);
+      if (W2) {
+        memset(tab2, 0, sizeof(uint32_t) * nh2 * W2);
+        memset(fcnt2, 0, sizeof(uint32_t) * nh2);
+      }
       // history positions inserted first (all, in order)
       for (int p = wlo; p < 0; p++) {
         if (p + 4 > 0 + sn && 0) break;
         uint32_t h = hsh(rd4(sg + p), MINM);
         ins(tab, h, p - wlo);
+        if (W2 && p + K2 <= sn) ins2(tab2, hsh2(sg + p), p - wlo);
       }
       // candidates in rounds: reads see the table as of the round's start
       uint32_t* snap = malloc(sizeof(uint32_t) * nh * WAYS);
       for (int r0 = 0; r0 < sn; r0 += ROUND) {
         memcpy(snap, tab, sizeof(uint32_t) * nh * WAYS);
+        if (W2) memcpy(snap2, tab2, sizeof(uint32_t) * nh2 * W2);
         for (int p = r0; p < r0 + ROUND && p < sn; p++) {
           cd[p] = 0;
           if (p + MINM > sn) continue;
@@ -154,15 +181,30 @@ int main(int argc, char** argv) {
             uint32_t v = snap[h * WAYS + w];
             if (!v) continue;
             int q = (int)v - 1 + wlo;
-            if (q >= p) continue;
+            if (q >= p || p - q > 32768) continue;  // deflate's window
             int lim = sn - p < 258 ? sn - p : 258;
             int L = mlen(sg + p, sg + q, lim);
             if (L >= MINM && (L > bestl || (L == bestl && p - q < bestd))) { bestl = L; bestd = p - q; }
           }
+          if (W2 && p + K2 <= sn) {
+            const uint32_t h2 = hsh2(sg + p);
+            for (int w = 0; w < W2; w++) {
+              uint32_t v = snap2[h2 * W2 + w];
+              if (!v) continue;
+              int q = (int)v - 1 + wlo;
+              if (q >= p || p - q > 32768) continue;
+              int lim = sn - p < 258 ? sn - p : 258;
+              int L = mlen(sg + p, sg + q, lim);
+              if (L >= MINM && (L > bestl || (L == bestl && p - q < bestd))) { bestl = L; bestd = p - q; }
+            }
+          }
           cd[p] = bestd;
         }
         for (int p = r0; p < r0 + ROUND && p < sn; p++)
+        {
           if (p + MINM <= sn) ins(tab, hsh(rd4(sg + p), MINM), p - wlo);
+          if (W2 && p + K2 <= sn) ins2(tab2, hsh2(sg + p), p - wlo);
+        }
       }
       free(snap);
       // parse
@@ -186,10 +228,23 @@ int main(int argc, char** argv) {
             int d1 = cd[p + la], L1 = d1 ? mlen(sg + p + la, sg + p + la - d1, lim1) : 0;
             if (L1 > L + la - 1) { defer = 1; break; }
           }
-          if (L >= MINM && !defer && !(L == 3 && d > 4096)) {
+          if (L >= MINM && !defer && !(L == 3 && d > 4096) && !(FAR4 && L == 4 && d > FAR4) && !(FAR5 && L == 5 && d > FAR5)) {
             int s, e, ds, de;
             lsym(L, &s, &e);
             dsym(d, &ds, &de);
+            if (FLEX && L > MINM) {
+              // the cut j in [p + MINM, p + L] whose match reaches farthest
+              const int E = RANGE ? end : sn;
+              int bj = p + L, br = -1;
+              for (int j = p + MINM; j <= p + L && j < E; j++) {
+                int lj = j + 258 <= E ? 258 : E - j;
+                int dj = cd[j], Lj = dj ? mlen(sg + j, sg + j - dj, lj) : 0;
+                int reach = Lj >= MINM ? j + Lj : j;
+                if (reach > br || (reach == br && j == p + L)) { br = reach; bj = j; }
+              }
+              L = bj - p;
+              lsym(L, &s, &e);
+            }
             fl[s]++; fd[ds]++; extra += e + de;
             p += L;
           } else {
