@@ -31,12 +31,12 @@
 //   1. candidates, in position order.  The 32 KiB of the block before the
 //      segment (its history) are inserted first, then round r covers
 //      segment positions 512r..512r+511, two adjacent threads per position
-//      (four bucket entries each, the better of the two kept).  A 4096-bucket
-//      hash table of 4-byte prefixes keeps each bucket's 8 latest positions
+//      (eight bucket entries each, the better of the two kept).  A 2048-bucket
+//      hash table of 4-byte prefixes keeps each bucket's 16 latest positions
 //      (a 16-bit counter per bucket picks the slot; one barrier per round,
 //      so a slot may already hold a later position of the same round, which
 //      is skipped).  Each position keeps the longest verified match among its
-//      <= 8 candidates within 32 KiB, nearest first on a tie, and drops a
+//      <= 16 candidates within 32 KiB, nearest first on a tie, and drops a
 //      4-byte one farther than kFar4: its distance (u16) and length (u8) go
 //      to the segment's scratch slot, because the table and 96 KiB of
 //      per-position results do not fit the LDS together; they come back into
@@ -56,11 +56,11 @@
 //   3. after a workgroup prefix sum of the bit counts, the tokens are emitted
 //      (ds_or) into the image (over the window's LDS), if that is smaller than
 //      stored; a stored segment is copied by K7b from the source.
-// Zipf text of tools/bench_deflate.py: 0.3162 of its size at 20.9 GB/s (round
-// 3: 0.327 at 16.0 GB/s with 8 ways of 2,048 buckets, 16 KiB of history and
-// one-step lazy matching; zlib -6: 0.311).  tools/k7model/k7model.c models
-// the variants (32 ways of 1,024 buckets reach 0.3103 measured, at 7.6 GB/s).
-// LDS: 150.5 of the CU's 160 KiB.
+// Zipf text of tools/bench_deflate.py: 0.3120 of its size at 16.2 GB/s (zlib
+// -6: 0.3114; round 3: 0.327 at 16.0 GB/s with 8 ways of 2,048 buckets, 16
+// KiB of history and one-step lazy matching; 8 ways of 4,096 buckets here:
+// 0.3162 at 23.1 GB/s).  tools/k7model/k7model.c models the variants.
+// LDS: 141 of the CU's 160 KiB.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -77,24 +77,24 @@ constexpr uint32_t kRound = kThreads / kPair;  // positions per candidate round
 constexpr uint32_t kParse = 512;            // parse ranges (threads t >= kParse have empty ones)
 constexpr uint32_t kSub = kSeg / kParse;    // 64 bytes per range
 constexpr uint32_t kWThreads = 512;         // K7b
-constexpr uint32_t kHashBits = 12;
-constexpr uint32_t kWays = 8;                 // positions kept per bucket (16-bit entries)
+constexpr uint32_t kHashBits = 11;
+constexpr uint32_t kWays = 16;                // positions kept per bucket (16-bit entries)
 constexpr uint32_t kHist = 32768;             // history bytes before a segment (within its block)
 constexpr uint32_t kHistWords = kHist / 4;
 constexpr uint32_t kWindow = 32768;           // deflate's largest distance
 constexpr uint32_t kParseRounds = 8;          // bound on the start hand-off rounds
 constexpr uint32_t kRepSet = 2048;            // slots of the early-out's repeat sample set
 constexpr uint32_t kDataWords = kSeg / 4 + 8;        // + slack for the 16-byte reads past the end
-// The segment and the candidate array live in LDS with one pad dword per
-// parse range (kSub/4 data dwords, kSub/2 candidate dwords): thread t's range
-// starts kSub bytes after thread t-1's, which without padding puts the 64
-// lanes of a wave on a few banks.
-constexpr uint32_t kDataShift = 31 - __builtin_clz(kSub / 4);
+constexpr uint32_t kDataPhys = (kDataWords + 15u) & ~15u;  // whole swizzle groups
+// The candidate array lives in LDS with one pad dword per parse range (kSub/2
+// candidate dwords): thread t's range starts kSub bytes after thread t-1's,
+// which without padding puts the 64 lanes of a wave on a few banks.  The
+// window's words are XOR-swizzled instead (sw below), which keeps 8-byte pairs
+// whole for ds_read_b64.
 constexpr uint32_t kCdShift = 31 - __builtin_clz(kSub / 2);
-constexpr uint32_t kDataPhys = kDataWords + (kDataWords >> kDataShift) + 1;
 constexpr uint32_t kCdPhys = (kSeg / 2 + (kSeg / 2 >> kCdShift)) * 2;  // u16 slots
 constexpr uint32_t kImgWords = (kSeg + 16) / 4 + 4;  // stored image (5 + kSeg) or a smaller fixed one
-// hash table: 4096 x 8 u16 entries (window position + 1), then 4096 u16
+// hash table: 2048 x 16 u16 entries (window position + 1), then 2048 u16
 // counters, in the region that holds the candidate distances after step 1
 constexpr uint32_t kTabWords = (1u << kHashBits) * kWays / 2 + (1u << kHashBits) / 2;
 // scratch bytes per segment: the candidate distances (u16 per position) and
@@ -129,11 +129,16 @@ struct ZBlock {
 __device__ __forceinline__ uint32_t lds4(const uint32_t* w, uint32_t p) {
   return __builtin_amdgcn_alignbyte(w[(p >> 2) + 1], w[p >> 2], p & 3u);
 }
-__device__ __forceinline__ uint32_t dphys(uint32_t k) { return k + (k >> kDataShift); }
+// Window words in LDS: word k at k ^ 2 * ((k / 16) % 8), a permutation inside
+// each 16-word group that keeps every even/odd pair together (ds_read_b64)
+// and puts words 16 apart (the starts of neighbouring parse ranges, the
+// literal reads of the recording pass) on different banks.  History and
+// segment share it (the segment starts at word kHistWords, a multiple of 128).
+__device__ __forceinline__ uint32_t sw(uint32_t k) { return k ^ (((k >> 4) & 7u) << 1); }
 // 4 bytes at byte p of the padded segment
 __device__ __forceinline__ uint32_t seg4(const uint32_t* w, uint32_t p) {
   const uint32_t i = p >> 2;
-  return __builtin_amdgcn_alignbyte(w[dphys(i + 1u)], w[dphys(i)], p & 3u);
+  return __builtin_amdgcn_alignbyte(w[sw(i + 1u)], w[sw(i)], p & 3u);
 }
 __device__ __forceinline__ uint32_t cphys(uint32_t p) {
   const uint32_t wd = p >> 1;
@@ -210,16 +215,15 @@ __device__ __forceinline__ void load_segment(uint32_t* data, const uint8_t* src,
   sh = (uint32_t)(a & 3u);
   const uint32_t* base = reinterpret_cast<const uint32_t*>(a - sh);
   const uint32_t nw = (n + sh + 3u) >> 2;
-  for (uint32_t k = threadIdx.x; k < kDataWords; k += kThreads) data[dphys(k)] = k < nw ? base[k] : 0u;
+  for (uint32_t k = threadIdx.x; k < kDataWords; k += kThreads) data[sw(k)] = k < nw ? base[k] : 0u;
 }
 
-// Window word i: the history's words first (unpadded: the parse never walks
-// them), then the segment's (padded).  hw = history words present.  The two
-// are one LDS array (data == hist + kHistWords), so a word is one load
-// whichever part it is in.
+// Window word i: the history's words first, then the segment's, one LDS
+// array (data == hist + kHistWords); hw = history words present (0 or
+// kHistWords), so window word i is array word kHistWords - hw + i.
 __device__ __forceinline__ uint32_t wword(const uint32_t* hist, const uint32_t* data, uint32_t hw, uint32_t i) {
   (void)data;
-  return hist[i < hw ? i : kHistWords + dphys(i - hw)];
+  return hist[sw(kHistWords - hw + i)];
 }
 // 4 bytes at window byte b (window position + sh)
 __device__ __forceinline__ uint32_t win4(const uint32_t* hist, const uint32_t* data, uint32_t hw, uint32_t b) {
@@ -227,24 +231,34 @@ __device__ __forceinline__ uint32_t win4(const uint32_t* hist, const uint32_t* d
   return __builtin_amdgcn_alignbyte(wword(hist, data, hw, i + 1u), wword(hist, data, hw, i), b & 3u);
 }
 
-// 16 bytes at segment byte b (position + sh) / window byte b, as 4 dwords:
-// five independent LDS loads, so a thread's candidates overlap their latency
-__device__ __forceinline__ void seg16(const uint32_t* data, uint32_t b, uint32_t (&c)[4]) {
-  const uint32_t i = b >> 2, r = b & 3u;
+// 16 bytes from byte r of array word i (base 8-byte aligned), as 4 dwords:
+// three ds_read_b64 of the aligned pairs around them (a random b64 costs the
+// LDS about what a random b32 does, so 3 loads instead of 5)
+__device__ __forceinline__ void load16(const uint32_t* base, uint32_t i, uint32_t r, uint32_t (&c)[4]) {
+  const uint32_t i0 = i & ~1u;
+  uint32_t v[6];
+#pragma unroll
+  for (uint32_t j = 0; j < 3u; j++) {
+    const uint2 x = *reinterpret_cast<const uint2*>(base + sw(i0 + 2u * j));
+    v[2 * j] = x.x;
+    v[2 * j + 1] = x.y;
+  }
+  // (a mask select: written as v[j + odd] the compiler indexes the array in scratch)
+  const uint32_t m = 0u - (i & 1u);
   uint32_t w[5];
 #pragma unroll
-  for (int j = 0; j < 5; j++) w[j] = data[dphys(i + (uint32_t)j)];
+  for (int j = 0; j < 5; j++) w[j] = (v[j] & ~m) | (v[j + 1] & m);
 #pragma unroll
   for (int j = 0; j < 4; j++) c[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], r);
 }
+// 16 bytes at segment byte b (position + sh) / window byte b
+__device__ __forceinline__ void seg16(const uint32_t* data, uint32_t b, uint32_t (&c)[4]) {
+  load16(data, b >> 2, b & 3u, c);
+}
 __device__ __forceinline__ void win16(const uint32_t* hist, const uint32_t* data, uint32_t hw, uint32_t b,
                                       uint32_t (&c)[4]) {
-  const uint32_t i = b >> 2, r = b & 3u;
-  uint32_t w[5];
-#pragma unroll
-  for (int j = 0; j < 5; j++) w[j] = wword(hist, data, hw, i + (uint32_t)j);
-#pragma unroll
-  for (int j = 0; j < 4; j++) c[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], r);
+  (void)data;
+  load16(hist, kHistWords - hw + (b >> 2), b & 3u, c);
 }
 // leading equal bytes of two 16-byte strings (0..16)
 __device__ __forceinline__ uint32_t eq16(const uint32_t (&a)[4], const uint32_t (&b)[4]) {
@@ -463,42 +477,10 @@ __device__ __forceinline__ uint32_t walk_tokens(const uint16_t* cd, const uint32
   return bits;
 }
 
-// ---- dynamic Huffman codes (RFC 1951 §3.2.7), built by one thread ----------
-// keys[0..m): (freq << 9 | symbol), ascending.  Code lengths <= limit into
-// lens[symbol] (a length-limited code by halving the frequencies until the
-// Huffman tree is shallow enough: always a complete code).  w, par, dep:
-// scratch of 2m entries.
-__device__ void huff_lengths(const uint32_t* keys, uint32_t m, uint32_t limit, uint8_t* lens, uint32_t* w,
-                             uint16_t* par, uint8_t* dep) {
-  if (m == 1u) {
-    lens[keys[0] & 511u] = 1u;
-    return;
-  }
-  for (uint32_t shift = 0;; shift++) {
-    for (uint32_t i = 0; i < m; i++) w[i] = ((keys[i] >> 9) >> shift) | 1u;
-    uint32_t i = 0, j = m;
-    for (uint32_t k = m; k < 2u * m - 1u; k++) {
-      uint32_t a, b;
-      if (i < m && (j >= k || w[i] <= w[j])) a = i++; else a = j++;
-      if (i < m && (j >= k || w[i] <= w[j])) b = i++; else b = j++;
-      w[k] = w[a] + w[b];
-      par[a] = (uint16_t)k;
-      par[b] = (uint16_t)k;
-    }
-    dep[2u * m - 2u] = 0u;
-    uint32_t maxd = 0u;
-    for (int x = (int)(2u * m) - 3; x >= 0; x--) {
-      dep[x] = (uint8_t)(dep[par[x]] + 1u);
-      if ((uint32_t)x < m && dep[x] > maxd) maxd = dep[x];
-    }
-    if (maxd <= limit) break;
-  }
-  for (uint32_t i = 0; i < m; i++) lens[keys[i] & 511u] = dep[i];
-}
-
-// The two-queue merge of huff_lengths alone, for the parallel depth pass:
-// leaves 0..m) in key order, internal nodes m..2m-1); par[node] = pbase +
-// its parent.  Same tie rule as huff_lengths (leaf first).
+// ---- dynamic Huffman codes (RFC 1951 §3.2.7) -------------------------------
+// The two-queue merge of a Huffman tree, for the parallel depth pass: keys
+// (freq << 9 | symbol) ascending, leaves 0..m) in key order, internal nodes
+// m..2m-1); par[node] = pbase + its parent; leaf first on equal weights.
 __device__ void huff_merge(const uint32_t* keys, uint32_t m, uint32_t shift, uint32_t* w, uint32_t* par,
                            uint32_t pbase) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
@@ -555,46 +537,98 @@ __device__ __forceinline__ uint32_t rle_runs(uint32_t cur, uint32_t r, uint32_t*
   return nr;
 }
 
-// Canonical codes (RFC 1951 §3.2.2) as reversed code | length << 16.
-__device__ void canon_codes(const uint8_t* lens, uint32_t nsym, uint32_t* out, uint32_t* blc) {
-  for (uint32_t b = 0; b < 16u; b++) blc[b] = 0u;
-  for (uint32_t s = 0; s < nsym; s++) blc[lens[s]]++;
-  blc[0] = 0u;
-  uint32_t code = 0u, next[16];
-  next[0] = 0u;
-#pragma unroll
-  for (uint32_t b = 1; b < 16u; b++) {
-    code = (code + blc[b - 1u]) << 1;
-    next[b] = code;
-  }
-#pragma unroll
-  for (uint32_t b = 0; b < 16u; b++) blc[b] = next[b];
-  for (uint32_t s = 0; s < nsym; s++) {
-    const uint32_t l = lens[s];
-    out[s] = l ? (rev(blc[l]++, l) | (l << 16)) : 0u;
-  }
-}
-
 // Order of the code-length code lengths in the header (RFC 1951 §3.2.7).
 __device__ const uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-// Serial insertion sort of the nonzero frequencies of f[0..nsym) into keys.
-__device__ uint32_t sort_small(const uint32_t* f, uint32_t nsym, uint32_t* keys) {
-  uint32_t m = 0u;
-  for (uint32_t s = 0; s < nsym; s++) {
-    if (!f[s]) continue;
-    const uint32_t key = (f[s] << 9) | s;
-    uint32_t j = m++;
-    while (j > 0u && keys[j - 1u] > key) {
-      keys[j] = keys[j - 1u];
-      j--;
-    }
-    keys[j] = key;
+// position of each code-length symbol in kClOrder
+__device__ const uint8_t kClPos[19] = {3, 17, 15, 13, 11, 9, 7, 5, 4, 6, 8, 10, 12, 14, 16, 18, 0, 1, 2};
+
+__device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t o = ((uint64_t)(uint32_t)__shfl_xor((int)(v >> 32), d) << 32) | (uint32_t)__shfl_xor((int)(uint32_t)v, d);
+    v = o < v ? o : v;
   }
-  return m;
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_max32(uint32_t v) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) v = max(v, (uint32_t)__shfl_xor((int)v, d));
+  return v;
 }
 
-// Inclusive prefix sum over the workgroup; `tot` = the total.
+// The code-length code (<= 19 symbols, lengths <= 7) built by one wave, lane
+// l = symbol l, the tree's internal nodes on lanes 19.. as they are made:
+// each merge takes the two smallest available nodes by (weight, leaf before
+// internal, key) with two wave minimum reductions, depths by pointer jumping
+// over the parent lanes; a tree deeper than 7 is rebuilt from halved
+// frequencies (always a complete code).  Then the canonical codes (RFC 1951
+// §3.2.2) and HCLEN.  All 64 lanes call it; f = the lane's frequency (0 past
+// 18).  Writes cll[0..19), clc[0..19) and returns HCLEN.
+__device__ uint32_t cl_code(uint32_t f, uint8_t* cll, uint32_t* clc) {
+  constexpr uint64_t kNone = ~0ull;
+  const uint32_t l = threadIdx.x & 63u;
+  const bool leaf = l < 19u && f != 0u;
+  const uint64_t nz = __builtin_amdgcn_ballot_w64(leaf);
+  const uint32_t mc = (uint32_t)__builtin_popcountll(nz);
+  uint32_t len = 0u;
+  if (mc == 1u) {  // one used symbol: two codes of one bit (RFC 1951 §3.2.7)
+    const uint32_t x = (uint32_t)__builtin_ctzll(nz);
+    len = l == x || l == (x ? 0u : 1u) ? 1u : 0u;
+  } else {
+    for (uint32_t shift = 0;; shift++) {
+      uint32_t wgt = leaf ? (f >> shift) | 1u : 0u, par = l;
+      bool avail = leaf;
+      for (uint32_t k = 0; k + 1u < mc; k++) {
+        // sortable: weight | internal | key (leaves: freq << 9 | symbol; internal: creation index) | lane
+        const uint64_t key = ((uint64_t)wgt << 32) | ((uint64_t)(l >= 19u) << 31) |
+                             ((uint64_t)(l < 19u ? (f << 9) | l : l - 19u) << 6) | l;
+        const uint64_t m1 = wave_min64(avail ? key : kNone);
+        const uint32_t a = (uint32_t)(m1 & 63u);
+        const uint64_t m2 = wave_min64(avail && l != a ? key : kNone);
+        const uint32_t b = (uint32_t)(m2 & 63u);
+        const uint32_t nn = 19u + k;
+        if (l == a || l == b) {
+          par = nn;
+          avail = false;
+        }
+        if (l == nn) {
+          wgt = (uint32_t)(m1 >> 32) + (uint32_t)(m2 >> 32);
+          avail = true;
+        }
+      }
+      // depth = steps to the root (the last node made, its own parent)
+      uint32_t d = par != l ? 1u : 0u, p = par;
+#pragma unroll
+      for (int r = 0; r < 6; r++) {  // depth <= 18 < 2^6
+        const uint32_t dp = (uint32_t)__shfl((int)d, (int)p), pp = (uint32_t)__shfl((int)p, (int)p);
+        d += dp;
+        p = pp;
+      }
+      len = leaf ? d : 0u;
+      if (wave_max32(len) <= 7u) break;
+    }
+  }
+  // canonical codes: the first code of each length, then the rank among the
+  // same length's smaller symbols
+  uint32_t code = 0u, first = 0u, prev = 0u;
+  for (uint32_t bl = 1; bl <= 7u; bl++) {
+    code = (code + prev) << 1;
+    if (len == bl) first = code;
+    prev = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(l < 19u && len == bl));
+  }
+  uint32_t rank = 0u;
+  for (uint32_t bl = 1; bl <= 7u; bl++) {
+    const uint64_t mb = __builtin_amdgcn_ballot_w64(l < 19u && len == bl);
+    if (len == bl) rank = (uint32_t)__builtin_popcountll(mb & ((1ull << l) - 1ull));
+  }
+  if (l < 19u) {
+    cll[l] = (uint8_t)len;
+    clc[l] = len ? rev(first + rank, len) | (len << 16) : 0u;
+  }
+  return max(4u, wave_max32(l < 19u && len ? (uint32_t)kClPos[l] + 1u : 0u));
+}
+
 __device__ __forceinline__ uint32_t wg_incl_sum(uint32_t x, uint32_t* wsum, uint32_t& tot) {
   const uint32_t l = threadIdx.x & 63u, w = threadIdx.x >> 6;
   for (int d = 1; d < 64; d <<= 1) {
@@ -609,6 +643,41 @@ __device__ __forceinline__ uint32_t wg_incl_sum(uint32_t x, uint32_t* wsum, uint
   for (uint32_t k = 0; k < kWaves; k++) tot += wsum[k];
   __syncthreads();
   return before + x;
+}
+
+// Workgroup inclusive prefix sum of x[0] and totals of x[0..N) in one pair
+// of barriers (wsum: N * kWaves words).
+template <int N>
+__device__ __forceinline__ uint32_t wg_sums(const uint32_t (&x)[N], uint32_t* wsum, uint32_t (&tot)[N]) {
+  const uint32_t l = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  uint32_t v = x[0];
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)v, d);
+    if (l >= (uint32_t)d) v += y;
+  }
+  uint32_t r[N];
+  r[0] = v;
+#pragma unroll
+  for (int i = 1; i < N; i++) {
+    uint32_t u = x[i];
+    for (int d = 32; d >= 1; d >>= 1) u += (uint32_t)__shfl_xor((int)u, d);
+    r[i] = u;
+  }
+  if (l == 63u) {
+#pragma unroll
+    for (int i = 0; i < N; i++) wsum[i * kWaves + w] = r[i];
+  }
+  __syncthreads();
+  uint32_t before = 0u;
+  for (uint32_t k = 0; k < w; k++) before += wsum[k];
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    uint32_t t = 0u;
+    for (uint32_t k = 0; k < kWaves; k++) t += wsum[i * kWaves + k];
+    tot[i] = t;
+  }
+  __syncthreads();
+  return before + v;
 }
 
 }  // namespace hbxz
@@ -752,7 +821,7 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
   using namespace hbxz;
   // history words, then the segment's; after the parse, the Huffman scratch
   // and then the coded image
-  __shared__ uint32_t win[kHistWords + kDataPhys];
+  __shared__ __attribute__((aligned(16))) uint32_t win[kHistWords + kDataPhys];
   uint32_t* const hist = win;
   uint32_t* const data = win + kHistWords;
   // the hash table (step 1), then the candidate distances (steps 2-3)
@@ -760,10 +829,12 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
   uint16_t* const cd = reinterpret_cast<uint16_t*>(tab);
   __shared__ uint32_t starts[kThreads + 1];  // each thread's parse start (step 2)
   __shared__ uint32_t wsum[kWaves];
+  __shared__ uint32_t wsum4[4 * kWaves];
   __shared__ unsigned long long wadler[2 * kWaves];
   __shared__ uint32_t hll[288], hd[32], llc[288], dcc[32], rle[320], clf[19], clc[19], zpar[8], zctl[8];
   __shared__ __attribute__((aligned(4))) uint8_t zl[320];
   __shared__ uint8_t cll[20];
+  __shared__ unsigned long long rmask[5];  // code-length run starts (header RLE)
   static_assert(kImgWords <= kHistWords + kDataPhys, "the image fits the window's LDS");
   const uint32_t g = blockIdx.x;
   // K7e ran first: its stored segments are done (the early-out of step 0 in
@@ -785,7 +856,7 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
   const uint32_t hl = s ? kHist : 0u, hw = hl / 4u;
   if (hl) {
     const uint32_t* hb = reinterpret_cast<const uint32_t*>(seg_src - sh - hl);
-    for (uint32_t k = t; k < hw; k += kThreads) hist[k] = hb[k];
+    for (uint32_t k = t; k < hw; k += kThreads) hist[sw(k)] = hb[k];
   }
   for (uint32_t k = t; k < kTabWords; k += kThreads) tab[k] = 0u;
   for (uint32_t k = t; k < 288u; k += kThreads) hll[k] = k == 256u ? 1u : 0u;  // EOB once
@@ -828,17 +899,23 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
     constexpr uint32_t kMine = kWays / kPair;
     static_assert(kMine == 4u || kMine == 8u, "one 8- or 16-byte load of a thread's entries");
     const uint32_t part = t % kPair;
+    // a position's first 16 bytes are loaded one round ahead (the segment's
+    // words do not change in step 1), so a round's critical path starts at
+    // the bucket read
+    uint32_t curn[4];
+    seg16(data, t / kPair + sh, curn);
     for (uint32_t r = 0; r < kSeg / kRound; r++) {
       const uint32_t p = kRound * r + t / kPair;
       const uint32_t w = p + hl;
-      const uint32_t x = seg4(data, p + sh);
+      const uint32_t cur[4] = {curn[0], curn[1], curn[2], curn[3]};
+      const uint32_t x = cur[0];
       const bool live = p + 4u <= n;
       const uint32_t h = zhash(x);
       uint32_t best = 0u, bl = 0u;
       if (live) {
         uint32_t cs[kMine / 2];
         if constexpr (kMine == 8u) {
-          const uint4 c = *reinterpret_cast<const uint4*>(&tab16[h * kWays]);
+          const uint4 c = *reinterpret_cast<const uint4*>(&tab16[h * kWays + kMine * part]);
           cs[0] = c.x;
           cs[1] = c.y;
           cs[2] = c.z;
@@ -848,13 +925,15 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
           cs[0] = c.x;
           cs[1] = c.y;
         }
+        // this position goes into the table now (the pair's bucket reads came
+        // first in the wave's LDS order): its latency overlaps the compares;
+        // later positions of the round may see it, earlier ones skip it
+        if (part == 0u) insert(w, h);
         const uint32_t lim = min(258u, n - p);
         // the candidates' first 16 bytes at once (independent loads); a
         // slot may already hold a later position of this round (no barrier
         // between reads and inserts): only earlier positions within 32 KiB
         // are candidates
-        uint32_t cur[4];
-        seg16(data, p + sh, cur);
         uint32_t L[kMine], D[kMine];
   #pragma unroll
         for (uint32_t k = 0; k < kMine; k++) {
@@ -880,8 +959,11 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
           }
         }
       }
+      if (r + 1u < kSeg / kRound) seg16(data, p + kRound + sh, curn);
       if constexpr (kPair == 2u) {
-        const uint32_t obl = (uint32_t)__shfl_xor((int)bl, 1), obest = (uint32_t)__shfl_xor((int)best, 1);
+        // the partner lane's result by a DPP quad permutation [1,0,3,2] (no LDS trip)
+        const uint32_t obl = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)bl, 0xB1, 0xF, 0xF, false);
+        const uint32_t obest = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0xB1, 0xF, 0xF, false);
         if (obl > bl || (obl == bl && obest < best)) {
           bl = obl;
           best = obest;
@@ -894,7 +976,6 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
           A += x & 0xFFu;
           J += p * (x & 0xFFu);
         }
-        if (live) insert(w, h);
       }
       __syncthreads();
     }
@@ -970,15 +1051,21 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
     else
       (void)parse<true>(data, l8, cd, hll, hd, sh, n, p_s, rend, p_e, fbits, extra);
     K7P(5);
-    uint32_t etot, ntok;
-    fincl = wg_incl_sum(fbits, wsum, ftot);
-    (void)wg_incl_sum(extra, wsum, etot);
-    fixed_bytes = ((3u + ftot + 7u + 3u + 7u) >> 3) + 4u;  // header, tokens, EOB, sync flush
-    // entropy estimate of a dynamic code: build one only if it can win
+    // the fixed-code bits (prefix and total), extra bits, token and distance
+    // counts: one pass; then the entropy estimate of a dynamic code (build
+    // one only if it can win)
     const uint32_t f_t = t < 286u ? hll[t] : (t >= 288u && t < 318u ? hd[t - 288u] : 0u);
-    (void)wg_incl_sum(t < 286u ? f_t : 0u, wsum, ntok);
-    uint32_t ndist;
-    (void)wg_incl_sum(t >= 288u ? f_t : 0u, wsum, ndist);
+    uint32_t etot, ntok, ndist;
+    {
+      const uint32_t xs[4] = {fbits, extra, t < 286u ? f_t : 0u, t >= 288u ? f_t : 0u};
+      uint32_t ts[4];
+      fincl = wg_sums<4>(xs, wsum4, ts);
+      ftot = ts[0];
+      etot = ts[1];
+      ntok = ts[2];
+      ndist = ts[3];
+    }
+    fixed_bytes = ((3u + ftot + 7u + 3u + 7u) >> 3) + 4u;  // header, tokens, EOB, sync flush
     const float nn = t < 286u ? (float)ntok : (float)max(ndist, 1u);
     const uint32_t h_t = f_t ? (uint32_t)((float)f_t * (__log2f(nn) - __log2f((float)f_t))) : 0u;
     uint32_t htot;
@@ -989,15 +1076,11 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
       // scratch in the window (idle since the recording pass)
       uint32_t* keys = win;                                      // 512 litlen keys, sorted
       uint32_t* keysd = win + 512;                               // 32 distance keys, sorted
-      uint32_t* keys2 = win + 544;                               // 32 code-length keys
       uint32_t* hw = win + 576;                                  // weights: litlen 572, distance 60 at +576
       uint32_t* npar = win + 1792;                               // tree parents, distance nodes at +576
       uint32_t* nanc = win + 2816;                               // pointer-jumping ancestors
       uint32_t* ndep = win + 3840;                               // depths
       uint32_t* blc = win + 4864;                                // 2 x 16 length counts
-      uint32_t* cw = win + 4896;                                 // code-length code: weights (38)
-      uint16_t* cpar = reinterpret_cast<uint16_t*>(win + 4960);  // 38
-      uint8_t* cdep = reinterpret_cast<uint8_t*>(win + 4992);    // 38
       for (uint32_t k = t; k < 512u; k += kThreads) keys[k] = (k < 286u && hll[k]) ? (hll[k] << 9) | k : 0xFFFFFFFFu;
       for (uint32_t k = t; k < 320u; k += kThreads) zl[k] = 0u;
       if (t < 32u) blc[t] = 0u;
@@ -1009,21 +1092,41 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
       // symbol k; every thread reads the same frequency per step (an LDS
       // broadcast).  (A one-wave bitonic sort of 512 keys took ~25 % of the
       // segment's code construction.)
-      if (t < 286u && hll[t] != 0u) {
-        const uint32_t key = (hll[t] << 9) | t;
-        uint32_t r = 0u;
-        for (uint32_t q = 0; q < 286u; q++) {
-          const uint32_t f = hll[q];
-          r += f != 0u && ((f << 9) | q) < key;
-        }
-        keys[r] = key;
-      } else if (t >= 288u && t < 318u) {
-        const uint32_t k = t - 288u;
-        const uint32_t key = hd[k] ? (hd[k] << 9) | k : 0xFFFFFFFFu;
-        if (key != 0xFFFFFFFFu) {
+      {
+        // the frequencies in registers (lane l of every wave: litlen symbols
+        // l, l + 64, ..., distance symbol l), read back by readlane: no LDS
+        // round trip per compare
+        const uint32_t lane = t & 63u;
+        uint32_t fr[5];
+  #pragma unroll
+        for (uint32_t c = 0; c < 5u; c++) fr[c] = 64u * c + lane < 286u ? hll[64u * c + lane] : 0u;
+        const uint32_t fd = lane < 30u ? hd[lane] : 0u;
+        if (t < 286u && hll[t] != 0u) {
+          const uint32_t key = (hll[t] << 9) | t;
           uint32_t r = 0u;
-          for (uint32_t q = 0; q < 30u; q++) r += hd[q] && ((hd[q] << 9) | q) < key;
-          keysd[r] = key;
+          auto count = [&](uint32_t v, uint32_t q0) {
+            for (uint32_t j = 0; j < 64u; j++) {
+              const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j);
+              r += f != 0u && ((f << 9) | (q0 + j)) < key;
+            }
+          };
+          count(fr[0], 0u);
+          count(fr[1], 64u);
+          count(fr[2], 128u);
+          count(fr[3], 192u);
+          count(fr[4], 256u);
+          keys[r] = key;
+        } else if (t >= 288u && t < 318u) {
+          const uint32_t k = t - 288u;
+          if (hd[k]) {
+            const uint32_t key = (hd[k] << 9) | k;
+            uint32_t r = 0u;
+            for (uint32_t j = 0; j < 30u; j++) {
+              const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)fd, (int)j);
+              r += f != 0u && ((f << 9) | j) < key;
+            }
+            keysd[r] = key;
+          }
         }
       }
       const uint32_t ml = (uint32_t)__syncthreads_count(t < 286u && hll[t] != 0u);  // >= 1 (EOB)
@@ -1121,31 +1224,29 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
       const uint32_t nl = hlit + hdist;
       auto zv = [&](uint32_t i) -> uint32_t { return i < hlit ? zl[i] : zl[288u + i - hlit]; };
       uint32_t cur = 0u, run = 0u, cnt = 0u;
-      if (t < nl && (t == 0u || zv(t - 1u) != zv(t))) {
+      // run starts as one bit mask per wave (nl <= 316: waves 0..4); a run
+      // ends at the next start
+      const bool rstart = t < nl && (t == 0u || zv(t - 1u) != zv(t));
+      const uint64_t bm = __builtin_amdgcn_ballot_w64(rstart);
+      if ((t & 63u) == 0u && t < 320u) rmask[t >> 6] = bm;
+      __syncthreads();
+      if (rstart) {
         cur = zv(t);
-        run = 1u;
-        while (t + run < nl && zv(t + run) == cur) run++;
+        const uint32_t wv = t >> 6, b = t & 63u;
+        uint64_t m = b < 63u ? rmask[wv] & (~0ull << (b + 1u)) : 0ull;
+        uint32_t w2 = wv;
+        while (m == 0ull && ++w2 < 5u) m = rmask[w2];
+        const uint32_t nx = m ? min(nl, 64u * w2 + (uint32_t)__builtin_ctzll(m)) : nl;
+        run = nx - t;
         cnt = rle_runs<false>(cur, run, nullptr, nullptr);
       }
       uint32_t nr;
       const uint32_t at = wg_incl_sum(cnt, wsum, nr) - cnt;
       if (cnt) rle_runs<true>(cur, run, rle + at, clf);
       __syncthreads();
-      if (t == 0) {  // the code-length code: <= 19 symbols, serial
-        for (uint32_t k = 0; k < 19u; k++) cll[k] = 0u;
-        const uint32_t mc = sort_small(clf, 19u, keys2);
-        if (mc == 1u) {
-          const uint32_t x = keys2[0] & 511u;
-          cll[x] = 1u;
-          cll[x ? 0u : 1u] = 1u;
-        } else {
-          huff_lengths(keys2, mc, 7u, cll, cw, cpar, cdep);
-        }
-        canon_codes(cll, 19u, clc, blc);
-        uint32_t hclen = 4u;
-        for (uint32_t k = 0; k < 19u; k++)
-          if (cll[kClOrder[k]]) hclen = max(hclen, k + 1u);
-        zctl[4] = hclen;
+      if (t < 64u) {  // the code-length code: one wave
+        const uint32_t hcl = cl_code(t < 19u ? clf[t] : 0u, cll, clc);
+        if (t == 0u) zctl[4] = hcl;
       }
       __syncthreads();
       const uint32_t hclen = zctl[4];
