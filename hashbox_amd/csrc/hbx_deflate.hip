@@ -41,9 +41,9 @@
 //      to the segment's scratch slot, because the table and 96 KiB of
 //      per-position results do not fit the LDS together; they come back into
 //      the table's and the history's LDS once the table is done.
-//   2. the parse, greedy with two-step lazy matching (a longer match at p+1,
-//      or one longer by 2 at p+2, defers p as a literal; zlib's lazy matching
-//      looks one step ahead), from the stored lengths alone (no byte
+//   2. the parse, greedy with three-step lazy matching (a match at p+k longer
+//      than the one at p by k or more, k = 1..3, defers p as a literal; zlib's
+//      lazy matching looks one step ahead), from the stored lengths alone (no byte
 //      compares).  Thread t < 512 owns the 64-byte range [64t, 64t+64) but a
 //      match may run past its end (up to 258 bytes), and the next thread then
 //      starts where it ended: every thread first parses from its range start
@@ -56,7 +56,7 @@
 //   3. after a workgroup prefix sum of the bit counts, the tokens are emitted
 //      (ds_or) into the image (over the window's LDS), if that is smaller than
 //      stored; a stored segment is copied by K7b from the source.
-// Zipf text of tools/bench_deflate.py: 0.3120 of its size at 16.2 GB/s (zlib
+// Zipf text of tools/bench_deflate.py: 0.3115 of its size at 16.0 GB/s (zlib
 // -6: 0.3114; round 3: 0.327 at 16.0 GB/s with 8 ways of 2,048 buckets, 16
 // KiB of history and one-step lazy matching; 8 ways of 4,096 buckets here:
 // 0.3162 at 23.1 GB/s).  tools/k7model/k7model.c models the variants.
@@ -320,7 +320,7 @@ __device__ __forceinline__ void dist_sym(uint32_t dist, uint32_t& sym, uint32_t&
   }
 }
 
-// Step 2: the greedy parse of one thread, two-step lazy, with the candidate
+// Step 2: the greedy parse of one thread, three-step lazy, with the candidate
 // distances in `cd` (d = 0: none).  Dry (REC = false): from s while p < rend
 // (the thread's range end), matches up to min(258, n - p); returns where the
 // last token ends, which may be past rend.  Final (REC = true): from s while
@@ -328,7 +328,7 @@ __device__ __forceinline__ void dist_sym(uint32_t dist, uint32_t& sym, uint32_t&
 // overwrite the candidate slots they cover (already consumed): a literal at p
 // is 0x8000 | byte in slot p; a match is len in slot p and dist in slot p+1.
 // Symbol frequencies go to hll/hd; `bits` = fixed-code bits, `extra` = extra
-// bits (the same under any code).  Lookahead to p + 1 and p + 2 only while
+// bits (the same under any code).  Lookahead to p + 1 .. p + 3 only while
 // that is < rend, in both passes, so a converged final parse repeats the dry
 // one token for token (and never reads a slot past the thread's own range,
 // since its tokens end at or past rend).
@@ -366,11 +366,10 @@ __device__ __forceinline__ uint32_t parse(const uint32_t* data, const uint8_t* l
       d1 = cd[cphys(p + 1u)];
       len1 = d1 ? len_at(p + 1u) : 0u;
       defer = len1 > len;  // lazy: p becomes a literal, the longer match starts at p + 1
-      if (!defer && p + 2u < rend) {
-        // second step: a match at p + 2 longer than len + 1 also defers p
-        // (p + 1 then defers to it in turn)
-        defer = len_at(p + 2u) > len + 1u;
-      }
+      // further steps: a match at p + k longer than len + k - 1 also defers
+      // p (p + 1 .. p + k - 1 then defer to it in turn)
+      if (!defer && p + 2u < rend) defer = len_at(p + 2u) > len + 1u;
+      if (!defer && p + 3u < rend) defer = len_at(p + 3u) > len + 2u;
     }
     if (len >= 4u && !defer) {
       if (REC) {
