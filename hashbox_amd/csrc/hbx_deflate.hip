@@ -56,7 +56,7 @@
 //   3. after a workgroup prefix sum of the bit counts, the tokens are emitted
 //      (ds_or) into the image (over the window's LDS), if that is smaller than
 //      stored; a stored segment is copied by K7b from the source.
-// Zipf text of tools/bench_deflate.py: 0.3115 of its size at 16.0 GB/s (zlib
+// Zipf text of tools/bench_deflate.py: 0.3115 of its size at 16.3 GB/s (zlib
 // -6: 0.3114; round 3: 0.327 at 16.0 GB/s with 8 ways of 2,048 buckets, 16
 // KiB of history and one-step lazy matching; 8 ways of 4,096 buckets here:
 // 0.3162 at 23.1 GB/s).  tools/k7model/k7model.c models the variants.
@@ -866,6 +866,7 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
   uint32_t A = 0u, J = 0u;  // sum x, sum j*x over this thread's positions (j < 32768: J < 2^32)
   uint32_t fbits = 0u, fincl = 0u, ftot = 0u, fixed_bytes = 0xFFFFFFFFu;
   uint32_t p_s = 0u, p_e = 0u;  // this thread's tokens: positions [p_s, p_e)
+  uint32_t hoff = 0u;           // dynamic header: bit offset of run-length symbol t among them
   const uint32_t stored_bytes = 5u + n;
   // this segment's scratch slot: the candidate distances, later the image
   uint32_t* const slot = scratch + (uint64_t)g * (kSlot / 4u);
@@ -1257,7 +1258,7 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
       }
       if (t < 286u) tcost = hll[t] * zl[t];  // EOB included (hll[256] = 1)
       else if (t >= 288u && t < 318u) tcost = hd[t - 288u] * zl[t];
-      (void)wg_incl_sum(hcost, wsum, hb_body);
+      hoff = wg_incl_sum(hcost, wsum, hb_body) - hcost;
       (void)wg_incl_sum(tcost, wsum, tok_body);
       if (t == 0) {
         const uint32_t hb = 3u + 5u + 5u + 4u + 3u * hclen + hb_body;
@@ -1298,23 +1299,31 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
       incl = wg_incl_sum(mine, wsum, tot);
     }
     const uint32_t base = mode == 2u ? zpar[1] : 3u;
-    if (t == 0) {
-      uint32_t o = 0u;
-      if (mode == 1u) {
+    if (mode == 1u) {
+      if (t == 0) {
+        uint32_t o = 0u;
         emit_bits(img, o, 2u, 3u);  // BFINAL 0, BTYPE 01
-      } else {
-        const uint32_t hlit = zpar[3] & 0xFFFFu, hdist = zpar[3] >> 16;
-        const uint32_t hclen = zpar[4] & 0xFFFFu, nr = zpar[4] >> 16;
+      }
+    } else {
+      // the dynamic block header, one field per thread at its bit offset
+      const uint32_t hlit = zpar[3] & 0xFFFFu, hdist = zpar[3] >> 16;
+      const uint32_t hclen = zpar[4] & 0xFFFFu, nr = zpar[4] >> 16;
+      if (t == 0) {
+        uint32_t o = 0u;
         emit_bits(img, o, 4u, 3u);  // BFINAL 0, BTYPE 10
         emit_bits(img, o, hlit - 257u, 5u);
         emit_bits(img, o, hdist - 1u, 5u);
         emit_bits(img, o, hclen - 4u, 4u);
-        for (uint32_t k = 0; k < hclen; k++) emit_bits(img, o, cll[kClOrder[k]], 3u);
-        for (uint32_t k = 0; k < nr; k++) {
-          const uint32_t sy = rle[k] & 31u, e = clc[sy];
-          emit_bits(img, o, e & 0xFFFFu, e >> 16);
-          if (sy >= 16u) emit_bits(img, o, rle[k] >> 8, sy == 16u ? 2u : sy == 17u ? 3u : 7u);
-        }
+      }
+      if (t < hclen) {  // code-length code lengths, 3 bits each, in kClOrder
+        uint32_t o = 17u + 3u * t;
+        emit_bits(img, o, cll[kClOrder[t]], 3u);
+      }
+      if (t < nr) {  // run-length coded code lengths (hoff: the prefix of their bits)
+        uint32_t o = 17u + 3u * hclen + hoff;
+        const uint32_t sy = rle[t] & 31u, e = clc[sy];
+        emit_bits(img, o, e & 0xFFFFu, e >> 16);
+        if (sy >= 16u) emit_bits(img, o, rle[t] >> 8, sy == 16u ? 2u : sy == 17u ? 3u : 7u);
       }
     }
     walk_tokens<true>(cd, llc, dcc, img, p_s, p_e, base + incl - mine);
