@@ -56,7 +56,7 @@
 //   3. after a workgroup prefix sum of the bit counts, the tokens are emitted
 //      (ds_or) into the image (over the window's LDS), if that is smaller than
 //      stored; a stored segment is copied by K7b from the source.
-// Zipf text of tools/bench_deflate.py: 0.3115 of its size at 16.3 GB/s (zlib
+// Zipf text of tools/bench_deflate.py: 0.3115 of its size at 16.6 GB/s (zlib
 // -6: 0.3114; round 3: 0.327 at 16.0 GB/s with 8 ways of 2,048 buckets, 16
 // KiB of history and one-step lazy matching; 8 ways of 4,096 buckets here:
 // 0.3162 at 23.1 GB/s).  tools/k7model/k7model.c models the variants.
@@ -1065,11 +1065,13 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
       ntok = ts[2];
       ndist = ts[3];
     }
+    K7P(12);
     fixed_bytes = ((3u + ftot + 7u + 3u + 7u) >> 3) + 4u;  // header, tokens, EOB, sync flush
     const float nn = t < 286u ? (float)ntok : (float)max(ndist, 1u);
     const uint32_t h_t = f_t ? (uint32_t)((float)f_t * (__log2f(nn) - __log2f((float)f_t))) : 0u;
     uint32_t htot;
     (void)wg_incl_sum(h_t, wsum, htot);
+    K7P(13);
     const uint32_t best_other = min(fixed_bytes, stored_bytes) * 8u;
     const bool try_dyn = htot + etot + 600u < best_other;
     if (try_dyn) {
@@ -1082,48 +1084,46 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
       uint32_t* ndep = win + 3840;                               // depths
       uint32_t* blc = win + 4864;                                // 2 x 16 length counts
       for (uint32_t k = t; k < 512u; k += kThreads) keys[k] = (k < 286u && hll[k]) ? (hll[k] << 9) | k : 0xFFFFFFFFu;
+      // the sort's compare source: litlen keys at 0..287, distance keys at 288..319
+      uint32_t* ksrc = win + 6144;
+      for (uint32_t k = t; k < 320u; k += kThreads)
+        ksrc[k] = k < 286u   ? (hll[k] ? (hll[k] << 9) | k : 0xFFFFFFFFu)
+                : k < 288u   ? 0xFFFFFFFFu
+                : k < 318u   ? (hd[k - 288u] ? (hd[k - 288u] << 9) | (k - 288u) : 0xFFFFFFFFu)
+                             : 0xFFFFFFFFu;
       for (uint32_t k = t; k < 320u; k += kThreads) zl[k] = 0u;
       if (t < 32u) blc[t] = 0u;
       if (t < 19u) clf[t] = 0u;
       if (t < 8u) zctl[t] = 0u;
       __syncthreads();
+      K7P(14);
       // rank sorts, ascending (keys are unique: the symbol is in the low
       // bits): thread t < 286 places litlen symbol t, thread 288 + k distance
-      // symbol k; every thread reads the same frequency per step (an LDS
-      // broadcast).  (A one-wave bitonic sort of 512 keys took ~25 % of the
-      // segment's code construction.)
+      // symbol k.  (A one-wave bitonic sort of 512 keys took ~25 % of the
+      // segment's code construction; one compare per LDS read or readlane
+      // 32 k cycles, four per read 9 k.)
       {
-        // the frequencies in registers (lane l of every wave: litlen symbols
-        // l, l + 64, ..., distance symbol l), read back by readlane: no LDS
-        // round trip per compare
-        const uint32_t lane = t & 63u;
-        uint32_t fr[5];
-  #pragma unroll
-        for (uint32_t c = 0; c < 5u; c++) fr[c] = 64u * c + lane < 286u ? hll[64u * c + lane] : 0u;
-        const uint32_t fd = lane < 30u ? hd[lane] : 0u;
+        // every thread compares its key with all of them, four per LDS
+        // broadcast read (ksrc: the keys of symbol order, absent = ~0u)
+        const uint4* k4 = reinterpret_cast<const uint4*>(ksrc);
         if (t < 286u && hll[t] != 0u) {
           const uint32_t key = (hll[t] << 9) | t;
           uint32_t r = 0u;
-          auto count = [&](uint32_t v, uint32_t q0) {
-            for (uint32_t j = 0; j < 64u; j++) {
-              const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j);
-              r += f != 0u && ((f << 9) | (q0 + j)) < key;
-            }
-          };
-          count(fr[0], 0u);
-          count(fr[1], 64u);
-          count(fr[2], 128u);
-          count(fr[3], 192u);
-          count(fr[4], 256u);
+  #pragma unroll 8
+          for (uint32_t q = 0; q < 288u / 4u; q++) {
+            const uint4 v = k4[q];
+            r += (v.x < key) + (v.y < key) + (v.z < key) + (v.w < key);
+          }
           keys[r] = key;
         } else if (t >= 288u && t < 318u) {
           const uint32_t k = t - 288u;
           if (hd[k]) {
             const uint32_t key = (hd[k] << 9) | k;
             uint32_t r = 0u;
-            for (uint32_t j = 0; j < 30u; j++) {
-              const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)fd, (int)j);
-              r += f != 0u && ((f << 9) | j) < key;
+  #pragma unroll
+            for (uint32_t q = 288u / 4u; q < 320u / 4u; q++) {
+              const uint4 v = k4[q];
+              r += (v.x < key) + (v.y < key) + (v.z < key) + (v.w < key);
             }
             keysd[r] = key;
           }

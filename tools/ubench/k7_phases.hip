@@ -99,9 +99,10 @@ int main(int argc, char** argv) {
   }
   // inside huffman+mode (dynamic code only): 5 -> 8 sort, 8 -> 9 trees, 9 -> 10 lengths and codes,
   // 10 -> 11 header runs, 11 -> 6 costs
-  const int sub[][2] = {{5, 8}, {8, 9}, {9, 10}, {10, 11}, {11, 6}};
-  const char* sn[] = {"  huff: sort", "  huff: trees", "  huff: lengths", "  huff: header rle", "  huff: costs"};
-  for (int i = 0; i < 5; i++) {
+  const int sub[][2] = {{5, 8}, {8, 9}, {9, 10}, {10, 11}, {11, 6}, {5, 12}, {12, 13}, {13, 14}, {14, 8}};
+  const char* sn[] = {"  huff: sort", "  huff: trees", "  huff: lengths", "  huff: header rle", "  huff: costs",
+                      "    sort: sums", "    sort: entropy", "    sort: init", "    sort: rank"};
+  for (int i = 0; i < 9; i++) {
     std::vector<double> v;
     for (uint32_t g = 0; g < np; g++) {
       const unsigned long long a = pr[16 * g + sub[i][0]], b = pr[16 * g + sub[i][1]];
