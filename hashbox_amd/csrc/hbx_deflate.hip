@@ -67,6 +67,8 @@
 
 #include <cstdint>
 
+#include "hbx_device.h"  // DPP wave scans
+
 namespace hbxz {
 
 constexpr uint32_t kSeg = 32768;  // bytes per segment (one workgroup)
@@ -630,10 +632,7 @@ __device__ uint32_t cl_code(uint32_t f, uint8_t* cll, uint32_t* clc) {
 
 __device__ __forceinline__ uint32_t wg_incl_sum(uint32_t x, uint32_t* wsum, uint32_t& tot) {
   const uint32_t l = threadIdx.x & 63u, w = threadIdx.x >> 6;
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)x, d);
-    if (l >= (uint32_t)d) x += y;
-  }
+  x = hbx::wave_incl_sum(x);  // DPP
   if (l == 63u) wsum[w] = x;
   __syncthreads();
   uint32_t before = 0u;
@@ -649,19 +648,11 @@ __device__ __forceinline__ uint32_t wg_incl_sum(uint32_t x, uint32_t* wsum, uint
 template <int N>
 __device__ __forceinline__ uint32_t wg_sums(const uint32_t (&x)[N], uint32_t* wsum, uint32_t (&tot)[N]) {
   const uint32_t l = threadIdx.x & 63u, w = threadIdx.x >> 6;
-  uint32_t v = x[0];
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)v, d);
-    if (l >= (uint32_t)d) v += y;
-  }
+  const uint32_t v = hbx::wave_incl_sum(x[0]);  // DPP; lane 63 holds each wave total
   uint32_t r[N];
   r[0] = v;
 #pragma unroll
-  for (int i = 1; i < N; i++) {
-    uint32_t u = x[i];
-    for (int d = 32; d >= 1; d >>= 1) u += (uint32_t)__shfl_xor((int)u, d);
-    r[i] = u;
-  }
+  for (int i = 1; i < N; i++) r[i] = hbx::wave_incl_sum(x[i]);
   if (l == 63u) {
 #pragma unroll
     for (int i = 0; i < N; i++) wsum[i * kWaves + w] = r[i];
