@@ -865,9 +865,9 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
   uint8_t* const lg = reinterpret_cast<uint8_t*>(slot) + kSlotLens;
   uint8_t* const l8 = reinterpret_cast<uint8_t*>(hist);  // the lengths, after step 1
   {
-    // 1. candidates in position order + Adler partials.  tab16[h*8 + k]:
+    // 1. candidates in position order + Adler partials.  tab16[h*kWays + k]:
     //    window position + 1 of bucket h's k-th entry; cnt16[h]: inserts
-    //    so far (the slot of the next one, mod 8).  Each position's candidate
+    //    so far (the slot of the next one, mod kWays).  Each position's candidate
     //    distance goes to the slot in global memory (the table and the 64 KiB
     //    of distances do not fit the LDS together) and comes back into the
     //    table's LDS once the table is done.
