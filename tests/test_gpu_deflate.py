@@ -219,3 +219,21 @@ def test_parse_handoff_that_does_not_settle(engine):
             b[j::64 * k + j + 1] = b"\x01" * len(b[j::64 * k + j + 1])
             blocks.append(bytes(b))
     _check(engine, blocks)
+
+
+def test_history_reaches_back_32k(engine):
+    """A segment's matches may reach the whole 32 KiB before it (round 4;
+    16 KiB before): X Y X Y with 12 KiB of random letters each (order-0
+    entropy 4.7 bits, so no segment is stored by the early-out) puts the
+    second copies at distance 24 KiB, and the second segment ([32, 48) KiB)
+    lies entirely inside them: with the history it costs almost nothing, an
+    order-0 code alone would take ~9.4 KiB for it.  Then a copy at exactly the
+    window's reach, distance 32,768.  Strict inflate checks every distance."""
+    rng = np.random.default_rng(7)
+    letters = lambda n: rng.integers(97, 123, n, dtype=np.uint8).tobytes()  # noqa: E731
+    x, y = letters(12 << 10), letters(12 << 10)
+    (z,) = _check(engine, [x + y + x + y])
+    assert len(z) < 0.6 * (24 << 10) + 2048, len(z)  # X0 Y0 at order-0 cost, the copies nearly free (no history: >= 23 KiB)
+    w = letters(32 << 10)
+    (z2,) = _check(engine, [w + w[:16 << 10]])
+    assert len(z2) < 0.6 * (32 << 10) + 2048, len(z2)  # (no history: >= 28 KiB)
