@@ -768,6 +768,17 @@ extern "C" __global__ __launch_bounds__(256) void hbx_k7_deflate_entropy(const h
       if ((uint32_t)p + 4u <= n) rep |= sample(x);
     }
   }
+  // the history's samples too (round 4): a segment whose repeats lie only in
+  // the 32 KiB before it (in its block) is parsed, not stored, since K7a's
+  // matches reach there.  Only the history's word-aligned positions: a
+  // repeated stretch of a few hundred bytes still holds several sampled
+  // positions at each of the four alignments, and the pass costs a quarter
+  // (random data 690 -> 440 GB/s sampling every position); a repeat inside
+  // the history alone only costs a parse
+  if (s) {
+    const uint32_t* hb = base - kHist / 4u;  // the aligned base was the segment's start rounded down
+    for (uint32_t k = t; k < kHist / 4u; k += kEThreads) rep |= sample(hb[k]);
+  }
   if (rep) rep_any = 1u;
   __syncthreads();
   // per-symbol bits rounded, summed over the workgroup (K7a's formula)

@@ -237,3 +237,13 @@ def test_history_reaches_back_32k(engine):
     w = letters(32 << 10)
     (z2,) = _check(engine, [w + w[:16 << 10]])
     assert len(z2) < 0.6 * (32 << 10) + 2048, len(z2)  # (no history: >= 28 KiB)
+
+
+def test_random_repeat_in_history_is_parsed(engine):
+    """K7e samples a segment's history as well as the segment: random bytes
+    whose only repeat lies in the 32 KiB before the segment are parsed (and
+    matched there), not stored.  The first 32 KiB segment stays stored."""
+    rng = np.random.default_rng(11)
+    w = rng.integers(0, 256, 32 << 10, dtype=np.uint8).tobytes()
+    (z,) = _check(engine, [w + w[:16 << 10]])
+    assert len(z) < (32 << 10) + 1024, len(z)  # stored first segment + a nearly free second
