@@ -105,6 +105,21 @@ constexpr uint32_t kTabWords = (1u << kHashBits) * kWays / 2 + (1u << kHashBits)
 constexpr uint32_t kSlot = 3u * kSeg;
 constexpr uint32_t kSlotLens = 2u * kSeg;  // byte offset of the lengths
 static_assert(kSlot >= kImgWords * 4u, "the image fits its slot");
+// after the parse (K7a -> K7h), in words: the tokens at 0 (later the image),
+// each thread's token range start, end and fixed-code bits, the symbol
+// counts (litlen 0..285 and distances at 288..317, as the code lengths are
+// indexed; then the fixed-code and extra bit totals), and K7h's placement of
+// the image in its group's piece (byte offset, bytes, members)
+constexpr uint32_t kSlotThr = (kCdPhys / 2u + 15u) & ~15u;
+constexpr uint32_t kSlotRec = kSlotThr + 3u * 1024u;
+constexpr uint32_t kRecWords = 322;
+constexpr uint32_t kSlotMeta = kSlotRec + kRecWords + 2u;
+static_assert((kSlotMeta + 4u) * 4u <= kSlot, "the hand-off fits the slot");
+// kGroup consecutive segments of a block share one dynamic code (one header,
+// one end of block and sync flush) when that is smaller; the group's piece is
+// assembled by K7b in LDS, so it is at most kGroupBytes
+constexpr uint32_t kGroup = 4;
+constexpr uint32_t kGroupBytes = 65536;
 constexpr uint32_t kTabLds = kTabWords > kCdPhys / 2u ? kTabWords : kCdPhys / 2u;  // table, then distances
 // window positions + 1 are u16 entries, and a bucket's u16 insert counter
 // never carries into its neighbour's
@@ -701,6 +716,8 @@ __device__ __forceinline__ uint32_t zblock_of(const hbxz::ZBlock* blocks, uint32
 namespace hbxz {
 constexpr uint32_t kModeSrcStored = 3u;    // SegInfo.mode: stored, K7b copies the bytes from the source
 constexpr uint32_t kModeParse = 0xFFu;     // SegInfo.mode set by K7e: K7a decides
+constexpr uint32_t kModeGroupHead = 4u;    // first segment of a shared-code group: bytes = the group's piece
+constexpr uint32_t kModeGroupMember = 5u;  // a later member: its bits are in the head's piece (bytes = 0)
 constexpr uint32_t kEThreads = 256;
 }  // namespace hbxz
 
@@ -728,10 +745,6 @@ extern "C" __global__ __launch_bounds__(256) void hbx_k7_deflate_entropy(const h
   const uint64_t off = (uint64_t)s * kSeg;
   const uint32_t n = (uint32_t)min((uint64_t)kSeg, bk.len - off);
   const uint32_t t = threadIdx.x;
-  if (n < 4096u) {
-    if (t == 0) info[g].mode = kModeParse;
-    return;
-  }
   const uint64_t a = bk.src + off;
   const uint32_t sh = (uint32_t)(a & 3u);
   const uint32_t* base = reinterpret_cast<const uint32_t*>(a - sh);
@@ -805,7 +818,8 @@ extern "C" __global__ __launch_bounds__(256) void hbx_k7_deflate_entropy(const h
       As += wad[w][0];
       Js += wad[w][1];
     }
-    const bool incompressible = (float)hsum >= 7.97f * (float)n && rep_any == 0u;
+    // (every segment's Adler partials come from here; K7a no longer sums them)
+    const bool incompressible = n >= 4096u && (float)hsum >= 7.97f * (float)n && rep_any == 0u;
     SegInfo si;
     si.mode = incompressible ? kModeSrcStored : kModeParse;
     si.bytes = 5u + n;
@@ -829,14 +843,8 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
   __shared__ uint32_t tab[kTabLds];
   uint16_t* const cd = reinterpret_cast<uint16_t*>(tab);
   __shared__ uint32_t starts[kThreads + 1];  // each thread's parse start (step 2)
-  __shared__ uint32_t wsum[kWaves];
   __shared__ uint32_t wsum4[4 * kWaves];
-  __shared__ unsigned long long wadler[2 * kWaves];
-  __shared__ uint32_t hll[288], hd[32], llc[288], dcc[32], rle[320], clf[19], clc[19], zpar[8], zctl[8];
-  __shared__ __attribute__((aligned(4))) uint8_t zl[320];
-  __shared__ uint8_t cll[20];
-  __shared__ unsigned long long rmask[5];  // code-length run starts (header RLE)
-  static_assert(kImgWords <= kHistWords + kDataPhys, "the image fits the window's LDS");
+  __shared__ uint32_t hll[288], hd[32];
   const uint32_t g = blockIdx.x;
   // K7e ran first: its stored segments are done (the early-out of step 0 in
   // rounds 1-3 lives there now), every other segment is parsed
@@ -865,11 +873,8 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
   __syncthreads();
 
   K7P(1);
-  uint32_t A = 0u, J = 0u;  // sum x, sum j*x over this thread's positions (j < 32768: J < 2^32)
-  uint32_t fbits = 0u, fincl = 0u, ftot = 0u, fixed_bytes = 0xFFFFFFFFu;
+  uint32_t fbits = 0u;
   uint32_t p_s = 0u, p_e = 0u;  // this thread's tokens: positions [p_s, p_e)
-  uint32_t hoff = 0u;           // dynamic header: bit offset of run-length symbol t among them
-  const uint32_t stored_bytes = 5u + n;
   // this segment's scratch slot: the candidate distances, later the image
   uint32_t* const slot = scratch + (uint64_t)g * (kSlot / 4u);
   uint16_t* const cdg = reinterpret_cast<uint16_t*>(slot);
@@ -974,10 +979,6 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
       if (part == 0u) {
         cdg[p] = (uint16_t)best;
         lg[p] = (uint8_t)(bl ? bl - 3u : 0u);
-        if (p < n) {
-          A += x & 0xFFu;
-          J += p * (x & 0xFFu);
-        }
       }
       __syncthreads();
     }
@@ -1053,29 +1054,124 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
     else
       (void)parse<true>(data, l8, cd, hll, hd, sh, n, p_s, rend, p_e, fbits, extra);
     K7P(5);
-    // the fixed-code bits (prefix and total), extra bits, token and distance
-    // counts: one pass; then the entropy estimate of a dynamic code (build
-    // one only if it can win)
+    // the tokens, each thread's range and fixed-code bits, and the symbol
+    // counts go to the slot for K7h (the distances and lengths there are
+    // consumed); the EOB is not counted here
+    const uint32_t xs[2] = {fbits, extra};
+    uint32_t ts[2];
+    (void)wg_sums<2>(xs, wsum4, ts);  // its barriers also order the counts' atomics
+    for (uint32_t k = t; k < kCdPhys / 2u; k += kThreads) slot[k] = tab[k];
+    slot[kSlotThr + t] = p_s;
+    slot[kSlotThr + kThreads + t] = p_e;
+    slot[kSlotThr + 2u * kThreads + t] = fbits;
+    uint32_t* const rec = slot + kSlotRec;
+    if (t < 320u) rec[t] = t < 286u ? (t == 256u ? 0u : hll[t]) : (t >= 288u && t < 318u ? hd[t - 288u] : 0u);
+    if (t == 0u) {
+      rec[320] = ts[0];
+      rec[321] = ts[1];
+    }
+  }
+}
+
+
+// K7h: codes one parsed segment from K7a's hand-off in its slot.  The parsed
+// segments of a group (kGroup consecutive segments of one block, none stored
+// by K7e) share one dynamic code built from their summed counts: the first
+// member's bits start with the header, the last member's end with the end of
+// block and the sync flush, and member m's bits continue member m-1's at bit
+// S_m = header + the bits of members 0..m-1 (each member's bit count follows
+// from its counts and the code's lengths).  Every member builds the same code
+// from the same counts, so the decision and every offset agree across the
+// group's workgroups with no communication between them.  A member's image
+// starts at bit S_m mod 8 of the byte K7b ORs it into (S_m / 8 of the piece).
+// The group shares only if its piece is smaller than the sum of its members'
+// fixed-or-stored sizes and fits kGroupBytes; otherwise each member is coded
+// alone (dynamic, fixed or stored, whichever is smallest; rounds 1-4).
+extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_code(const hbxz::ZBlock* __restrict__ blocks,
+                                                                                uint32_t nb, uint32_t nseg,
+                                                                                hbxz::SegInfo* __restrict__ info,
+                                                                                uint32_t* __restrict__ scratch) {
+  using namespace hbxz;
+  __shared__ __attribute__((aligned(16))) uint32_t cdw[kCdPhys / 2u];  // the tokens
+  const uint16_t* const cd = reinterpret_cast<const uint16_t*>(cdw);
+  __shared__ __attribute__((aligned(16))) uint32_t win[kImgWords];  // Huffman scratch, then the image
+  __shared__ uint32_t mrec[kGroup][kRecWords];
+  __shared__ uint32_t wsum[kWaves];
+  __shared__ uint32_t wsum4[4 * kWaves];
+  __shared__ uint32_t hll[288], hd[32], llc[288], dcc[32], rle[320], clf[19], clc[19], zpar[8], zctl[8];
+  __shared__ uint32_t gpar[3 * kGroup + 2];
+  __shared__ __attribute__((aligned(4))) uint8_t zl[320];
+  __shared__ uint8_t cll[20];
+  __shared__ unsigned long long rmask[5];  // code-length run starts (header RLE)
+  static_assert(6464u <= kImgWords, "the Huffman scratch fits the image's LDS");
+  static_assert(kGroup <= 4u, "member bit sums in wsum4");
+  const uint32_t g = blockIdx.x;
+  if (g >= nseg) return;
+  const SegInfo si0 = info[g];
+  if (si0.mode == kModeSrcStored) return;
+  K7P(6);
+  const ZBlock bk = blocks[zblock_of(blocks, nb, g)];
+  const uint32_t s = g - bk.seg0;
+  const uint32_t n = (uint32_t)min((uint64_t)kSeg, bk.len - (uint64_t)s * kSeg);
+  const uint32_t t = threadIdx.x;
+  const uint32_t gs = s - s % kGroup, gn = min(kGroup, bk.nseg - gs), my = s - gs;
+  uint32_t* const slot = scratch + (uint64_t)g * (kSlot / 4u);
+  for (uint32_t k = t; k < kCdPhys / 2u; k += kThreads) cdw[k] = slot[k];
+  const uint32_t p_s = slot[kSlotThr + t], p_e = slot[kSlotThr + kThreads + t];
+  const uint32_t fbits = slot[kSlotThr + 2u * kThreads + t];
+  // a member's mode is K7e's (parse or stored) or, once coded, one that is
+  // stored only when its group does not share: either way "not stored by
+  // K7e" reads the same for every member of a sharing group
+  const bool live = t >= gn || info[bk.seg0 + gs + t].mode != kModeSrcStored;
+  const bool grp = __syncthreads_and(live) && gn >= 2u;
+  const uint32_t own = grp ? my : 0u;
+  for (uint32_t m = 0; m < kGroup; m++) {
+    if (!(grp ? m < gn : m == 0u)) continue;
+    const uint32_t* rec = scratch + (uint64_t)(grp ? g - my + m : g) * (kSlot / 4u) + kSlotRec;
+    for (uint32_t k = t; k < kRecWords; k += kThreads) mrec[m][k] = rec[k];
+  }
+  __syncthreads();
+  uint32_t fincl, ftot;
+  fincl = wg_incl_sum(fbits, wsum, ftot);
+  const uint32_t stored_bytes = 5u + n;
+  const uint32_t fixed_bytes = ((3u + ftot + 7u + 3u + 7u) >> 3) + 4u;  // header, tokens, EOB, sync flush
+  uint32_t hoff = 0u;  // dynamic header: bit offset of run-length symbol t among them
+  uint32_t mode = 0u, nbytes = stored_bytes, ibase = 0u;
+  bool shared = false;
+  #pragma nounroll
+  for (uint32_t pass = grp ? 0u : 1u; pass < 2u; pass++) {
+    const bool G = pass == 0u;  // the group's code, else this segment's own
+    if (t < 320u) {
+      uint32_t c = 0u;
+      if (G) {
+        for (uint32_t m = 0; m < gn; m++) c += mrec[m][t];
+      } else {
+        c = mrec[own][t];
+      }
+      if (t == 256u) c = 1u;  // the EOB, once
+      if (t < 288u) hll[t] = c; else hd[t - 288u] = c;
+    }
+    __syncthreads();
+    uint32_t etot = 0u;
+    for (uint32_t m = 0; m < (G ? gn : 1u); m++) etot += mrec[G ? m : own][321];
+    // the entropy estimate of a dynamic code (alone: build one only if it can win)
     const uint32_t f_t = t < 286u ? hll[t] : (t >= 288u && t < 318u ? hd[t - 288u] : 0u);
-    uint32_t etot, ntok, ndist;
+    uint32_t ntok, ndist;
     {
-      const uint32_t xs[4] = {fbits, extra, t < 286u ? f_t : 0u, t >= 288u ? f_t : 0u};
-      uint32_t ts[4];
-      fincl = wg_sums<4>(xs, wsum4, ts);
-      ftot = ts[0];
-      etot = ts[1];
-      ntok = ts[2];
-      ndist = ts[3];
+      const uint32_t xs[2] = {t < 286u ? f_t : 0u, t >= 288u ? f_t : 0u};
+      uint32_t ts[2];
+      (void)wg_sums<2>(xs, wsum4, ts);
+      ntok = ts[0];
+      ndist = ts[1];
     }
     K7P(12);
-    fixed_bytes = ((3u + ftot + 7u + 3u + 7u) >> 3) + 4u;  // header, tokens, EOB, sync flush
     const float nn = t < 286u ? (float)ntok : (float)max(ndist, 1u);
     const uint32_t h_t = f_t ? (uint32_t)((float)f_t * (__log2f(nn) - __log2f((float)f_t))) : 0u;
     uint32_t htot;
     (void)wg_incl_sum(h_t, wsum, htot);
     K7P(13);
     const uint32_t best_other = min(fixed_bytes, stored_bytes) * 8u;
-    const bool try_dyn = htot + etot + 600u < best_other;
+    const bool try_dyn = G || htot + etot + 600u < best_other;
     if (try_dyn) {
       // scratch in the window (idle since the recording pass)
       uint32_t* keys = win;                                      // 512 litlen keys, sorted
@@ -1275,11 +1371,52 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
     } else if (t == 0) {
       zpar[0] = 0u;
     }
+    __syncthreads();
+    if (G) {
+      // each member's bits under the group's code, its place in the piece
+      if (t < kGroup) zctl[t] = 0u;
+      __syncthreads();
+      if (t < 320u && zl[t])
+        for (uint32_t m = 0; m < gn; m++) atomicAdd(&zctl[m], mrec[m][t] * zl[t]);
+      __syncthreads();
+      if (t < gn) atomicAdd(&zctl[t], mrec[t][321]);  // + its extra bits
+      __syncthreads();
+      if (t == 0u) {
+        const uint32_t hb = zpar[1], eob = llc[256] >> 16;
+        uint32_t S = hb, alone = 0u, ok = 1u, total = 0u;
+        for (uint32_t m = 0; m < gn; m++) {
+          const uint32_t T = zctl[m];
+          const uint32_t o0 = m ? (S & 7u) : hb;  // where its first token goes in its image
+          const uint32_t B = m ? (S >> 3) : 0u;
+          const uint32_t end = o0 + T;
+          const uint32_t il = m + 1u == gn ? ((end + eob + 3u + 7u) >> 3) + 4u : (end + 7u) >> 3;
+          if (il + 8u > 4u * kImgWords) ok = 0u;
+          gpar[3 * m] = B;
+          gpar[3 * m + 1] = il;
+          gpar[3 * m + 2] = o0;
+          S += T;
+          total = B + il;
+          const uint32_t nm = (uint32_t)min((uint64_t)kSeg, bk.len - (uint64_t)(gs + m) * kSeg);
+          const uint32_t fm = ((3u + mrec[m][320] + 7u + 3u + 7u) >> 3) + 4u;
+          alone += min(5u + nm, fm);
+        }
+        gpar[3 * kGroup] = ok && total <= kGroupBytes && total < alone ? 1u : 0u;
+        gpar[3 * kGroup + 1] = total;
+      }
+      __syncthreads();
+      shared = gpar[3 * kGroup] != 0u;
+      if (shared) {
+        mode = 2u;
+        ibase = gpar[3 * my + 2];
+        nbytes = gpar[3 * my + 1];
+        break;
+      }
+      continue;  // code alone
+    }
+    mode = zpar[0];  // 2 dynamic, 0 not (then fixed or stored)
+    if (mode == 0u && fixed_bytes < stored_bytes) mode = 1u;
+    ibase = mode == 2u ? zpar[1] : 3u;
   }
-  __syncthreads();
-  K7P(6);
-  uint32_t mode = zpar[0];  // 2 dynamic, 1 fixed, 0 stored
-  if (mode == 0u && fixed_bytes < stored_bytes) mode = 1u;
   if (mode == 1u) {  // fixed code tables
     for (uint32_t k = t; k < 288u; k += kThreads)
       llc[k] = k < 144u ? rev(0x30u + k, 8u) | (8u << 16)
@@ -1288,25 +1425,26 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
                         : rev(0xC0u + k - 280u, 8u) | (8u << 16);
     for (uint32_t k = t; k < 32u; k += kThreads) dcc[k] = rev(k, 5u) | (5u << 16);
   }
-  uint32_t* img = win;  // the window is idle (the tokens are in cd)
-  uint32_t nbytes = stored_bytes;
+  K7P(7);
+  uint32_t* img = win;  // the Huffman scratch is idle now
   if (mode != 0u) {
     __syncthreads();
     for (uint32_t k = t; k < kImgWords; k += kThreads) img[k] = 0u;
     __syncthreads();
-    // 3. emit: this thread's tokens at its prefix offset after the block header
+    // this thread's tokens at its prefix offset after the block header (or,
+    // in a group, after the bits before it in its first byte)
     uint32_t mine = fbits, incl = fincl, tot = ftot;
     if (mode == 2u) {
       mine = walk_tokens<false>(cd, llc, dcc, nullptr, p_s, p_e, 0u);
       incl = wg_incl_sum(mine, wsum, tot);
     }
-    const uint32_t base = mode == 2u ? zpar[1] : 3u;
+    const bool head = !shared || my == 0u, last = !shared || my + 1u == gn;
     if (mode == 1u) {
       if (t == 0) {
         uint32_t o = 0u;
         emit_bits(img, o, 2u, 3u);  // BFINAL 0, BTYPE 01
       }
-    } else {
+    } else if (head) {
       // the dynamic block header, one field per thread at its bit offset
       const uint32_t hlit = zpar[3] & 0xFFFFu, hdist = zpar[3] >> 16;
       const uint32_t hclen = zpar[4] & 0xFFFFu, nr = zpar[4] >> 16;
@@ -1328,52 +1466,44 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
         if (sy >= 16u) emit_bits(img, o, rle[t] >> 8, sy == 16u ? 2u : sy == 17u ? 3u : 7u);
       }
     }
-    walk_tokens<true>(cd, llc, dcc, img, p_s, p_e, base + incl - mine);
+    walk_tokens<true>(cd, llc, dcc, img, p_s, p_e, ibase + incl - mine);
     __syncthreads();
     if (t == 0) {
-      uint32_t o = base + tot;
-      emit_bits(img, o, llc[256] & 0xFFFFu, llc[256] >> 16);  // end of block
-      const uint32_t e = (o + 3u + 7u) >> 3;                  // + the empty stored block's 3 header bits
-      uint8_t* ob = reinterpret_cast<uint8_t*>(img);
-      ob[e] = 0x00;
-      ob[e + 1] = 0x00;
-      ob[e + 2] = 0xFF;
-      ob[e + 3] = 0xFF;
-      zpar[5] = e + 4u;
+      uint32_t o = ibase + tot, e = (o + 7u) >> 3;
+      if (last) {
+        emit_bits(img, o, llc[256] & 0xFFFFu, llc[256] >> 16);  // end of block
+        e = (o + 3u + 7u) >> 3;                                 // + the empty stored block's 3 header bits
+        uint8_t* ob = reinterpret_cast<uint8_t*>(img);
+        ob[e] = 0x00;
+        ob[e + 1] = 0x00;
+        ob[e + 2] = 0xFF;
+        ob[e + 3] = 0xFF;
+        e += 4u;
+      }
+      zpar[5] = e;
     }
     __syncthreads();
-    nbytes = zpar[5];
+    nbytes = zpar[5];  // in a group: equal to gpar's il (the walk and the counts agree)
   } else {
     mode = kModeSrcStored;  // stored: K7b copies the bytes from the source
   }
-  K7P(7);
   if (mode != kModeSrcStored)
     for (uint32_t k = t; k < (nbytes + 3u) / 4u; k += kThreads) slot[k] = img[k];
-
-  // Adler partials: B = sum (n - j) x_j = n*A - J  (64-bit, then mod)
-  unsigned long long A64 = A, J64 = J;
-  for (int dd = 32; dd >= 1; dd >>= 1) {
-    A64 += (unsigned long long)__shfl_xor((long long)A64, dd);
-    J64 += (unsigned long long)__shfl_xor((long long)J64, dd);
-  }
-  if ((t & 63u) == 0u) {
-    wadler[2 * (t >> 6)] = A64;
-    wadler[2 * (t >> 6) + 1] = J64;
-  }
-  __syncthreads();
   if (t == 0) {
-    unsigned long long As = 0, Js = 0;
-    for (uint32_t k = 0; k < kWaves; k++) {
-      As += wadler[2 * k];
-      Js += wadler[2 * k + 1];
+    SegInfo si = si0;
+    if (shared) {
+      slot[kSlotMeta] = gpar[3 * my];
+      slot[kSlotMeta + 1] = nbytes;
+      slot[kSlotMeta + 2] = gn;
+      si.mode = my == 0u ? kModeGroupHead : kModeGroupMember;
+      si.bytes = my == 0u ? gpar[3 * kGroup + 1] : 0u;
+    } else {
+      si.mode = mode;
+      si.bytes = nbytes;
     }
-    SegInfo si;
-    si.mode = mode;
-    si.bytes = nbytes;
-    si.a = (uint32_t)(As % kAdlerMod);
-    si.b = (uint32_t)(((unsigned long long)n * As - Js) % kAdlerMod);
     info[g] = si;
   }
+  K7P(15);
 }
 
 // One wave per block: segment offsets (exclusive scan), header, trailer.
@@ -1448,6 +1578,7 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_write(uint32_t 
   const uint32_t t = threadIdx.x;
   const SegInfo si = info[g];
   const uint32_t nbytes = si.bytes;
+  if (si.mode == kModeGroupMember) return;  // written with its group's head
   if (si.mode == kModeSrcStored) {  // 00 | LEN | ~LEN | the segment's bytes, straight from the source
     const ZBlock bk = blocks[zblock_of(blocks, nb, g)];
     const uint32_t n = nbytes - 5u;
@@ -1476,6 +1607,48 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_write(uint32_t 
     return;
   }
   const uint32_t* slot = scratch + (uint64_t)g * (kSlot / 4u);
+  if (si.mode == kModeGroupHead) {
+    // the group's piece, straight from the members' images: member m's
+    // image covers piece bytes [B_m, B_m + il_m), and where two members meet
+    // a byte holds bits of both (OR).  No LDS: this path would otherwise set
+    // K7b's LDS, and with it the occupancy of the stored-segment copies.
+    const uint32_t gn = slot[kSlotMeta + 2];
+    uint32_t Bm[kGroup], Lm[kGroup];
+    const uint8_t* Mb[kGroup];
+  #pragma unroll
+    for (uint32_t m = 0; m < kGroup; m++) {
+      const uint32_t* ms = scratch + (uint64_t)(g + min(m, gn - 1u)) * (kSlot / 4u);
+      Bm[m] = m < gn ? ms[kSlotMeta] : 0u;
+      Lm[m] = m < gn ? ms[kSlotMeta + 1] : 0u;
+      Mb[m] = reinterpret_cast<const uint8_t*>(ms);
+    }
+    auto piece4 = [&](uint32_t q) -> uint32_t {  // piece bytes q .. q + 3, little-endian
+      uint32_t v = 0u;
+  #pragma unroll
+      for (uint32_t m = 0; m < kGroup; m++) {
+        if (q + 4u <= Bm[m] || q >= Bm[m] + Lm[m]) continue;  // also every m >= gn (Lm = 0)
+        const int32_t r = (int32_t)q - (int32_t)Bm[m];
+        if (r >= 0 && (uint32_t)r + 4u <= Lm[m]) {  // four image bytes at any alignment
+          v |= *reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(
+              reinterpret_cast<uintptr_t>(Mb[m] + r));
+        } else {
+          for (int32_t j = 0; j < 4; j++)
+            if (r + j >= 0 && (uint32_t)(r + j) < Lm[m]) v |= (uint32_t)Mb[m][r + j] << (8 * j);
+        }
+      }
+      return v;
+    };
+    uint8_t* D = reinterpret_cast<uint8_t*>(seg_off[g]);
+    const uint32_t lead = (uint32_t)((4u - (reinterpret_cast<uint64_t>(D) & 3u)) & 3u);
+    const uint32_t head = min(lead, nbytes);
+    if (t < head) D[t] = (uint8_t)piece4(t);
+    const uint32_t nw = (nbytes - head) >> 2;
+    uint32_t* Dw = reinterpret_cast<uint32_t*>(D + head);
+    for (uint32_t k = t; k < nw; k += kWThreads) Dw[k] = piece4(head + 4u * k);
+    const uint32_t done = head + 4u * nw;
+    if (t < nbytes - done) D[done + t] = (uint8_t)piece4(done + t);
+    return;
+  }
   for (uint32_t k = t; k < kImgWords + 2u; k += kWThreads) img[k] = k < (nbytes + 3u) / 4u ? slot[k] : 0u;
   __syncthreads();
   // image [0, nbytes) -> the stream at byte address D

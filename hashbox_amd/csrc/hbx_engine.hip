@@ -1758,6 +1758,8 @@ int z_start(hbx_ctx* c, ZPend& zp, const uint64_t* cut_ends, const uint64_t* out
                      (uint32_t)nseg, Z.info.as<hbxz::SegInfo>());
   hipLaunchKernelGGL(hbx_k7_deflate_size, dim3((uint32_t)nseg), dim3(hbxz::kThreads), 0, s, dz, (uint32_t)n,
                      (uint32_t)nseg, Z.info.as<hbxz::SegInfo>(), Z.img.as<uint32_t>());
+  hipLaunchKernelGGL(hbx_k7_deflate_code, dim3((uint32_t)nseg), dim3(hbxz::kThreads), 0, s, dz, (uint32_t)n,
+                     (uint32_t)nseg, Z.info.as<hbxz::SegInfo>(), Z.img.as<uint32_t>());
   HBX_TRY(c, hipGetLastError());
   hipLaunchKernelGGL(hbx_k7_deflate_plan, dim3((uint32_t)n), dim3(64), 0, s, dz, (uint32_t)n,
                      Z.info.as<hbxz::SegInfo>(), Z.off.as<uint64_t>(), Z.len.as<uint64_t>());
@@ -2293,6 +2295,8 @@ int deflate_device(hbx_ctx* c, uint64_t n, const uint64_t* src, const uint64_t* 
     hipLaunchKernelGGL(hbx_k7_deflate_entropy, dim3((uint32_t)nseg), dim3(hbxz::kEThreads), 0, s, dz, (uint32_t)n,
                        (uint32_t)nseg, c->d_zinfo.as<hbxz::SegInfo>());
     hipLaunchKernelGGL(hbx_k7_deflate_size, dim3((uint32_t)nseg), dim3(hbxz::kThreads), 0, s, dz, (uint32_t)n,
+                       (uint32_t)nseg, c->d_zinfo.as<hbxz::SegInfo>(), c->d_zimg.as<uint32_t>());
+    hipLaunchKernelGGL(hbx_k7_deflate_code, dim3((uint32_t)nseg), dim3(hbxz::kThreads), 0, s, dz, (uint32_t)n,
                        (uint32_t)nseg, c->d_zinfo.as<hbxz::SegInfo>(), c->d_zimg.as<uint32_t>());
     HBX_TRY(c, hipGetLastError());
   }

@@ -247,3 +247,28 @@ def test_random_repeat_in_history_is_parsed(engine):
     w = rng.integers(0, 256, 32 << 10, dtype=np.uint8).tobytes()
     (z,) = _check(engine, [w + w[:16 << 10]])
     assert len(z) < (32 << 10) + 1024, len(z)  # stored first segment + a nearly free second
+
+
+def test_shared_code_groups(engine):
+    """Round 4: kGroup = 4 consecutive parsed segments of a block share one
+    dynamic code (K7h): one header, one end of block and sync flush, and each
+    member's bits continue the previous member's mid-byte.  Edges: partial
+    groups (2, 3, 5, 9 segments), a last member of a few bits (a 4-byte match
+    at distance 4), a member of zeros (a few hundred bits), a stored random
+    segment inside a group (no sharing there), and a text block whose group
+    pieces must each end in the only sync flush of the group."""
+    seg = 32768
+    t = _text(12 * seg, 3)
+    rng = np.random.default_rng(5)
+    rnd = rng.integers(0, 256, seg, dtype=np.uint8).tobytes()
+    blocks = [t[:n] for n in (seg + 1, seg + 3, 2 * seg + 5, 3 * seg + 1, 4 * seg, 4 * seg + 3, 5 * seg + 17,
+                              9 * seg + 100)]
+    blocks.append(t[: seg - 4] + b"wxyz" + b"wxyz")  # second segment: one 4-byte match
+    blocks.append(t[:seg] + bytes(seg) + t[seg : 3 * seg])  # zeros in the middle of a group
+    blocks.append(t[:seg] + rnd + t[seg : 3 * seg])  # a stored member: the group codes alone
+    blocks.append(rnd + t[: 3 * seg] + rnd + t[3 * seg : 6 * seg])
+    _check(engine, blocks)
+    big = _text(4 << 20, 9)
+    (z,) = _check(engine, [big])
+    # 128 segments in 32 groups: one sync flush (00 00 FF FF) per group + the final block's
+    assert z.count(b"\x00\x00\xff\xff") <= 128 // 4 + 2, z.count(b"\x00\x00\xff\xff")

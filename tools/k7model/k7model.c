@@ -18,6 +18,7 @@
 //   -F          FIFO buckets (the WAYS latest positions per hash)
 //   -f D4 / -g D5  length-4 / -5 matches farther than D4 / D5 are taken as literals
 //   -P 1        flexible parsing: a match is cut where the next one reaches farthest
+//   -S SHARE    segments that share one dynamic code and header (1 in K7)
 //   -x W2       a second FIFO table of W2 ways keyed by K2 bytes (-k K2, -y BITS2)
 //   cc -O2 -o k7model k7model.c -lm ; ./k7model [flags] < corpus
 #include <math.h>
@@ -30,6 +31,8 @@
 static int WAYS = 4, HBITS = 11, RANGE = 64, SEG = 32768, HIST = 0, HLEN = 0, MINM = 4, LAZY = 1, ROUND = 512;
 static long BLOCK = 4 << 20;
 static int W2 = 0, K2 = 8, B2 = 11, FAR4 = 0, FAR5 = 0, FLEX = 0;
+static int SHARE = 1;  // -S: segments that share one dynamic code (and header)
+static double hdr_total = 0;
 static int FIFO = 0;  // -F: a bucket keeps its WAYS latest positions (a per-bucket counter) instead of one per residue
 static uint32_t* fcnt;
 static void ins(uint32_t* tab, uint32_t h, int rel) {
@@ -95,6 +98,38 @@ static void huff(const long* f, int n, int lim, int* len) {
     for (int i = 0; i < n; i++) if (g[i]) g[i] = (g[i] + 1) / 2;
   }
 }
+// exact dynamic header bits (RFC 1951 §3.2.7): run-length coded code lengths
+// under a length-7 code-length code
+static double hdr_bits(const int* ll, const int* dl, int hlit, int hdist) {
+  static const int ord[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+  int seq[320], n = 0;
+  for (int i = 0; i < hlit; i++) seq[n++] = ll[i];
+  for (int i = 0; i < hdist; i++) seq[n++] = dl[i];
+  long f[19] = {0};
+  double extra = 0;
+  for (int i = 0; i < n;) {
+    int j = i;
+    while (j < n && seq[j] == seq[i]) j++;
+    int r = j - i;
+    if (seq[i] == 0) {
+      while (r >= 11) { int q = r > 138 ? 138 : r; f[18]++; extra += 7; r -= q; }
+      if (r >= 3) { f[17]++; extra += 3; r = 0; }
+      f[0] += r;
+    } else {
+      f[seq[i]]++; r--;
+      while (r >= 3) { int q = r > 6 ? 6 : r; f[16]++; extra += 2; r -= q; }
+      f[seq[i]] += r;
+    }
+    i = j;
+  }
+  int cl[19];
+  huff(f, 19, 7, cl);
+  int hclen = 4;
+  for (int k = 0; k < 19; k++) if (cl[ord[k]]) hclen = k + 1 > hclen ? k + 1 : hclen;
+  double b = 3 + 14 + 3.0 * hclen + extra;
+  for (int k = 0; k < 19; k++) b += (double)f[k] * cl[k];
+  return b;
+}
 static void lsym(int L, int* s, int* e) {
   if (L <= 10) { *s = 254 + L; *e = 0; return; }
   if (L == 258) { *s = 285; *e = 0; return; }
@@ -110,8 +145,9 @@ static void dsym(int D, int* s, int* e) {
 
 int main(int argc, char** argv) {
   int c;
-  while ((c = getopt(argc, argv, "w:b:r:s:Hh:m:l:B:R:Fx:k:y:f:g:P:")) != -1) {
+  while ((c = getopt(argc, argv, "w:b:r:s:Hh:m:l:B:R:Fx:k:y:f:g:P:S:")) != -1) {
     if (c == 'P') FLEX = atoi(optarg);
+    if (c == 'S') SHARE = atoi(optarg);
     if (c == 'f') FAR4 = atoi(optarg);
     if (c == 'g') FAR5 = atoi(optarg);
     if (c == 'x') W2 = atoi(optarg);
@@ -145,6 +181,9 @@ int main(int argc, char** argv) {
   double total_bits = 0;
   long nseg = 0;
   for (size_t b0 = 0; b0 < n; b0 += BLOCK) {
+    long fl[288] = {0}, fd[32] = {0};
+    long extra = 0;
+    int in_group = 0;
     const size_t bl = (n - b0 < (size_t)BLOCK) ? n - b0 : (size_t)BLOCK;
     const uint8_t* blk = buf + b0;
     for (size_t s0 = 0; s0 < bl; s0 += SEG) {
@@ -208,9 +247,7 @@ int main(int argc, char** argv) {
       }
       free(snap);
       // parse
-      long fl[288] = {0}, fd[32] = {0};
-      long extra = 0;
-      fl[256] = 1;
+      fl[256] += 1;
       const int rng = RANGE ? RANGE : sn;
       int p = 0;
       for (int t0 = 0; t0 < sn; t0 += rng) {
@@ -253,6 +290,8 @@ int main(int argc, char** argv) {
           }
         }
       }
+      nseg++;
+      if (++in_group < SHARE && s0 + SEG < bl) continue;
       int ll[288], dl[32];
       huff(fl, 286, 15, ll);
       huff(fd, 30, 15, dl);
@@ -260,15 +299,19 @@ int main(int argc, char** argv) {
       int hlit = 257, hdist = 1;
       for (int i = 0; i < 286; i++) { bits += (double)fl[i] * ll[i]; if (ll[i] && i >= 257) hlit = i + 1; }
       for (int i = 0; i < 30; i++) { bits += (double)fd[i] * dl[i]; if (dl[i]) hdist = i + 1; }
-      bits += 3 + 14 + 3 * 19 + 4.0 * (hlit + hdist);  // header (approx.)
-      bits += 3 + 32 + 8;                               // sync flush
-      double stored = 8.0 * (5 + sn);
-      total_bits += bits < stored ? bits : stored;
-      nseg++;
+      const double hb = hdr_bits(ll, dl, hlit, hdist);
+      hdr_total += hb;
+      bits += hb;
+      bits += 3 + 32 + 8;  // sync flush
+      total_bits += bits;
+      in_group = 0;
+      extra = 0;
+      memset(fl, 0, sizeof fl);
+      memset(fd, 0, sizeof fd);
     }
     total_bits += 8 * 11;  // zlib header, final empty block, Adler
   }
-  printf("bytes %zu  out %.0f  ratio %.4f  (ways %d bits %d range %d seg %d hist %d/%d min %d lazy %d block %ld)\n", n,
-         total_bits / 8, total_bits / 8 / n, WAYS, HBITS, RANGE, SEG, HIST, HLEN, MINM, LAZY, BLOCK);
+  printf("bytes %zu  out %.0f  ratio %.4f  hdr %.2f%%  (ways %d bits %d range %d seg %d hist %d/%d min %d lazy %d block %ld)\n", n,
+         total_bits / 8, total_bits / 8 / n, 100.0 * hdr_total / total_bits, WAYS, HBITS, RANGE, SEG, HIST, HLEN, MINM, LAZY, BLOCK);
   return 0;
 }

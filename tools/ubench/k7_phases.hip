@@ -1,4 +1,4 @@
-// K7a (hbx_k7_deflate_size) phase times on a Zipf-word text corpus: the
+// K7a + K7h (hbx_k7_deflate_size, hbx_k7_deflate_code) phase times on a Zipf-word text corpus: the
 // kernel built with HBX_K7_PROBE=1 stamps (argv: MiB [random]) s_memtime at its phase boundaries
 // (hbx_deflate.hip K7P); this prints the median cycles per phase over all
 // segments, the kernel time and the coded size.
@@ -67,6 +67,8 @@ int main(int argc, char** argv) {
     (void)hipEventRecord(e0, 0);
     hipLaunchKernelGGL(hbx_k7_deflate_size, dim3(nseg), dim3(hbxz::kThreads), 0, 0, d_zb, (uint32_t)zb.size(), nseg,
                        d_info, d_img);
+    hipLaunchKernelGGL(hbx_k7_deflate_code, dim3(nseg), dim3(hbxz::kThreads), 0, 0, d_zb, (uint32_t)zb.size(), nseg,
+                       d_info, d_img);
     (void)hipEventRecord(e1, 0);
     if (hipEventSynchronize(e1) != hipSuccess) {
       std::fprintf(stderr, "launch failed\n");
@@ -80,26 +82,30 @@ int main(int argc, char** argv) {
   std::vector<unsigned long long> pr((size_t)np * 16);
   (void)hipMemcpyFromSymbol(pr.data(), HIP_SYMBOL(hbx_k7_probe), pr.size() * 8);
   uint64_t out = 0;
-  uint32_t modes[4] = {0, 0, 0, 0};
+  uint32_t modes[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (auto& x : info) {
     out += x.bytes;
-    modes[x.mode & 3u]++;
+    modes[x.mode & 7u]++;
   }
-  std::printf("# %u segments, %.1f MiB text, kernel %.3f ms = %.2f GB/s, coded/input %.4f, modes stored/fixed/dyn/src-stored %u/%u/%u/%u\n",
-              nseg, total / 1048576.0, ms, total / (ms * 1e6), (double)out / total, modes[0], modes[1], modes[2], modes[3]);
+  std::printf("# %u segments, %.1f MiB text, K7a+K7h %.3f ms = %.2f GB/s, coded/input %.4f, modes stored/fixed/dyn/src-stored/group-head/group-member %u/%u/%u/%u/%u/%u\n",
+              nseg, total / 1048576.0, ms, total / (ms * 1e6), (double)out / total, modes[0], modes[1], modes[2], modes[3],
+              modes[4], modes[5]);
+  // K7a: 0..5; K7h: 6 (start) .. 7 (emission) .. 15 (end)
+  const int ph2[][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {6, 7}, {7, 15}};
   const char* names[] = {"load+init", "history inserts", "candidates", "dry parse+handoff", "final parse",
-                         "huffman+mode", "emit+copy"};
+                         "K7h reload+code", "K7h emit+copy"};
   for (int ph = 0; ph < 7; ph++) {
     std::vector<double> v;
+    const int a = ph2[ph][0], b = ph2[ph][1];
     for (uint32_t g = 0; g < np; g++)
-      if (pr[16 * g + ph + 1] >= pr[16 * g + ph] && pr[16 * g + ph] != 0) v.push_back((double)(pr[16 * g + ph + 1] - pr[16 * g + ph]));
+      if (pr[16 * g + b] >= pr[16 * g + a] && pr[16 * g + a] != 0) v.push_back((double)(pr[16 * g + b] - pr[16 * g + a]));
     std::sort(v.begin(), v.end());
     if (v.empty()) continue;
     std::printf("%-20s median %10.0f  p90 %10.0f cycles (n=%zu)\n", names[ph], v[v.size() / 2], v[v.size() * 9 / 10], v.size());
   }
-  // inside huffman+mode (dynamic code only): 5 -> 8 sort, 8 -> 9 trees, 9 -> 10 lengths and codes,
-  // 10 -> 11 header runs, 11 -> 6 costs
-  const int sub[][2] = {{5, 8}, {8, 9}, {9, 10}, {10, 11}, {11, 6}, {5, 12}, {12, 13}, {13, 14}, {14, 8}};
+  // inside K7h's code build (dynamic code only; a group's pass, or the segment's own): 14 -> 8 sort,
+  // 8 -> 9 trees, 9 -> 10 lengths and codes, 10 -> 11 header runs, 11 -> 7 costs and the group decision
+  const int sub[][2] = {{14, 8}, {8, 9}, {9, 10}, {10, 11}, {11, 7}, {6, 12}, {12, 13}, {13, 14}, {14, 8}};
   const char* sn[] = {"  huff: sort", "  huff: trees", "  huff: lengths", "  huff: header rle", "  huff: costs",
                       "    sort: sums", "    sort: entropy", "    sort: init", "    sort: rank"};
   for (int i = 0; i < 9; i++) {
