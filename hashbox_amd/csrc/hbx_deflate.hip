@@ -9,23 +9,29 @@
 // 1951) and inflates to the block's data; that is what the tests check.
 //
 // Layout of one block's stream (one workgroup per 32 KiB segment; segments
-// are coded independently, so there is no serial dependence between them):
+// are parsed independently, so there is no serial dependence between them):
 //
-//   78 9C | seg 0 | seg 1 | ... | 01 00 00 FF FF | adler32 (BE)
+//   78 9C | piece | piece | ... | 01 00 00 FF FF | adler32 (BE)
 //
-//   seg = one non-final fixed- or dynamic-Huffman block (BTYPE 01 / 10) of
-//         LZ77 tokens, closed by an empty stored block (a sync flush: 3 zero
-//         bits, pad, 00 00 FF FF) so the segment ends on a byte boundary; or,
-//         if that is not smaller, one non-final stored block (00 | LEN | ~LEN
-//         | data).  Matches may reach back into the 16 KiB of the block before
-//         the segment (its history; the inflater's window holds it).
+//   piece = one non-final dynamic-Huffman block (BTYPE 10) of the LZ77 tokens
+//           of a group of up to four consecutive segments under one code
+//           (round 4), or of one segment under its own fixed or dynamic code,
+//           closed by an empty stored block (a sync flush: 3 zero bits, pad,
+//           00 00 FF FF) so the piece ends on a byte boundary; or, if that is
+//           not smaller, one non-final stored block (00 | LEN | ~LEN | data).
+//           Matches may reach back into the 32 KiB of the block before the
+//           segment (its history; the inflater's window holds it).
 //
-// K7a hbx_k7_deflate_size   per segment: LZ77 parse, coded image into a
-//                           scratch slot, its size, mode and Adler partials
-// K7s hbx_k7_deflate_plan   per block: segment offsets, header, trailer with
+// K7e hbx_k7_deflate_entropy per segment: incompressible early-out (stored),
+//                           Adler partials
+// K7a hbx_k7_deflate_size   per parsed segment: LZ77 parse; tokens, ranges
+//                           and symbol counts into its scratch slot
+// K7h hbx_k7_deflate_code   per parsed segment: the group's (or its own)
+//                           code, its image into the slot, its size and mode
+// K7s hbx_k7_deflate_plan   per block: piece offsets, header, trailer with
 //                           the combined Adler-32, stream length
-// K7b hbx_k7_deflate_write  per segment: its image from the slot to the
-//                           stream at its byte offset
+// K7b hbx_k7_deflate_write  per piece: the image (or the group's members'
+//                           images, or the source bytes) to the stream
 //
 // The LZ77 parse (one 1024-thread workgroup per 32 KiB segment):
 //   1. candidates, in position order.  The 32 KiB of the block before the
@@ -53,14 +59,14 @@
 //      starts are made ascending and each thread's final parse is clipped to
 //      its successor's start, which keeps the stream exact either way).  The
 //      final parse records the tokens, symbol frequencies and fixed-code bits;
-//   3. after a workgroup prefix sum of the bit counts, the tokens are emitted
-//      (ds_or) into the image (over the window's LDS), if that is smaller than
-//      stored; a stored segment is copied by K7b from the source.
-// Zipf text of tools/bench_deflate.py: 0.3115 of its size at 16.6 GB/s (zlib
-// -6: 0.3114; round 3: 0.327 at 16.0 GB/s with 8 ways of 2,048 buckets, 16
-// KiB of history and one-step lazy matching; 8 ways of 4,096 buckets here:
-// 0.3162 at 23.1 GB/s).  tools/k7model/k7model.c models the variants.
-// LDS: 141 of the CU's 160 KiB.
+//   3. (K7h) after a workgroup prefix sum of the bit counts, the tokens are
+//      emitted (ds_or) into the image, if that is smaller than stored; a
+//      stored segment is copied by K7b from the source.
+// Zipf text of tools/bench_deflate.py: 0.3108 of its size at 16.0 GB/s (zlib
+// -6: 0.3114; 0.3115 with a code per segment; round 3: 0.327 at 16.0 GB/s
+// with 8 ways of 2,048 buckets, 16 KiB of history and one-step lazy matching;
+// 8 ways of 4,096 buckets here: 0.3162 at 23.1 GB/s).  tools/k7model/
+// k7model.c models the variants.  LDS: K7a 141, K7h 108 of the CU's 160 KiB.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -130,7 +136,7 @@ constexpr uint32_t kFar4 = 1024;  // farthest 4-byte match kept
 
 struct SegInfo {
   uint32_t bytes;  // coded bytes of the segment (stored or fixed image)
-  uint32_t mode;   // 0 stored, 1 fixed Huffman, 2 dynamic Huffman
+  uint32_t mode;   // 1 fixed, 2 dynamic Huffman; 3 stored (from the source); 4/5 group head/member; 0xFF parse
   uint32_t a, b;   // Adler partials: sum x, sum (n - j) x_j  (mod 65521)
 };
 
