@@ -122,10 +122,9 @@ constexpr uint32_t kRecWords = 322;
 constexpr uint32_t kSlotMeta = kSlotRec + kRecWords + 2u;
 static_assert((kSlotMeta + 4u) * 4u <= kSlot, "the hand-off fits the slot");
 // kGroup consecutive segments of a block share one dynamic code (one header,
-// one end of block and sync flush) when that is smaller; the group's piece is
-// assembled by K7b in LDS, so it is at most kGroupBytes
+// one end of block and sync flush) when that is smaller; K7b assembles the
+// group's piece from the members' images
 constexpr uint32_t kGroup = 4;
-constexpr uint32_t kGroupBytes = 65536;
 constexpr uint32_t kTabLds = kTabWords > kCdPhys / 2u ? kTabWords : kCdPhys / 2u;  // table, then distances
 // window positions + 1 are u16 entries, and a bucket's u16 insert counter
 // never carries into its neighbour's
@@ -1091,7 +1090,7 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_size
 // group's workgroups with no communication between them.  A member's image
 // starts at bit S_m mod 8 of the byte K7b ORs it into (S_m / 8 of the piece).
 // The group shares only if its piece is smaller than the sum of its members'
-// fixed-or-stored sizes and fits kGroupBytes; otherwise each member is coded
+// fixed-or-stored sizes; otherwise each member is coded
 // alone (dynamic, fixed or stored, whichever is smallest; rounds 1-4).
 extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_code(const hbxz::ZBlock* __restrict__ blocks,
                                                                                 uint32_t nb, uint32_t nseg,
@@ -1406,7 +1405,7 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_code
           const uint32_t fm = ((3u + mrec[m][320] + 7u + 3u + 7u) >> 3) + 4u;
           alone += min(5u + nm, fm);
         }
-        gpar[3 * kGroup] = ok && total <= kGroupBytes && total < alone ? 1u : 0u;
+        gpar[3 * kGroup] = ok && total < alone ? 1u : 0u;
         gpar[3 * kGroup + 1] = total;
       }
       __syncthreads();

@@ -255,8 +255,9 @@ def test_shared_code_groups(engine):
     member's bits continue the previous member's mid-byte.  Edges: partial
     groups (2, 3, 5, 9 segments), a last member of a few bits (a 4-byte match
     at distance 4), a member of zeros (a few hundred bits), a stored random
-    segment inside a group (no sharing there), and a text block whose group
-    pieces must each end in the only sync flush of the group."""
+    segment inside a group (no sharing there), a group piece past 64 KiB
+    (7-bit random bytes), and a text block whose group pieces must each end
+    in the only sync flush of the group."""
     seg = 32768
     t = _text(12 * seg, 3)
     rng = np.random.default_rng(5)
@@ -267,6 +268,7 @@ def test_shared_code_groups(engine):
     blocks.append(t[:seg] + bytes(seg) + t[seg : 3 * seg])  # zeros in the middle of a group
     blocks.append(t[:seg] + rnd + t[seg : 3 * seg])  # a stored member: the group codes alone
     blocks.append(rnd + t[: 3 * seg] + rnd + t[3 * seg : 6 * seg])
+    blocks.append(rng.integers(0, 128, 4 * seg + 7, dtype=np.uint8).tobytes())  # 7 bits/B: a ~112 KiB group piece
     _check(engine, blocks)
     big = _text(4 << 20, 9)
     (z,) = _check(engine, [big])
