@@ -274,3 +274,23 @@ def test_shared_code_groups(engine):
     (z,) = _check(engine, [big])
     # 128 segments in 32 groups: one sync flush (00 00 FF FF) per group + the final block's
     assert z.count(b"\x00\x00\xff\xff") <= 128 // 4 + 2, z.count(b"\x00\x00\xff\xff")
+
+
+def test_group_that_codes_alone(engine):
+    """A group whose shared code loses (K7h's second pass): random segments
+    that K7e still parses (each holds a repeated 256-byte run, so a sampled
+    value repeats) code as stored, member by member; and a text member with
+    such a random member, where the shared code may or may not win.  Both
+    must inflate exactly and stay within the stored size."""
+    seg = 32768
+    rng = np.random.default_rng(23)
+
+    def rnd_with_repeat():
+        r = bytearray(rng.integers(0, 256, seg, dtype=np.uint8).tobytes())
+        r[20000:20256] = r[1000:1256]
+        return bytes(r)
+
+    a, b, c = rnd_with_repeat(), rnd_with_repeat(), rnd_with_repeat()
+    z1, z2, z3 = _check(engine, [a + b, a + b + c, _text(seg, 4) + b])
+    assert len(z1) <= 2 * (seg + 5) + 11, len(z1)
+    assert len(z2) <= 3 * (seg + 5) + 11, len(z2)
