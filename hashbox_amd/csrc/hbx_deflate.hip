@@ -1109,7 +1109,7 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_code
   __shared__ uint8_t cll[20];
   __shared__ unsigned long long rmask[5];  // code-length run starts (header RLE)
   static_assert(6464u <= kImgWords, "the Huffman scratch fits the image's LDS");
-  static_assert(kGroup <= 4u, "member bit sums in wsum4");
+  static_assert(kGroup <= 8u, "member bit sums in zctl");
   const uint32_t g = blockIdx.x;
   if (g >= nseg) return;
   const SegInfo si0 = info[g];
