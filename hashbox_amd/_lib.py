@@ -34,7 +34,7 @@ EXPORTS = [
     "hbx_wire_encode_id", "hbx_wire_encode_block_header", "hbx_wire_parse",
     "hbx_verify_submit_device", "hbx_inflate_blocks_device", "hbx_store_paths_zcb", "hbx_after_stream",
     "hbx_set_join_lag", "hbx_k3_wave_times", "hbx_input_after_oldest", "hbx_knobs",
-    "hbx_input_fence", "hbx_set_k3_probe",
+    "hbx_input_fence", "hbx_set_k3_probe", "hbx_store_paths_status",
 ]
 # Functions returning something other than an int status.
 _NON_STATUS = ("hbx_ctx_destroy", "hbx_last_error", "hbx_max_chunks", "hbx_file_entry_size",
@@ -162,6 +162,7 @@ def load() -> ctypes.CDLL:
     L.hbx_inflate_blocks_device.argtypes = [P, P, U64, P, P, P, P, P, P, P]
     L.hbx_verify_submit_device.argtypes = [P, P, U64, P, P, P, P, P, P, P, P, PU64]
     L.hbx_store_paths_z.argtypes = [P, U64, P, P, P, P, P, P, P, ctypes.c_uint32, U64, P, P, P, P]
+    L.hbx_store_paths_status.argtypes = [P, U64, P, P, P, P, P, P, P, P, ctypes.c_uint32, U64, P, P, P, P, P, P]
     for name in EXPORTS:
         if name not in _NON_STATUS:
             getattr(L, name).restype = I

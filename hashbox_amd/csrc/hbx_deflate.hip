@@ -135,7 +135,7 @@ constexpr uint32_t kFar4 = 1024;  // farthest 4-byte match kept
 
 struct SegInfo {
   uint32_t bytes;  // coded bytes of the segment (stored or fixed image)
-  uint32_t mode;   // 1 fixed, 2 dynamic Huffman; 3 stored (from the source); 4/5 group head/member; 0xFF parse
+  uint32_t mode;   // 1 fixed, 2 dynamic Huffman; 3/6 stored (from the source; K7e/K7h); 4/5 group head/member; 0xFF parse
   uint32_t a, b;   // Adler partials: sum x, sum (n - j) x_j  (mod 65521)
 };
 
@@ -723,6 +723,12 @@ constexpr uint32_t kModeSrcStored = 3u;    // SegInfo.mode: stored, K7b copies t
 constexpr uint32_t kModeParse = 0xFFu;     // SegInfo.mode set by K7e: K7a decides
 constexpr uint32_t kModeGroupHead = 4u;    // first segment of a shared-code group: bytes = the group's piece
 constexpr uint32_t kModeGroupMember = 5u;  // a later member: its bits are in the head's piece (bytes = 0)
+// K7h's own "stored" decision.  K7b treats it as kModeSrcStored, but it is a
+// value of its own: K7h reads its group siblings' info[].mode (was the member
+// stored by K7e?) while those siblings' K7h may already be overwriting it, so
+// K7h never writes kModeSrcStored and "!= kModeSrcStored" keeps meaning "not
+// stored by K7e" whatever a sibling has written by then (advisor r04).
+constexpr uint32_t kModeOwnStored = 6u;
 constexpr uint32_t kEThreads = 256;
 }  // namespace hbxz
 
@@ -1124,9 +1130,9 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_code
   for (uint32_t k = t; k < kCdPhys / 2u; k += kThreads) cdw[k] = slot[k];
   const uint32_t p_s = slot[kSlotThr + t], p_e = slot[kSlotThr + kThreads + t];
   const uint32_t fbits = slot[kSlotThr + 2u * kThreads + t];
-  // a member's mode is K7e's (parse or stored) or, once coded, one that is
-  // stored only when its group does not share: either way "not stored by
-  // K7e" reads the same for every member of a sharing group
+  // a member's mode is K7e's (parse or stored) or, once its own K7h has
+  // coded it, 1/2/4/5/kModeOwnStored: never kModeSrcStored, so "not stored by
+  // K7e" reads the same before and after a sibling's write (kModeOwnStored)
   const bool live = t >= gn || info[bk.seg0 + gs + t].mode != kModeSrcStored;
   const bool grp = __syncthreads_and(live) && gn >= 2u;
   const uint32_t own = grp ? my : 0u;
@@ -1490,9 +1496,9 @@ extern "C" __global__ __launch_bounds__(hbxz::kThreads) void hbx_k7_deflate_code
     __syncthreads();
     nbytes = zpar[5];  // in a group: equal to gpar's il (the walk and the counts agree)
   } else {
-    mode = kModeSrcStored;  // stored: K7b copies the bytes from the source
+    mode = kModeOwnStored;  // stored: K7b copies the bytes from the source
   }
-  if (mode != kModeSrcStored)
+  if (mode != kModeOwnStored)
     for (uint32_t k = t; k < (nbytes + 3u) / 4u; k += kThreads) slot[k] = img[k];
   if (t == 0) {
     SegInfo si = si0;
@@ -1584,7 +1590,7 @@ extern "C" __global__ __launch_bounds__(512) void hbx_k7_deflate_write(uint32_t 
   const SegInfo si = info[g];
   const uint32_t nbytes = si.bytes;
   if (si.mode == kModeGroupMember) return;  // written with its group's head
-  if (si.mode == kModeSrcStored) {  // 00 | LEN | ~LEN | the segment's bytes, straight from the source
+  if (si.mode == kModeSrcStored || si.mode == kModeOwnStored) {  // 00 | LEN | ~LEN | the segment's bytes, straight from the source
     const ZBlock bk = blocks[zblock_of(blocks, nb, g)];
     const uint32_t n = nbytes - 5u;
     const uint8_t* src = reinterpret_cast<const uint8_t*>(bk.src) + (uint64_t)(g - bk.seg0) * kSeg;

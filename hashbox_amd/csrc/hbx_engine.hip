@@ -16,6 +16,8 @@
 #include <fcntl.h>
 #include <unistd.h>
 
+#include <cerrno>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -1642,8 +1644,15 @@ namespace {
 
 // Read whole files into dst + offs[i] with `threads` threads (files are
 // independent).  Returns 0 or HBX_ERR_IO with the offending path in err.
+// With `status` (per file of this list), the failures the reference treats
+// per file are recorded there instead of failing the call, and the file is
+// skipped (hbx_store_paths_status): an open() failure (os.Open returns it,
+// storeDir logs and continues: store.go:101-103, 221-224) and a read failing
+// with EBADF (minorPathError, hashback_unix.go:57-63).  Any other read error
+// or a short file is a panic in storeFile (CopyNOrPanic, utils.go:95-99):
+// the call fails either way.
 int read_files(uint64_t n, const char* const* paths, const uint64_t* lens, const uint64_t* offs,
-               uint8_t* dst, uint32_t threads, std::string& err) {
+               uint8_t* dst, uint32_t threads, std::string& err, int32_t* status = nullptr) {
   std::atomic<uint64_t> next{0};
   std::atomic<int> failed{0};
   std::mutex emu;
@@ -1651,21 +1660,35 @@ int read_files(uint64_t n, const char* const* paths, const uint64_t* lens, const
     for (;;) {
       const uint64_t i = next.fetch_add(1);
       if (i >= n || failed.load()) return;
+      if (status) status[i] = 0;
       const int fd = ::open(paths[i], O_RDONLY | O_CLOEXEC);
-      bool ok = fd >= 0;
+      int e = fd < 0 ? errno : 0;
+      if (fd < 0 && status) {
+        status[i] = e ? e : EIO;
+        continue;
+      }
       uint64_t got = 0;
-      while (ok && got < lens[i]) {
+      while (fd >= 0 && got < lens[i]) {
         const ssize_t r = ::pread(fd, dst + offs[i] + got, lens[i] - got, (off_t)got);
-        if (r <= 0) ok = false;
-        else got += (uint64_t)r;
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) {
+          e = r < 0 ? errno : 0;  // 0: end of file before lens[i] bytes
+          break;
+        }
+        got += (uint64_t)r;
       }
       if (fd >= 0) ::close(fd);
-      if (!ok) {
-        failed.store(1);
-        std::lock_guard<std::mutex> g(emu);
-        err = std::string("cannot read ") + std::to_string(lens[i]) + " bytes of " + paths[i];
-        return;
+      if (fd >= 0 && got == lens[i]) continue;
+      if (status && e == EBADF) {
+        status[i] = EBADF;
+        continue;
       }
+      failed.store(1);
+      std::lock_guard<std::mutex> g(emu);
+      err = std::string("cannot read ") + std::to_string(lens[i]) + " bytes of " + paths[i] + ": " +
+            (fd < 0 ? std::string("open: ") + std::strerror(e)
+                    : e ? std::string(std::strerror(e)) : "end of file after " + std::to_string(got) + " bytes");
+      return;
     }
   };
   const uint32_t nt = std::max<uint32_t>(1, std::min<uint64_t>(threads, n));
@@ -1818,7 +1841,8 @@ int z_finish(const hbx_ctx* c, ZPend& zp, const uint64_t* out_base, const hbx_fi
 
 int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uint64_t* lens,
                      uint64_t* cut_ends, uint8_t* ids, const uint64_t* out_base, const uint64_t* caps,
-                     hbx_file_summary* sums, uint32_t io_threads, uint64_t batch_bytes, const ZOut& z);
+                     hbx_file_summary* sums, uint32_t io_threads, uint64_t batch_bytes, const ZOut& z,
+                     int32_t* status = nullptr);
 }  // namespace
 
 int hbx_store_paths(hbx_ctx* c, uint64_t n, const char* const* paths, const uint64_t* lens,
@@ -1830,6 +1854,22 @@ int hbx_store_paths(hbx_ctx* c, uint64_t n, const char* const* paths, const uint
   std::lock_guard<std::mutex> g(c->mu);
   return store_paths_impl(c, n, paths, lens, cut_ends, ids, out_base, caps, sums, io_threads, batch_bytes,
                           ZOut{});
+}
+
+int hbx_store_paths_status(hbx_ctx* c, uint64_t n, const char* const* paths, const uint64_t* lens,
+                           uint64_t* cut_ends, uint8_t* ids, const uint64_t* out_base, const uint64_t* caps,
+                           hbx_file_summary* sums, int32_t* status, uint32_t io_threads, uint64_t batch_bytes,
+                           uint8_t* zout, const uint64_t* zbase, uint64_t* zoff, uint64_t* zlen,
+                           hbx_batch_ready_fn ready, void* user) {
+  if (!c) return HBX_ERR_ARG;
+  const bool z = zout || zbase || zoff || zlen;
+  if (n && (!paths || !lens || !out_base || !caps || !status)) return HBX_ERR_ARG;
+  if (n && z && (!sums || !zout || !zbase || !zoff || !zlen)) return HBX_ERR_ARG;
+  if (!z && ready) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  for (uint64_t i = 0; i < n; i++) status[i] = 0;
+  return store_paths_impl(c, n, paths, lens, cut_ends, ids, out_base, caps, sums, io_threads, batch_bytes,
+                          z ? ZOut{zout, zbase, zoff, zlen, ready, user} : ZOut{}, status);
 }
 
 uint64_t hbx_deflate_file_bound(uint64_t len) {
@@ -1864,7 +1904,8 @@ int hbx_store_paths_zcb(hbx_ctx* c, uint64_t n, const char* const* paths, const 
 namespace {
 int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uint64_t* lens,
                      uint64_t* cut_ends, uint8_t* ids, const uint64_t* out_base, const uint64_t* caps,
-                     hbx_file_summary* sums, uint32_t io_threads, uint64_t batch_bytes, const ZOut& z) {
+                     hbx_file_summary* sums, uint32_t io_threads, uint64_t batch_bytes, const ZOut& z,
+                     int32_t* status) {
   if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
   HBX_TRY(c, hipSetDevice(c->device));
   if (batch_bytes < (64ull << 20)) batch_bytes = 64ull << 20;
@@ -1920,7 +1961,7 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
   }
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   bool slot_used[2] = {false, false};
-  std::vector<uint64_t> offs;
+  std::vector<uint64_t> offs, skip_lens;
   uint64_t f = 0, k = 0;
   int rc = HBX_OK;
   // with compression, each collected batch is compressed from its arena on
@@ -2004,7 +2045,7 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
     if (slot_used[p] && (rc = c->hip(hipEventSynchronize(c->h2d_done[p]), "h2d wait"))) break;
     double t2 = now();
     rc = read_files(f - first, paths + first, lens + first, offs.data(), c->h_read[p].as<uint8_t>(),
-                    io_threads, c->err);
+                    io_threads, c->err, status ? status + first : nullptr);
     c->io_s[0] += now() - t2;
     c->io_s[1] += t1 - t0;
     c->io_s[2] += t2 - t1;
@@ -2019,7 +2060,15 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
       break;
     if ((rc = c->hip(hipEventRecord(c->h2d_done[p], c->stream), "hipEventRecord"))) break;
     slot_used[p] = true;
-    rc = submit_batch(c, arena.p, f - first, offs.data(), lens + first, cut_ends, ids,
+    // a skipped file (status != 0) goes in as an empty file: no chunks
+    const uint64_t* blens = lens + first;
+    if (status) {
+      skip_lens.assign(lens + first, lens + f);
+      for (uint64_t i = first; i < f; i++)
+        if (status[i]) skip_lens[i - first] = 0;
+      blens = skip_lens.data();
+    }
+    rc = submit_batch(c, arena.p, f - first, offs.data(), blens, cut_ends, ids,
                       out_base + first, caps + first, sums ? sums + first : nullptr, budget);
     if (z.zout && rc == HBX_OK) jobs.push_back(ZJob{first, f - first, static_cast<const uint8_t*>(arena.p), offs});
     k++;
@@ -2110,10 +2159,21 @@ int hbx_input_after_oldest(hbx_ctx* c) {
 int hbx_input_fence(hbx_ctx* c, void* stream) {
   if (!c) return HBX_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
+  if (c->broken) return c->fail(HBX_ERR_STATE, "context is unusable after a failed submit; destroy it");
   HBX_TRY(c, hipSetDevice(c->device));
   if (int frc = flush_input_wait(c)) return frc;
-  if (stream && c->input_fence_set)
-    HBX_TRY(c, hipStreamWaitEvent(static_cast<hipStream_t>(stream), c->order_free[c->input_fence_L % 3], 0));
+  if (!stream || !c->input_fence_set) return HBX_OK;
+  // Nothing to wait for once launch L is known complete.  The ring slot of L
+  // is recorded again by launch L + 3: a fence called that late waits for
+  // that later launch instead (issued after L on the same stream, so it
+  // completes after L: conservative, never early).
+  const uint64_t L = c->input_fence_L;
+  hipEvent_t e = c->order_free[L % 3];
+  if (L < c->k3_done_upto || hipEventQuery(e) == hipSuccess) {
+    c->input_fence_set = false;
+    return HBX_OK;
+  }
+  HBX_TRY(c, hipStreamWaitEvent(static_cast<hipStream_t>(stream), e, 0));
   return HBX_OK;
 }
 
@@ -2452,15 +2512,48 @@ int hbx_inflate_blocks_device(hbx_ctx* c, const void* d_in, uint64_t n, const ui
     if (no_split || in_lens[i] < 2ull * hbxs::kSplitRegion) return false;
     return force_split || in_lens[i] * 10 < out_caps[i] * 8;
   };
+  // Scratch of one split stream: regions of kSplitRegion compressed bytes,
+  // each with room for twice its share of the stream's output capacity in
+  // 16-bit symbols, at most kSplitSymCap (a region that needs more overflows
+  // and the stream is inflated again by the wave kernel).
+  constexpr uint64_t kSplitSymCap = 4ull << 20;
+  auto region_syms = [&](uint64_t len, uint64_t cap, uint32_t& cnt) {
+    cnt = (uint32_t)((len + hbxs::kSplitRegion - 1) / hbxs::kSplitRegion);
+    const uint64_t share = (2ull * cap + cnt - 1) / cnt;
+    return std::min<uint64_t>(((share + 63) & ~63ull) + 4096, kSplitSymCap);
+  };
   uint64_t long_streams = 0;
   for (uint64_t i = 0; i < n; i++) long_streams += splits(perm[i]) ? 1 : 0;
   // enough streams to fill the SIMDs on their own: no split (it costs a
   // second pass over 2 bytes per output byte)
-  const bool split_any = long_streams > 0 && (force_split || long_streams < 2048);
+  bool split_any = long_streams > 0 && (force_split || long_streams < 2048);
+  // The split path's scratch has a budget (a quarter of the free device
+  // memory, at most 16 GiB): the longest candidates take it in order, the
+  // rest go to the wave kernel, which needs no scratch (advisor r04).
+  std::vector<uint8_t> take(n, 0);
+  if (split_any) {
+    size_t fr = 0, tot = 0;
+    uint64_t budget = 256ull << 20;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess) budget = std::max<uint64_t>(budget, std::min<uint64_t>(fr / 4, 16ull << 30));
+    uint64_t used = 0;
+    long_streams = 0;
+    for (uint64_t k = 0; k < n; k++) {
+      const uint32_t i = perm[k];
+      if (!splits(i)) continue;
+      uint32_t cnt = 0;
+      const uint64_t syms = region_syms(in_lens[i], out_caps[i], cnt);
+      const uint64_t b = 2ull * syms * cnt;  // scratch bytes of its regions
+      if (used + b > budget) continue;
+      used += b;
+      take[i] = 1;
+      long_streams++;
+    }
+    split_any = long_streams > 0;
+  }
   // split streams last, so the wave kernel takes the prefix [0, nw)
   if (split_any)
-    std::stable_partition(perm.begin(), perm.end(), [&](uint32_t i) { return !splits(i); });
-  const uint64_t nw = split_any ? n - long_streams : n;
+    std::stable_partition(perm.begin(), perm.end(), [&](uint32_t i) { return !take[i]; });
+  uint64_t nw = split_any ? n - long_streams : n;
   std::vector<InflateDesc> desc(n);
   for (uint64_t k = 0; k < n; k++) {
     const uint32_t i = perm[k];
@@ -2472,6 +2565,40 @@ int hbx_inflate_blocks_device(hbx_ctx* c, const void* d_in, uint64_t n, const ui
   hipStream_t s = c->stream;
   HBX_TRY(c, c->d_idesc.ensure(n * sizeof(InflateDesc)));
   HBX_TRY(c, c->d_ires.ensure(n * 8));
+  // The region table and every split buffer exist before the first kernel is
+  // queued: a failure then leaves nothing running, and an allocation that
+  // fails sends those streams to the wave kernel instead of failing the call.
+  std::vector<SplitRegion> reg;
+  std::vector<uint32_t> meta;
+  if (split_any) {
+    meta.assign(3 * (n - nw), 0u);
+    uint64_t sym = 0;
+    for (uint64_t k = nw; k < n; k++) {
+      uint32_t cnt = 0;
+      const uint32_t scap = (uint32_t)region_syms(desc[k].len, desc[k].cap, cnt);
+      meta[k - nw] = (uint32_t)k;
+      meta[(n - nw) + (k - nw)] = (uint32_t)reg.size();
+      meta[2 * (n - nw) + (k - nw)] = cnt;
+      const uint32_t first = (uint32_t)reg.size();
+      for (uint32_t r = 0; r < cnt; r++) {
+        reg.push_back(SplitRegion{(uint32_t)k, r, first, cnt, sym, scap, 0u});
+        sym += scap;
+      }
+    }
+    const uint64_t nreg = reg.size();
+    bool ok = nreg <= 0x7FFFFFFFull;
+    for (auto [buf, bytes] : {std::pair<DevBuf*, uint64_t>{&c->d_sreg, nreg * sizeof(SplitRegion)},
+                              {&c->d_sstart, nreg * 8}, {&c->d_sres, nreg * sizeof(SplitResult)},
+                              {&c->d_sscratch, sym * 2 + 64}, {&c->d_smeta, meta.size() * 4}})
+      if (ok && buf->ensure(bytes) != hipSuccess) {
+        (void)hipGetLastError();  // the failed allocation is not an error of this call
+        ok = false;
+      }
+    if (!ok) {  // every stream to the wave kernel
+      split_any = false;
+      nw = n;
+    }
+  }
   HBX_TRY(c, hipMemcpyAsync(c->d_idesc.p, desc.data(), n * sizeof(InflateDesc), hipMemcpyHostToDevice, s));
   uint32_t* dres = c->d_ires.as<uint32_t>();
   const InflateDesc* ddesc = c->d_idesc.as<InflateDesc>();
@@ -2482,32 +2609,7 @@ int hbx_inflate_blocks_device(hbx_ctx* c, const void* d_in, uint64_t n, const ui
     hipLaunchKernelGGL(hbx_k8_inflate, dim3((uint32_t)nw), dim3(64), 0, s, ddesc, (uint32_t)nw, dres, dres + n);
   HBX_TRY(c, hipGetLastError());
   if (split_any) {
-    // regions of kSplitRegion compressed bytes; each gets scratch for twice
-    // its share of the stream's output capacity (a region that needs more
-    // overflows and the stream is inflated again by the wave kernel)
-    std::vector<SplitRegion> reg;
-    std::vector<uint32_t> meta(3 * (n - nw));
-    uint64_t sym = 0;
-    for (uint64_t k = nw; k < n; k++) {
-      const uint32_t cnt = (uint32_t)((desc[k].len + hbxs::kSplitRegion - 1) / hbxs::kSplitRegion);
-      const uint64_t share = (2ull * desc[k].cap + cnt - 1) / cnt;
-      const uint32_t scap = (uint32_t)std::min<uint64_t>(((share + 63) & ~63ull) + 4096, 0x7FFFFFFFull);
-      meta[k - nw] = (uint32_t)k;
-      meta[(n - nw) + (k - nw)] = (uint32_t)reg.size();
-      meta[2 * (n - nw) + (k - nw)] = cnt;
-      const uint32_t first = (uint32_t)reg.size();
-      for (uint32_t r = 0; r < cnt; r++) {
-        reg.push_back(SplitRegion{(uint32_t)k, r, first, cnt, sym, scap, 0u});
-        sym += scap;
-      }
-    }
     const uint64_t nreg = reg.size(), ns = n - nw;
-    if (nreg > 0x7FFFFFFFull) return c->fail(HBX_ERR_ARG, "too many inflate regions");
-    HBX_TRY(c, c->d_sreg.ensure(nreg * sizeof(SplitRegion)));
-    HBX_TRY(c, c->d_sstart.ensure(nreg * 8));
-    HBX_TRY(c, c->d_sres.ensure(nreg * sizeof(SplitResult)));
-    HBX_TRY(c, c->d_sscratch.ensure(sym * 2 + 64));
-    HBX_TRY(c, c->d_smeta.ensure(meta.size() * 4));
     HBX_TRY(c, hipMemcpyAsync(c->d_sreg.p, reg.data(), nreg * sizeof(SplitRegion), hipMemcpyHostToDevice, s));
     HBX_TRY(c, hipMemcpyAsync(c->d_smeta.p, meta.data(), meta.size() * 4, hipMemcpyHostToDevice, s));
     const SplitRegion* dreg = c->d_sreg.as<SplitRegion>();
@@ -2554,6 +2656,9 @@ int hbx_inflate_blocks_device(hbx_ctx* c, const void* d_in, uint64_t n, const ui
     out_lens[perm[k]] = res[k];
     status[perm[k]] = res[n + k];
   }
+  // the split scratch is not kept past the call once it is large (the stream
+  // is idle here: everything above was synchronized)
+  if (c->d_sscratch.cap > (256ull << 20)) c->d_sscratch.release();
   return HBX_OK;
 }
 

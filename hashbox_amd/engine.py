@@ -56,6 +56,7 @@ class FileChunks:
     content_type: int  # 2 FileData, 3 FileChain (0 for an empty file)
     content_id: bytes  # entry.ContentBlockID
     zstreams: Optional[list] = None  # zlib stream per chunk, uint8 views (store_paths(compress=True))
+    errno: int = 0  # store_paths(skip_unreadable=True): the errno of a file skipped (no chunks), else 0
 
     @property
     def n_chunks(self) -> int:
@@ -489,7 +490,8 @@ class Engine:
                     batch_bytes: int = 1 << 30, compress: bool = False,
                     on_batch: Optional[Callable[[int, int], None]] = None,
                     on_files: Optional[Callable[[int, List[FileChunks]], None]] = None,
-                    sizes: Optional[Sequence[int]] = None) -> List[FileChunks]:
+                    sizes: Optional[Sequence[int]] = None,
+                    skip_unreadable: bool = False) -> List[FileChunks]:
         """storeFile for many files on disk, end to end: the library reads them
         into pinned memory on ``io_threads`` threads and overlaps reading the
         next batch with the copy + kernels of the current one.  With
@@ -504,8 +506,14 @@ class Engine:
         ``sizes`` are the files' byte sizes when the caller already has them
         (storeFile takes the walker's FileEntry with FileSize, store.go:84,
         247); otherwise each path is stat'ed here.  A file shorter than its
-        size fails the call (HBX_ERR_IO); bytes past it are not read.  ``last_call_s`` holds
-        the library call's wall seconds."""
+        size fails the call (HBX_ERR_IO); bytes past it are not read.  With
+        ``skip_unreadable`` (hbx_store_paths_status) a file the reference skips
+        without stopping the walk -- open() failing (store.go:101-103,
+        221-224) or a read failing with EBADF (minorPathError,
+        hashback_unix.go:57-63) -- comes back with no chunks and its errno in
+        ``FileChunks.errno``, and the rest of its batch is stored; any other
+        read error still fails the call.  ``last_call_s`` holds the library
+        call's wall seconds."""
         if (on_batch is not None or on_files is not None) and not compress:
             raise ValueError("on_batch / on_files need compress=True (hbx_store_paths_zcb)")
         enc = [os.fsencode(p) for p in paths]
@@ -517,13 +525,27 @@ class Engine:
                 raise ValueError("sizes must have one entry per path")
         arr = (ctypes.c_char_p * max(len(enc), 1))(*enc)
         caps, base, cuts, ids, sums = self._alloc_out(lens)
+        status = np.zeros(max(len(enc), 1), np.int32) if skip_unreadable else None
+
+        def with_status(res):
+            if status is not None:
+                for r, e in zip(res, status[:len(res)].tolist()):
+                    r.errno = int(e)
+            return res
+
         if not compress:
             t0 = time.perf_counter()
-            self._check(self._L.hbx_store_paths(self._ctx, len(enc), ctypes.cast(arr, ctypes.c_void_p),
-                                                _p(lens), _p(cuts), _p(ids), _p(base), _p(caps), sums,
-                                                int(io_threads), int(batch_bytes)), "hbx_store_paths")
+            if status is None:
+                self._check(self._L.hbx_store_paths(self._ctx, len(enc), ctypes.cast(arr, ctypes.c_void_p),
+                                                    _p(lens), _p(cuts), _p(ids), _p(base), _p(caps), sums,
+                                                    int(io_threads), int(batch_bytes)), "hbx_store_paths")
+            else:
+                self._check(self._L.hbx_store_paths_status(
+                    self._ctx, len(enc), ctypes.cast(arr, ctypes.c_void_p), _p(lens), _p(cuts), _p(ids), _p(base),
+                    _p(caps), sums, _p(status), int(io_threads), int(batch_bytes), None, None, None, None, None,
+                    None), "hbx_store_paths_status")
             self.last_call_s = time.perf_counter() - t0
-            return self._unpack(lens, caps, base, cuts, ids, sums)
+            return with_status(self._unpack(lens, caps, base, cuts, ids, sums))
         fb = np.array([self._L.hbx_deflate_file_bound(int(x)) for x in lens], np.uint64)
         zbase = np.zeros(max(lens.size, 1), np.uint64)
         if lens.size > 1:
@@ -540,11 +562,18 @@ class Engine:
             r = FileChunks(cuts[b:b + k].copy(), ids[b:b + k].copy(), int(s.content_type),
                            bytes(s.content_id) if k else b"")
             r.zstreams = [zout[int(zoff[b + i]):int(zoff[b + i] + zlen[b + i])] for i in range(k)]
+            if status is not None:  # written when the file was read, before its batch was reported
+                r.errno = int(status[f])
             return r
 
         t0 = time.perf_counter()
+        if status is not None:  # the same with per-file outcomes (hbx_store_paths_status)
+            zargs_st = zargs[:9] + (_p(status),) + zargs[9:]
         if on_batch is None and on_files is None:
-            self._check(self._L.hbx_store_paths_z(*zargs), "hbx_store_paths_z")
+            if status is None:
+                self._check(self._L.hbx_store_paths_z(*zargs), "hbx_store_paths_z")
+            else:
+                self._check(self._L.hbx_store_paths_status(*zargs_st, None, None), "hbx_store_paths_status")
         else:
             raised = []
 
@@ -559,12 +588,16 @@ class Engine:
                 except BaseException as e:  # never unwind through C
                     raised.append(e)
             cb = _lib.BATCH_READY(ready)
-            self._check(self._L.hbx_store_paths_zcb(*zargs, ctypes.cast(cb, ctypes.c_void_p), None),
-                        "hbx_store_paths_zcb")
+            if status is None:
+                self._check(self._L.hbx_store_paths_zcb(*zargs, ctypes.cast(cb, ctypes.c_void_p), None),
+                            "hbx_store_paths_zcb")
+            else:
+                self._check(self._L.hbx_store_paths_status(*zargs_st, ctypes.cast(cb, ctypes.c_void_p), None),
+                            "hbx_store_paths_status")
             if raised:
                 raise raised[0]
         self.last_call_s = time.perf_counter() - t0
-        res = self._unpack(lens, caps, base, cuts, ids, sums)
+        res = with_status(self._unpack(lens, caps, base, cuts, ids, sums))
         for f, r in enumerate(res):
             b = int(base[f])
             r.zstreams = [zout[int(zoff[b + i]):int(zoff[b + i] + zlen[b + i])]  # views, no copy

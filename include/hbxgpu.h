@@ -314,7 +314,12 @@ int hbx_deflate_blocks(hbx_ctx *ctx, uint64_t n, const uint8_t *const *datas, co
  * client.go:249-258).  sums is required.  Chunk i of file f (index
  * out_base[f] + i, like cut_ends) gets its zlib stream at zout[zoff[..]] with
  * length zlen[..]; file f's streams are packed from zout[zbase[f]], which
- * needs hbx_deflate_file_bound(lens[f]) bytes. */
+ * needs hbx_deflate_file_bound(lens[f]) bytes.
+ * Device memory: each compression stage (two in flight) holds, besides its
+ * output, 96 KiB of scratch per 32 KiB segment of the batch, about 3x the
+ * batch's bytes (hbx_deflate.hip kSlot: the parse hand-off and the coded
+ * image of every segment); hbx_deflate_blocks* hold the same per call.  Size
+ * batch_bytes with that in mind. */
 uint64_t hbx_deflate_file_bound(uint64_t len);
 int hbx_store_paths_z(hbx_ctx *ctx, uint64_t n_files, const char *const *paths, const uint64_t *lens,
                       uint64_t *cut_ends, uint8_t *ids, const uint64_t *out_base, const uint64_t *caps,
@@ -415,6 +420,27 @@ int hbx_store_paths_zcb(hbx_ctx *ctx, uint64_t n_files, const char *const *paths
                         hbx_file_summary *summaries, uint32_t io_threads, uint64_t batch_bytes,
                         uint8_t *zout, const uint64_t *zbase, uint64_t *zoff, uint64_t *zlen,
                         hbx_batch_ready_fn ready, void *user);
+
+/* hbx_store_paths* with per-file outcomes (replaces the error handling of
+ * storeFile/storePath/storeDir, hashback/store.go:85-94, 101-103, 221-224,
+ * 356-359).  status (n_files int32, required) receives 0 for a file stored, or
+ * the errno of a file the reference skips without stopping the tree walk:
+ *   - open() failed (os.Open, store.go:101-103: storeDir logs "Skipping
+ *     (ERROR)" and goes on with the next entry, :221-224);
+ *   - a read failed with EBADF (minorPathError, hashback_unix.go:57-63:
+ *     storePath keeps the previous backup's entry, store.go:356-359).
+ * Such a file gets no chunks (summary n_chunks 0, content type 0); every other
+ * file of its batch is stored as usual.  Any other read failure (an I/O error,
+ * a file shorter than lens[i]) is what storeFile panics on (CopyNOrPanic,
+ * pkg/core/utils.go:95-99): the call fails with HBX_ERR_IO and the path in
+ * hbx_last_error, as hbx_store_paths does for every failure.  zout, zbase,
+ * zoff, zlen all NULL: no compression (hbx_store_paths); else as
+ * hbx_store_paths_zcb (ready may be NULL: hbx_store_paths_z). */
+int hbx_store_paths_status(hbx_ctx *ctx, uint64_t n_files, const char *const *paths, const uint64_t *lens,
+                           uint64_t *cut_ends, uint8_t *ids, const uint64_t *out_base, const uint64_t *caps,
+                           hbx_file_summary *summaries, int32_t *status, uint32_t io_threads,
+                           uint64_t batch_bytes, uint8_t *zout, const uint64_t *zbase, uint64_t *zoff,
+                           uint64_t *zlen, hbx_batch_ready_fn ready, void *user);
 
 /* Device arena helpers (allocations include HBX_ARENA_SLACK). */
 int hbx_arena_alloc(hbx_ctx *ctx, uint64_t bytes, void **d_ptr);

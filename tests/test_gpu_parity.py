@@ -3,6 +3,8 @@
 Chunk boundaries, block IDs, content type and content ID must equal the
 oracle's restatement of hashback/store.go:111-196 + pkg/core/block.go:96-111.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -189,6 +191,58 @@ def test_store_paths_end_to_end(oracle, tmp_path, join_lag):
     with _pt.raises(ValueError):
         engine.store_paths(paths[:2], sizes=[1])
     engine.close()
+
+
+@pytest.mark.parametrize("compress", [False, True])
+def test_store_paths_per_file_status(engine, oracle, tmp_path, compress):
+    """hbx_store_paths_status (verdict r04 item 5): one file of a 1,000-file
+    batch cannot be opened (deleted after the walker's stat, ENOENT).  The
+    reference's storeDir logs it and goes on (store.go:101-103, 221-224), so
+    the call succeeds, that file gets no chunks and its errno, and the other
+    999 are bit-exact.  A read error the reference panics on (a file shorter
+    than its size, CopyNOrPanic utils.go:95-99; a directory) still fails the
+    whole call."""
+    import errno
+    from hashbox_amd import HbxError
+    g = np.random.Generator(np.random.PCG64(77))
+    sizes = np.exp(g.uniform(np.log(1), np.log(3 << 20), 1000)).astype(np.int64)
+    pool = g.integers(0, 256, 8 << 20, dtype=np.uint8)
+    datas, paths = [], []
+    for i, n in enumerate(sizes):
+        o = int(g.integers(0, pool.size - int(n)))
+        datas.append(pool[o:o + int(n)])
+        p = tmp_path / f"s{i:04d}.bin"
+        datas[-1].tofile(p)
+        paths.append(str(p))
+    bad = 471
+    os.unlink(paths[bad])
+    got = engine.store_paths(paths, sizes=sizes, batch_bytes=256 << 20, compress=compress, skip_unreadable=True)
+    refs = oracle.store_batch_mt(datas, 16)
+    for i, (r, gg) in enumerate(zip(refs, got)):
+        if i == bad:
+            assert gg.errno == errno.ENOENT and gg.n_chunks == 0 and gg.content_type == 0
+            continue
+        assert gg.errno == 0
+        _check(gg, r)
+        if compress:
+            assert len(gg.zstreams) == r.n_chunks
+    # without per-file status the same batch fails loudly, naming the file
+    with pytest.raises(HbxError, match=f"s{bad:04d}.bin"):
+        engine.store_paths(paths, sizes=sizes, batch_bytes=256 << 20, compress=compress)
+    # errors the reference panics on fail the call even with per-file status
+    datas[bad].tofile(paths[bad])
+    short = list(sizes)
+    short[3] += 1
+    with pytest.raises(HbxError, match="end of file"):
+        engine.store_paths(paths, sizes=short, compress=compress, skip_unreadable=True)
+    with pytest.raises(HbxError):
+        engine.store_paths([str(tmp_path)] + paths[:2], sizes=[4096] + list(sizes[:2]), compress=compress,
+                           skip_unreadable=True)
+    # and the context is fine afterwards
+    got = engine.store_paths(paths[:20], sizes=sizes[:20], compress=compress, skip_unreadable=True)
+    for r, gg in zip(refs[:20], got):
+        assert gg.errno == 0
+        _check(gg, r)
 
 
 def _device_batches(oracle, nb, seed):
