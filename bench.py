@@ -128,6 +128,8 @@ def parse():
     ap.add_argument("--e2e-steps", type=int, default=20,
                     help="steps of the pinned-host leg reported under key 'e2e' after the device-resident "
                          "lines (0 = skip)")
+    ap.add_argument("--no-lifetime", action="store_true",
+                    help="skip the probed lifetime decomposition after the timed window (key 'lifetime')")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the oracle check of the last collected and the last drained batch")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPUs; gloo for tests")
@@ -388,6 +390,59 @@ def k3_probe_stats(w):
     out["slowest10"] = [{"end_us": float(end[i]), "xcc": int(xcc[i]), "se": int(se[i]), "cu": int(cu[i]),
                          "simd": int(simd[i]), "R": int(R[i])} for i in order[:10]]
     return out
+
+
+K3_VALU_FLOOR_CYCLES = 320 * SIMD_CYCLES_PER_VALU  # one MD5 block's 320 VALU at one wave per SIMD
+# K1's whole mix (SDWA add/sub, v_lshl_add, v_max3, v_dot4, DPP adds) issues
+# at 4.19-4.20 cycles per wave-instruction per SIMD at four waves per SIMD
+# (profiles/r03b/valu_issue.txt): K1's per-SIMD issue ceiling
+K1_CYCLES_PER_VALU_4W = 4.20
+
+
+def lifetime_leg(eng, arenas, offs, lens, R, B, lead, nfull, head, dist, gpu):
+    """Where a batch's lifetime goes (verdict r04 item 3), from a short
+    probed run after the timed window (hbx_set_k3_probe: per-wave s_memtime /
+    s_memrealtime stamps around the first group's cooperative phase; the
+    probe changes no result).  Throughput = R resident batches / lifetime, and
+    lifetime / the serial floor of the longest chunk = staging x launch
+    overhead x lead:
+      staging         cycles per block / the 1,312 of 320 VALU at 4.1 cycles
+      launch_overhead K3's average launch / (B x cycles per block / clock)
+      lead            R / (R - lead): batches resident but not in K3
+    plus the step's excess over K3's launch (the scan loop)."""
+    eng.set_k3_probe(True)
+    try:
+        steady(eng, arenas, offs, lens, R, 2, 2, dist, gpu)
+        w = eng.k3_wave_times().astype(np.int64)
+    finally:
+        eng.set_k3_probe(False)
+    coop = w[w[:, 7] > 0]
+    if not len(coop):
+        return None
+    R_w = coop[:, 3] & 0xffff
+    full = coop[R_w == R_w.max()]
+    cyc = (full[:, 5] - full[:, 4]).astype(np.float64)
+    ticks = (full[:, 6] - (full[:, 1] & ((1 << 56) - 1))).astype(np.float64)
+    cpb = float(np.median(cyc / full[:, 7]))
+    ghz = float(np.median(cyc / np.maximum(ticks, 1) * 0.1))
+    launch_ms = float(head["roofline"]["avg_launch_ms"])
+    hashing_ms = B * cpb / ghz * 1e-6
+    step_ms = float(head["ms_per_step"])
+    floor_ms = nfull * K3_VALU_FLOOR_CYCLES / ghz * 1e-6
+    busy = int((w[:, 1] & ((1 << 56) - 1) != 0).sum())
+    return {
+        "source": "bench.py lifetime_leg: hbx_set_k3_probe over 2 steps after the timed window (full-slice waves, "
+                  "first group's cooperative phase)",
+        "cycles_per_block": round(cpb, 1), "clock_ghz": round(ghz, 4),
+        "floor_cycles_per_block": K3_VALU_FLOOR_CYCLES, "full_slice_waves": int(len(full)),
+        "staging": round(cpb / K3_VALU_FLOOR_CYCLES, 4),
+        "launch_overhead": round(launch_ms / hashing_ms, 4),
+        "lead": round(R / max(1, R - lead), 4),
+        "step_over_launch": round(step_ms / launch_ms, 4),
+        "lifetime_ms": round(R * step_ms, 2), "serial_floor_ms": round(floor_ms, 2),
+        "lifetime_over_floor": round(R * step_ms / floor_ms, 4),
+        "k3_busy_waves": busy,
+    }
 
 
 def max_over_ranks(x, dist, dev, op="max"):
@@ -740,6 +795,13 @@ def run(a, S, rank, world, local_world, dist, dev, red_dev):
         if zipf_repeat is not None and wl == "zipf":
             lines[wl]["repeat_fraction"] = round(zipf_repeat, 4)
 
+    life = None
+    if not a.no_lifetime and a.alias_depth == 0 and not a.e2e:
+        nfull = (min(fbytes, 8 << 20) + 8) >> 6
+        life = lifetime_leg(eng, arenas, offs, lens, R, B, lead, nfull, lines[workloads[0]], dist, dev)
+        if zipf_repeat is not None:  # the arenas hold the Zipf corpus now: the probe ran over it
+            life["probed_over"] = "the Zipf arenas (MD5 cycles per block do not depend on the bytes)"
+
     e2e = None
     if a.e2e_steps > 0 and not a.e2e and a.alias_depth == 0:
         e2e = e2e_leg(a, eng, arenas, offs, lens, P, lanes, dist, dev, red_dev, world, rank, job_batch, threads)
@@ -794,6 +856,26 @@ def run(a, S, rank, world, local_world, dist, dev, red_dev):
                            "gibs": round(sum(lens) / GIB / (float(latency[4]) * 1e-3), 3),
                            "stages_ms": [round(float(x), 3) for x in latency]}
     out["cpu_baseline"] = cpu
+    if life is not None:
+        out["lifetime"] = life
+        # the two loops' VALU ceilings, each for its own issue mode
+        # (profiles/r03b/valu_issue.txt): K3 is bound by ONE wave's issue
+        # (a chain's speed at fixed residency), K1 by the SIMD's issue at
+        # four waves of an all-half-rate mix, on the CUs K3 leaves
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        k3_cus = -(-life["k3_busy_waves"] // 4)
+        k1_simds = max(1, cus - k3_cus) * 4
+        k1_ms = float(head["kernel_ms_per_step"]["k1_digest_scan"])
+        k1_need = sum(int(n) for n in lens) * K1_WAVE_VALU_PER_BYTE * K1_CYCLES_PER_VALU_4W
+        out["valu_roofline"]["k3"] = {
+            "bound": "one wave's VALU issue (one MD5 wave per SIMD; a chain's speed)",
+            "peak_cycles_per_block": K3_VALU_FLOOR_CYCLES, "achieved_cycles_per_block": life["cycles_per_block"],
+            "frac": round(K3_VALU_FLOOR_CYCLES / life["cycles_per_block"], 4)}
+        out["valu_roofline"]["k1"] = {
+            "bound": f"SIMD issue at four waves per SIMD, half-rate mix ({K1_CYCLES_PER_VALU_4W} cycles per "
+                     "wave-VALU), on the CUs K3 leaves",
+            "simds": k1_simds, "launch_ms": k1_ms, "clock_ghz": life["clock_ghz"],
+            "frac": round(k1_need / (k1_simds * k1_ms * 1e-3 * life["clock_ghz"] * 1e9), 4)}
     if e2e is not None:
         out["e2e"] = e2e
     if "zipf" in lines and workloads[0] != "zipf":

@@ -189,6 +189,7 @@ struct hbx_ctx {
   uint32_t k4_window = 1024;  // K4's LDS window of ids (HBX_K4_WINDOW, 1..1024: tests)
   int k2_own = -1;            // ensure_cut_stream: -1 = by join lag (HBX_K2_STREAM for A/B)
   uint32_t md5_wgs = 256;     // K3 grid: one 256-thread workgroup per CU (set from the device)
+  uint32_t k3_prod = 0;       // K3P: a producer wave per MD5 wave (HBX_K3_PROD for A/B)
   uint32_t md5_slice = 16384; // K3 time slice: full MD5 blocks per chain per launch (0 = unlimited)
   // K1 gate (hbx_k1_gate): a batch's K1 waits until every workgroup of the K3
   // launch of the same submit has been dispatched.  k3_started counts K3
@@ -620,10 +621,16 @@ int md5_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
     c->k3_open.push_back(L);
   }
   const uint32_t waves = c->md5_wgs * (kK3Threads / 64);
-  hipLaunchKernelGGL(hbx_k3_block_md5, dim3(c->md5_wgs), dim3(kK3Threads), 0, s,
-                     c->d_order[slot].as<OrderEntry>(), static_cast<const uint32_t*>(c->d_octl[slot].as<uint32_t>()),
-                     budget, c->d_gate.as<uint32_t>(), c->k3_dispatched, c->k3_waves + waves - 1u, tslot,
-                     c->h_probe.p ? c->h_probe.as<uint64_t>() : nullptr);
+  if (c->k3_prod)
+    hipLaunchKernelGGL(hbx_k3p_block_md5, dim3(c->md5_wgs), dim3(kK3PThreads), 0, s,
+                       c->d_order[slot].as<OrderEntry>(), static_cast<const uint32_t*>(c->d_octl[slot].as<uint32_t>()),
+                       budget, c->d_gate.as<uint32_t>(), c->k3_dispatched, c->k3_waves + waves - 1u, tslot,
+                       c->h_probe.p ? c->h_probe.as<uint64_t>() : nullptr);
+  else
+    hipLaunchKernelGGL(hbx_k3_block_md5, dim3(c->md5_wgs), dim3(kK3Threads), 0, s,
+                       c->d_order[slot].as<OrderEntry>(), static_cast<const uint32_t*>(c->d_octl[slot].as<uint32_t>()),
+                       budget, c->d_gate.as<uint32_t>(), c->k3_dispatched, c->k3_waves + waves - 1u, tslot,
+                       c->h_probe.p ? c->h_probe.as<uint64_t>() : nullptr);
   HBX_TRY(c, hipGetLastError());
   c->k3_dispatched += c->md5_wgs;
   c->k3_waves += waves;
@@ -1195,6 +1202,9 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = ab_env("HBX_MD5_SLICE")) c->md5_slice = (uint32_t)std::max(0, std::atoi(v));
   if (const char* v = ab_env("HBX_K1_GATE")) c->k1_gate = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_LEAN_MARKS")) c->lean_marks = std::atoi(v) ? 1u : 0u;
+  if (const char* v = ab_env("HBX_K3_PROD")) c->k3_prod = std::atoi(v) ? 1u : 0u;
+  // (tests: a K3 grid of a few workgroups, so every wave takes many groups)
+  if (const char* v = ab_env("HBX_K3_WGS")) c->md5_wgs = (uint32_t)std::min<int>(std::max(1, ncu), std::max(1, std::atoi(v)));
   if (hipSetDevice(device) != hipSuccess || make_stream(&c->stream, "HBX_SCAN_CUS", ncu, "0:4096") != hipSuccess) {
     delete c;
     return HBX_ERR_HIP;
@@ -1303,9 +1313,9 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
       out, (size_t)cap,
       "{\"ab_env\": %d, \"md5_slice\": %u, \"join_lag\": %u, \"tile_iters\": %u, \"k1_gate\": %u, "
       "\"md5_wgs\": %u, \"plan_mode\": %d, \"k2_own\": %d, \"k4_window\": %u, \"k3_probe\": %d, "
-      "\"lean_marks\": %u, \"k8_split_streams\": %llu, \"k8_split_fallbacks\": %llu}",
+      "\"lean_marks\": %u, \"k3_prod\": %u, \"k8_split_streams\": %llu, \"k8_split_fallbacks\": %llu}",
       (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_gate, c->md5_wgs,
-      plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks,
+      plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks, c->k3_prod,
       (unsigned long long)c->k8_split_streams, (unsigned long long)c->k8_split_fallbacks);
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }
@@ -1321,7 +1331,7 @@ int hbx_set_k3_probe(hbx_ctx* c, int on) {
     c->h_probe.release();
     return HBX_OK;
   }
-  const size_t n = (size_t)c->md5_wgs * (kK3Threads / 64) * 32;
+  const size_t n = (size_t)c->md5_wgs * (kK3Threads / 64) * 64;
   HBX_TRY(c, c->h_probe.ensure(n));
   std::memset(c->h_probe.p, 0, n);
   return HBX_OK;
@@ -1335,7 +1345,7 @@ int hbx_k3_wave_times(hbx_ctx* c, uint64_t* out, uint32_t max_waves, uint32_t* n
   HBX_TRY(c, hipSetDevice(c->device));
   HBX_TRY(c, hipStreamSynchronize(c->hstream));
   const uint32_t n = c->md5_wgs * (kK3Threads / 64);
-  if (out) std::memcpy(out, c->h_probe.p, (size_t)std::min(n, max_waves) * 32);
+  if (out) std::memcpy(out, c->h_probe.p, (size_t)std::min(n, max_waves) * 64);
   *n_waves = n;
   return HBX_OK;
 }

@@ -1042,12 +1042,150 @@ constexpr uint32_t kCoopMinBudget = 8u;
 constexpr int kK3Threads = 256;  // one wave per SIMD
 constexpr uint32_t kK3WaveLds = Coop<16>::WaveLds;
 
+// ---------------------------------------------------- K3 producer waves --
+// K3P (hbx_k3p_block_md5): each MD5 wave gets a producer wave that issues the
+// cooperative global loads of its stages and writes the 272-B LDS rows, so
+// the MD5 wave's instruction stream is 4 ds_read_b128 + 320 VALU per block
+// (verdict r04 item 1).  The pair hands stages over through two LDS counters,
+// cumulative over the launch: flags[0] = stages written, flags[1] = stages
+// the MD5 wave is done with.  Stage x lives in LDS half x & 1.  The MD5 wave
+// frees the last stage of a group only once the whole group is done (its
+// partial rounds and lane remainders stage through the same LDS), so the
+// producer writes a group's first two stages only after that.
+__device__ __forceinline__ uint32_t k3p_flag(uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void k3p_wait_ge(uint32_t* p, uint32_t want) {
+  for (;;) {
+    const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane((int)k3p_flag(p));
+    if ((int32_t)(v - want) >= 0) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");  // no LDS access of the stage moves above the wait
+}
+__device__ __forceinline__ void k3p_publish(uint32_t* p, uint32_t v) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the stage's LDS writes (or reads) are done
+  if ((threadIdx.x & 63u) == 0u) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// The MD5 wave's side of one group: blocks 0..Rr-1 of the cooperative phase
+// from the producer's stages S, S+1, ..  Each block's 4 ds_read_b128 are
+// issued one block ahead (the next stage's first block once the producer has
+// published it), so the LDS latency hides behind a block of VALU; two
+// register sets alternate without copies.  A stage is freed once its last
+// block is hashed (its reads have returned: the block consumed them; LDS
+// operations of a wave execute in order, so the release needs no wait), except
+// the group's last stage (freed by the caller once the group is done).
+__device__ __forceinline__ void k3p_consume(uint8_t* wl, uint32_t* flags, uint32_t S, uint32_t Rr, uint32_t (&h)[4]) {
+  const uint8_t* base = wl + (threadIdx.x & 63u) * Coop<16>::Row;
+  auto rd4 = [&](uint32_t b, u32x4(&W)[4]) {
+    const uint8_t* p = base + ((S + (b >> 2)) & 1u) * Coop<16>::Half + 64u * (b & 3u);
+#pragma unroll
+    for (int i = 0; i < 4; i++) W[i] = *reinterpret_cast<const u32x4*>(p + 16 * i);
+  };
+  auto step = [&](uint32_t b, const u32x4(&W)[4], u32x4(&N)[4]) {
+    const uint32_t nb = b + 1u;
+    if (nb < Rr) {  // wave-uniform
+      if ((nb & 3u) == 0u) k3p_wait_ge(&flags[0], S + (nb >> 2) + 1u);
+      rd4(nb, N);
+    }
+    const uint32_t m[16] = {W[0].x, W[0].y, W[0].z, W[0].w, W[1].x, W[1].y, W[1].z, W[1].w,
+                            W[2].x, W[2].y, W[2].z, W[2].w, W[3].x, W[3].y, W[3].z, W[3].w};
+    md5_compress(h, m);
+    if ((nb & 3u) == 0u && nb < Rr) {  // stage (nb >> 2) - 1 is done
+      asm volatile("" ::: "memory");
+      if ((threadIdx.x & 63u) == 0u)
+        __hip_atomic_store(&flags[1], S + (nb >> 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  };
+  u32x4 WA[4], WB[4];
+  k3p_wait_ge(&flags[0], S + 1u);
+  rd4(0u, WA);
+  for (uint32_t b = 0; b < Rr; b += 2u) {
+    step(b, WA, WB);
+    if (b + 1u < Rr) step(b + 1u, WB, WA);
+  }
+}
+
+// The group's wave-minimum count and the chain of this lane, exactly as the
+// MD5 wave computes them (both roles walk the same groups).
+struct K3Group {
+  const Chain* chp;
+  Chain ch;
+  uint32_t cnt, R;
+  bool active;
+};
+__device__ __forceinline__ K3Group k3_group(const OrderEntry* __restrict__ order, uint32_t n_total, uint32_t g,
+                                            uint32_t budget) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t k = 64u * g + lane;
+  K3Group G;
+  G.active = k < n_total;
+  // idle lanes stay alive for the wave-wide loop bound: they run an empty
+  // slice over the group's first chain and store nothing
+  G.chp = reinterpret_cast<const Chain*>(order[G.active ? k : 64u * g].chain);
+  G.ch = *G.chp;
+  const uint32_t len = G.active ? G.ch.len : 0u;
+  const uint32_t b0 = G.active ? G.ch.next : 0u;
+  G.cnt = G.active ? chain_cnt(len, b0, budget) : 0u;
+  // R = the wave's smallest count: all 64 chains advance R blocks together
+  G.R = ~wave_max_all(G.active ? ~G.cnt : 0u);
+  return G;
+}
+
+// The producer's side of one group: the stages S, S+1, .. of Rr blocks of the
+// wave's 64 chains, lane l's chain message stream starting at `src` (16-B
+// loads at any byte offset, as md5_coop).  Returns the group's stage count.
+__device__ __forceinline__ uint32_t k3p_produce(uint8_t* wl, uint32_t* flags, uint32_t S, uint64_t src, uint32_t Rr) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t t = lane % 16u, sub = lane / 16u;
+  const uint32_t wr = sub * Coop<16>::Row + 16u * t;
+  const uint32_t ngr = 4u * Rr, nst = (ngr + 15u) / 16u;
+  uint64_t Q[16];
+#pragma unroll
+  for (int q = 0; q < 16; q++) Q[q] = shfl64(src, 4u * (uint32_t)q + sub) + 16ull * t;
+  u32x4 GA[16], GB[16];
+  coop_load<16>(GA, Q, 0u, t, ngr);
+  coop_load<16>(GB, Q, min(1u, nst - 1u), t, ngr);
+  for (uint32_t s = 0; s < nst; s += 2u) {
+    k3p_wait_ge(&flags[1], s < 2u ? S : S + s - 1u);
+    coop_write<16>(wl, wr, (S + s) & 1u, GA);
+    k3p_publish(&flags[0], S + s + 1u);
+    coop_load<16>(GA, Q, min(s + 2u, nst - 1u), t, ngr);
+    if (s + 1u < nst) {
+      k3p_wait_ge(&flags[1], s + 1u < 2u ? S : S + s);
+      coop_write<16>(wl, wr, (S + s + 1u) & 1u, GB);
+      k3p_publish(&flags[0], S + s + 2u);
+      coop_load<16>(GB, Q, min(s + 3u, nst - 1u), t, ngr);
+    }
+  }
+  return nst;
+}
+
+// The producer wave of pair `flags`: the same groups as its MD5 wave; for a
+// group on the cooperative path (R >= kCoopMinBudget), the stages of blocks
+// next+1 .. next+R-1 of its 64 chains, two register sets in flight.
+__device__ void k3p_producer(uint8_t* wl, uint32_t* flags, const OrderEntry* __restrict__ order,
+                             const uint32_t* __restrict__ n_order, uint32_t budget, uint32_t g0, uint32_t nwaves) {
+  const uint32_t n_total = *n_order;
+  const uint32_t groups = (n_total + 63u) / 64u;
+  uint32_t S = 0;  // stages of this launch so far
+  for (uint32_t g = g0; g < groups; g += nwaves) {
+    const K3Group G = k3_group(order, n_total, g, budget);
+    if (G.R < kCoopMinBudget) continue;  // wave-uniform: the MD5 wave takes the lane path
+    S += k3p_produce(wl, flags, S, G.ch.src + 64ull * (G.ch.next + 1u) - 8ull, G.R - 1u);  // from block next+1
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (clamped re-reads of the last stage)
+}
+
 // One wave's share of a K3 launch (VGPR + AGPR, no scratch).  `wl` = this
-// wave's LDS.
+// wave's LDS.  PROD: a producer wave feeds the cooperative stages (K3P,
+// `flags` = the pair's counters); else the wave loads and stages them itself.
+template <bool PROD>
 __device__ __forceinline__ void k3_body(
     uint8_t* wl, const OrderEntry* __restrict__ order, const uint32_t* __restrict__ n_order, uint32_t budget,
     uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last, uint64_t* __restrict__ tslot,
-    uint64_t* __restrict__ probe) {
+    uint64_t* __restrict__ probe, uint32_t* flags = nullptr) {
   // the MD5 chains are issue-bound: win the SIMD's issue arbitration against
   // co-resident waves of other kernels
   __builtin_amdgcn_s_setprio(3);
@@ -1077,8 +1215,9 @@ __device__ __forceinline__ void k3_body(
   // diagnostics (hbx_set_k3_probe): per wave its start, the end of its first
   // group's start-up (loads + prologue), its end, R and the largest count
   const uint64_t pt0 = probe ? __builtin_amdgcn_s_memrealtime() : 0ull;
-  uint64_t pt1 = 0ull;
+  uint64_t pt1 = 0ull, pc1 = 0ull, pc2 = 0ull, pt2 = 0ull;  // + the first group's cooperative phase, in cycles
   uint32_t pR = 0u, pmax = 0u;
+  uint32_t S = 0;  // PROD: stages of this launch so far (the producer counts the same)
   for (uint32_t g = g0; g < groups; g += nwaves) {
     const uint32_t k = 64u * g + lane;
     const bool active = k < n_total;
@@ -1100,10 +1239,20 @@ __device__ __forceinline__ void k3_body(
       md5_block_at(src, ch.len, h, ch.next);  // every lane now at a block >= 1
       if (probe && g == g0) {
         pt1 = __builtin_amdgcn_s_memrealtime();
+        pc1 = __builtin_amdgcn_s_memtime();
         pR = R;
         pmax = wave_max_all(cnt);
       }
-      md5_coop<16>(wl, src, h, ch.next + 1u, R - 1u);
+      if constexpr (PROD) {  // stages from the producer wave; the group's last is freed at its end
+        k3p_consume(wl, flags, S, R - 1u, h);
+        S += (4u * (R - 1u) + 15u) / 16u;
+      } else {
+        md5_coop<16>(wl, src, h, ch.next + 1u, R - 1u);
+      }
+      if (probe && g == g0) {
+        pc2 = __builtin_amdgcn_s_memtime();
+        pt2 = __builtin_amdgcn_s_memrealtime();
+      }
       // A group that straddles two order bins mixes counts (e.g. 4,229 and
       // 4,093 blocks): the lanes still holding blocks go on cooperatively
       // while the others shadow the first of them and discard (the lane-mode
@@ -1130,9 +1279,10 @@ __device__ __forceinline__ void k3_body(
           rem -= R2;
         }
       }
-      md5_run<>(src, len, h, pos, rem, finish);
+      md5_run<PROD ? 4 : HBX_MD5_RING>(src, len, h, pos, rem, finish);
+      if constexpr (PROD) k3p_publish(&flags[1], S);  // the LDS is the producer's again
     } else {
-      md5_run<>(src, len, h, b0, cnt, finish);
+      md5_run<PROD ? 4 : HBX_MD5_RING>(src, len, h, b0, cnt, finish);
     }
     if (finish) {
       *(__attribute__((address_space(1))) u32x4*)ch.out = u32x4{h[0], h[1], h[2], h[3]};
@@ -1143,7 +1293,7 @@ __device__ __forceinline__ void k3_body(
     }
   }
   if (probe && (threadIdx.x & 63u) == 0u) {
-    uint64_t* p = probe + 4u * (blockIdx.x * (kK3Threads / 64) + wave);
+    uint64_t* p = probe + 8u * (blockIdx.x * (kK3Threads / 64) + wave);
     // hardware placement: HW_ID (wave, SIMD, CU, SH, SE) and XCC_ID
     const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));
     const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11)) & 0xfu;
@@ -1151,6 +1301,13 @@ __device__ __forceinline__ void k3_body(
     p[1] = pt1 | ((uint64_t)xcc << 56);
     p[2] = __builtin_amdgcn_s_memrealtime();
     p[3] = (uint64_t)min(pR, 0xffffu) | ((uint64_t)min(pmax, 0xffffu) << 16) | ((uint64_t)hw << 32);
+    // the first group's cooperative phase (R - 1 blocks of each chain):
+    // shader cycles (s_memtime) and 100 MHz ticks, so cycles per block and the
+    // clock follow (bench.py's lifetime decomposition)
+    p[4] = pc1;
+    p[5] = pc2;
+    p[6] = pt2;
+    p[7] = pR ? pR - 1u : 0u;
   }
   if (started && tslot && (threadIdx.x & 63u) == 0u) {
     const uint32_t tk = __hip_atomic_fetch_add(started + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -1167,7 +1324,29 @@ extern "C" __global__ __launch_bounds__(kK3Threads, 1) void hbx_k3_block_md5(
     uint64_t* __restrict__ probe) {
   __shared__ __attribute__((aligned(16))) uint8_t k3_lds[kK3Threads / 64][kK3WaveLds];
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  k3_body(k3_lds[wave], order, n_order, budget, started, t_first, t_last, tslot, probe);
+  k3_body<false>(k3_lds[wave], order, n_order, budget, started, t_first, t_last, tslot, probe);
+}
+
+// K3P: the same with a producer wave per MD5 wave (waves 4-7 load for waves
+// 0-3 of the workgroup; 512 threads, one workgroup per CU).  Same arguments,
+// results and launch accounting (only the MD5 waves count in started[1]).
+constexpr int kK3PThreads = 512;
+extern "C" __global__ __launch_bounds__(kK3PThreads, 1) void hbx_k3p_block_md5(
+    const OrderEntry* __restrict__ order, const uint32_t* __restrict__ n_order, uint32_t budget,
+    uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last, uint64_t* __restrict__ tslot,
+    uint64_t* __restrict__ probe) {
+  __shared__ __attribute__((aligned(16))) uint8_t k3_lds[4][kK3WaveLds];
+  __shared__ uint32_t k3_flags[4][2];
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t pair = wave & 3u;
+  if (threadIdx.x < 8u) k3_flags[threadIdx.x >> 1][threadIdx.x & 1u] = 0u;
+  __syncthreads();
+  if (wave < 4u) {
+    k3_body<true>(k3_lds[pair], order, n_order, budget, started, t_first, t_last, tslot, probe, k3_flags[pair]);
+  } else {
+    __builtin_amdgcn_s_setprio(2);
+    k3p_producer(k3_lds[pair], k3_flags[pair], order, n_order, budget, blockIdx.x * 4u + pair, gridDim.x * 4u);
+  }
 }
 
 // K1 gate (scan stream, just before a batch's K1): holds the K1 back until

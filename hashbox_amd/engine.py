@@ -307,11 +307,13 @@ class Engine:
 
     def k3_wave_times(self) -> np.ndarray:
         """Diagnostics (:meth:`set_k3_probe`): per-wave records of the
-        latest K3 launch, shape (waves, 4): start, start-up end | XCC << 56,
-        end (100 MHz ticks), R | max count << 16 | HW_ID << 32."""
+        latest K3 launch, shape (waves, 8): start, start-up end | XCC << 56,
+        end (100 MHz ticks), R | max count << 16 | HW_ID << 32, then the
+        first group's cooperative phase: s_memtime at its start and end,
+        s_memrealtime at its end, blocks per chain (R - 1)."""
         n = ctypes.c_uint32(0)
         self._check(self._L.hbx_k3_wave_times(self._ctx, None, 0, ctypes.byref(n)), "hbx_k3_wave_times")
-        out = np.zeros((max(n.value, 1), 4), np.uint64)
+        out = np.zeros((max(n.value, 1), 8), np.uint64)
         self._check(self._L.hbx_k3_wave_times(self._ctx, _p(out), n.value, ctypes.byref(n)), "hbx_k3_wave_times")
         return out[:n.value]
 

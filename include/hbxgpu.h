@@ -490,9 +490,13 @@ int hbx_set_k3_probe(hbx_ctx *ctx, int on);
 /* Diagnostics: with the probe on (hbx_set_k3_probe),
  * every K3 launch records per wave {start, end of its start-up (first
  * group's loads and prologue block) | XCC id << 56, end, R | max count << 16
- * | HW_ID << 32} (times in s_memrealtime ticks, 100 MHz; R and the count
- * saturate at 65535).  Copies the latest launch's records (4 x u64 per wave, up
- * to max_waves) after the hash stream drains; *n_waves = waves per launch. */
+ * | HW_ID << 32, s_memtime (shader cycles) at the start and the end of the
+ * first group's cooperative phase, s_memrealtime at its end, the blocks of
+ * each chain it hashed (R - 1)} (times in s_memrealtime ticks, 100 MHz; R and
+ * the count saturate at 65535; the last four are 0 for a wave whose first
+ * group took the lane path).  Copies the latest launch's records (8 x u64 per
+ * wave, up to max_waves) after the hash stream drains; *n_waves = waves per
+ * launch. */
 int hbx_k3_wave_times(hbx_ctx *ctx, uint64_t *out, uint32_t max_waves, uint32_t *n_waves);
 /* Tile length of K1 in 64 KiB iterations, 1..1024; 0 (the default) sizes
  * tiles per batch: about two per CU, 16..256 iterations (1-16 MiB). */

@@ -60,7 +60,9 @@ def test_state_rules(oracle):
         e.submit_device(dev.data_ptr(), offs, sizes)
         got.append(e.wait())
         w = e.k3_wave_times()  # the probe's per-wave records of the latest K3 launch
-        assert w.shape[1] == 4 and (w[:, 2] >= w[:, 0]).all()
+        assert w.shape[1] == 8 and (w[:, 2] >= w[:, 0]).all()
+        coop = w[w[:, 7] > 0]  # waves whose first group ran the cooperative phase: cycles advance
+        assert (coop[:, 5] >= coop[:, 4]).all() and (coop[:, 6] >= (coop[:, 1] & ((1 << 56) - 1))).all()
         e.set_k3_probe(False)
         assert e.knobs()["k3_probe"] == 0
     for g in got:

@@ -297,6 +297,49 @@ def test_pipelined_batches_time_sliced(oracle, md5_slice, join_lag):
         assert n[3] >= 1 and ms[3] > 0
 
 
+@pytest.mark.parametrize("prod", ["0", "1"])
+@pytest.mark.parametrize("md5_slice,join_lag,wgs", [(9, 1, 0), (64, 3, 0), (4096, 1, 0), (4096, 2, 0), (16384, 1, 0),
+                                                    (0, 1, 0), (64, 1, 1), (4096, 1, 2), (0, 3, 1)])
+def test_k3_producer_waves(oracle, monkeypatch, md5_slice, join_lag, wgs, prod):
+    """K3 with and without a producer wave per MD5 wave (hbx_k3p_block_md5 /
+    hbx_k3_block_md5, HBX_K3_PROD): the stages a producer hands over through
+    the LDS counters, groups on the lane path (slices below 8 blocks), groups
+    that straddle two bins (partial rounds self-staged in the same LDS), many
+    groups per wave (more groups than waves at small slices), a deep
+    pipeline and a forced drain, with the probe on for one batch; bit-exact.
+    wgs > 0 shrinks the K3 grid to that many workgroups (HBX_K3_WGS), so each
+    MD5 wave and its producer walk many groups in one launch."""
+    from hashbox_amd import Engine
+    monkeypatch.setenv("HBX_AB", "1")
+    monkeypatch.setenv("HBX_K3_PROD", prod)
+    if wgs:
+        monkeypatch.setenv("HBX_K3_WGS", str(wgs))
+    batches = _device_batches(oracle, 3, 71 + md5_slice % 5)
+    got, order = [], []
+    with Engine(0, md5_slice=md5_slice, join_lag=join_lag) as e:
+        assert e.knobs()["k3_prod"] == int(prod) and (not wgs or e.knobs()["md5_wgs"] == wgs)
+        for i in [0, 1, 2, 0, 2, 1, 1, 0, 2, 2, 0, 1]:
+            dev, offs, sizes, _ = batches[i]
+            e.submit_device(dev.data_ptr(), offs, sizes)
+            order.append(i)
+            if e.pending() >= 6:
+                got.append(e.wait())
+        while e.pending():
+            got.append(e.wait())
+        e.set_k3_probe(True)
+        for i in (1, 2):
+            e.submit_device(batches[i][0].data_ptr(), batches[i][1], batches[i][2])
+            order.append(i)
+        got += [e.wait(), e.wait()]
+        w = e.k3_wave_times()
+        assert (w[:, 2] >= w[:, 0]).all()
+        e.set_k3_probe(False)
+    assert len(got) == len(order)
+    for i, g in zip(order, got):
+        for a, r in zip(g, batches[i][3]):
+            _check(a, r)
+
+
 @pytest.mark.parametrize("join_lag", [1, 2, 3, 4])
 def test_pipelined_steady_state(oracle, join_lag):
     """A deep pipeline as bench.py drives it: submit, and wait only once

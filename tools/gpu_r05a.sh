@@ -1,11 +1,16 @@
 #!/bin/bash
-# Round 5, first box: the K3 producer-wave microbenchmark (tools/ubench/k3_prod)
-# and the round-4 tree's bench line under the driver's command (baseline).
+# Round 5, first box: the K3 producer-wave microbenchmark (tools/ubench/k3_prod),
+# the K3P parity tests, and the bench line under the driver's command with
+# and without K3P (HBX_AB=1 HBX_K3_PROD=1).
 set -o pipefail
 O=gpurun_out/r05a
 mkdir -p $O
 timeout -k 10 180 tools/ubench/k3_prod 64 32768 4096 3 > $O/k3_prod.txt 2>&1; rc=$?
 cat $O/k3_prod.txt
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench20.json 2> $O/bench20.err || { tail -20 $O/bench20.err; exit 1; }
-python3 -c "import json;d=json.load(open('$O/bench20.json'));print(d['value'], d['zipf']['value'], d['check_vs_oracle'], d['roofline']['frac'], d['kernel_ms_per_step'])"
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q -k "producer" --timeout 120 --timeout-method thread > $O/pytest_k3p.log 2>&1 || { tail -30 $O/pytest_k3p.log; exit 1; }
+tail -2 $O/pytest_k3p.log
+for v in 0 1; do
+  HBX_AB=1 HBX_K3_PROD=$v timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --e2e-steps 0 --no-cpu-baseline > $O/bench20_p$v.json 2> $O/bench20_p$v.err || { tail -20 $O/bench20_p$v.err; exit 1; }
+  python3 -c "import json;d=json.load(open('$O/bench20_p$v.json'));print('prod=$v', d['value'], d['zipf']['value'], d['check_vs_oracle'], d['zipf']['check_vs_oracle'], d['roofline']['frac'], d['kernel_ms_per_step'], d.get('lifetime'), d['valu_roofline'].get('k1'))"
+done

@@ -68,22 +68,8 @@ __global__ __launch_bounds__(256, 1) void k3_base(const uint64_t* __restrict__ a
 }
 
 // ----------------------------------------------------------------- prod --
-__device__ __forceinline__ uint32_t lds_load_relaxed(uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void wait_ge(uint32_t* p, uint32_t want) {
-  for (;;) {
-    const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_load_relaxed(p));
-    if (v >= want) break;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  asm volatile("" ::: "memory");  // no LDS read of the stage moves above the wait
-}
-__device__ __forceinline__ void publish(uint32_t* p, uint32_t v) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the stage's LDS writes (or reads) are done
-  if ((threadIdx.x & 63u) == 0u) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
+// The product's K3P pair code (hbx_kernels.hip k3p_consume / k3p_produce) on
+// one group per pair: blocks 1..R-1 of the wave's 64 chains.
 template <int PRIO_P>
 __global__ __launch_bounds__(512, 1) void k3_prod(const uint64_t* __restrict__ addr, uint32_t R,
                                                    u32x4* __restrict__ out, uint64_t* __restrict__ stamps) {
@@ -92,54 +78,24 @@ __global__ __launch_bounds__(512, 1) void k3_prod(const uint64_t* __restrict__ a
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t pair = wave & 3u;
-  const bool producer = wave >= 4u;
   if (threadIdx.x < 8u) flags[threadIdx.x >> 1][threadIdx.x & 1u] = 0u;
   __syncthreads();
   const uint32_t gw = blockIdx.x * 4u + pair;
-  uint8_t* wl = lds[pair];
   const uint8_t* c = reinterpret_cast<const uint8_t*>(addr[64u * gw + lane]);
-  const uint32_t Rr = R - 1u;                // blocks 1..R-1 cooperatively
-  const uint32_t ngr = 4u * Rr;              // 16-B granules
-  const uint32_t nst = (ngr + 15u) / 16u;    // 4-block stages
-  if (!producer) {
+  if (wave < 4u) {
     uint64_t* st = stamps + 8u * gw;
     __builtin_amdgcn_s_setprio(3);
     stamp(st, 0);
     uint32_t h[4];
     md5_init(h);
     md5_block_at(c, kLen, h, 0u);
-    const uint32_t rd = lane * Coop<16>::Row;
-    for (uint32_t s = 0; s < nst; s++) {
-      wait_ge(&flags[pair][0], s + 1u);
-      coop_hash<16>(wl, rd, s & 1u, s, Rr, h);
-      publish(&flags[pair][1], s + 1u);
-    }
+    k3p_consume(lds[pair], flags[pair], 0u, R - 1u, h);
     out[64u * gw + lane] = u32x4{h[0], h[1], h[2], h[3]};
     stamp(st, 1);
     if (lane == 0u) st[4] = __builtin_amdgcn_s_getreg(4 | (31 << 11));
   } else {
     __builtin_amdgcn_s_setprio(PRIO_P);
-    const uint64_t S = reinterpret_cast<uint64_t>(c) + 64ull - 8ull;  // message block 1
-    const uint32_t t = lane % 16u, sub = lane / 16u;
-    uint64_t Q[16];
-#pragma unroll
-    for (int q = 0; q < 16; q++) Q[q] = shfl64(S, 4u * (uint32_t)q + sub) + 16ull * t;
-    const uint32_t wr = sub * Coop<16>::Row + 16u * t;
-    u32x4 GA[16], GB[16];
-    coop_load<16>(GA, Q, 0u, t, ngr);
-    coop_load<16>(GB, Q, min(1u, nst - 1u), t, ngr);
-    for (uint32_t s = 0; s < nst; s += 2u) {
-      if (s >= 2u) wait_ge(&flags[pair][1], s - 1u);
-      coop_write<16>(wl, wr, 0u, GA);
-      publish(&flags[pair][0], s + 1u);
-      coop_load<16>(GA, Q, min(s + 2u, nst - 1u), t, ngr);
-      if (s + 1u < nst) {
-        wait_ge(&flags[pair][1], s);
-        coop_write<16>(wl, wr, 1u, GB);
-        publish(&flags[pair][0], s + 2u);
-        coop_load<16>(GB, Q, min(s + 3u, nst - 1u), t, ngr);
-      }
-    }
+    k3p_produce(lds[pair], flags[pair], 0u, reinterpret_cast<uint64_t>(c) + 64ull - 8ull, R - 1u);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0u) stamps[8u * gw + 5] = __builtin_amdgcn_s_getreg(4 | (31 << 11));
   }
