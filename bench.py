@@ -349,7 +349,8 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
     if dist:
         dist.barrier()
     tot_ms, tot_n = eng.stage_totals()
-    probe = k3_probe_stats(eng.k3_wave_times()) if eng.knobs().get("k3_probe") else None
+    probe_raw = eng.k3_wave_times() if eng.knobs().get("k3_probe") else None  # the window's last launch
+    probe = k3_probe_stats(probe_raw) if probe_raw is not None else None
     t_d = time.perf_counter()
     drained = None
     while order:
@@ -358,7 +359,8 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
     t2 = time.perf_counter()
     return {"el": t1 - t0, "drain": t2 - t_d, "fill_to_drained": t2 - t_fill,
             "batches_total": state["j"], "tot_ms": tot_ms, "tot_n": tot_n,
-            "last": last, "drained": drained, "arena_res": arena_res, "host": host, "probe": probe}
+            "last": last, "drained": drained, "arena_res": arena_res, "host": host, "probe": probe,
+            "probe_raw": probe_raw}
 
 
 def k3_probe_stats(w):
@@ -411,9 +413,8 @@ def lifetime_leg(eng, arenas, offs, lens, R, B, lead, nfull, head, dist, gpu):
       lead            R / (R - lead): batches resident but not in K3
     plus the step's excess over K3's launch (the scan loop)."""
     eng.set_k3_probe(True)
-    try:
-        steady(eng, arenas, offs, lens, R, 2, 2, dist, gpu)
-        w = eng.k3_wave_times().astype(np.int64)
+    try:  # the records of the last launch of the steps, a steady-state one (not the drain's)
+        w = steady(eng, arenas, offs, lens, R, 3, 3, dist, gpu)["probe_raw"].astype(np.int64)
     finally:
         eng.set_k3_probe(False)
     coop = w[w[:, 7] > 0]
@@ -431,8 +432,8 @@ def lifetime_leg(eng, arenas, offs, lens, R, B, lead, nfull, head, dist, gpu):
     floor_ms = nfull * K3_VALU_FLOOR_CYCLES / ghz * 1e-6
     busy = int((w[:, 1] & ((1 << 56) - 1) != 0).sum())
     return {
-        "source": "bench.py lifetime_leg: hbx_set_k3_probe over 2 steps after the timed window (full-slice waves, "
-                  "first group's cooperative phase)",
+        "source": "bench.py lifetime_leg: hbx_set_k3_probe, the last launch of 3 steady-state steps after the timed "
+                  "window (full-slice waves, first group's cooperative phase)",
         "cycles_per_block": round(cpb, 1), "clock_ghz": round(ghz, 4),
         "floor_cycles_per_block": K3_VALU_FLOOR_CYCLES, "full_slice_waves": int(len(full)),
         "staging": round(cpb / K3_VALU_FLOOR_CYCLES, 4),

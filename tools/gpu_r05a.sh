@@ -10,7 +10,8 @@ cat $O/k3_prod.txt
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q -k "producer" --timeout 120 --timeout-method thread > $O/pytest_k3p.log 2>&1 || { tail -30 $O/pytest_k3p.log; exit 1; }
 tail -2 $O/pytest_k3p.log
-for v in 0 1; do
-  HBX_AB=1 HBX_K3_PROD=$v timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --e2e-steps 0 --no-cpu-baseline > $O/bench20_p$v.json 2> $O/bench20_p$v.err || { tail -20 $O/bench20_p$v.err; exit 1; }
-  python3 -c "import json;d=json.load(open('$O/bench20_p$v.json'));print('prod=$v', d['value'], d['zipf']['value'], d['check_vs_oracle'], d['zipf']['check_vs_oracle'], d['roofline']['frac'], d['kernel_ms_per_step'], d.get('lifetime'), d['valu_roofline'].get('k1'))"
+for cfg in "0 1" "1 1" "1 2" "0 2"; do
+  set -- $cfg
+  HBX_AB=1 HBX_K3_PROD=$1 timeout -k 10 300 python bench.py --gpus 1 --steps 60 --warmup 5 --e2e-steps 0 --no-cpu-baseline --join-lag $2 > $O/bench_p$1_l$2.json 2> $O/bench_p$1_l$2.err || { tail -20 $O/bench_p$1_l$2.err; exit 1; }
+  python3 -c "import json;d=json.load(open('$O/bench_p$1_l$2.json'));print('prod=$1 lag=$2', d['value'], d['zipf']['value'], d['check_vs_oracle'], d['zipf']['check_vs_oracle'], d['roofline']['frac'], d['kernel_ms_per_step'], d.get('lifetime'), d['valu_roofline'].get('k1'))"
 done

@@ -101,6 +101,45 @@ __global__ __launch_bounds__(512, 1) void k3_prod(const uint64_t* __restrict__ a
   }
 }
 
+// ------------------------------------------------------------ floors --
+// The MD5 wave's cost without the memory side: `cons` hashes the LDS stages
+// (4 ds_read_b128 per block, k3p_consume) with every stage published up front
+// and no producer; `valu` compresses blocks from registers only (the bare
+// VALU chain of the compiled md5_compress).  Digests are not compared.
+template <int MODE>
+__global__ __launch_bounds__(256, 1) void k3_floor(const uint64_t* __restrict__ addr, uint32_t R,
+                                                    u32x4* __restrict__ out, uint64_t* __restrict__ stamps) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4][kCoopWaveLds];
+  __shared__ uint32_t flags[4][2];
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t lane = threadIdx.x & 63u;
+  if (threadIdx.x < 8u) flags[threadIdx.x >> 1][threadIdx.x & 1u] = (threadIdx.x & 1u) ? 0u : 0x7fffffffu;
+  for (uint32_t i = threadIdx.x; i < 4u * kCoopWaveLds / 4u; i += 256u)
+    reinterpret_cast<uint32_t*>(&lds[0][0])[i] = i * 0x9e3779b9u;
+  __syncthreads();
+  const uint32_t gw = blockIdx.x * 4u + wave;
+  uint64_t* st = stamps + 8u * gw;
+  __builtin_amdgcn_s_setprio(3);
+  uint32_t h[4];
+  md5_init(h);
+  h[0] ^= (uint32_t)addr[64u * gw + lane];
+  stamp(st, 0);
+  if constexpr (MODE == 0) {
+    k3p_consume(lds[wave], flags[wave], 0u, R, h);
+  } else {
+    uint32_t m[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) m[j] = h[j & 3] * (uint32_t)(j + 1);
+    for (uint32_t b = 0; b < R; b++) {
+      m[b & 15u] ^= b;  // (a runtime index: the block's words change every block)
+      md5_compress(h, m);
+    }
+  }
+  stamp(st, 1);
+  out[64u * gw + lane] = u32x4{h[0], h[1], h[2], h[3]};
+  if (lane == 0u) st[4] = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+}
+
 // ------------------------------------------------------------- streamer --
 // 1024-thread workgroups holding 128 KiB of (unused) LDS, like K1: they cannot
 // share a CU with a K3 workgroup.
@@ -164,9 +203,9 @@ int main(int argc, char** argv) {
   std::vector<uint64_t> hs(8ull * waves);
   printf("# %u chains x %u blocks (%.2f GB per launch), buffer %.0f GiB, %u workgroups\n", S, R,
          64.0 * R * S / 1e9, big / 1073741824.0, wgs);
-  printf("# kernel, beside, ms, GB/s, clock_GHz(med), cycles_per_block(med wave), p10, p90, simds_ok\n");
-  const char* names[] = {"base", "prod_p0", "prod_p2"};
-  for (int kind = 0; kind < 3; kind++) {
+  printf("# kernel, beside, ms, GB/s, clock_GHz(med), cycles_per_block(med wave), p10, p90, workgroups whose MD5 waves hold 4 distinct SIMDs\n");
+  const char* names[] = {"base", "prod_p0", "prod_p2", "floor_cons", "floor_valu"};
+  for (int kind = 0; kind < 5; kind++) {
     for (int beside = 0; beside < 2; beside++) {
       float best = 1e30f;
       for (int r = 0; r < reps; r++) {
@@ -177,8 +216,12 @@ int main(int argc, char** argv) {
           hipLaunchKernelGGL(k3_base, dim3(wgs), dim3(256), 0, sk, d_addr, R, o, d_st);
         else if (kind == 1)
           hipLaunchKernelGGL(k3_prod<0>, dim3(wgs), dim3(512), 0, sk, d_addr, R, o, d_st);
-        else
+        else if (kind == 2)
           hipLaunchKernelGGL(k3_prod<2>, dim3(wgs), dim3(512), 0, sk, d_addr, R, o, d_st);
+        else if (kind == 3)
+          hipLaunchKernelGGL(k3_floor<0>, dim3(wgs), dim3(256), 0, sk, d_addr, R, o, d_st);
+        else
+          hipLaunchKernelGGL(k3_floor<1>, dim3(wgs), dim3(256), 0, sk, d_addr, R, o, d_st);
         CK(hipGetLastError());
         CK(hipEventRecord(e1, sk));
         if (beside) {
@@ -202,17 +245,21 @@ int main(int argc, char** argv) {
           cpb.push_back(cyc / R);
           clk.push_back(cyc / rt * 0.1);
         }
-        const uint32_t hw = (uint32_t)s[4], simd = (hw >> 4) & 3u;
-        if (kind == 0 ? simd == (w & 3u) : simd == (w & 3u) && (((uint32_t)s[5] >> 4) & 3u) == simd) simd_ok++;
+      }
+      // the MD5 waves of each workgroup on four distinct SIMDs (HW_ID)
+      for (uint32_t wg = 0; wg < wgs; wg++) {
+        uint32_t m = 0;
+        for (uint32_t k = 0; k < 4u; k++) m |= 1u << (((uint32_t)hs[8ull * (4u * wg + k) + 4] >> 4) & 3u);
+        simd_ok += m == 15u ? 1 : 0;
       }
       std::sort(cpb.begin(), cpb.end());
       std::sort(clk.begin(), clk.end());
       auto q = [](const std::vector<double>& v, double f) { return v.empty() ? 0.0 : v[(size_t)(f * (v.size() - 1))]; };
       printf("%s, %d, %.3f, %.1f, %.3f, %.1f, %.1f, %.1f, %d/%u\n", names[kind], beside, best,
-             64.0 * R * S / (best * 1e6), q(clk, 0.5), q(cpb, 0.5), q(cpb, 0.1), q(cpb, 0.9), simd_ok, waves);
+             64.0 * R * S / (best * 1e6), q(clk, 0.5), q(cpb, 0.5), q(cpb, 0.1), q(cpb, 0.9), simd_ok, wgs);
       fflush(stdout);
     }
-    if (kind > 0) {
+    if (kind > 0 && kind < 3) {
       std::vector<u32x4> a(S), b(S);
       CK(hipMemcpy(a.data(), d_outa, 16ull * S, hipMemcpyDeviceToHost));
       CK(hipMemcpy(b.data(), d_outb, 16ull * S, hipMemcpyDeviceToHost));
