@@ -1072,38 +1072,79 @@ __device__ __forceinline__ void k3p_publish(uint32_t* p, uint32_t v) {
 // from the producer's stages S, S+1, ..  Each block's 4 ds_read_b128 are
 // issued one block ahead (the next stage's first block once the producer has
 // published it), so the LDS latency hides behind a block of VALU; two
-// register sets alternate without copies.  A stage is freed once its last
-// block is hashed (its reads have returned: the block consumed them; LDS
-// operations of a wave execute in order, so the release needs no wait), except
-// the group's last stage (freed by the caller once the group is done).
+// register sets alternate without copies.
+//
+// The reads and their wait are hand-placed (inline asm): the compiler's own
+// wait counting loses track across this loop and waited for the block just
+// prefetched (lgkmcnt(3..0) before each block: ~140 of ~1,500 cycles per
+// block, tools/ubench/k3_prod floor_cons).  Here one asm issues block b+1's
+// 4 reads and then waits lgkmcnt(4): LDS operations of a wave complete in
+// order, so "at most the 4 just issued outstanding" means block b's reads have
+// landed, whatever older LDS operations (the flag poll, a release) the
+// compiler placed in between.  The asm takes block b's registers as in/out
+// operands, so no use of them moves above the wait.  No SMEM is issued inside
+// the loop (it would count in lgkmcnt out of order).
+//
+// A stage is freed once its last block is hashed (its reads have landed: the
+// block waited for them), except the group's last stage (freed by the caller
+// once the group is done).
 __device__ __forceinline__ void k3p_consume(uint8_t* wl, uint32_t* flags, uint32_t S, uint32_t Rr, uint32_t (&h)[4]) {
-  const uint8_t* base = wl + (threadIdx.x & 63u) * Coop<16>::Row;
-  auto rd4 = [&](uint32_t b, u32x4(&W)[4]) {
-    const uint8_t* p = base + ((S + (b >> 2)) & 1u) * Coop<16>::Half + 64u * (b & 3u);
-#pragma unroll
-    for (int i = 0; i < 4; i++) W[i] = *reinterpret_cast<const u32x4*>(p + 16 * i);
+  const uint32_t row = (uint32_t)(uintptr_t)(wl + (threadIdx.x & 63u) * Coop<16>::Row);  // LDS address
+  auto stage_at = [&](uint32_t k) { return row + ((S + k) & 1u) * Coop<16>::Half; };
+  // the 4 reads of a block into N, then wait until only those are outstanding:
+  // W (the block read before them) has landed
+  auto next_wait = [&](uint32_t a, u32x4(&N)[4], u32x4(&W)[4]) {
+    asm volatile(
+        "ds_read_b128 %0, %8\n\t"
+        "ds_read_b128 %1, %8 offset:16\n\t"
+        "ds_read_b128 %2, %8 offset:32\n\t"
+        "ds_read_b128 %3, %8 offset:48\n\t"
+        "s_waitcnt lgkmcnt(4)"
+        : "=&v"(N[0]), "=&v"(N[1]), "=&v"(N[2]), "=&v"(N[3]), "+v"(W[0]), "+v"(W[1]), "+v"(W[2]), "+v"(W[3])
+        : "v"(a)
+        : "memory");
   };
-  auto step = [&](uint32_t b, const u32x4(&W)[4], u32x4(&N)[4]) {
-    const uint32_t nb = b + 1u;
-    if (nb < Rr) {  // wave-uniform
-      if ((nb & 3u) == 0u) k3p_wait_ge(&flags[0], S + (nb >> 2) + 1u);
-      rd4(nb, N);
-    }
+  auto hash = [&](const u32x4(&W)[4]) {
     const uint32_t m[16] = {W[0].x, W[0].y, W[0].z, W[0].w, W[1].x, W[1].y, W[1].z, W[1].w,
                             W[2].x, W[2].y, W[2].z, W[2].w, W[3].x, W[3].y, W[3].z, W[3].w};
     md5_compress(h, m);
-    if ((nb & 3u) == 0u && nb < Rr) {  // stage (nb >> 2) - 1 is done
-      asm volatile("" ::: "memory");
-      if ((threadIdx.x & 63u) == 0u)
-        __hip_atomic_store(&flags[1], S + (nb >> 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
   };
+  const uint32_t nst = (4u * Rr + 15u) / 16u;  // >= 2 (Rr >= kCoopMinBudget - 1)
   u32x4 WA[4], WB[4];
   k3p_wait_ge(&flags[0], S + 1u);
-  rd4(0u, WA);
-  for (uint32_t b = 0; b < Rr; b += 2u) {
-    step(b, WA, WB);
-    if (b + 1u < Rr) step(b + 1u, WB, WA);
+  asm volatile(
+      "ds_read_b128 %0, %4\n\t"
+      "ds_read_b128 %1, %4 offset:16\n\t"
+      "ds_read_b128 %2, %4 offset:32\n\t"
+      "ds_read_b128 %3, %4 offset:48"
+      : "=&v"(WA[0]), "=&v"(WA[1]), "=&v"(WA[2]), "=&v"(WA[3])
+      : "v"(stage_at(0u))
+      : "memory");
+  // every stage but the last: 4 blocks, each prefetching the next (the 4th
+  // the next stage's first, once the producer has published that stage)
+  for (uint32_t k = 0; k + 1u < nst; k++) {
+    const uint32_t a0 = stage_at(k);
+    next_wait(a0 + 64u, WB, WA);
+    hash(WA);
+    next_wait(a0 + 128u, WA, WB);
+    hash(WB);
+    next_wait(a0 + 192u, WB, WA);
+    hash(WA);
+    k3p_wait_ge(&flags[0], S + k + 2u);
+    next_wait(stage_at(k + 1u), WA, WB);
+    hash(WB);
+    asm volatile("" ::: "memory");  // stage k is done (its reads have landed: the blocks waited for them)
+    if ((threadIdx.x & 63u) == 0u) __hip_atomic_store(&flags[1], S + k + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  // the last stage (1-4 blocks; its first is in WA): no prefetch
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(WA[0]), "+v"(WA[1]), "+v"(WA[2]), "+v"(WA[3]) : : "memory");
+  hash(WA);
+  const uint8_t* last = wl + (threadIdx.x & 63u) * Coop<16>::Row + ((S + nst - 1u) & 1u) * Coop<16>::Half;
+  for (uint32_t u = 1; 4u * (nst - 1u) + u < Rr; u++) {
+    u32x4 W[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) W[i] = *reinterpret_cast<const u32x4*>(last + 64u * u + 16u * i);
+    hash(W);
   }
 }
 
