@@ -190,6 +190,7 @@ struct hbx_ctx {
   int k2_own = -1;            // ensure_cut_stream: -1 = by join lag (HBX_K2_STREAM for A/B)
   uint32_t md5_wgs = 256;     // K3 grid: one 256-thread workgroup per CU (set from the device)
   uint32_t k3_prod = 0;       // K3P: a producer wave per MD5 wave (HBX_K3_PROD for A/B)
+  uint32_t plan_cut = 0;      // at join lag 2, preplan on the cut stream (mode 3; HBX_PLAN_CUT for A/B)
   uint32_t md5_slice = 16384; // K3 time slice: full MD5 blocks per chain per launch (0 = unlimited)
   // K1 gate (hbx_k1_gate): a batch's K1 waits until every workgroup of the K3
   // launch of the same submit has been dispatched.  k3_started counts K3
@@ -482,10 +483,19 @@ int ensure_plan_buffers(hbx_ctx* c, uint64_t extra);
 //   and the hash stream carries nothing but K3 launches.  At lag 2 the same
 //   schedule would make K1 j wait for K2 of batch j-1 (measured 1,575 GiB/s at
 //   8 files per GPU, vs 1,890 for mode 1).
+// * lag 2, mode 3 (preplan on the cut stream, c->plan_cut): the same preplan
+//   as mode 2, but on the cut stream, right behind batch j-1's K2 and K2r
+//   (whose chains it adds) and before batch j's K2: neither the scan stream
+//   nor the hash stream waits for it, and the hash stream carries nothing but
+//   K3 launches.
 int plan_mode_of(const hbx_ctx* c) {
+  if (c->join_lag == 2 && c->plan_cut && c->cstream != c->stream) return 3;
   return c->join_lag >= 3 ? 2 : c->join_lag == 2 ? 1 : 0;
 }
-hipStream_t plan_stream(const hbx_ctx* c) { return plan_mode_of(c) == 1 ? c->hstream : c->stream; }
+hipStream_t plan_stream(const hbx_ctx* c) {
+  const int m = plan_mode_of(c);
+  return m == 1 ? c->hstream : m == 3 ? c->cstream : c->stream;
+}
 
 // K2 + K2r get a stream of their own once the join lag allows it (or
 // HBX_K2_STREAM=1): K1 of the next batch then no longer queues behind this
@@ -696,7 +706,8 @@ int md5_step(hbx_ctx* c, uint32_t budget, bool drain = false) {
 // the FIFO yet, hence the + 1).  Nothing is planned when no chain would be in
 // flight; the next submit then plans inline.
 int preplan(hbx_ctx* c, uint32_t budget) {
-  if (plan_mode_of(c) != 2 || c->preplanned || c->hstream == c->stream) return HBX_OK;
+  const int mode = plan_mode_of(c);
+  if ((mode != 2 && mode != 3) || c->preplanned || c->hstream == c->stream) return HBX_OK;
   Batch* nb = nullptr;
   if (!c->unjoined.empty() && c->unjoined.size() + 1 >= c->join_lag && c->join_lag >= 2) nb = c->unjoined.front();
   bool live = nb != nullptr;
@@ -1203,6 +1214,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = ab_env("HBX_K1_GATE")) c->k1_gate = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_LEAN_MARKS")) c->lean_marks = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_PROD")) c->k3_prod = std::atoi(v) ? 1u : 0u;
+  if (const char* v = ab_env("HBX_PLAN_CUT")) c->plan_cut = std::atoi(v) ? 1u : 0u;
   // (tests: a K3 grid of a few workgroups, so every wave takes many groups)
   if (const char* v = ab_env("HBX_K3_WGS")) c->md5_wgs = (uint32_t)std::min<int>(std::max(1, ncu), std::max(1, std::atoi(v)));
   if (hipSetDevice(device) != hipSuccess || make_stream(&c->stream, "HBX_SCAN_CUS", ncu, "0:4096") != hipSuccess) {

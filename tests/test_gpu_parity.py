@@ -298,9 +298,10 @@ def test_pipelined_batches_time_sliced(oracle, md5_slice, join_lag):
 
 
 @pytest.mark.parametrize("prod", ["0", "1"])
-@pytest.mark.parametrize("md5_slice,join_lag,wgs", [(9, 1, 0), (64, 3, 0), (4096, 1, 0), (4096, 2, 0), (16384, 1, 0),
-                                                    (0, 1, 0), (64, 1, 1), (4096, 1, 2), (0, 3, 1)])
-def test_k3_producer_waves(oracle, monkeypatch, md5_slice, join_lag, wgs, prod):
+@pytest.mark.parametrize("md5_slice,join_lag,wgs,plan_cut", [
+    (9, 1, 0, "0"), (64, 3, 0, "0"), (4096, 1, 0, "0"), (4096, 2, 0, "0"), (16384, 1, 0, "0"), (0, 1, 0, "0"),
+    (64, 1, 1, "0"), (4096, 1, 2, "0"), (0, 3, 1, "0"), (4096, 2, 0, "1"), (64, 2, 0, "1"), (9, 2, 1, "1")])
+def test_k3_producer_waves(oracle, monkeypatch, md5_slice, join_lag, wgs, plan_cut, prod):
     """K3 with and without a producer wave per MD5 wave (hbx_k3p_block_md5 /
     hbx_k3_block_md5, HBX_K3_PROD): the stages a producer hands over through
     the LDS counters, groups on the lane path (slices below 8 blocks), groups
@@ -308,16 +309,20 @@ def test_k3_producer_waves(oracle, monkeypatch, md5_slice, join_lag, wgs, prod):
     groups per wave (more groups than waves at small slices), a deep
     pipeline and a forced drain, with the probe on for one batch; bit-exact.
     wgs > 0 shrinks the K3 grid to that many workgroups (HBX_K3_WGS), so each
-    MD5 wave and its producer walk many groups in one launch."""
+    MD5 wave and its producer walk many groups in one launch.  plan_cut: at
+    join lag 2 the next launch is planned ahead on the cut stream (mode 3)."""
     from hashbox_amd import Engine
     monkeypatch.setenv("HBX_AB", "1")
     monkeypatch.setenv("HBX_K3_PROD", prod)
+    monkeypatch.setenv("HBX_PLAN_CUT", plan_cut)
     if wgs:
         monkeypatch.setenv("HBX_K3_WGS", str(wgs))
     batches = _device_batches(oracle, 3, 71 + md5_slice % 5)
     got, order = [], []
     with Engine(0, md5_slice=md5_slice, join_lag=join_lag) as e:
-        assert e.knobs()["k3_prod"] == int(prod) and (not wgs or e.knobs()["md5_wgs"] == wgs)
+        k = e.knobs()
+        assert k["k3_prod"] == int(prod) and (not wgs or k["md5_wgs"] == wgs)
+        assert k["plan_mode"] == (3 if plan_cut == "1" else {1: 0, 2: 1}.get(join_lag, 2)), k
         for i in [0, 1, 2, 0, 2, 1, 1, 0, 2, 2, 0, 1]:
             dev, offs, sizes, _ = batches[i]
             e.submit_device(dev.data_ptr(), offs, sizes)
