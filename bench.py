@@ -566,8 +566,11 @@ def residency_plan(files, file_mib, world, rank, scaling="strong", free_bytes=0,
     nf = len(lens)
     # small per-GPU batches (strong scaling) are scan-latency-bound at lag 1:
     # lag 3 plans each launch a step ahead (tools/gpu_pipe_sweep.sh: 8 files
-    # 1,576 -> 1,976 GiB/s, 16 files 1,752 -> 2,185); at 64 files lag 1 is best
-    lag = join_lag if join_lag > 0 else (3 if nf < 64 else 1)
+    # 1,576 -> 1,976 GiB/s, 16 files 1,752 -> 2,185).  At 64 files, since
+    # round 5, lag 2: with K3P the launch is shorter than the lag-1 scan loop
+    # (gate -> K1 -> K2 -> K2r -> plan), and at lag 2 the plan runs ahead on
+    # the cut stream (plan mode 3): 2,326 vs 2,280-2,292 GiB/s (profiles/r05f)
+    lag = join_lag if join_lag > 0 else (3 if nf < 64 else 2)
     ld = lead if lead >= 0 else lag + 1
     offs, total = W.pack_layout(lens)
     # launches a batch needs before its chains are all hashed

@@ -189,8 +189,13 @@ struct hbx_ctx {
   uint32_t k4_window = 1024;  // K4's LDS window of ids (HBX_K4_WINDOW, 1..1024: tests)
   int k2_own = -1;            // ensure_cut_stream: -1 = by join lag (HBX_K2_STREAM for A/B)
   uint32_t md5_wgs = 256;     // K3 grid: one 256-thread workgroup per CU (set from the device)
-  uint32_t k3_prod = 0;       // K3P: a producer wave per MD5 wave (HBX_K3_PROD for A/B)
-  uint32_t plan_cut = 0;      // at join lag 2, preplan on the cut stream (mode 3; HBX_PLAN_CUT for A/B)
+  // K3P: a producer wave per MD5 wave (HBX_K3_PROD=0 for the self-staging K3,
+  // A/B): 1,435 vs 1,586 cycles per block inside the bench schedule, +1.7 %
+  // (200 steps) and +2.9 % at 8 files per GPU (profiles/r05f)
+  uint32_t k3_prod = 1;
+  // at join lag 2, preplan on the cut stream (mode 3; HBX_PLAN_CUT=0: mode 1,
+  // the plan on the hash stream): +2.7 % with K3P (profiles/r05e)
+  uint32_t plan_cut = 1;
   uint32_t md5_slice = 16384; // K3 time slice: full MD5 blocks per chain per launch (0 = unlimited)
   // K1 gate (hbx_k1_gate): a batch's K1 waits until every workgroup of the K3
   // launch of the same submit has been dispatched.  k3_started counts K3

@@ -96,7 +96,7 @@ def test_residency_plan_per_world(world, scaling):
         assert P["need"] + P["join_lag"] <= P["R"], P
         assert P["B"] * P["need"] >= nfull
         assert P["hbm_bytes"] <= 0.95 * free
-        assert P["join_lag"] == (3 if P["files_per_gpu"] < 64 else 1)
+        assert P["join_lag"] == (3 if P["files_per_gpu"] < 64 else 2)
         seen.extend(P["mine"])
         host += bench.check_host_bytes(P)
     if scaling == "strong":

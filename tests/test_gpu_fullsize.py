@@ -1,11 +1,13 @@
 """GPU: the benchmark's operating point, bit-exact.  configs[1] (64 x 128 MiB
 random per batch) and a Zipf-duplicated 8 GiB corpus (configs[3] scheme, ~50 %
 repeats) run through exactly bench.py's pipelined schedule — hbx_reserve, the
-slice sized for 33 resident batches with lead 2 (4,229 blocks per chain per
-launch), fill to 33 in flight, then collect-one/submit-one — and every file of
-every collected batch is compared with the oracle's literal storeFile loop
-(store.go:111-196) on all host cores.  In-flight batches share three
-read-only arenas, so the exact steady-state schedule runs in 24 GiB of HBM."""
+slice sized for 33 resident batches with the default join lag 2 and lead 3
+(4,370 blocks per chain per launch; K3P and plan mode 3, the engine's
+defaults), fill to 33 in flight, then collect-one/submit-one — and every
+file of every collected batch is compared with the oracle's literal
+storeFile loop (store.go:111-196) on all host cores; configs[1] also at join
+lag 1, lead 2 (4,229 blocks).  In-flight batches share three read-only
+arenas, so the exact steady-state schedule runs in 24 GiB of HBM."""
 import os
 from collections import deque
 
@@ -34,15 +36,17 @@ def _oracle_of(oracle, arena, offs, lens):
     return refs
 
 
-def _run_schedule(arenas, offs, lens, steps, R=33, lead=2):
+def _run_schedule(arenas, offs, lens, steps, R=33, lag=2):
     """bench.py's steady(): R submitted before any collect, then collect the
     oldest + submit one; drain at the end.  Returns [(arena index, results)]."""
     import torch
     from hashbox_amd import Engine
     nfull = ((8 << 20) + 8) >> 6
-    B = -(-nfull // (R - lead))
+    B = -(-nfull // (R - (lag + 1)))
     out, order = [], deque()
-    with Engine(0, md5_slice=B) as e:
+    with Engine(0, md5_slice=B, join_lag=lag) as e:
+        k = e.knobs()
+        assert k["k3_prod"] == 1 and k["plan_mode"] == {1: 0, 2: 3}[lag], k
         e.reserve(R + 1, len(lens), int(sum(lens)))
         for j in range(steps):
             if len(order) >= R:
@@ -56,10 +60,11 @@ def _run_schedule(arenas, offs, lens, steps, R=33, lead=2):
             out.append((order.popleft(), e.wait()))
         torch.cuda.synchronize()
         ms2, n2 = e.stage_totals()
-    # one K3 launch per submit after the first (the lag of one step), plus
-    # the final drain: no forced drain happened inside the schedule
-    assert int(n[0]) == steps and int(n[3]) == steps - 1, (n, steps)
-    assert int(n2[3]) == steps, n2
+    # one K3 launch per submit after the first `lag` (a batch joins the launch
+    # `lag` submits after its own), plus the final drain: no forced drain
+    # happened inside the schedule
+    assert int(n[0]) == steps and int(n[3]) == steps - lag, (n, steps)
+    assert steps - lag < int(n2[3]) <= steps + 1, n2  # + the drain launch(es)
     return out
 
 
@@ -72,14 +77,15 @@ def _check(results, refs):
             assert g.content_type == (3 if r.n_chunks > 1 else 2)
 
 
-def test_configs1_full_size_steady_state(oracle):
+@pytest.mark.parametrize("lag", [2, 1])
+def test_configs1_full_size_steady_state(oracle, lag):
     import torch
     import workloads as W
     lens = [128 << 20] * 64
     offs, total = W.pack_layout(lens)
     arenas = W.random_arenas(3, total, 1000, torch.device("cuda", 0))
     refs = [_oracle_of(oracle, a, offs, lens) for a in arenas]
-    results = _run_schedule(arenas, offs, lens, steps=40)
+    results = _run_schedule(arenas, offs, lens, steps=40, lag=lag)
     assert len(results) == 40
     _check(results, refs)
     del arenas
