@@ -209,9 +209,12 @@ def test_configs4_hundred_thousand_files_on_disk(engine, oracle, big_tmp):
     assert total > 50e9, total  # BASELINE configs[4]: 100 k files, 4 KiB-4 MiB
     refs = oracle.store_batch_mt(datas, threads)
     plain = engine.store_paths(paths, sizes=sizes, batch_bytes=1 << 30)
-    for r, a in zip(refs, plain):
+    # the content id (store.go:187-196): the one chunk's id, else the chain
+    # block's id over the chunk ids (oracle chain_id, hashback.go:156-170)
+    cids = [r.ids[0].tobytes() if r.n_chunks == 1 else oracle.chain_id(r.ids) for r in refs]
+    for r, a, cid in zip(refs, plain, cids):
         _same(a, r)
-        assert a.content_id == r.content_id and a.content_type == r.content_type
+        assert a.content_type == (2 if r.n_chunks == 1 else 3) and a.content_id == cid
     del plain
     seen = []
 
@@ -226,9 +229,9 @@ def test_configs4_hundred_thousand_files_on_disk(engine, oracle, big_tmp):
         nxt += count
     assert nxt == n and len(seen) > 4
     single = 0
-    for r, b in zip(refs, comp):
+    for r, b, cid in zip(refs, comp, cids):
         _same(b, r)
-        assert b.content_id == r.content_id and b.content_type == r.content_type
+        assert b.content_id == cid and b.content_type == (2 if r.n_chunks == 1 else 3)
         assert len(b.zstreams) == r.n_chunks
         single += r.n_chunks == 1
     assert 0 < single < n
