@@ -11,3 +11,5 @@ timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 tail -1 $O/smoke.log
 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench20.json 2> $O/bench20.err || { tail -20 $O/bench20.err; exit 1; }
 python3 -c "import json;d=json.load(open('$O/bench20.json'));print(d['value'], d['zipf']['value'], d['check_vs_oracle'], d['zipf']['check_vs_oracle'], d['roofline']['frac'], d['valu_roofline'].get('k3'), d['valu_roofline'].get('k1'), 'e2e', d.get('e2e',{}).get('value'), d['cpu_baseline']['value'], d.get('lifetime'))"
+timeout -k 10 300 python tools/diag_slow_cu.py --steps 30 > $O/slow_cu.txt 2>&1 || { tail -20 $O/slow_cu.txt; exit 1; }
+tail -8 $O/slow_cu.txt
