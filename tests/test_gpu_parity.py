@@ -21,6 +21,18 @@ def _check(got, ref):
     assert got.content_id == ref.content_id
 
 
+def _check_mt(oracle, got, ref):
+    """Against oracle.store_batch_mt (cut ends and block ids only): the content
+    type and id follow store.go:187-196 (one chunk: its id; else the chain
+    block's id, oracle chain_id)."""
+    assert np.array_equal(got.cut_ends, ref.cut_ends), (got.cut_ends[:8], ref.cut_ends[:8])
+    assert np.array_equal(got.ids, ref.ids), "block ids differ"
+    k = ref.n_chunks
+    assert got.content_type == (0 if k == 0 else 2 if k == 1 else 3)
+    if k:
+        assert got.content_id == (ref.ids[0].tobytes() if k == 1 else oracle.chain_id(ref.ids))
+
+
 EDGE_SIZES = [0, 1, 5, 55, 56, 57, 63, 64, 65, 119, 120, 121, 4095, 4096, MIN - 1, MIN, MIN + 1,
               2 * MIN - 1, 2 * MIN, 2 * MIN + 1, 2 * MIN + 2, 3 * MIN + 17, MAXB - 1, MAXB,
               MAXB + 1, MAXB + 2 * MIN + 1, 2 * MAXB + 12345]
@@ -223,7 +235,7 @@ def test_store_paths_per_file_status(engine, oracle, tmp_path, compress):
             assert gg.errno == errno.ENOENT and gg.n_chunks == 0 and gg.content_type == 0
             continue
         assert gg.errno == 0
-        _check(gg, r)
+        _check_mt(oracle, gg, r)
         if compress:
             assert len(gg.zstreams) == r.n_chunks
     # without per-file status the same batch fails loudly, naming the file
@@ -242,7 +254,7 @@ def test_store_paths_per_file_status(engine, oracle, tmp_path, compress):
     got = engine.store_paths(paths[:20], sizes=sizes[:20], compress=compress, skip_unreadable=True)
     for r, gg in zip(refs[:20], got):
         assert gg.errno == 0
-        _check(gg, r)
+        _check_mt(oracle, gg, r)
 
 
 def _device_batches(oracle, nb, seed):
