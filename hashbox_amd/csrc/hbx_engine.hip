@@ -196,6 +196,10 @@ struct hbx_ctx {
   // at join lag 2, preplan on the cut stream (mode 3; HBX_PLAN_CUT=0: mode 1,
   // the plan on the hash stream): +2.7 % with K3P (profiles/r05e)
   uint32_t plan_cut = 1;
+  // K3Q: items per group (parts of each slice, handed out through a queue;
+  // 0 = off, K3P's static groups; HBX_K3_ITEMS for A/B)
+  uint32_t k3_items = 0;
+  PinBuf h_err;  // K3Q: set by a wave that gave up waiting for an item (never expected)
   uint32_t md5_slice = 16384; // K3 time slice: full MD5 blocks per chain per launch (0 = unlimited)
   // K1 gate (hbx_k1_gate): a batch's K1 waits until every workgroup of the K3
   // launch of the same submit has been dispatched.  k3_started counts K3
@@ -249,7 +253,7 @@ struct hbx_ctx {
   bool ssum_used[2] = {false, false};
   // K3 launch orders (triple-buffered by launch index % 3): plan j (scan
   // stream) writes order[j%3] from order[(j-1)%3]; K3 j (hash stream) reads it
-  DevBuf d_order[3], d_octl[3];
+  DevBuf d_order[3], d_octl[3], d_q[3];  // (+ K3Q's item queue per slot)
   hipEvent_t plan_done[3] = {nullptr, nullptr, nullptr};   // plan j%3 written
   hipEvent_t order_free[3] = {nullptr, nullptr, nullptr};  // K3 that read slot j%3 done
   bool order_used[3] = {false, false, false};
@@ -636,7 +640,18 @@ int md5_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
     c->k3_open.push_back(L);
   }
   const uint32_t waves = c->md5_wgs * (kK3Threads / 64);
-  if (c->k3_prod)
+  const uint32_t parts = c->k3_items && budget != kBudgetAll && budget >= 64u * c->k3_items ? c->k3_items : 0u;
+  if (parts && !c->h_err.p) {
+    HBX_TRY(c, c->h_err.ensure(64));
+    std::memset(c->h_err.p, 0, 64);
+  }
+  if (parts)
+    hipLaunchKernelGGL(hbx_k3q_block_md5, dim3(c->md5_wgs), dim3(kK3PThreads), 0, s,
+                       c->d_order[slot].as<OrderEntry>(), static_cast<const uint32_t*>(c->d_octl[slot].as<uint32_t>()),
+                       budget, c->d_gate.as<uint32_t>(), c->k3_dispatched, c->k3_waves + waves - 1u, tslot,
+                       c->h_probe.p ? c->h_probe.as<uint64_t>() : nullptr, c->d_octl[slot].as<uint32_t>() + 1,
+                       c->d_q[slot].as<uint64_t>(), (uint32_t)(L + 1), parts, c->h_err.as<uint32_t>());
+  else if (c->k3_prod)
     hipLaunchKernelGGL(hbx_k3p_block_md5, dim3(c->md5_wgs), dim3(kK3PThreads), 0, s,
                        c->d_order[slot].as<OrderEntry>(), static_cast<const uint32_t*>(c->d_octl[slot].as<uint32_t>()),
                        budget, c->d_gate.as<uint32_t>(), c->k3_dispatched, c->k3_waves + waves - 1u, tslot,
@@ -740,6 +755,7 @@ int ensure_plan_buffers(hbx_ctx* c, uint64_t extra) {
   const int slot = (int)(c->launches % 3);
   int rc = ensure_shared(c, c->d_order[slot], bound * sizeof(OrderEntry));
   if (!rc) rc = ensure_shared(c, c->d_octl[slot], 256);
+  if (!rc) rc = ensure_shared(c, c->d_q[slot], (bound / 64 + 2) * 8 * 8);  // groups x up to 8 parts
   if (!rc) rc = ensure_shared(c, c->d_plan, 2 * kPlanBins * sizeof(uint32_t));
   return rc;
 }
@@ -1128,6 +1144,12 @@ int wait_oldest(hbx_ctx* c) {
     if (c->launches == l0 || k > 2) return c->fail(HBX_ERR_STATE, "drain launched nothing (internal)");
   }
   HBX_TRY(c, hipEventSynchronize(b->ev[4]));
+  if (c->h_err.p && *static_cast<volatile uint32_t*>(c->h_err.p)) {  // a K3Q wave gave up: results wrong
+    c->pending.pop_front();
+    c->parked.push_back(b);
+    c->broken = true;
+    return c->fail(HBX_ERR_STATE, "K3 item queue: a wave timed out waiting for an item (internal); destroy the context");
+  }
   c->pending.pop_front();
   // ev[4] follows the K3 launch that finalized b (the result stream waited for it)
   if (b->joined) c->k3_done_upto = std::max<uint64_t>(c->k3_done_upto, b->final_launch + 1);
@@ -1220,6 +1242,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = ab_env("HBX_LEAN_MARKS")) c->lean_marks = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_PROD")) c->k3_prod = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_PLAN_CUT")) c->plan_cut = std::atoi(v) ? 1u : 0u;
+  if (const char* v = ab_env("HBX_K3_ITEMS")) c->k3_items = (uint32_t)std::min(8, std::max(0, std::atoi(v)));
   // (tests: a K3 grid of a few workgroups, so every wave takes many groups)
   if (const char* v = ab_env("HBX_K3_WGS")) c->md5_wgs = (uint32_t)std::min<int>(std::max(1, ncu), std::max(1, std::atoi(v)));
   if (hipSetDevice(device) != hipSuccess || make_stream(&c->stream, "HBX_SCAN_CUS", ncu, "0:4096") != hipSuccess) {
@@ -1260,7 +1283,7 @@ void hbx_ctx_destroy(hbx_ctx* c) {
                        c->plan_done[2], c->order_free[0], c->order_free[1], c->order_free[2]})
     if (e) (void)hipEventDestroy(e);
   for (DevBuf* b : {&c->d_ssum[0], &c->d_ssum[1], &c->d_order[0], &c->d_order[1], &c->d_order[2],
-                    &c->d_octl[0], &c->d_octl[1], &c->d_octl[2], &c->d_gate,
+                    &c->d_octl[0], &c->d_octl[1], &c->d_octl[2], &c->d_q[0], &c->d_q[1], &c->d_q[2], &c->d_gate,
                     &c->d_stage, &c->d_msg, &c->d_plan, &c->d_vdesc, &c->d_vlinks,
                     &c->d_vout, &c->d_vexp, &c->d_zeros, &c->d_zblk, &c->d_zinfo, &c->d_zoff,
                     &c->d_zlen, &c->d_zout, &c->d_zimg, &c->d_idesc, &c->d_ires, &c->d_sreg, &c->d_sstart,
@@ -1280,6 +1303,7 @@ void hbx_ctx_destroy(hbx_ctx* c) {
   }
   c->h_k3t.release();
   c->h_probe.release();
+  c->h_err.release();
   for (DevBuf& d : c->d_ring) d.release();
   for (hipEvent_t e : c->h2d_done)
     if (e) (void)hipEventDestroy(e);
@@ -1330,9 +1354,9 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
       out, (size_t)cap,
       "{\"ab_env\": %d, \"md5_slice\": %u, \"join_lag\": %u, \"tile_iters\": %u, \"k1_gate\": %u, "
       "\"md5_wgs\": %u, \"plan_mode\": %d, \"k2_own\": %d, \"k4_window\": %u, \"k3_probe\": %d, "
-      "\"lean_marks\": %u, \"k3_prod\": %u, \"k8_split_streams\": %llu, \"k8_split_fallbacks\": %llu}",
+      "\"lean_marks\": %u, \"k3_prod\": %u, \"k3_items\": %u, \"k8_split_streams\": %llu, \"k8_split_fallbacks\": %llu}",
       (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_gate, c->md5_wgs,
-      plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks, c->k3_prod,
+      plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks, c->k3_prod, c->k3_items,
       (unsigned long long)c->k8_split_streams, (unsigned long long)c->k8_split_fallbacks);
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }
@@ -1400,6 +1424,7 @@ int hbx_reserve(hbx_ctx* c, uint32_t batches, uint64_t files, uint64_t bytes) {
   for (int t = 0; t < 3 && !rc; t++) {
     rc = ensure_shared(c, c->d_order[t], ((uint64_t)batches * caps + 64) * sizeof(OrderEntry));
     if (!rc) rc = ensure_shared(c, c->d_octl[t], 256);
+    if (!rc) rc = ensure_shared(c, c->d_q[t], (((uint64_t)batches * caps + 64) / 64 + 2) * 8 * 8);
   }
   if (rc) return rc;
   std::vector<Batch*> ready;

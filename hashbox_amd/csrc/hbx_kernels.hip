@@ -1019,7 +1019,11 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
     for (uint32_t wv = 0; wv < (tid >> 6); wv++) before += wsum[wv];
     const uint32_t mine = hist[tid];
     pos[tid] = before + inc - v + (mine ? atomicAdd(&gh[kPlanBins + tid], mine) : 0u);
-    if (blockIdx.x == 0 && tid == kPlanThreads - 1) *n_out = before + inc;
+    if (blockIdx.x == 0 && tid == kPlanThreads - 1) {
+      *n_out = before + inc;
+      n_out[1] = 0u;  // K3Q's item queue head and tail for this order slot
+      n_out[2] = 0u;
+    }
   }
   __syncthreads();
   for (uint32_t e = gt; e < n_all; e += gn) {
@@ -1203,6 +1207,151 @@ __device__ __forceinline__ uint32_t k3p_produce(uint8_t* wl, uint32_t* flags, ui
   return nst;
 }
 
+// ----------------------------------------------------------- K3 items --
+// K3Q (hbx_k3q_block_md5): the launch's work is cut into items (g, h), part h
+// of P of group g's slice (at most ceil(budget / P) blocks of each chain),
+// handed out dynamically: every wave takes the next item from a queue, and
+// finishing (g, h) queues (g, h+1).  A chain still advances exactly min(rem,
+// budget) blocks per launch (the planner's and the engine's schedule are
+// unchanged), but its slice may continue on another CU: a CU that runs slow
+// (which one varies launch by launch, tools/diag_slow_cu.py) no longer holds
+// its groups' whole slices, only the part it is on, and the launch's tail
+// shrinks from a slow CU's full slice to about one part.  The queue lives in
+// the order slot's control words (octl[1] head, octl[2] tail, zeroed by the
+// plan) and q[] (entries tagged with the launch, so no clearing); a part's
+// chain states reach the next CU through an agent-scope release (the MD5 wave
+// after its stores) and acquire (the wave that takes the next part).
+constexpr uint32_t kItemExit = 0xFFFFFFFFu;
+constexpr uint32_t kItemSpinTicks = 20000000u;  // 200 ms of s_memrealtime: a lost push, never a normal wait
+
+// One lane's share of a work unit: its chain (or, for a lane with nothing to
+// hash in it, a shadow chain with >= R blocks, whose data it reads and
+// discards), and the blocks it hashes.
+struct K3Lane {
+  Chain* chp;
+  const uint8_t* src;  // chain bytes the lane reads (its own, or the shadow's)
+  uint32_t next;       // first block of `src` the cooperative phase starts from (after the prologue block)
+  uint32_t len, b0, cnt;
+  bool finish, live;   // finish: tail blocks + id; live: its chain state is written back
+  uint32_t h[4];
+};
+template <bool ITEMS>
+__device__ __forceinline__ K3Lane k3_lane(const OrderEntry* __restrict__ order, uint32_t n_total, uint32_t g,
+                                          uint32_t part, uint32_t budget, uint32_t per_part) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t k = 64u * g + lane;
+  const bool active = k < n_total;
+  K3Lane L;
+  if constexpr (!ITEMS) {
+    // idle lanes stay alive for the wave-wide loop bound: they run an empty
+    // slice over the group's first chain and store nothing
+    L.chp = reinterpret_cast<Chain*>(order[active ? k : 64u * g].chain);
+    const Chain ch = *L.chp;
+    L.len = active ? ch.len : 0u;
+    L.b0 = active ? ch.next : 0u;
+    L.cnt = active ? chain_cnt(L.len, L.b0, budget) : 0u;
+    L.finish = active && L.b0 + L.cnt == ((L.len + 8u) >> 6);
+    L.live = active;
+    L.src = reinterpret_cast<const uint8_t*>(ch.src);
+    L.next = ch.next;
+    L.h[0] = ch.h[0];
+    L.h[1] = ch.h[1];
+    L.h[2] = ch.h[2];
+    L.h[3] = ch.h[3];
+  } else {
+    const OrderEntry o = order[active ? k : 64u * g];
+    L.chp = reinterpret_cast<Chain*>(o.chain);
+    const Chain ch = *L.chp;
+    const uint32_t nfull = (ch.len + 8u) >> 6;
+    // this launch's slice of the chain: the planner's rem (1 + blocks left
+    // before the launch) and the budget; part `part` of it
+    const uint32_t total = min(o.rem - 1u, budget);
+    const uint32_t start = nfull - (o.rem - 1u);
+    const uint64_t lo64 = (uint64_t)part * per_part;
+    const uint32_t lo = lo64 < total ? (uint32_t)lo64 : total;
+    const uint32_t hi = (uint64_t)lo + per_part < total ? lo + per_part : total;
+    const uint32_t last = total ? (total - 1u) / per_part : 0u;  // the part that finishes it
+    L.live = active && part <= last && ch.next != kChainDone;
+    L.len = L.live ? ch.len : 0u;
+    L.b0 = L.live ? ch.next : 0u;  // == start + lo
+    L.cnt = L.live ? hi - lo : 0u;
+    L.finish = L.live && part == last && start + total == nfull;
+    (void)start;
+    L.src = reinterpret_cast<const uint8_t*>(ch.src);
+    L.next = ch.next;
+    L.h[0] = ch.h[0];
+    L.h[1] = ch.h[1];
+    L.h[2] = ch.h[2];
+    L.h[3] = ch.h[3];
+    // lanes with nothing to hash here shadow the lane with the most blocks
+    // (a lane that only finishes -- its tail blocks, no full block -- keeps
+    // its own chain, and k3_wave_R then sends the wave down the lane path)
+    const uint32_t mx = wave_max_all(L.cnt);
+    if (mx) {
+      const int Ls = __builtin_ctzll(__builtin_amdgcn_ballot_w64(L.cnt == mx));
+      const uint64_t sa = reinterpret_cast<uint64_t>(L.src);
+      const uint64_t ss = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(sa >> 32), Ls) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sa, Ls);
+      const uint32_t ns = (uint32_t)__builtin_amdgcn_readlane((int)L.next, Ls);
+      if (L.cnt == 0u && !L.finish) {
+        L.src = reinterpret_cast<const uint8_t*>(ss);
+        L.next = ns;
+      }
+    }
+  }
+  return L;
+}
+// R = the wave's smallest count over the lanes that hash: all 64 chains
+// advance R blocks together through page-local cooperative loads (the others
+// shadow a chain with >= R blocks), then each lane its own remainder
+template <bool ITEMS>
+__device__ __forceinline__ uint32_t k3_wave_R(const K3Lane& L) {
+  if constexpr (!ITEMS) return ~wave_max_all(L.live ? ~L.cnt : 0u);
+  // items: over the lanes that hash here (a lane that only finishes counts
+  // with 0: the lane path); none at all -> 0
+  const uint32_t m = wave_max_all((L.cnt || L.finish) ? ~L.cnt : 0u);
+  return m ? ~m : 0u;
+}
+
+// The MD5 wave takes the launch's next item (lane 0, broadcast); items
+// [0, G) are the groups' first parts, later ones come from q as parts finish.
+__device__ __forceinline__ uint32_t k3q_pop(uint32_t* __restrict__ qc, const uint64_t* __restrict__ q, uint32_t G,
+                                            uint32_t total, uint32_t tag, uint32_t* __restrict__ err) {
+  uint32_t item = kItemExit;
+  if ((threadIdx.x & 63u) == 0u) {
+    const uint32_t sl = __hip_atomic_fetch_add(&qc[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (sl < G) {
+      item = sl;
+    } else if (sl < total) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      for (;;) {
+        const uint64_t v = __hip_atomic_load(&q[sl - G], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(v >> 32) == tag) {
+          item = (uint32_t)v;
+          break;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)kItemSpinTicks) {  // never expected: stop, report
+          if (err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+  }
+  item = (uint32_t)__builtin_amdgcn_readlane((int)item, 0);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the chain states the item's last part stored
+  return item;
+}
+// After a part's chain states are stored: make them visible, queue the next part.
+__device__ __forceinline__ void k3q_push(uint32_t* __restrict__ qc, uint64_t* __restrict__ q, uint32_t tag,
+                                         uint32_t item) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  if ((threadIdx.x & 63u) == 0u) {
+    const uint32_t t = __hip_atomic_fetch_add(&qc[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&q[t], ((uint64_t)tag << 32) | item, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // The producer wave of pair `flags`: the same groups as its MD5 wave; for a
 // group on the cooperative path (R >= kCoopMinBudget), the stages of blocks
 // next+1 .. next+R-1 of its 64 chains, two register sets in flight.
@@ -1218,15 +1367,45 @@ __device__ void k3p_producer(uint8_t* wl, uint32_t* flags, const OrderEntry* __r
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (clamped re-reads of the last stage)
 }
+// K3Q's producer: the items its MD5 wave announces (flags[2] = item, flags[3]
+// = items announced), until kItemExit.
+__device__ void k3q_producer(uint8_t* wl, uint32_t* flags, const OrderEntry* __restrict__ order,
+                             const uint32_t* __restrict__ n_order, uint32_t budget, uint32_t parts,
+                             uint32_t per_part) {
+  const uint32_t n_total = *n_order;
+  const uint32_t G = (n_total + 63u) / 64u;
+  uint32_t S = 0;
+  for (uint32_t seq = 1;; seq++) {
+    k3p_wait_ge(&flags[3], seq);
+    const uint32_t item = (uint32_t)__builtin_amdgcn_readfirstlane((int)k3p_flag(&flags[2]));
+    if (item == kItemExit) break;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const K3Lane L = k3_lane<true>(order, n_total, item % G, item / G, budget, per_part);
+    const uint32_t R = k3_wave_R<true>(L);
+    if (R < kCoopMinBudget) continue;  // the MD5 wave takes the lane path
+    S += k3p_produce(wl, flags, S, reinterpret_cast<uint64_t>(L.src) + 64ull * (L.next + 1u) - 8ull, R - 1u);
+  }
+  (void)parts;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 
 // One wave's share of a K3 launch (VGPR + AGPR, no scratch).  `wl` = this
 // wave's LDS.  PROD: a producer wave feeds the cooperative stages (K3P,
 // `flags` = the pair's counters); else the wave loads and stages them itself.
-template <bool PROD>
+// ITEMS (K3Q, with PROD): the work comes as items from the launch's queue
+// (`qc`, `q`, `tag`; `parts` per group) instead of groups g0, g0 + nwaves, ..
+struct K3Queue {
+  uint32_t* qc;
+  uint64_t* q;
+  uint32_t tag, parts;
+  uint32_t* err;
+};
+template <bool PROD, bool ITEMS = false>
 __device__ __forceinline__ void k3_body(
     uint8_t* wl, const OrderEntry* __restrict__ order, const uint32_t* __restrict__ n_order, uint32_t budget,
     uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last, uint64_t* __restrict__ tslot,
-    uint64_t* __restrict__ probe, uint32_t* flags = nullptr) {
+    uint64_t* __restrict__ probe, uint32_t* flags = nullptr, K3Queue Q = K3Queue{}) {
+  static_assert(PROD || !ITEMS, "items need the producer waves");
   // the MD5 chains are issue-bound: win the SIMD's issue arbitration against
   // co-resident waves of other kernels
   __builtin_amdgcn_s_setprio(3);
@@ -1239,7 +1418,6 @@ __device__ __forceinline__ void k3_body(
     const uint32_t tk = __hip_atomic_fetch_add(started, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     if (tslot && tk == t_first) tslot[0] = __builtin_amdgcn_s_memrealtime();
   }
-  const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t n_total = *n_order;
   const uint32_t groups = (n_total + 63u) / 64u;
@@ -1251,34 +1429,41 @@ __device__ __forceinline__ void k3_body(
   // (Dealing the groups round-robin over ceil(groups / 4) workgroups rounded
   // to a multiple of the 8 XCDs, to even out K3's CUs per XCD, mixed long and
   // short waves on every CU: K3 3.52 -> 3.41 ms but K1 3.25 -> 3.54 ms beside
-  // it, 2,235 -> 2,091 GiB/s at 33 resident batches.)
+  // it, 2,235 -> 2,091 GiB/s at 33 resident batches.)  K3Q keeps the same
+  // waves busy (the first `groups` of them) and hands them items instead.
   const uint32_t g0 = blockIdx.x * (kK3Threads / 64) + wave;
+  const uint32_t per_part = ITEMS ? (budget == kBudgetAll ? kBudgetAll : (budget + Q.parts - 1u) / Q.parts) : 0u;
   // diagnostics (hbx_set_k3_probe): per wave its start, the end of its first
   // group's start-up (loads + prologue), its end, R and the largest count
   const uint64_t pt0 = probe ? __builtin_amdgcn_s_memrealtime() : 0ull;
   uint64_t pt1 = 0ull, pc1 = 0ull, pc2 = 0ull, pt2 = 0ull;  // + the first group's cooperative phase, in cycles
   uint32_t pR = 0u, pmax = 0u;
   uint32_t S = 0;  // PROD: stages of this launch so far (the producer counts the same)
-  for (uint32_t g = g0; g < groups; g += nwaves) {
-    const uint32_t k = 64u * g + lane;
-    const bool active = k < n_total;
-    // idle lanes stay alive for the wave-wide loop bound: they run an empty
-    // slice over the group's first chain and store nothing
-    Chain* __restrict__ chp = reinterpret_cast<Chain*>(order[active ? k : 64u * g].chain);
-    const Chain ch = *chp;
-    const uint32_t len = active ? ch.len : 0u;
-    const uint32_t b0 = active ? ch.next : 0u;
-    const uint32_t cnt = active ? chain_cnt(len, b0, budget) : 0u;
-    const bool finish = active && b0 + cnt == ((len + 8u) >> 6);
-    uint32_t h[4] = {ch.h[0], ch.h[1], ch.h[2], ch.h[3]};
-    const uint8_t* src = reinterpret_cast<const uint8_t*>(ch.src);
-    // R = the wave's smallest count: all 64 chains advance R blocks together
-    // through page-local cooperative loads (idle lanes shadow the group's
-    // first chain, whose count is >= R), then each lane its own remainder
-    const uint32_t R = ~wave_max_all(active ? ~cnt : 0u);
+  uint32_t seq = 0;  // ITEMS: items announced to the producer
+  bool first = true;
+  for (uint32_t g = g0;; g += nwaves) {
+    uint32_t part = 0u, item = 0u;
+    if constexpr (ITEMS) {
+      item = g0 < groups ? k3q_pop(Q.qc, Q.q, groups, groups * Q.parts, Q.tag, Q.err) : kItemExit;
+      if ((threadIdx.x & 63u) == 0u) {  // announce it to the producer (kItemExit: it stops too)
+        __hip_atomic_store(&flags[2], item, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      k3p_publish(&flags[3], ++seq);
+      if (item == kItemExit) break;
+      g = item % groups;
+      part = item / groups;
+    } else {
+      if (g >= groups) break;
+    }
+    K3Lane L = k3_lane<ITEMS>(order, n_total, g, part, budget, per_part);
+    uint32_t(&h)[4] = L.h;
+    const uint8_t* src = L.src;
+    const uint32_t len = L.len, b0 = L.b0, cnt = L.cnt;
+    const bool finish = L.finish;
+    const uint32_t R = k3_wave_R<ITEMS>(L);
     if (R >= kCoopMinBudget) {  // wave-uniform
-      md5_block_at(src, ch.len, h, ch.next);  // every lane now at a block >= 1
-      if (probe && g == g0) {
+      md5_block_at(src, len, h, L.next);  // every lane now at a block >= 1
+      if (probe && first) {
         pt1 = __builtin_amdgcn_s_memrealtime();
         pc1 = __builtin_amdgcn_s_memtime();
         pR = R;
@@ -1288,9 +1473,9 @@ __device__ __forceinline__ void k3_body(
         k3p_consume(wl, flags, S, R - 1u, h);
         S += (4u * (R - 1u) + 15u) / 16u;
       } else {
-        md5_coop<16>(wl, src, h, ch.next + 1u, R - 1u);
+        md5_coop<16>(wl, src, h, L.next + 1u, R - 1u);
       }
-      if (probe && g == g0) {
+      if (probe && first) {
         pc2 = __builtin_amdgcn_s_memtime();
         pt2 = __builtin_amdgcn_s_memrealtime();
       }
@@ -1299,19 +1484,19 @@ __device__ __forceinline__ void k3_body(
       // while the others shadow the first of them and discard (the lane-mode
       // path would take ~1.5x per block, and such a wave was the launch's
       // last by 120 us: bench --k3-probe).
-      uint32_t pos = b0 + R, rem = active ? cnt - R : 0u;
+      uint32_t pos = b0 + R, rem = cnt ? cnt - R : 0u;
       for (int round = 0; round < 4; round++) {
         const uint32_t mx = wave_max_all(rem ? ~rem : 0u);
         if (mx == 0u || ~mx < kCoopMinBudget) break;  // wave-uniform
         const uint32_t R2 = ~mx;
-        const bool part = rem != 0u;
-        const int L = __builtin_ctzll(__builtin_amdgcn_ballot_w64(part));
-        const uint64_t s_sh = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(reinterpret_cast<uint64_t>(src) >> 32), L) << 32) |
-                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)reinterpret_cast<uint64_t>(src), L);
-        const uint32_t p_sh = (uint32_t)__builtin_amdgcn_readlane((int)pos, L);
+        const bool part_ = rem != 0u;
+        const int Lr = __builtin_ctzll(__builtin_amdgcn_ballot_w64(part_));
+        const uint64_t s_sh = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(reinterpret_cast<uint64_t>(src) >> 32), Lr) << 32) |
+                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)reinterpret_cast<uint64_t>(src), Lr);
+        const uint32_t p_sh = (uint32_t)__builtin_amdgcn_readlane((int)pos, Lr);
         uint32_t hk[4] = {h[0], h[1], h[2], h[3]};
-        md5_coop<16>(wl, part ? src : reinterpret_cast<const uint8_t*>(s_sh), hk, part ? pos : p_sh, R2);
-        if (part) {
+        md5_coop<16>(wl, part_ ? src : reinterpret_cast<const uint8_t*>(s_sh), hk, part_ ? pos : p_sh, R2);
+        if (part_) {
           h[0] = hk[0];
           h[1] = hk[1];
           h[2] = hk[2];
@@ -1326,12 +1511,16 @@ __device__ __forceinline__ void k3_body(
       md5_run<PROD ? 4 : HBX_MD5_RING>(src, len, h, b0, cnt, finish);
     }
     if (finish) {
-      *(__attribute__((address_space(1))) u32x4*)ch.out = u32x4{h[0], h[1], h[2], h[3]};
-      chp->next = kChainDone;
-    } else if (active) {
-      *reinterpret_cast<uint4*>(&chp->h[0]) = make_uint4(h[0], h[1], h[2], h[3]);
-      chp->next = b0 + cnt;
+      *(__attribute__((address_space(1))) u32x4*)L.chp->out = u32x4{h[0], h[1], h[2], h[3]};
+      L.chp->next = kChainDone;
+    } else if (L.live && (!ITEMS || cnt)) {
+      *reinterpret_cast<uint4*>(&L.chp->h[0]) = make_uint4(h[0], h[1], h[2], h[3]);
+      L.chp->next = b0 + cnt;
     }
+    if constexpr (ITEMS) {
+      if (part + 1u < Q.parts) k3q_push(Q.qc, Q.q, Q.tag, item + groups);
+    }
+    first = false;
   }
   if (probe && (threadIdx.x & 63u) == 0u) {
     uint64_t* p = probe + 8u * (blockIdx.x * (kK3Threads / 64) + wave);
@@ -1387,6 +1576,32 @@ extern "C" __global__ __launch_bounds__(kK3PThreads, 1) void hbx_k3p_block_md5(
   } else {
     __builtin_amdgcn_s_setprio(2);
     k3p_producer(k3_lds[pair], k3_flags[pair], order, n_order, budget, blockIdx.x * 4u + pair, gridDim.x * 4u);
+  }
+}
+
+// K3Q: K3P with the launch's work handed out as items (parts of a group's
+// slice) through a queue (see k3q_pop).  qc = the order slot's head and tail
+// (octl + 1, zeroed by the plan), q its entries, tag = launch index + 1,
+// parts = items per group (>= 1), err = a word set if a wave ever gave up
+// waiting for an item (never expected; the results are then wrong).
+extern "C" __global__ __launch_bounds__(kK3PThreads, 1) void hbx_k3q_block_md5(
+    const OrderEntry* __restrict__ order, const uint32_t* __restrict__ n_order, uint32_t budget,
+    uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last, uint64_t* __restrict__ tslot,
+    uint64_t* __restrict__ probe, uint32_t* __restrict__ qc, uint64_t* __restrict__ q, uint32_t tag, uint32_t parts,
+    uint32_t* __restrict__ err) {
+  __shared__ __attribute__((aligned(16))) uint8_t k3_lds[4][kK3WaveLds];
+  __shared__ uint32_t k3_flags[4][4];  // [pair]: stages written, stages freed, item, items announced
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t pair = wave & 3u;
+  if (threadIdx.x < 16u) k3_flags[threadIdx.x >> 2][threadIdx.x & 3u] = 0u;
+  __syncthreads();
+  if (wave < 4u) {
+    k3_body<true, true>(k3_lds[pair], order, n_order, budget, started, t_first, t_last, tslot, probe, k3_flags[pair],
+                        K3Queue{qc, q, tag, parts, err});
+  } else {
+    __builtin_amdgcn_s_setprio(2);
+    const uint32_t per_part = budget == kBudgetAll ? kBudgetAll : (budget + parts - 1u) / parts;
+    k3q_producer(k3_lds[pair], k3_flags[pair], order, n_order, budget, parts, per_part);
   }
 }
 

@@ -309,7 +309,7 @@ def test_pipelined_batches_time_sliced(oracle, md5_slice, join_lag):
         assert n[3] >= 1 and ms[3] > 0
 
 
-@pytest.mark.parametrize("prod", ["0", "1"])
+@pytest.mark.parametrize("prod", ["0", "1", "q2", "q4"])
 @pytest.mark.parametrize("md5_slice,join_lag,wgs,plan_cut", [
     (9, 1, 0, "0"), (64, 3, 0, "0"), (4096, 1, 0, "0"), (4096, 2, 0, "0"), (16384, 1, 0, "0"), (0, 1, 0, "0"),
     (64, 1, 1, "0"), (4096, 1, 2, "0"), (0, 3, 1, "0"), (4096, 2, 0, "1"), (64, 2, 0, "1"), (9, 2, 1, "1")])
@@ -321,11 +321,14 @@ def test_k3_producer_waves(oracle, monkeypatch, md5_slice, join_lag, wgs, plan_c
     groups per wave (more groups than waves at small slices), a deep
     pipeline and a forced drain, with the probe on for one batch; bit-exact.
     wgs > 0 shrinks the K3 grid to that many workgroups (HBX_K3_WGS), so each
-    MD5 wave and its producer walk many groups in one launch.  plan_cut: at
+    MD5 wave and its producer walk many groups in one launch.  q2/q4: K3Q,
+    each slice in 2 / 4 items handed out through the launch's queue (a
+    chain's slice continues on another wave, possibly another CU).  plan_cut: at
     join lag 2 the next launch is planned ahead on the cut stream (mode 3)."""
     from hashbox_amd import Engine
     monkeypatch.setenv("HBX_AB", "1")
-    monkeypatch.setenv("HBX_K3_PROD", prod)
+    monkeypatch.setenv("HBX_K3_PROD", "0" if prod == "0" else "1")
+    monkeypatch.setenv("HBX_K3_ITEMS", prod[1:] if prod.startswith("q") else "0")
     monkeypatch.setenv("HBX_PLAN_CUT", plan_cut)
     if wgs:
         monkeypatch.setenv("HBX_K3_WGS", str(wgs))
@@ -333,7 +336,8 @@ def test_k3_producer_waves(oracle, monkeypatch, md5_slice, join_lag, wgs, plan_c
     got, order = [], []
     with Engine(0, md5_slice=md5_slice, join_lag=join_lag) as e:
         k = e.knobs()
-        assert k["k3_prod"] == int(prod) and (not wgs or k["md5_wgs"] == wgs)
+        assert k["k3_prod"] == (prod != "0") and (not wgs or k["md5_wgs"] == wgs)
+        assert k["k3_items"] == (int(prod[1:]) if prod.startswith("q") else 0)
         assert k["plan_mode"] == (3 if plan_cut == "1" else {1: 0, 2: 1}.get(join_lag, 2)), k
         for i in [0, 1, 2, 0, 2, 1, 1, 0, 2, 2, 0, 1]:
             dev, offs, sizes, _ = batches[i]
