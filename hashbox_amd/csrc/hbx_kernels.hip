@@ -1261,7 +1261,12 @@ __device__ __forceinline__ K3Lane k3_lane(const OrderEntry* __restrict__ order, 
   } else {
     const OrderEntry o = order[active ? k : 64u * g];
     L.chp = reinterpret_cast<Chain*>(o.chain);
-    const Chain ch = *L.chp;
+    Chain ch = *L.chp;
+    // the fields a previous part (maybe on another CU or XCD) stored: loaded
+    // past the non-coherent caches (agent-scope atomics), no cache-wide fence
+    ch.next = __hip_atomic_load(&L.chp->next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int i = 0; i < 4; i++) ch.h[i] = __hip_atomic_load(&L.chp->h[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t nfull = (ch.len + 8u) >> 6;
     // this launch's slice of the chain: the planner's rem (1 + blocks left
     // before the launch) and the budget; part `part` of it
@@ -1325,7 +1330,7 @@ __device__ __forceinline__ uint32_t k3q_pop(uint32_t* __restrict__ qc, const uin
     } else if (sl < total) {
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       for (;;) {
-        const uint64_t v = __hip_atomic_load(&q[sl - G], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t v = __hip_atomic_load(&q[sl - G], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if ((uint32_t)(v >> 32) == tag) {
           item = (uint32_t)v;
           break;
@@ -1338,17 +1343,18 @@ __device__ __forceinline__ uint32_t k3q_pop(uint32_t* __restrict__ qc, const uin
       }
     }
   }
-  item = (uint32_t)__builtin_amdgcn_readlane((int)item, 0);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the chain states the item's last part stored
-  return item;
+  return (uint32_t)__builtin_amdgcn_readlane((int)item, 0);
 }
-// After a part's chain states are stored: make them visible, queue the next part.
+// After a part's chain states are stored (agent-scope atomic stores, drained
+// here): queue the next part.  (Agent-scope fences instead write back and
+// invalidate the XCD's whole L2 per part: K3 3.45 -> 3.56 ms at 4 parts,
+// 3.79 at 8, profiles/r05h.)
 __device__ __forceinline__ void k3q_push(uint32_t* __restrict__ qc, uint64_t* __restrict__ q, uint32_t tag,
                                          uint32_t item) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // (flat stores count in both)
   if ((threadIdx.x & 63u) == 0u) {
     const uint32_t t = __hip_atomic_fetch_add(&qc[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&q[t], ((uint64_t)tag << 32) | item, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&q[t], ((uint64_t)tag << 32) | item, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1379,7 +1385,6 @@ __device__ void k3q_producer(uint8_t* wl, uint32_t* flags, const OrderEntry* __r
     k3p_wait_ge(&flags[3], seq);
     const uint32_t item = (uint32_t)__builtin_amdgcn_readfirstlane((int)k3p_flag(&flags[2]));
     if (item == kItemExit) break;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     const K3Lane L = k3_lane<true>(order, n_total, item % G, item / G, budget, per_part);
     const uint32_t R = k3_wave_R<true>(L);
     if (R < kCoopMinBudget) continue;  // the MD5 wave takes the lane path
@@ -1510,12 +1515,23 @@ __device__ __forceinline__ void k3_body(
     } else {
       md5_run<PROD ? 4 : HBX_MD5_RING>(src, len, h, b0, cnt, finish);
     }
-    if (finish) {
-      *(__attribute__((address_space(1))) u32x4*)L.chp->out = u32x4{h[0], h[1], h[2], h[3]};
-      L.chp->next = kChainDone;
-    } else if (L.live && (!ITEMS || cnt)) {
-      *reinterpret_cast<uint4*>(&L.chp->h[0]) = make_uint4(h[0], h[1], h[2], h[3]);
-      L.chp->next = b0 + cnt;
+    if constexpr (!ITEMS) {
+      if (finish) {
+        *(__attribute__((address_space(1))) u32x4*)L.chp->out = u32x4{h[0], h[1], h[2], h[3]};
+        L.chp->next = kChainDone;
+      } else if (L.live) {
+        *reinterpret_cast<uint4*>(&L.chp->h[0]) = make_uint4(h[0], h[1], h[2], h[3]);
+        L.chp->next = b0 + cnt;
+      }
+    } else {  // the next part may run on another CU: agent-scope stores (see k3_lane)
+      if (finish) {
+        *(__attribute__((address_space(1))) u32x4*)L.chp->out = u32x4{h[0], h[1], h[2], h[3]};
+        __hip_atomic_store(&L.chp->next, kChainDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else if (L.live && cnt) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) __hip_atomic_store(&L.chp->h[i], h[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&L.chp->next, b0 + cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     if constexpr (ITEMS) {
       if (part + 1u < Q.parts) k3q_push(Q.qc, Q.q, Q.tag, item + groups);
