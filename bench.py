@@ -85,7 +85,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md), GB/s
 GIB = 1 << 30
 KNAMES = ["k1_digest_scan", "k2_cut_chain", "k2c_chain_plan", "k3_block_md5", "k4_content_id"]
 KERNEL_OF = {"k1_digest_scan": "hbx_k1_digest_scan_dma", "k2_cut_chain": "hbx_k2_cut_chain",
-             "k2c_chain_plan": "hbx_k2c_plan", "k3_block_md5": "hbx_k3_block_md5",
+             "k2c_chain_plan": "hbx_k2c_plan", "k3_block_md5": "hbx_k3p_block_md5",  # K3P, the default since round 5
              "k4_content_id": "hbx_k4_content_id"}
 
 

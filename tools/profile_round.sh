@@ -16,7 +16,8 @@ KT=$(find $OUT/trace -name "*kernel_trace.csv" | head -1)
 KS=$(find $OUT/trace -name "*kernel_stats.csv" | head -1)
 cp $KS $OUT/kernel_stats.csv
 python3 tools/trace_timed.py $KT $OUT/bench_under_trace.json > $OUT/timed_stats.txt
-python3 tools/window_timeline.py $KT 200 --seg=0:20 --seg=20:100 --seg=100:200 >> $OUT/timed_stats.txt
+LAG=$(python3 -c "import json;print(json.load(open('$OUT/bench_under_trace.json'))['config']['join_lag'])")
+python3 tools/window_timeline.py $KT 200 --seg=0:20 --seg=20:100 --seg=100:200 --lag=$LAG >> $OUT/timed_stats.txt
 cat $OUT/timed_stats.txt
 timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "hbx_" --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py --steps 100 --warmup 2 --workload random --no-cpu-baseline --no-check --e2e-steps 0 > $OUT/pmc_fetch.log 2>&1 || { tail -5 $OUT/pmc_fetch.log; exit 1; }
 python3 tools/pmc_traffic.py $(find $OUT/pmc_fetch -name "*counter_collection.csv" | head -1) $OUT/${TAG}_traffic.json > /dev/null

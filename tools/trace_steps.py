@@ -14,7 +14,7 @@ first = int(sys.argv[2]) if len(sys.argv) > 2 else -20
 n = int(sys.argv[3]) if len(sys.argv) > 3 else 4
 ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0],
              r.get("Queue_Id", r.get("Stream_Id", ""))) for r in rows)
-k3 = [e for e in ev if e[2] == "hbx_k3_block_md5"]
+k3 = [e for e in ev if e[2] in ("hbx_k3_block_md5", "hbx_k3p_block_md5", "hbx_k3q_block_md5")]
 a, b = k3[first][0], k3[first + n][1] if first + n < 0 or first + n < len(k3) else k3[-1][1]
 t0 = a
 for s, e, name, q in ev:

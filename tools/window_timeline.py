@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-step timeline of bench.py's timed window from a rocprofv3 kernel trace.
 
-usage: python tools/window_timeline.py <kernel_trace.csv> <steps> [--all] [--seg a:b ...]
+usage: python tools/window_timeline.py <kernel_trace.csv> <steps> [--all] [--seg a:b ...] [--lag L]
 
 The bench (one workload, e.g. --workload random) ends with one drain K3
 launch after the window, so the window holds the last `steps` K1 launches
@@ -23,10 +23,11 @@ def spans(*names):
                   if r["Kernel_Name"].split("(")[0] in names)
 
 
-k3 = spans("hbx_k3_block_md5")
+LAG = next((int(a.split("=", 1)[1]) for a in sys.argv if a.startswith("--lag=")), 1)  # drain launches after the window
+k3 = spans("hbx_k3_block_md5", "hbx_k3p_block_md5", "hbx_k3q_block_md5")
 k2 = spans("hbx_k2_cut_chain")
 k1 = spans("hbx_k1_digest_scan_dma", "hbx_k1_digest_scan_lite", "hbx_k1_digest_scan")
-w3 = k3[-(K + 1):-1]
+w3 = k3[-(K + LAG):-LAG]
 w1 = k1[-K:]
 w2 = k2[-K:]
 t0 = w1[0][0]
