@@ -117,6 +117,10 @@ def parse():
     ap.add_argument("--join-lag", type=int, default=0,
                     help="submits between a batch's own and the K3 launch its chains join "
                          "(hbx_set_join_lag; 0 = auto: 3 below 64 files per GPU, else 1)")
+    ap.add_argument("--k3-period", type=int, default=0,
+                    help="one K3 launch every P submits with P x the slice (hbx_set_k3_period, 1..8; 0 = auto: "
+                         "1 at 64 or more files per GPU, else the largest of 8, 4, 2 up to 64 / files that "
+                         "divides --steps)")
     ap.add_argument("--lead", type=int, default=-1,
                     help="steps an arena stays resident beyond the launches its batch needs: R = launches "
                          "per batch + lead (-1 = join lag + 1).  Lead = join lag is the least that lets the next "
@@ -271,12 +275,14 @@ def path_roofline(alg_bps, batch_bytes):
 
 
 # -------------------------------------------------------------- pipeline --
-def lane_occupancy(arena_res, R, B, need, lanes):
+def lane_occupancy(arena_res, R, B, need, lanes, period=1):
     """Chains in flight per steady-state K3 launch, from the collected cut
     lists: batch x is in its t-th launch (t < need) in launch x + t, and a
     chunk of `nfull` full message blocks is still in the order list then iff
     t == 0 or nfull > t * B (K2c drops it after the launch that finishes it).
-    Launch m holds batches m, m-1, .., m-need+1 (arena (m - t) % R)."""
+    Launch m holds batches m, m-1, .., m-need+1 (arena (m - t) % R).  With a
+    K3 period P, B is the launch's budget and P batches join each launch:
+    launch m holds the P arenas (mP - tP - q) % R, q < P, in their t-th."""
     per_arena = []
     for i in range(R):
         res = arena_res.get(i)
@@ -286,7 +292,8 @@ def lane_occupancy(arena_res, R, B, need, lanes):
                              for r in res if r.n_chunks] or [np.zeros(0, np.int64)])
         per_arena.append([int(nf.size) if t == 0 else int(np.count_nonzero(nf > t * B))
                           for t in range(need)])
-    active = [sum(per_arena[(m - t) % R][t] for t in range(need)) for m in range(R)]
+    active = [sum(per_arena[(m * period - t * period - q) % R][t] for t in range(need) for q in range(period))
+              for m in range(R)]
     return {"active_chains_mean": round(float(np.mean(active)), 1), "active_chains_max": int(max(active)),
             "lanes": lanes, "occupancy_mean": round(float(np.mean(active)) / lanes, 4),
             "occupancy_max": round(max(active) / lanes, 4)}
@@ -401,7 +408,7 @@ K3_VALU_FLOOR_CYCLES = 320 * SIMD_CYCLES_PER_VALU  # one MD5 block's 320 VALU at
 K1_CYCLES_PER_VALU_4W = 4.20
 
 
-def lifetime_leg(eng, arenas, offs, lens, R, B, lead, nfull, head, dist, gpu):
+def lifetime_leg(eng, arenas, offs, lens, R, B, lead, nfull, head, dist, gpu, period=1):
     """Where a batch's lifetime goes (verdict r04 item 3), from a short
     probed run after the timed window (hbx_set_k3_probe: per-wave s_memtime /
     s_memrealtime stamps around the first group's cooperative phase; the
@@ -411,10 +418,12 @@ def lifetime_leg(eng, arenas, offs, lens, R, B, lead, nfull, head, dist, gpu):
       staging         cycles per block / the 1,312 of 320 VALU at 4.1 cycles
       launch_overhead K3's average launch / (B x cycles per block / clock)
       lead            R / (R - lead): batches resident but not in K3
-    plus the step's excess over K3's launch (the scan loop)."""
+    plus the step's excess over K3's launch (the scan loop).  With a K3
+    period P, B is the launch's budget (P x the slice), a launch spans P
+    steps, and a batch waits up to P - 1 more submits to join."""
     eng.set_k3_probe(True)
     try:  # the records of the last launch of the steps, a steady-state one (not the drain's)
-        w = steady(eng, arenas, offs, lens, R, 3, 3, dist, gpu)["probe_raw"].astype(np.int64)
+        w = steady(eng, arenas, offs, lens, R, max(3, period), max(3, period), dist, gpu)["probe_raw"].astype(np.int64)
     finally:
         eng.set_k3_probe(False)
     coop = w[w[:, 7] > 0]
@@ -438,8 +447,8 @@ def lifetime_leg(eng, arenas, offs, lens, R, B, lead, nfull, head, dist, gpu):
         "floor_cycles_per_block": K3_VALU_FLOOR_CYCLES, "full_slice_waves": int(len(full)),
         "staging": round(cpb / K3_VALU_FLOOR_CYCLES, 4),
         "launch_overhead": round(launch_ms / hashing_ms, 4),
-        "lead": round(R / max(1, R - lead), 4),
-        "step_over_launch": round(step_ms / launch_ms, 4),
+        "lead": round(R / max(1, R - lead - period + 1), 4),
+        "step_over_launch": round(step_ms * period / launch_ms, 4),
         "lifetime_ms": round(R * step_ms, 2), "serial_floor_ms": round(floor_ms, 2),
         "lifetime_over_floor": round(R * step_ms / floor_ms, 4),
         "k3_busy_waves": busy,
@@ -455,7 +464,7 @@ def max_over_ranks(x, dist, dev, op="max"):
 
 
 def run_workload(a, name, eng, arenas, offs, lens, R, B, need, lanes, dist, gpu, dev, world, rank,
-                 job_batch_bytes, check_threads, before_submit=None):
+                 job_batch_bytes, check_threads, before_submit=None, period=1):
     """One steady-state measurement; returns the JSON fields of its line.
     `gpu` is this rank's device, `dev` the device of the reductions."""
     r = steady(eng, arenas, offs, lens, R, a.steps, a.warmup, dist, gpu, before_submit,
@@ -463,16 +472,17 @@ def run_workload(a, name, eng, arenas, offs, lens, R, B, need, lanes, dist, gpu,
     el = max_over_ranks(r["el"], dist, dev)
     tot_ms, tot_n = r["tot_ms"], r["tot_n"]
     k1_n, k3_n = int(tot_n[0]), int(tot_n[3])
-    window_exact = k1_n == a.steps and k3_n == a.steps
+    # one K3 launch per `period` submits (a.steps is a multiple of the period)
+    window_exact = k1_n == a.steps and k3_n * period == a.steps
     if not window_exact:
         raise RuntimeError(f"{name}: timed window holds {k1_n} K1 and {k3_n} K3 launches, expected "
-                           f"{a.steps} each (a forced drain or an empty batch inside the window)")
+                           f"{a.steps} and {a.steps // period} (a forced drain or an empty batch inside the window)")
     rank_batch = int(sum(int(n) for n in lens))
     avg_ms = tot_ms / np.maximum(tot_n, 1)
     # dominant kernel: K3.  Algorithmic bytes per launch = the rank's batch
-    # bytes (one K3 launch per step advances every chain in flight; in steady
-    # state the chains hashed per launch add up to one batch), over the K3
-    # launches of the window only.
+    # bytes x the K3 period (one K3 launch per `period` steps advances every
+    # chain in flight; in steady state the chains hashed per launch add up to
+    # `period` batches), over the K3 launches of the window only.
     per_launch = a.steps * rank_batch / k3_n
     achieved = per_launch / (avg_ms[3] * 1e-3) / 1e9
     traffic, traffic_src = measured_traffic(KERNEL_OF["k3_block_md5"], per_launch, rank_batch)
@@ -528,7 +538,7 @@ def run_workload(a, name, eng, arenas, offs, lens, R, B, need, lanes, dist, gpu,
         # bytes the step actually reads (K1 + K3, PMC FETCH_SIZE) against the
         # spec peak, and the algorithmic rate against the two-read ceiling
         "path_roofline": path_roofline(a.steps * rank_batch / el, rank_batch),
-        "k3_lanes": lane_occupancy(r["arena_res"], R, B, need, lanes),
+        "k3_lanes": lane_occupancy(r["arena_res"], R, B * period, need, lanes, period),
         "kernel_ms_per_step": {n: round(float(v) / a.steps, 4) for n, v in zip(KNAMES, tot_ms)},
         "window_launches": {n: int(v) for n, v in zip(KNAMES, tot_n)},
         # host time per step inside the window (rank 0's): submit, and collect (incl. any wait)
@@ -546,7 +556,7 @@ ARENA_SLACK = 64 << 20  # per resident batch beyond its packed bytes (allocator 
 
 def residency_plan(files, file_mib, world, rank, scaling="strong", free_bytes=0, hbm_frac=0.95,
                    ranks_per_device=1, arenas=0, md5_slice=-1, join_lag=0, lead=-1, e2e=False,
-                   alias_depth=0):
+                   alias_depth=0, k3_period=0, steps=0):
     """The pipeline each rank runs, a pure function so the
     CPU tests can check it for N = 1..8.  Files of the job: `files` x
     `file_mib` MiB; strong scaling gives this rank its LPT share of each
@@ -554,7 +564,10 @@ def residency_plan(files, file_mib, world, rank, scaling="strong", free_bytes=0,
     R batches stay resident (as many as `hbm_frac` of the free HBM holds),
     each K3 launch advances every chain by B blocks, a batch needs `need`
     launches and its chains join `lag` submits after its own:
-    need + lag <= R keeps the window free of forced drains."""
+    need + lag <= R keeps the window free of forced drains.  With a K3 period
+    P (one launch every P submits, P x B blocks per chain each) a batch waits
+    up to lag + P - 1 submits to join and its launches are P submits apart:
+    need x P + lead + P - 1 <= R."""
     from hashbox_amd.shard import lpt_assign
     import workloads as W
     fbytes = file_mib << 20
@@ -572,29 +585,36 @@ def residency_plan(files, file_mib, world, rank, scaling="strong", free_bytes=0,
     # the cut stream (plan mode 3): 2,326 vs 2,280-2,292 GiB/s (profiles/r05f)
     lag = join_lag if join_lag > 0 else (3 if nf < 64 else 2)
     ld = lead if lead >= 0 else lag + 1
+    if k3_period > 0:
+        per = k3_period
+    else:  # small per-GPU batches: the launch's fixed start-up and tail once per P steps
+        per = next((p for p in (8, 4, 2) if p <= 64 // nf and (steps <= 0 or steps % p == 0)), 1) if nf < 64 else 1
     offs, total = W.pack_layout(lens)
     # launches a batch needs before its chains are all hashed
     nfull = (min(fbytes, 8 << 20) + 8) >> 6
     r_fit = max(ld + 1, int(free_bytes * hbm_frac / max(1, ranks_per_device)) // (total + ARENA_SLACK))
     if e2e:
         r_fit = min(r_fit, ld + 2)  # PCIe-bound: a shallow pipeline suffices
+    def slice_for(R):  # launches of P x B blocks, P submits apart, within R - lead - (P - 1) submits
+        launches = max(1, (R - ld - per + 1) // per)
+        return -(-nfull // (launches * per))
     if md5_slice < 0:
         R = arenas if arenas > 0 else r_fit
-        B = -(-nfull // max(1, R - ld))
+        B = slice_for(R)
     else:
         B = md5_slice
-        R = arenas if arenas > 0 else min((1 if B == 0 else -(-nfull // B)) + ld, r_fit)
+        R = arenas if arenas > 0 else min((1 if B == 0 else -(-nfull // (B * per))) * per + ld + per - 1, r_fit)
     physical = R
     if alias_depth > 0:  # diagnostics: D in flight over the R physical arenas
         R = alias_depth
         if md5_slice < 0:
-            B = -(-nfull // max(1, R - ld))
-    need = 1 if B == 0 else -(-nfull // B)
-    if need + lag > R:
-        raise ValueError(f"pipeline depth {R} < launches per batch {need} + join lag {lag}: raise --arenas "
-                         "or the slice")
+            B = slice_for(R)
+    need = 1 if B == 0 else -(-nfull // (B * per))  # K3 launches per batch
+    if need * per + lag + per - 1 > R:
+        raise ValueError(f"pipeline depth {R} < launches per batch {need} x period {per} + join lag {lag} + "
+                         f"{per - 1}: raise --arenas or the slice")
     return {"mine": mine, "lens": lens, "files_per_gpu": nf, "join_lag": lag, "lead": ld, "offs": offs,
-            "arena_bytes": total, "R": R, "physical_arenas": physical, "B": B, "need": need,
+            "arena_bytes": total, "R": R, "physical_arenas": physical, "B": B, "need": need, "k3_period": per,
             "hbm_bytes": physical * (total + ARENA_SLACK), "file_bytes": fbytes}
 
 
@@ -647,7 +667,8 @@ def main():
     if a.plan_only:
         P = S["plan"]
         mine = {"rank": rank, **{k: P[k] for k in ("files_per_gpu", "join_lag", "lead", "R", "physical_arenas",
-                                                   "B", "need", "hbm_bytes", "file_bytes", "arena_bytes")},
+                                                   "B", "need", "k3_period", "hbm_bytes", "file_bytes",
+                                                   "arena_bytes")},
                 "mine": P["mine"], "check_host_bytes": check_host_bytes(P)}
         plans = [mine]
         if dist:
@@ -673,7 +694,7 @@ def setup(a, rank, world, local_world, ndev, dev_idx, dev):
         torch.cuda.set_device(dev_idx)
         free, _ = torch.cuda.mem_get_info(dev)
     P = residency_plan(a.files, a.file_mib, world, rank, a.scaling, free, a.hbm_frac, share, a.arenas,
-                       a.md5_slice, a.join_lag, a.lead, a.e2e, a.alias_depth)
+                       a.md5_slice, a.join_lag, a.lead, a.e2e, a.alias_depth, a.k3_period, a.steps)
     if a.plan_only:
         return {"plan": P}
     from hashbox_amd import Engine
@@ -692,7 +713,7 @@ def setup(a, rank, world, local_world, ndev, dev_idx, dev):
         arenas = [arenas[i % P["physical_arenas"]] for i in range(R)]
     ballast = torch.zeros(int(a.ballast_gib * GIB), dtype=torch.uint8, device=dev) if a.ballast_gib else None
     torch.cuda.synchronize(dev)
-    eng = Engine(dev_idx, md5_slice=B, join_lag=lag)
+    eng = Engine(dev_idx, md5_slice=B, join_lag=lag, k3_period=P["k3_period"])
     if a.k3_probe:  # the probe alone (hbx_set_k3_probe), no other HBX_* switch
         eng.set_k3_probe(True)
     # every batch slot, chain table and summary buffer of the pipeline is
@@ -736,6 +757,7 @@ def e2e_leg(a, eng, arenas, offs, lens, P, lanes, dist, dev, red_dev, world, ran
         torch.from_numpy(host).copy_(arenas[0][:used])
         torch.cuda.synchronize(dev)
         eng.set_md5_slice(B_e)
+        eng.set_k3_period(1)  # PCIe-bound, shallow: one launch per step
 
         def before(i):
             eng.memcpy_h2d_async(arenas[i].data_ptr(), hp.value, used)
@@ -765,6 +787,7 @@ def run(a, S, rank, world, local_world, dist, dev, red_dev):
     P, eng, arenas, latency = S["plan"], S["eng"], S["arenas"], S["latency"]
     lens, offs, total = P["lens"], P["offs"], P["arena_bytes"]
     R, B, need, lag, lead, nf = P["R"], P["B"], P["need"], P["join_lag"], P["lead"], P["files_per_gpu"]
+    per = P["k3_period"]
     n_phys = P["physical_arenas"]
     fbytes = P["file_bytes"]
     cores, threads = S["cores"], S["threads"]
@@ -795,14 +818,14 @@ def run(a, S, rank, world, local_world, dist, dev, red_dev):
         if wl == "zipf":
             zipf_repeat = W.zipf_fill(arenas, int(offs[-1]) + lens[-1], a.seed + 4 + 7919 * rank)
         lines[wl] = run_workload(a, wl, eng, arenas, offs, lens, R, B, need, lanes, dist, dev, red_dev,
-                                 world, rank, job_batch, threads, before)
+                                 world, rank, job_batch, threads, before, per)
         if zipf_repeat is not None and wl == "zipf":
             lines[wl]["repeat_fraction"] = round(zipf_repeat, 4)
 
     life = None
     if not a.no_lifetime and a.alias_depth == 0 and not a.e2e:
         nfull = (min(fbytes, 8 << 20) + 8) >> 6
-        life = lifetime_leg(eng, arenas, offs, lens, R, B, lead, nfull, lines[workloads[0]], dist, dev)
+        life = lifetime_leg(eng, arenas, offs, lens, R, B * per, lead, nfull, lines[workloads[0]], dist, dev, per)
         if zipf_repeat is not None:  # the arenas hold the Zipf corpus now: the probe ran over it
             life["probed_over"] = "the Zipf arenas (MD5 cycles per block do not depend on the bytes)"
 
@@ -847,7 +870,7 @@ def run(a, S, rank, world, local_world, dist, dev, red_dev):
                                    else " on every GPU, each rank its own files)") if world > 1 else ")"),
                    "files_per_step": a.files, "files_per_gpu": nf, "file_bytes": fbytes,
                    "md5_slice_blocks": B, "pipeline_depth": R, "launches_per_batch": need,
-                   "scan_lead": lead, "join_lag": lag,
+                   "scan_lead": lead, "join_lag": lag, "k3_period": per,
                    "parallelism": f"file-sharded x{world} ({a.scaling} scaling; independent HIP streams, "
                                   "no data-path collective)",
                    "seeds": f"each rank generates its own share on its device: random arenas seed {a.seed} + "

@@ -33,7 +33,7 @@ EXPORTS = [
     "hbx_deflate_file_bound", "hbx_store_paths_z",
     "hbx_wire_encode_id", "hbx_wire_encode_block_header", "hbx_wire_parse",
     "hbx_verify_submit_device", "hbx_inflate_blocks_device", "hbx_store_paths_zcb", "hbx_after_stream",
-    "hbx_set_join_lag", "hbx_k3_wave_times", "hbx_input_after_oldest", "hbx_knobs",
+    "hbx_set_join_lag", "hbx_set_k3_period", "hbx_k3_wave_times", "hbx_input_after_oldest", "hbx_knobs",
     "hbx_input_fence", "hbx_set_k3_probe", "hbx_store_paths_status",
 ]
 # Functions returning something other than an int status.
@@ -125,6 +125,7 @@ def load() -> ctypes.CDLL:
     L.hbx_pending.argtypes = [P]
     L.hbx_set_md5_slice.argtypes = [P, ctypes.c_uint32]
     L.hbx_set_join_lag.argtypes = [P, ctypes.c_uint32]
+    L.hbx_set_k3_period.argtypes = [P, ctypes.c_uint32]
     L.hbx_input_after_oldest.argtypes = [P]
     L.hbx_input_fence.argtypes = [P, P]
     L.hbx_set_k3_probe.argtypes = [P, I]

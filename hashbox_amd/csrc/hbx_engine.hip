@@ -185,7 +185,13 @@ struct hbx_ctx {
   uint32_t join_lag = 1;      // hbx_set_join_lag
   // where and when K2c plans run follows from the join lag (plan_mode_of)
   bool preplanned = false;    // the plan of launch `launches` is enqueued (mode 2)
-  Batch* pre_nb = nullptr;    // the batch whose chains that plan adds
+  std::vector<Batch*> pre_nb; // the batches whose chains that plan adds
+  // K3 period (hbx_set_k3_period): one K3 launch every `k3_period` submits,
+  // with `k3_period` x the slice per chain, joining every batch old enough:
+  // the launch's fixed start-up and tail are paid once per period (small
+  // per-GPU batches, the N = 8 share of configs[2]).  k3_tick counts submits.
+  uint32_t k3_period = 1;
+  uint64_t k3_tick = 0;
   uint32_t k4_window = 1024;  // K4's LDS window of ids (HBX_K4_WINDOW, 1..1024: tests)
   int k2_own = -1;            // ensure_cut_stream: -1 = by join lag (HBX_K2_STREAM for A/B)
   uint32_t md5_wgs = 256;     // K3 grid: one 256-thread workgroup per CU (set from the device)
@@ -497,6 +503,12 @@ int ensure_plan_buffers(hbx_ctx* c, uint64_t extra);
 //   (whose chains it adds) and before batch j's K2: neither the scan stream
 //   nor the hash stream waits for it, and the hash stream carries nothing but
 //   K3 launches.
+// The blocks per chain of one K3 launch for a per-submit slice `budget`.
+uint32_t launch_budget(const hbx_ctx* c, uint32_t budget) {
+  if (budget == kBudgetAll || c->k3_period <= 1) return budget;
+  return (uint32_t)std::min<uint64_t>((uint64_t)budget * c->k3_period, kBudgetAll - 1);
+}
+
 int plan_mode_of(const hbx_ctx* c) {
   if (c->join_lag == 2 && c->plan_cut && c->cstream != c->stream) return 3;
   return c->join_lag >= 3 ? 2 : c->join_lag == 2 ? 1 : 0;
@@ -534,7 +546,7 @@ int flush_input_wait(hbx_ctx* c) {
   return HBX_OK;
 }
 
-int plan_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
+int plan_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
   hipStream_t s = plan_stream(c);
   const int slot = (int)(c->launches % 3), ps = (int)((c->launches + 2) % 3);
   int rc = ensure_plan_buffers(c, 0);  // nb (if any) is already in pending
@@ -548,11 +560,17 @@ int plan_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
   // list is not read at all (hbx_reserve may have reallocated it)
   bool has_prev = false;
   for (Batch* b : c->pending)
-    if (b != nb && b->joined && !b->finalized) has_prev = true;
+    if (b->joined && !b->finalized && std::find(nbs.begin(), nbs.end(), b) == nbs.end()) has_prev = true;
   has_prev = has_prev && c->launches > 0;
-  const bool fresh = nb && nb->n;
-  // the joining batch's chains come from K2r (cut stream) or K6p (scan stream)
-  if (fresh && !(s == c->stream && c->cstream == s)) HBX_TRY(c, hipStreamWaitEvent(s, nb->ev[2], 0));
+  FreshSet fs{};
+  for (Batch* nb : nbs) {
+    if (!nb->n) continue;
+    fs.f[fs.k] = nb->d_fresh.as<OrderEntry>();
+    fs.n[fs.k] = nb->d_fcnt.as<uint32_t>();
+    fs.k++;
+    // the joining batch's chains come from K2r (cut stream) or K6p (scan stream)
+    if (!(s == c->stream && c->cstream == s)) HBX_TRY(c, hipStreamWaitEvent(s, nb->ev[2], 0));
+  }
   // the plan stream changed (hbx_set_join_lag): the trailing bin fill queued on
   // the old one must not land inside this plan
   if (c->plan_zeroed_on && c->plan_zeroed_on != s) {
@@ -571,9 +589,7 @@ int plan_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
         hipLaunchKernelGGL(hbx_k2c_plan, dim3(kPlanGroups), dim3(kPlanThreads), 0, s,
                            has_prev ? c->d_order[ps].as<OrderEntry>() : nullptr,
                            has_prev ? c->d_octl[ps].as<uint32_t>() : nullptr, c->last_budget,
-                           fresh ? nb->d_fresh.as<OrderEntry>() : nullptr,
-                           fresh ? nb->d_fcnt.as<uint32_t>() : nullptr, budget,
-                           c->d_order[slot].as<OrderEntry>(), c->d_octl[slot].as<uint32_t>(),
+                           fs, budget, c->d_order[slot].as<OrderEntry>(), c->d_octl[slot].as<uint32_t>(),
                            c->d_plan.as<uint32_t>(), phase);
       HBX_TRY(c, hipGetLastError());
       HBX_TRY(c, hipEventRecord(t.b, s));
@@ -601,9 +617,7 @@ int plan_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
       hipLaunchKernelGGL(hbx_k2c_plan, dim3(kPlanGroups), dim3(kPlanThreads), 0, s,
                          has_prev ? c->d_order[ps].as<OrderEntry>() : nullptr,
                          has_prev ? c->d_octl[ps].as<uint32_t>() : nullptr, c->last_budget,
-                         fresh ? nb->d_fresh.as<OrderEntry>() : nullptr,
-                         fresh ? nb->d_fcnt.as<uint32_t>() : nullptr, budget,
-                         c->d_order[slot].as<OrderEntry>(), c->d_octl[slot].as<uint32_t>(),
+                         fs, budget, c->d_order[slot].as<OrderEntry>(), c->d_octl[slot].as<uint32_t>(),
                          c->d_plan.as<uint32_t>(), phase);
   }
   HBX_TRY(c, hipGetLastError());
@@ -616,7 +630,7 @@ int plan_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
 // blocks per chain.  Afterwards every pending batch has had one more launch;
 // those whose chains are now guaranteed complete are finalized.  A budget of
 // kBudgetAll completes every chain in flight.
-int md5_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
+int md5_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
   if (int frc = flush_input_wait(c)) return frc;  // (a preplanned launch comes without a plan_launch)
   hipStream_t s = c->hstream;
   const int slot = (int)(c->launches % 3);
@@ -670,10 +684,11 @@ int md5_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
   HBX_TRY(c, hipEventRecord(c->order_free[slot], s));
   c->order_used[slot] = true;
   c->launches++;
-  if (nb && budget == kBudgetAll) {  // per-batch stage times of a synchronous batch (hbx_stage_times)
-    HBX_TRY(c, hipEventRecord(nb->ev[3], s));
-    nb->ev3 = true;
-  }
+  if (budget == kBudgetAll)  // per-batch stage times of a synchronous batch (hbx_stage_times)
+    for (Batch* nb : nbs) {
+      HBX_TRY(c, hipEventRecord(nb->ev[3], s));
+      nb->ev3 = true;
+    }
   bool forked = false;
   for (Batch* b : c->pending) {
     if (b->finalized || !b->joined) continue;
@@ -692,53 +707,66 @@ int md5_launch(hbx_ctx* c, Batch* nb, uint32_t budget) {
 }
 
 // One pipeline step on the hash side: launch j = plan (the carried chains +
-// the chains of the oldest unjoined batch once it is join_lag submits old)
-// then K3 with `budget` blocks per chain.  Issued by every submit BEFORE the
-// new batch's own scan is enqueued, and by wait_oldest (`drain`, with
-// kBudgetAll: the oldest unjoined batch joins whatever its age).  Nothing is
-// launched when no chain is in flight.
+// the chains of every unjoined batch at least join_lag submits old) then K3
+// with `budget` blocks per chain.  Issued by every submit BEFORE the new
+// batch's own scan is enqueued (with a K3 period P, by every P-th submit
+// only, with P x the slice), and by wait_oldest (`drain`, with kBudgetAll:
+// the oldest unjoined batch joins whatever its age).  Nothing is launched
+// when no chain is in flight.
+// The unjoined batches (oldest first) that join a launch whose FIFO holds
+// `size` of them, `older` submits from now: those join_lag or more old then.
+uint32_t joiners(const hbx_ctx* c, uint64_t older, bool drain) {
+  const uint64_t size = c->unjoined.size();
+  uint64_t k = size + older >= c->join_lag ? size + older + 1 - c->join_lag : 0;
+  if (drain) k = std::max<uint64_t>(k, 1);
+  return (uint32_t)std::min<uint64_t>(std::min<uint64_t>(k, size), kMaxFresh);
+}
+
 int md5_step(hbx_ctx* c, uint32_t budget, bool drain = false) {
+  if (!drain && c->k3_period > 1 && c->k3_tick++ % c->k3_period != 0) return HBX_OK;  // not this submit
+  budget = launch_budget(c, budget);
   if (c->preplanned) {  // planned one launch ahead (mode 2): any budget may run it
-    Batch* nb = c->pre_nb;
+    std::vector<Batch*> nbs;
+    nbs.swap(c->pre_nb);
     c->preplanned = false;
-    c->pre_nb = nullptr;
-    if (nb) nb->joined = true;
-    return md5_launch(c, nb, budget);
+    for (Batch* nb : nbs) nb->joined = true;
+    return md5_launch(c, nbs, budget);
   }
-  Batch* nb = nullptr;
-  if (!c->unjoined.empty() && (drain || c->unjoined.size() >= c->join_lag)) nb = c->unjoined.front();
-  bool live = nb != nullptr;
+  std::vector<Batch*> nbs(c->unjoined.begin(), c->unjoined.begin() + joiners(c, 0, drain));
+  bool live = !nbs.empty();
   for (Batch* b : c->pending)
     if (b->joined && !b->finalized) live = true;
   if (!live) return HBX_OK;
-  int rc = plan_launch(c, nb, budget);
+  int rc = plan_launch(c, nbs, budget);
   if (rc) return rc;
-  if (nb) {
+  for (Batch* nb : nbs) {
     nb->joined = true;
     c->unjoined.pop_front();
   }
-  return md5_launch(c, nb, budget);
+  return md5_launch(c, nbs, budget);
 }
 
-// Mode 2: enqueue the plan of the NEXT launch now, on the scan stream, before
-// the submitting batch's own K1.  It adds the oldest unjoined batch once that
-// is join_lag submits old at the next submit (the submitting batch is not in
-// the FIFO yet, hence the + 1).  Nothing is planned when no chain would be in
-// flight; the next submit then plans inline.
+// Modes 2 and 3: enqueue the plan of the NEXT launch now, before the
+// submitting batch's own K1.  It adds the unjoined batches that are join_lag
+// submits old at the next submit (the submitting batch is not in the FIFO
+// yet, hence `older` 1).  With a K3 period, only when the next submit
+// launches.  Nothing is planned when no chain would be in flight; the next
+// submit then plans inline.
 int preplan(hbx_ctx* c, uint32_t budget) {
   const int mode = plan_mode_of(c);
   if ((mode != 2 && mode != 3) || c->preplanned || c->hstream == c->stream) return HBX_OK;
-  Batch* nb = nullptr;
-  if (!c->unjoined.empty() && c->unjoined.size() + 1 >= c->join_lag && c->join_lag >= 2) nb = c->unjoined.front();
-  bool live = nb != nullptr;
+  if (c->k3_period > 1 && c->k3_tick % c->k3_period != 0) return HBX_OK;
+  budget = launch_budget(c, budget);
+  std::vector<Batch*> nbs(c->unjoined.begin(), c->unjoined.begin() + joiners(c, 1, false));
+  bool live = !nbs.empty();
   for (Batch* b : c->pending)
     if (b->joined && !b->finalized) live = true;
   if (!live) return HBX_OK;
   int rc = ensure_plan_buffers(c, 0);  // its slot's last reader (K3 three launches back) is waited for
-  if (!rc) rc = plan_launch(c, nb, budget);
+  if (!rc) rc = plan_launch(c, nbs, budget);
   if (rc) return rc;
-  if (nb) c->unjoined.pop_front();
-  c->pre_nb = nb;
+  for (size_t i = 0; i < nbs.size(); i++) c->unjoined.pop_front();
+  c->pre_nb = std::move(nbs);
   c->preplanned = true;
   return HBX_OK;
 }
@@ -870,7 +898,8 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
   // min(remaining, budget) blocks, finishing it in the launch where the
   // remainder fits
   const uint64_t nfull = (std::min<uint64_t>(longest, HBX_MAX_BLOCK_SIZE) + 8) >> 6;
-  b->need = budget == kBudgetAll ? 1u : (uint32_t)std::max<uint64_t>(1, (nfull + budget - 1) / budget);
+  const uint64_t lb = launch_budget(c, budget);  // a K3 period multiplies the slice
+  b->need = budget == kBudgetAll ? 1u : (uint32_t)std::max<uint64_t>(1, (nfull + lb - 1) / lb);
   const uint64_t nt = c->h_tiles.size();
   // meta block: off | len | slice_base | cut_base | tiles
   const size_t meta_bytes = n * 8 * 4 + nt * sizeof(uint4);
@@ -1015,7 +1044,8 @@ int submit_verify(hbx_ctx* c, const uint8_t* arena, uint64_t n, const uint64_t* 
   b->v_expect = expect;
   b->v_ok = ok;
   b->v_nbad = n_bad;
-  b->need = budget == kBudgetAll ? 1u : (uint32_t)std::max<uint64_t>(1, (longest + budget - 1) / budget);
+  const uint64_t lb = launch_budget(c, budget);
+  b->need = budget == kBudgetAll ? 1u : (uint32_t)std::max<uint64_t>(1, (longest + lb - 1) / lb);
   // meta block: descriptors | links
   const size_t meta_bytes = n * sizeof(VerifyDesc) + 16 * nlinks_total;
   if (n) {  // every allocation first: the batch is not in the FIFO yet
@@ -1235,6 +1265,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->md5_wgs = (uint32_t)(ncu = prop.multiProcessorCount);
   if (const char* v = ab_env("HBX_TILE_ITERS")) c->tile_iters = (uint32_t)std::min(1024, std::max(0, std::atoi(v)));
+  if (const char* v = ab_env("HBX_K3_PERIOD")) c->k3_period = (uint32_t)std::min(kMaxFresh, std::max(1, std::atoi(v)));
   if (const char* v = ab_env("HBX_JOIN_LAG")) c->join_lag = (uint32_t)std::min(4, std::max(1, std::atoi(v)));
   if (const char* v = ab_env("HBX_K4_WINDOW")) c->k4_window = (uint32_t)std::min(1024, std::max(1, std::atoi(v)));
   if (const char* v = ab_env("HBX_MD5_SLICE")) c->md5_slice = (uint32_t)std::max(0, std::atoi(v));
@@ -1346,6 +1377,16 @@ int hbx_set_join_lag(hbx_ctx* c, uint32_t lag) {
   return ensure_cut_stream(c);
 }
 
+int hbx_set_k3_period(hbx_ctx* c, uint32_t period) {
+  if (!c || period < 1 || period > (uint32_t)kMaxFresh) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  // pending batches were counted against the launch budget of their submit
+  if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
+  c->k3_period = period;
+  c->k3_tick = 0;
+  return HBX_OK;
+}
+
 int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
   if (!c || !out || cap == 0) return HBX_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
@@ -1354,9 +1395,11 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
       out, (size_t)cap,
       "{\"ab_env\": %d, \"md5_slice\": %u, \"join_lag\": %u, \"tile_iters\": %u, \"k1_gate\": %u, "
       "\"md5_wgs\": %u, \"plan_mode\": %d, \"k2_own\": %d, \"k4_window\": %u, \"k3_probe\": %d, "
-      "\"lean_marks\": %u, \"k3_prod\": %u, \"k3_items\": %u, \"k8_split_streams\": %llu, \"k8_split_fallbacks\": %llu}",
+      "\"lean_marks\": %u, \"k3_prod\": %u, \"k3_items\": %u, \"k3_period\": %u, \"k8_split_streams\": %llu, "
+      "\"k8_split_fallbacks\": %llu}",
       (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_gate, c->md5_wgs,
       plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks, c->k3_prod, c->k3_items,
+      c->k3_period,
       (unsigned long long)c->k8_split_streams, (unsigned long long)c->k8_split_fallbacks);
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }
@@ -1970,11 +2013,12 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
   // arena once its batch has been collected.
   const uint32_t budget = c->md5_slice ? c->md5_slice : kBudgetAll;
   const uint64_t nfull_max = (HBX_MAX_BLOCK_SIZE + 8ull) >> 6;
-  // a batch's chains join the launch join_lag submits later: it completes
-  // join_lag - 1 + ceil(nfull/budget) submits after its own, so this many
-  // arenas keep the collect from forcing a drain
+  // a batch's chains join the launch join_lag submits later (up to P - 1
+  // more with a K3 period P) and need ceil(nfull / (P x budget)) launches P
+  // submits apart, so this many arenas keep the collect from forcing a drain
+  const uint64_t lb = launch_budget(c, budget), per = std::max<uint32_t>(1, c->k3_period);
   const size_t depth = budget == kBudgetAll ? 2 : (size_t)std::min<uint64_t>(
-      64, (nfull_max + budget - 1) / budget + c->join_lag + 1);
+      64, (nfull_max + lb - 1) / lb * per + c->join_lag + per);
   if (c->d_ring.size() < depth) c->d_ring.resize(depth);
   // size every staging buffer once, for the largest batch this call forms
   // (growing one later would re-pin host memory or drain the streams)

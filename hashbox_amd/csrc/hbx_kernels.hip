@@ -962,9 +962,11 @@ extern "C" __global__ __launch_bounds__(256) void hbx_k2r_new_chains(
 // ----------------------------------------------------------- K2c plan --
 // The order of one K3 launch: the entries of the previous launch's order
 // (`prev`, count *n_prev; their rem less what that launch, with budget
-// `bprev`, hashed; the ones it finished dropped) plus the `fresh` entries of a new
-// batch (count *n_fresh; either may be absent), binned by this launch's
-// count min(rem, budget).  Two launches of the same grid over the same
+// `bprev`, hashed; the ones it finished dropped) plus the fresh entries of
+// the batches joining it (`fs`: up to kMaxFresh lists, list i with count
+// *fs.n[i]; a K3 period > 1 joins several batches per launch; either part may
+// be absent), binned by this launch's count min(rem, budget).  Two launches
+// of the same grid over the same
 // partition:
 //   phase 0: per-workgroup histogram of the bins, added into gh[0, 1024)
 //   phase 1: every workgroup scans gh into bin bases, reserves its own range
@@ -975,18 +977,28 @@ extern "C" __global__ __launch_bounds__(256) void hbx_k2r_new_chains(
 constexpr int kPlanThreads = 1024;
 static_assert(kPlanThreads == (int)kPlanBins, "one planner thread per bin");
 constexpr uint32_t kPlanGroups = 32u;  // grid of both phases
+constexpr int kMaxFresh = 8;           // batches joining one launch (kernel argument by value)
+struct FreshSet {
+  const OrderEntry* f[kMaxFresh];
+  const uint32_t* n[kMaxFresh];
+  uint32_t k, pad;
+};
 
 extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
     const OrderEntry* __restrict__ prev, const uint32_t* __restrict__ n_prev_p, uint32_t bprev,
-    const OrderEntry* __restrict__ fresh, const uint32_t* __restrict__ n_fresh_p, uint32_t budget,
-    OrderEntry* __restrict__ out, uint32_t* __restrict__ n_out, uint32_t* __restrict__ gh,
-    uint32_t phase) {
+    FreshSet fs, uint32_t budget, OrderEntry* __restrict__ out, uint32_t* __restrict__ n_out,
+    uint32_t* __restrict__ gh, uint32_t phase) {
   __shared__ uint32_t hist[kPlanBins], pos[kPlanBins], wsum[kPlanThreads / 64];
   const uint32_t tid = threadIdx.x;
   const uint32_t gt = blockIdx.x * kPlanThreads + tid, gn = gridDim.x * kPlanThreads;
   const uint32_t n_prev = prev ? *n_prev_p : 0u;
-  const uint32_t n_fresh = fresh ? *n_fresh_p : 0u;
-  const uint32_t n_all = n_prev + n_fresh;
+  uint32_t fend[kMaxFresh];  // end of fresh list i in the combined list
+  uint32_t n_all = n_prev;
+#pragma unroll
+  for (int i = 0; i < kMaxFresh; i++) {
+    n_all += (uint32_t)i < fs.k ? *fs.n[i] : 0u;
+    fend[i] = n_all;
+  }
   // entry e of the combined list, advanced to this launch (rem 0 = finished)
   auto entry = [&](uint32_t e) {
     OrderEntry o;
@@ -994,7 +1006,15 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
       o = prev[e];
       o.rem = o.rem - 1u <= bprev ? 0u : o.rem - bprev;
     } else {
-      o = fresh[e - n_prev];
+      const OrderEntry* f = fs.f[0];
+      uint32_t base = n_prev;
+#pragma unroll
+      for (int i = 1; i < kMaxFresh; i++)
+        if (e >= fend[i - 1]) {
+          f = fs.f[i];
+          base = fend[i - 1];
+        }
+      o = f[e - base];
     }
     return o;
   };

@@ -96,7 +96,8 @@ class Engine:
     """One MI355X (one HIP stream) running the chunk + block-ID path."""
 
     def __init__(self, device: int = 0, tile_iters: Optional[int] = None,
-                 md5_slice: Optional[int] = None, join_lag: Optional[int] = None):
+                 md5_slice: Optional[int] = None, join_lag: Optional[int] = None,
+                 k3_period: Optional[int] = None):
         self._L = _lib.load()
         self._ctx = ctypes.c_void_p()
         rc = self._L.hbx_ctx_create(int(device), ctypes.byref(self._ctx))
@@ -112,6 +113,8 @@ class Engine:
             self.set_md5_slice(md5_slice)
         if join_lag is not None:
             self.set_join_lag(join_lag)
+        if k3_period is not None:
+            self.set_k3_period(k3_period)
 
     # ----------------------------------------------------------- plumbing --
     def _after_producer(self):
@@ -304,6 +307,12 @@ class Engine:
         """Submits between a batch's own and the MD5 launch its chains join
         (1..4; 2 gives a small batch's scan a whole extra step)."""
         self._check(self._L.hbx_set_join_lag(self._ctx, int(lag)), "hbx_set_join_lag")
+
+    def set_k3_period(self, period: int):
+        """One K3 launch every ``period`` submits (1..8) with ``period`` x the
+        slice per chain: small batches pay the launch's start-up and tail once
+        per period (hbx_set_k3_period)."""
+        self._check(self._L.hbx_set_k3_period(self._ctx, int(period)), "hbx_set_k3_period")
 
     def k3_wave_times(self) -> np.ndarray:
         """Diagnostics (:meth:`set_k3_probe`): per-wave records of the

@@ -509,6 +509,15 @@ int hbx_set_tile_iters(hbx_ctx *ctx, uint32_t iters);
  * complete `lag` - 1 launches later.  Fails with HBX_ERR_STATE while batches
  * are pending. */
 int hbx_set_join_lag(hbx_ctx *ctx, uint32_t lag);
+/* K3 period, 1..8 (default 1): one block-MD5 launch every `period` submits,
+ * advancing every chain by `period` x the slice (hbx_set_md5_slice) and
+ * joining every batch that is `lag` or more submits old (up to 8).  Each
+ * launch has a fixed start-up and a tail (its slowest CU); a period > 1 pays
+ * them once per `period` steps, which pays off for small batches (a rank's
+ * 1 GiB share of configs[2] at N = 8).  Results are identical for every
+ * setting; a batch completes up to `period` - 1 submits later.  Fails with
+ * HBX_ERR_STATE while batches are pending. */
+int hbx_set_k3_period(hbx_ctx *ctx, uint32_t period);
 
 #ifdef __cplusplus
 }

@@ -83,18 +83,23 @@ FREE_GIB = 268.0  # free HBM one MI355X reports to a fresh process (~95 % of it 
 @pytest.mark.parametrize("scaling", ["strong", "weak"])
 def test_residency_plan_per_world(world, scaling):
     """Every rank's plan at N = 1..8: the files of a step are split exactly
-    (strong) or whole per rank (weak); need + lag <= R (no forced drain in the
-    window); B x need covers an 8 MiB chunk; the arenas fit 95 % of free HBM;
-    the check legs' host copies of all ranks fit the box's host memory."""
+    (strong) or whole per rank (weak); need x P + lag + P - 1 <= R (no forced
+    drain in the window, K3 period P); P x B x need covers an 8 MiB chunk; the
+    arenas fit 95 % of free HBM; the check legs' host copies of all ranks fit
+    the box's host memory; the auto period is 1 at 64 files per GPU, else
+    min(8, 64 / files) and a divisor of the steps."""
     import bench
     free = int(FREE_GIB * (1 << 30))
     seen = []
     host = 0
     for rank in range(world):
-        P = bench.residency_plan(64, 128, world, rank, scaling, free)
+        P = bench.residency_plan(64, 128, world, rank, scaling, free, steps=20)
         nfull = ((8 << 20) + 8) >> 6
-        assert P["need"] + P["join_lag"] <= P["R"], P
-        assert P["B"] * P["need"] >= nfull
+        per = P["k3_period"]
+        assert P["need"] * per + P["join_lag"] + per - 1 <= P["R"], P
+        assert P["B"] * per * P["need"] >= nfull
+        nf = P["files_per_gpu"]
+        assert per == (1 if nf >= 64 else 4 if nf <= 16 else 2) and 20 % per == 0, P
         assert P["hbm_bytes"] <= 0.95 * free
         assert P["join_lag"] == (3 if P["files_per_gpu"] < 64 else 2)
         seen.extend(P["mine"])
@@ -147,9 +152,9 @@ def test_bench_plan_default_is_strong(world):
     plans = d["plans"]
     assert sorted(sum((p["mine"] for p in plans), [])) == list(range(64))
     assert all(p["files_per_gpu"] == 64 // world for p in plans)
-    assert all(p["need"] + p["join_lag"] <= p["R"] for p in plans)
+    assert all(p["need"] * p["k3_period"] + p["join_lag"] + p["k3_period"] - 1 <= p["R"] for p in plans)
     if world == 8:
-        assert all(p["join_lag"] == 3 and p["lead"] == 4 for p in plans)
+        assert all(p["join_lag"] == 3 and p["lead"] == 4 and p["k3_period"] == 8 for p in plans)
 
 
 def test_bench_plan_weak_opt_in():

@@ -391,6 +391,70 @@ def test_pipelined_steady_state(oracle, join_lag):
             _check(a, r)
 
 
+@pytest.mark.parametrize("period,md5_slice,join_lag,plan_cut", [
+    (2, 16384, 1, "1"), (3, 16384, 2, "1"), (4, 8192, 2, "0"), (3, 4096, 3, "1"), (8, 9, 2, "1"), (5, 3, 1, "1"),
+    (4, 0, 2, "1")])
+def test_k3_period(oracle, monkeypatch, period, md5_slice, join_lag, plan_cut):
+    """K3 period (hbx_set_k3_period): one K3 launch every `period` submits
+    with period x the slice per chain, several batches joining one plan (the
+    planner's fresh-list set), in a deep pipeline as bench.py drives it, then
+    a forced drain with batches still unjoined, then a refilled arena ring
+    (hbx_input_after_oldest).  Every batch bit-exact; the launch count follows
+    the period; the period is fixed while batches are pending."""
+    import torch
+    from hashbox_amd import Engine, HbxError
+    monkeypatch.setenv("HBX_AB", "1")
+    monkeypatch.setenv("HBX_PLAN_CUT", plan_cut)
+    batches = _device_batches(oracle, 3, 83 + period)
+    got, order = [], []
+    with Engine(0, md5_slice=md5_slice, join_lag=join_lag, k3_period=period) as e:
+        assert e.knobs()["k3_period"] == period
+        e.stage_totals(reset=True)
+        nfull = ((8 << 20) + 8) >> 6
+        lb = md5_slice * period if md5_slice else nfull
+        depth = -(-nfull // lb) * period + join_lag + period
+        n_sub = 6 * period + 3
+        for j in range(n_sub):
+            i = j % 3
+            dev, offs, sizes, _ = batches[i]
+            e.submit_device(dev.data_ptr(), offs, sizes)
+            order.append(i)
+            if e.pending() >= depth:
+                got.append(e.wait())
+        _, n = e.stage_totals()  # launches harvested so far <= launches issued: one per period
+        assert n[3] <= -(-n_sub // period) + 1, (n, period)
+        while e.pending():  # forced drains, batches unjoined
+            got.append(e.wait())
+        _, n = e.stage_totals()
+        assert n[0] == n_sub
+        with pytest.raises(HbxError):
+            e.submit_device(batches[0][0].data_ptr(), batches[0][1], batches[0][2])
+            order.append(0)
+            e.set_k3_period(1)
+        while e.pending():
+            got.append(e.wait())
+        # a ring of 2 arenas refilled with the batches' data while pending
+        big = max(b[0].numel() for b in batches)
+        ring = [torch.empty(big, dtype=torch.uint8, device="cuda:0") for _ in range(2)]
+        torch.cuda.synchronize()
+        for j in range(4 * period):
+            i = j % 3
+            if e.pending() >= 2:
+                e.input_after_oldest()
+                e.input_fence(torch.cuda.current_stream().cuda_stream)
+            ring[j % 2][:batches[i][0].numel()].copy_(batches[i][0])
+            e.submit_device(ring[j % 2].data_ptr(), batches[i][1], batches[i][2])
+            order.append(i)
+            if e.pending() >= 2:
+                got.append(e.wait())
+        while e.pending():
+            got.append(e.wait())
+    assert len(got) == len(order)
+    for i, g in zip(order, got):
+        for a, r in zip(g, batches[i][3]):
+            _check(a, r)
+
+
 @pytest.mark.parametrize("lean", ["1", "0"])
 def test_plan_stream_changes_in_one_context(oracle, monkeypatch, lean):
     """One context through join lags 1 -> 2 -> 3 -> 1: the plan moves from
