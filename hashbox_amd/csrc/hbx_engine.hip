@@ -201,7 +201,10 @@ struct hbx_ctx {
   uint32_t k3_prod = 1;
   // at join lag 2, preplan on the cut stream (mode 3; HBX_PLAN_CUT=0: mode 1,
   // the plan on the hash stream): +2.7 % with K3P (profiles/r05e)
-  uint32_t plan_cut = 1;
+  uint32_t plan_cut = 1;  // 2: at any join lag >= 2 (A/B)
+  // the batch meta reaches the device by hbx_meta_fetch, a kernel on the scan
+  // stream, instead of an SDMA copy (HBX_META_KERNEL=0 for A/B)
+  uint32_t meta_kernel = 1;
   // K3Q: items per group (parts of each slice, handed out through a queue;
   // 0 = off, K3P's static groups; HBX_K3_ITEMS for A/B)
   uint32_t k3_items = 0;
@@ -510,7 +513,7 @@ uint32_t launch_budget(const hbx_ctx* c, uint32_t budget) {
 }
 
 int plan_mode_of(const hbx_ctx* c) {
-  if (c->join_lag == 2 && c->plan_cut && c->cstream != c->stream) return 3;
+  if ((c->join_lag == 2 ? c->plan_cut : c->plan_cut > 1 && c->join_lag > 2) && c->cstream != c->stream) return 3;
   return c->join_lag >= 3 ? 2 : c->join_lag == 2 ? 1 : 0;
 }
 hipStream_t plan_stream(const hbx_ctx* c) {
@@ -949,7 +952,14 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   DevBuf& ssum = c->d_ssum[slot];
 
   if (int frc = flush_input_wait(c)) return frc;  // (no launch this submit: nothing flushed it yet)
-  HBX_TRY(c, hipMemcpyAsync(b->d_meta.p, hm, meta_bytes, hipMemcpyHostToDevice, s));
+  if (c->meta_kernel) {  // meta_bytes is a multiple of 16
+    const uint32_t n16 = (uint32_t)(meta_bytes / 16);
+    hipLaunchKernelGGL(hbx_meta_fetch, dim3(std::min<uint32_t>(64, (n16 + 255) / 256)), dim3(256), 0, s,
+                       static_cast<const uint4*>(b->h_meta.p), b->d_meta.as<uint4>(), n16);
+    HBX_TRY(c, hipGetLastError());
+  } else {
+    HBX_TRY(c, hipMemcpyAsync(b->d_meta.p, hm, meta_bytes, hipMemcpyHostToDevice, s));
+  }
   const uint64_t* d_off = b->d_meta.as<uint64_t>();
   const uint64_t* d_len = d_off + n;
   const uint64_t* d_sb = d_off + 2 * n;
@@ -1272,7 +1282,8 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = ab_env("HBX_K1_GATE")) c->k1_gate = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_LEAN_MARKS")) c->lean_marks = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_PROD")) c->k3_prod = std::atoi(v) ? 1u : 0u;
-  if (const char* v = ab_env("HBX_PLAN_CUT")) c->plan_cut = std::atoi(v) ? 1u : 0u;
+  if (const char* v = ab_env("HBX_PLAN_CUT")) c->plan_cut = (uint32_t)std::min(2, std::max(0, std::atoi(v)));
+  if (const char* v = ab_env("HBX_META_KERNEL")) c->meta_kernel = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_ITEMS")) c->k3_items = (uint32_t)std::min(8, std::max(0, std::atoi(v)));
   // (tests: a K3 grid of a few workgroups, so every wave takes many groups)
   if (const char* v = ab_env("HBX_K3_WGS")) c->md5_wgs = (uint32_t)std::min<int>(std::max(1, ncu), std::max(1, std::atoi(v)));
@@ -1395,11 +1406,12 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
       out, (size_t)cap,
       "{\"ab_env\": %d, \"md5_slice\": %u, \"join_lag\": %u, \"tile_iters\": %u, \"k1_gate\": %u, "
       "\"md5_wgs\": %u, \"plan_mode\": %d, \"k2_own\": %d, \"k4_window\": %u, \"k3_probe\": %d, "
-      "\"lean_marks\": %u, \"k3_prod\": %u, \"k3_items\": %u, \"k3_period\": %u, \"k8_split_streams\": %llu, "
+      "\"lean_marks\": %u, \"k3_prod\": %u, \"k3_items\": %u, \"k3_period\": %u, \"meta_kernel\": %u, "
+      "\"plan_cut\": %u, \"k8_split_streams\": %llu, "
       "\"k8_split_fallbacks\": %llu}",
       (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_gate, c->md5_wgs,
       plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks, c->k3_prod, c->k3_items,
-      c->k3_period,
+      c->k3_period, c->meta_kernel, c->plan_cut,
       (unsigned long long)c->k8_split_streams, (unsigned long long)c->k8_split_fallbacks);
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }

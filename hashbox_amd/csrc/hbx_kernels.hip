@@ -1660,6 +1660,18 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k1_gate(const uint32_t* __r
   }
 }
 
+// A batch's meta block (file offsets, lengths, slice and cut bases, K1's
+// tiles) from the pinned host staging buffer into device memory, read over
+// PCIe by this kernel on the scan stream in place of hipMemcpyAsync: an SDMA
+// copy between two kernels of one stream waits ~17 us for the previous K1's
+// completion signal and the next K1 ~25 us for the copy's, ~50 us per step
+// on the scan loop (profiles/r05k/scan_gaps.txt: 8 files per GPU, 500 us
+// per step); a kernel follows the previous kernel directly.  `n` 16-B words.
+extern "C" __global__ __launch_bounds__(256) void hbx_meta_fetch(const uint4* __restrict__ src,
+                                                                 uint4* __restrict__ dst, uint32_t n) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) dst[i] = src[i];
+}
+
 // ContentBlockID (store.go:187-196), one wave per file.  The file's ids are
 // staged into LDS by all 64 lanes at once (kK4Window per round trip) and the
 // chain-block message is generated from there: the ids are read twice

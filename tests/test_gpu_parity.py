@@ -312,7 +312,8 @@ def test_pipelined_batches_time_sliced(oracle, md5_slice, join_lag):
 @pytest.mark.parametrize("prod", ["0", "1", "q2", "q4"])
 @pytest.mark.parametrize("md5_slice,join_lag,wgs,plan_cut", [
     (9, 1, 0, "0"), (64, 3, 0, "0"), (4096, 1, 0, "0"), (4096, 2, 0, "0"), (16384, 1, 0, "0"), (0, 1, 0, "0"),
-    (64, 1, 1, "0"), (4096, 1, 2, "0"), (0, 3, 1, "0"), (4096, 2, 0, "1"), (64, 2, 0, "1"), (9, 2, 1, "1")])
+    (64, 1, 1, "0"), (4096, 1, 2, "0"), (0, 3, 1, "0"), (4096, 2, 0, "1"), (64, 2, 0, "1"), (9, 2, 1, "1"),
+    (64, 3, 0, "2"), (4096, 4, 1, "2")])
 def test_k3_producer_waves(oracle, monkeypatch, md5_slice, join_lag, wgs, plan_cut, prod):
     """K3 with and without a producer wave per MD5 wave (hbx_k3p_block_md5 /
     hbx_k3_block_md5, HBX_K3_PROD): the stages a producer hands over through
@@ -324,7 +325,8 @@ def test_k3_producer_waves(oracle, monkeypatch, md5_slice, join_lag, wgs, plan_c
     MD5 wave and its producer walk many groups in one launch.  q2/q4: K3Q,
     each slice in 2 / 4 items handed out through the launch's queue (a
     chain's slice continues on another wave, possibly another CU).  plan_cut: at
-    join lag 2 the next launch is planned ahead on the cut stream (mode 3)."""
+    join lag 2 (2: at any lag >= 2) the next launch is planned ahead on the cut
+    stream (mode 3)."""
     from hashbox_amd import Engine
     monkeypatch.setenv("HBX_AB", "1")
     monkeypatch.setenv("HBX_K3_PROD", "0" if prod == "0" else "1")
@@ -338,7 +340,8 @@ def test_k3_producer_waves(oracle, monkeypatch, md5_slice, join_lag, wgs, plan_c
         k = e.knobs()
         assert k["k3_prod"] == (prod != "0") and (not wgs or k["md5_wgs"] == wgs)
         assert k["k3_items"] == (int(prod[1:]) if prod.startswith("q") else 0)
-        assert k["plan_mode"] == (3 if plan_cut == "1" else {1: 0, 2: 1}.get(join_lag, 2)), k
+        cut = (plan_cut == "1" and join_lag == 2) or (plan_cut == "2" and join_lag >= 2)
+        assert k["plan_mode"] == (3 if cut else {1: 0, 2: 1}.get(join_lag, 2)), k
         for i in [0, 1, 2, 0, 2, 1, 1, 0, 2, 2, 0, 1]:
             dev, offs, sizes, _ = batches[i]
             e.submit_device(dev.data_ptr(), offs, sizes)
@@ -391,24 +394,28 @@ def test_pipelined_steady_state(oracle, join_lag):
             _check(a, r)
 
 
-@pytest.mark.parametrize("period,md5_slice,join_lag,plan_cut", [
-    (2, 16384, 1, "1"), (3, 16384, 2, "1"), (4, 8192, 2, "0"), (3, 4096, 3, "1"), (8, 9, 2, "1"), (5, 3, 1, "1"),
-    (4, 0, 2, "1")])
-def test_k3_period(oracle, monkeypatch, period, md5_slice, join_lag, plan_cut):
+@pytest.mark.parametrize("period,md5_slice,join_lag,plan_cut,meta", [
+    (2, 16384, 1, "1", "1"), (3, 16384, 2, "1", "1"), (4, 8192, 2, "0", "0"), (3, 4096, 3, "1", "1"),
+    (4, 8192, 3, "2", "1"), (8, 9, 2, "1", "1"), (5, 3, 1, "1", "0"), (4, 0, 2, "1", "1"), (1, 4096, 3, "2", "1")])
+def test_k3_period(oracle, monkeypatch, period, md5_slice, join_lag, plan_cut, meta):
     """K3 period (hbx_set_k3_period): one K3 launch every `period` submits
     with period x the slice per chain, several batches joining one plan (the
     planner's fresh-list set), in a deep pipeline as bench.py drives it, then
     a forced drain with batches still unjoined, then a refilled arena ring
     (hbx_input_after_oldest).  Every batch bit-exact; the launch count follows
-    the period; the period is fixed while batches are pending."""
+    the period; the period is fixed while batches are pending.  plan_cut 2:
+    the preplan on the cut stream at lag 3 too; meta 0: the batch meta by
+    SDMA copy instead of hbx_meta_fetch."""
     import torch
     from hashbox_amd import Engine, HbxError
     monkeypatch.setenv("HBX_AB", "1")
     monkeypatch.setenv("HBX_PLAN_CUT", plan_cut)
+    monkeypatch.setenv("HBX_META_KERNEL", meta)
     batches = _device_batches(oracle, 3, 83 + period)
     got, order = [], []
     with Engine(0, md5_slice=md5_slice, join_lag=join_lag, k3_period=period) as e:
-        assert e.knobs()["k3_period"] == period
+        k = e.knobs()
+        assert k["k3_period"] == period and k["meta_kernel"] == int(meta) and k["plan_cut"] == int(plan_cut)
         e.stage_totals(reset=True)
         nfull = ((8 << 20) + 8) >> 6
         lb = md5_slice * period if md5_slice else nfull
