@@ -123,7 +123,7 @@ def parse():
                          "divides --steps)")
     ap.add_argument("--lead", type=int, default=-1,
                     help="steps an arena stays resident beyond the launches its batch needs: R = launches "
-                         "per batch + lead (-1 = join lag + 1).  Lead = join lag is the least that lets the next "
+                         "per batch + lead (-1 = join lag + K3 period).  Lead = join lag is the least that lets the next "
                          "batch's scan overlap the launch finishing the old one (hbx_input_after_oldest), but at "
                          "the auto residency it puts 32 batches' chains in flight, past K3's 128-CU cliff")
     ap.add_argument("--e2e", action="store_true",
@@ -584,11 +584,14 @@ def residency_plan(files, file_mib, world, rank, scaling="strong", free_bytes=0,
     # (gate -> K1 -> K2 -> K2r -> plan), and at lag 2 the plan runs ahead on
     # the cut stream (plan mode 3): 2,326 vs 2,280-2,292 GiB/s (profiles/r05f)
     lag = join_lag if join_lag > 0 else (3 if nf < 64 else 2)
-    ld = lead if lead >= 0 else lag + 1
     if k3_period > 0:
         per = k3_period
     else:  # small per-GPU batches: the launch's fixed start-up and tail once per P steps
         per = next((p for p in (8, 4, 2) if p <= 64 // nf and (steps <= 0 or steps % p == 0)), 1) if nf < 64 else 1
+    # a K3 launch finalizes P batches at once, and the host's collect of the
+    # oldest blocks until that launch is done: P - 1 more steps of lead keep
+    # the scan stream fed meanwhile (profiles/r05m/scan_gaps.txt)
+    ld = lead if lead >= 0 else lag + per
     offs, total = W.pack_layout(lens)
     # launches a batch needs before its chains are all hashed
     nfull = (min(fbytes, 8 << 20) + 8) >> 6

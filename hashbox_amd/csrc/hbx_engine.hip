@@ -201,7 +201,9 @@ struct hbx_ctx {
   uint32_t k3_prod = 1;
   // at join lag 2, preplan on the cut stream (mode 3; HBX_PLAN_CUT=0: mode 1,
   // the plan on the hash stream): +2.7 % with K3P (profiles/r05e)
-  uint32_t plan_cut = 1;  // 2: at any join lag >= 2 (A/B)
+  // 2 (default): at lag 3 and 4 too, off the scan loop (8 files per GPU, K3
+  // period 4: 2,075-2,079 vs 2,031-2,049 GiB/s, profiles/r05l); 1: lag 2 only
+  uint32_t plan_cut = 2;
   // the batch meta reaches the device by hbx_meta_fetch, a kernel on the scan
   // stream, instead of an SDMA copy (HBX_META_KERNEL=0 for A/B)
   uint32_t meta_kernel = 1;

@@ -154,7 +154,7 @@ def test_bench_plan_default_is_strong(world):
     assert all(p["files_per_gpu"] == 64 // world for p in plans)
     assert all(p["need"] * p["k3_period"] + p["join_lag"] + p["k3_period"] - 1 <= p["R"] for p in plans)
     if world == 8:
-        assert all(p["join_lag"] == 3 and p["lead"] == 4 and p["k3_period"] == 8 for p in plans)
+        assert all(p["join_lag"] == 3 and p["lead"] == 11 and p["k3_period"] == 8 for p in plans)
 
 
 def test_bench_plan_weak_opt_in():

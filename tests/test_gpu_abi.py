@@ -85,4 +85,5 @@ def test_ab_switches_need_hbx_ab(monkeypatch):
     monkeypatch.setenv("HBX_AB", "1")
     with Engine(0) as e:
         k = e.knobs()
-    assert k["ab_env"] == 1 and k["lean_marks"] == 0 and k["join_lag"] == 3 and k["plan_mode"] == 2, k
+    # lag 3: the next launch is preplanned on the cut stream (plan_cut 2, mode 3)
+    assert k["ab_env"] == 1 and k["lean_marks"] == 0 and k["join_lag"] == 3 and k["plan_mode"] == 3, k
