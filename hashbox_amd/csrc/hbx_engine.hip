@@ -166,6 +166,7 @@ struct Batch {
 }  // namespace
 
 constexpr uint32_t kK3TimeRing = 4096;  // hbx_ctx::h_k3t slots (2 x u64 each)
+constexpr int kDoneRing = 16;         // hbx_ctx::order_free: completion events of the latest K3 launches
 
 struct hbx_ctx {
   int device = 0;
@@ -266,8 +267,14 @@ struct hbx_ctx {
   // stream) writes order[j%3] from order[(j-1)%3]; K3 j (hash stream) reads it
   DevBuf d_order[3], d_octl[3], d_q[3];  // (+ K3Q's item queue per slot)
   hipEvent_t plan_done[3] = {nullptr, nullptr, nullptr};   // plan j%3 written
-  hipEvent_t order_free[3] = {nullptr, nullptr, nullptr};  // K3 that read slot j%3 done
-  bool order_used[3] = {false, false, false};
+  // completion of K3 launch L: order_free[L % kDoneRing] (recorded again by
+  // launch L + kDoneRing).  The plan of launch j waits for launch j - 3, the
+  // last reader of its order slot; hbx_input_after_oldest for the launch that
+  // finished the oldest batch, which with a K3 period or a long lead is
+  // several launches back (with 3 events it fell back to the newest launch,
+  // serializing the next K1 behind the running K3: 8 files per GPU at K3
+  // period 8 and lead 11, 1,579 vs 2,079 GiB/s, profiles/r05n)
+  hipEvent_t order_free[kDoneRing] = {};
   uint64_t launches = 0;    // K3 launches planned so far
   uint32_t last_budget = 0; // budget of the last planned launch
   DevBuf d_stage;           // host-input arena
@@ -545,7 +552,7 @@ int ensure_cut_stream(hbx_ctx* c) {
 int flush_input_wait(hbx_ctx* c) {
   if (!c->input_wait_pending) return HBX_OK;
   c->input_wait_pending = false;
-  hipEvent_t e = c->order_free[c->input_wait_L % 3];
+  hipEvent_t e = c->order_free[c->input_wait_L % kDoneRing];
   if (hipEventQuery(e) == hipSuccess) return HBX_OK;
   HBX_TRY(c, hipStreamWaitEvent(c->stream, e, 0));
   return HBX_OK;
@@ -558,8 +565,10 @@ int plan_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
   if (rc) return rc;
   // the K3 launch that read this slot three launches ago must be done (lean:
   // no wait enqueued once the host has seen it complete, the usual case)
-  if (c->order_used[slot] && c->hstream != s && !(c->lean_marks && hipEventQuery(c->order_free[slot]) == hipSuccess))
-    HBX_TRY(c, hipStreamWaitEvent(s, c->order_free[slot], 0));
+  if (c->launches >= 3 && c->hstream != s) {
+    hipEvent_t e = c->order_free[(c->launches - 3) % kDoneRing];
+    if (!(c->lean_marks && hipEventQuery(e) == hipSuccess)) HBX_TRY(c, hipStreamWaitEvent(s, e, 0));
+  }
   // carried chains exist only while an older batch is unfinalized (a batch
   // is finalized once every chain of it is hashed); without one the previous
   // list is not read at all (hbx_reserve may have reallocated it)
@@ -686,8 +695,7 @@ int md5_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
   c->last_budget = budget;  // what the next plan advances this list by
   // the launch's one completion event: the plan three launches on waits for
   // it, and so does the result stream for the batches it completes
-  HBX_TRY(c, hipEventRecord(c->order_free[slot], s));
-  c->order_used[slot] = true;
+  HBX_TRY(c, hipEventRecord(c->order_free[L % kDoneRing], s));
   c->launches++;
   if (budget == kBudgetAll)  // per-batch stage times of a synchronous batch (hbx_stage_times)
     for (Batch* nb : nbs) {
@@ -700,7 +708,7 @@ int md5_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
     b->done++;
     if (budget == kBudgetAll || b->done >= b->need) {
       if (!forked && c->rstream != s) {  // the result stream picks up after this K3
-        HBX_TRY(c, hipStreamWaitEvent(c->rstream, c->order_free[slot], 0));
+        HBX_TRY(c, hipStreamWaitEvent(c->rstream, c->order_free[L % kDoneRing], 0));
         forked = true;
       }
       b->final_launch = L;
@@ -1307,8 +1315,8 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
     hbx_ctx_destroy(c);
     return HBX_ERR_HIP;
   }
-  for (int t = 0; t < 3; t++) {
-    if (hipEventCreateWithFlags(&c->plan_done[t], hipEventDisableTiming) == hipSuccess &&
+  for (int t = 0; t < kDoneRing; t++) {
+    if ((t >= 3 || hipEventCreateWithFlags(&c->plan_done[t], hipEventDisableTiming) == hipSuccess) &&
         hipEventCreateWithFlags(&c->order_free[t], hipEventDisableTiming) == hipSuccess)
       continue;
     hbx_ctx_destroy(c);
@@ -1324,7 +1332,9 @@ void hbx_ctx_destroy(hbx_ctx* c) {
   for (hipStream_t s : {c->stream, c->cstream, c->hstream, c->rstream})
     if (s) (void)hipStreamSynchronize(s);
   for (hipEvent_t e : {c->producer, c->ssum_free[0], c->ssum_free[1], c->plan_done[0], c->plan_done[1],
-                       c->plan_done[2], c->order_free[0], c->order_free[1], c->order_free[2]})
+                       c->plan_done[2]})
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->order_free)
     if (e) (void)hipEventDestroy(e);
   for (DevBuf* b : {&c->d_ssum[0], &c->d_ssum[1], &c->d_order[0], &c->d_order[1], &c->d_order[2],
                     &c->d_octl[0], &c->d_octl[1], &c->d_octl[2], &c->d_q[0], &c->d_q[1], &c->d_q[2], &c->d_gate,
@@ -2250,10 +2260,10 @@ int hbx_input_after_oldest(hbx_ctx* c) {
   if (!x->joined || c->hstream == c->stream) return HBX_OK;  // (empty batch / one stream: in order already)
   // the completion event of the launch that finished it (or of a later one,
   // if that slot has been recorded again since)
-  const uint64_t L = c->launches - x->final_launch <= 3 ? x->final_launch : c->launches - 1;
+  const uint64_t L = c->launches - x->final_launch <= kDoneRing ? x->final_launch : c->launches - 1;
   // (lean marks: nothing to enqueue once the host has seen it complete -- in
   // the steady state it finished two launches ago)
-  if (c->lean_marks && hipEventQuery(c->order_free[L % 3]) == hipSuccess) return HBX_OK;
+  if (c->lean_marks && hipEventQuery(c->order_free[L % kDoneRing]) == hipSuccess) return HBX_OK;
   c->input_fence_set = true;
   c->input_fence_L = L;
   if (c->lean_marks) {  // enqueued after the next plan (flush_input_wait), off the scan loop
@@ -2262,7 +2272,7 @@ int hbx_input_after_oldest(hbx_ctx* c) {
     c->input_wait_L = L;
     return HBX_OK;
   }
-  HBX_TRY(c, hipStreamWaitEvent(c->stream, c->order_free[L % 3], 0));
+  HBX_TRY(c, hipStreamWaitEvent(c->stream, c->order_free[L % kDoneRing], 0));
   return HBX_OK;
 }
 
@@ -2274,11 +2284,11 @@ int hbx_input_fence(hbx_ctx* c, void* stream) {
   if (int frc = flush_input_wait(c)) return frc;
   if (!stream || !c->input_fence_set) return HBX_OK;
   // Nothing to wait for once launch L is known complete.  The ring slot of L
-  // is recorded again by launch L + 3: a fence called that late waits for
+  // is recorded again by launch L + kDoneRing: a fence called that late waits for
   // that later launch instead (issued after L on the same stream, so it
   // completes after L: conservative, never early).
   const uint64_t L = c->input_fence_L;
-  hipEvent_t e = c->order_free[L % 3];
+  hipEvent_t e = c->order_free[L % kDoneRing];
   if (L < c->k3_done_upto || hipEventQuery(e) == hipSuccess) {
     c->input_fence_set = false;
     return HBX_OK;
