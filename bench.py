@@ -119,11 +119,10 @@ def parse():
                          "(hbx_set_join_lag; 0 = auto: 3 below 64 files per GPU, else 1)")
     ap.add_argument("--k3-period", type=int, default=0,
                     help="one K3 launch every P submits with P x the slice (hbx_set_k3_period, 1..8; 0 = auto: "
-                         "1 at 64 or more files per GPU, else the largest of 8, 4, 2 up to 64 / files that "
-                         "divides --steps)")
+                         "1 at 32 or more files per GPU, else 4 (or 2) if it divides --steps)")
     ap.add_argument("--lead", type=int, default=-1,
                     help="steps an arena stays resident beyond the launches its batch needs: R = launches "
-                         "per batch + lead (-1 = join lag + K3 period).  Lead = join lag is the least that lets the next "
+                         "per batch + lead (-1 = join lag + 1).  Lead = join lag is the least that lets the next "
                          "batch's scan overlap the launch finishing the old one (hbx_input_after_oldest), but at "
                          "the auto residency it puts 32 batches' chains in flight, past K3's 128-CU cliff")
     ap.add_argument("--e2e", action="store_true",
@@ -586,12 +585,14 @@ def residency_plan(files, file_mib, world, rank, scaling="strong", free_bytes=0,
     lag = join_lag if join_lag > 0 else (3 if nf < 64 else 2)
     if k3_period > 0:
         per = k3_period
-    else:  # small per-GPU batches: the launch's fixed start-up and tail once per P steps
-        per = next((p for p in (8, 4, 2) if p <= 64 // nf and (steps <= 0 or steps % p == 0)), 1) if nf < 64 else 1
-    # a K3 launch finalizes P batches at once, and the host's collect of the
-    # oldest blocks until that launch is done: P - 1 more steps of lead keep
-    # the scan stream fed meanwhile (profiles/r05m/scan_gaps.txt)
-    ld = lead if lead >= 0 else lag + per
+    else:  # small per-GPU batches: the launch's fixed start-up and tail once per 4 steps
+        # (profiles/r05j, r05o: 8 files 2,013 -> 2,056-2,083 GiB/s, 16 files 2,206 -> 2,183-2,249; 32
+        # files P1 2,277-2,294 vs P2 2,260-2,272)
+        per = next((p for p in (4, 2) if steps <= 0 or steps % p == 0), 1) if nf < 32 else 1
+    # (lead lag + P, so that the host's collect of the oldest batch never waits
+    # for the launch that finalized it, measured the same or 0.5-1 % slower:
+    # profiles/r05o)
+    ld = lead if lead >= 0 else lag + 1
     offs, total = W.pack_layout(lens)
     # launches a batch needs before its chains are all hashed
     nfull = (min(fbytes, 8 << 20) + 8) >> 6

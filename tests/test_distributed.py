@@ -86,8 +86,8 @@ def test_residency_plan_per_world(world, scaling):
     (strong) or whole per rank (weak); need x P + lag + P - 1 <= R (no forced
     drain in the window, K3 period P); P x B x need covers an 8 MiB chunk; the
     arenas fit 95 % of free HBM; the check legs' host copies of all ranks fit
-    the box's host memory; the auto period is 1 at 64 files per GPU, else
-    min(8, 64 / files) and a divisor of the steps."""
+    the box's host memory; the auto period is 1 at 32 or more files per GPU,
+    else 4 (20 steps)."""
     import bench
     free = int(FREE_GIB * (1 << 30))
     seen = []
@@ -99,7 +99,7 @@ def test_residency_plan_per_world(world, scaling):
         assert P["need"] * per + P["join_lag"] + per - 1 <= P["R"], P
         assert P["B"] * per * P["need"] >= nfull
         nf = P["files_per_gpu"]
-        assert per == (1 if nf >= 64 else 4 if nf <= 16 else 2) and 20 % per == 0, P
+        assert per == (1 if nf >= 32 else 4), P
         assert P["hbm_bytes"] <= 0.95 * free
         assert P["join_lag"] == (3 if P["files_per_gpu"] < 64 else 2)
         seen.extend(P["mine"])
@@ -154,7 +154,7 @@ def test_bench_plan_default_is_strong(world):
     assert all(p["files_per_gpu"] == 64 // world for p in plans)
     assert all(p["need"] * p["k3_period"] + p["join_lag"] + p["k3_period"] - 1 <= p["R"] for p in plans)
     if world == 8:
-        assert all(p["join_lag"] == 3 and p["lead"] == 11 and p["k3_period"] == 8 for p in plans)
+        assert all(p["join_lag"] == 3 and p["lead"] == 4 and p["k3_period"] == 4 for p in plans)
 
 
 def test_bench_plan_weak_opt_in():
