@@ -149,26 +149,11 @@ __device__ __forceinline__ K1State k1_prime(const uint32_t (&halo)[16], bool at_
   return st;
 }
 
-// Look-back exchange of the waves' iteration totals (K1 LB): per iteration
-// slot (it + 1) & 3, wave w's {sum A, sum C} and a tag it + 1 written after
-// it.  A wave needs the totals of the waves before it in its own iteration
-// (its start state) and of all 16 in the previous one (the running base), so
-// it waits for exactly those tags instead of a workgroup barrier: waves drift
-// by up to most of an iteration without stalling each other.  A slot is
-// rewritten four iterations later, by when every reader is past it (wave 0
-// at it + 4 needs all 16 totals of it + 3).
-struct K1Look {
-  uint2 tot[4][16];
-  uint32_t tag[4][16];
-};
-constexpr uint32_t kK1SpinLimit = 1u << 16;  // ~2 ms of s_sleep 1: a drift of 1000 iterations (never)
-
 // One 64 KiB iteration: thread (w, l) owns positions e_l .. e_l+63 of it;
 // `cur` are their bytes, `out` the bytes MIN earlier.  Returns, wave-uniform,
 // the slice's max digest and the digest just before the slice (= state).
-template <bool LB>
 __device__ __forceinline__ void k1_iteration(const uint32_t (&cur)[16], const uint32_t (&out)[16],
-                                             K1State& st, uint2 (&wtot)[2][16], K1Look& lk, uint32_t it,
+                                             K1State& st, uint2 (&wtot)[2][16], uint32_t it,
                                              uint32_t w, uint32_t l, uint32_t e_l, uint64_t qs,
                                              uint64_t N, uint32_t& smax, uint32_t& sprev) {
   const RunAgg ca = run_aggregates(cur);
@@ -177,40 +162,13 @@ __device__ __forceinline__ void k1_iteration(const uint32_t (&cur)[16], const ui
   const uint32_t C_l = e_l * A_l + J_l;
   const uint32_t iA = wave_incl_sum(A_l);
   const uint32_t iC = wave_incl_sum(C_l);
-  uint32_t WA, WC, totA = 0u, totC = 0u;
-  if (LB) {
-    const uint32_t sl = (it + 1u) & 3u, sp = it & 3u;
-    if (l == 63u) {
-      lk.tot[sl][w] = make_uint2(iA, iC);
-      __hip_atomic_store(&lk.tag[sl][w], it + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    // lanes 0-15: the previous iteration's 16 totals (tag it; none before
-    // iteration 0, whose base the priming set), lanes 16-31: this
-    // iteration's waves before w (tag it + 1)
-    const bool need = l < 16u ? it > 0u : (l < 32u && l - 16u < w);
-    uint32_t* tp = &lk.tag[l < 16u ? sp : sl][l & 15u];
-    const uint32_t want = l < 16u ? it : it + 1u;
-    for (uint32_t spin = 0;; spin++) {
-      const bool ok = !need || __hip_atomic_load(tp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == want;
-      if (__builtin_amdgcn_ballot_w64(!ok) == 0ull || spin >= kK1SpinLimit) break;
-      __builtin_amdgcn_s_sleep(1);
-    }
-    const uint2 t = need ? lk.tot[l < 16u ? sp : sl][l & 15u] : make_uint2(0u, 0u);
-    const uint32_t sA = row_incl_sum(t.x), sC = row_incl_sum(t.y);
-    st.S1c += readlane(sA, 15);  // the base moves past the previous iteration
-    st.s2c -= readlane(sC, 15);
-    WA = w ? readlane(sA, 16 + (int)w - 1) : 0u;
-    WC = w ? readlane(sC, 16 + (int)w - 1) : 0u;
-  } else {
-    if (l == 63u) wtot[it & 1u][w] = make_uint2(iA, iC);
-    __syncthreads();
-    const uint2 t = (l < 16u) ? wtot[it & 1u][l] : make_uint2(0u, 0u);
-    const uint32_t sA = row_incl_sum(t.x), sC = row_incl_sum(t.y);
-    WA = w ? readlane(sA, (int)w - 1) : 0u;
-    WC = w ? readlane(sC, (int)w - 1) : 0u;
-    totA = readlane(sA, 15);
-    totC = readlane(sC, 15);
-  }
+  if (l == 63u) wtot[it & 1u][w] = make_uint2(iA, iC);
+  __syncthreads();
+  const uint2 t = (l < 16u) ? wtot[it & 1u][l] : make_uint2(0u, 0u);
+  const uint32_t sA = row_incl_sum(t.x), sC = row_incl_sum(t.y);
+  const uint32_t WA = w ? readlane(sA, (int)w - 1) : 0u;
+  const uint32_t WC = w ? readlane(sC, (int)w - 1) : 0u;
+  const uint32_t totA = readlane(sA, 15), totC = readlane(sC, 15);
 
   // state before the lane's first position (*), then before position 32
   const uint32_t A_pre = WA + (iA - A_l), C_pre = WC + (iC - C_l);
@@ -230,7 +188,7 @@ __device__ __forceinline__ void k1_iteration(const uint32_t (&cur)[16], const ui
   }
   smax = readlane(wave_max_to_lane63(M), 63);
 
-  st.S1c += totA;  // (LB: 0 here; added at the next iteration's start)
+  st.S1c += totA;
   st.s2c -= totC;  // 65536*(...) vanishes mod 2^16
   st.pa = ca;
 }
@@ -294,13 +252,11 @@ constexpr uint32_t kDmaSlot = 4096;  // bytes per wave per iteration
 // tiles[t] = {file, first 64 KiB iteration, iterations, 0}; ssum[slice_base[f]
 // + j] = {max digest of slice j, digest before slice j}; ssum[dummy] absorbs
 // the writes of slices past a file's end.
-template <bool LB>
-__device__ __forceinline__ void k1_body(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
-                                        const uint64_t* __restrict__ file_len,
-                                        const uint64_t* __restrict__ slice_base, const uint4* __restrict__ tiles,
-                                        uint2* __restrict__ ssum, uint64_t dummy) {
+extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_dma(
+    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
+    const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ slice_base,
+    const uint4* __restrict__ tiles, uint2* __restrict__ ssum, uint64_t dummy) {
   __shared__ uint2 wtot[2][16];
-  __shared__ K1Look lk;
   __shared__ __attribute__((aligned(1024))) uint8_t land[kK1Threads / 64][2][kDmaSlot];
   const uint4 td = tiles[blockIdx.x];
   const uint32_t f = td.x;
@@ -348,10 +304,6 @@ __device__ __forceinline__ void k1_body(const uint8_t* __restrict__ arena, const
 #pragma unroll
   for (int k = 0; k < 16; k++) out[k] = 0u;
   if (q0 != 0) load_run64(make_rsrc_u(fb + q0 - kMinBlock, kMinBlock), e_l, 0u, out);
-  if (LB) {  // no tag may match before its slot is written (LDS starts with any bytes)
-    if (tid < 64u) lk.tag[tid >> 4][tid & 15u] = 0xffffffffu;
-    __syncthreads();
-  }
   K1State st = k1_prime(out, q0 == 0, wtot, w, l, e_l);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
@@ -373,7 +325,7 @@ __device__ __forceinline__ void k1_body(const uint8_t* __restrict__ arena, const
     issue(it + 2u, (it & 1u) ? lds1 : lds0);
     const uint64_t qs = q0 + (uint64_t)it * kMinBlock;
     uint32_t smax, sprev;
-    k1_iteration<LB>(cur, prev, st, wtot, lk, it, w, l, e_l, qs, N, smax, sprev);
+    k1_iteration(cur, prev, st, wtot, it, w, l, e_l, qs, N, smax, sprev);
     const bool ok = qs + (uint64_t)w * kSlice < N;
     k1_store_slice(ssum, ok ? sb + ((qs >> kSliceShift) + w) : dummy, l, smax, sprev);
   };
@@ -382,21 +334,6 @@ __device__ __forceinline__ void k1_body(const uint8_t* __restrict__ arena, const
     if (it + 1u < n_it) step(it + 1u, out, run_b);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup exits
-}
-
-// K1 with the look-back exchange (K1State, K1Look) and, for A/B
-// (HBX_K1_LB=0), with a workgroup barrier per iteration.
-extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_dma(
-    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
-    const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ slice_base,
-    const uint4* __restrict__ tiles, uint2* __restrict__ ssum, uint64_t dummy) {
-  k1_body<true>(arena, file_off, file_len, slice_base, tiles, ssum, dummy);
-}
-extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_bar(
-    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
-    const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ slice_base,
-    const uint4* __restrict__ tiles, uint2* __restrict__ ssum, uint64_t dummy) {
-  k1_body<false>(arena, file_off, file_len, slice_base, tiles, ssum, dummy);
 }
 
 // ------------------------------------------------------------------ K2 --

@@ -104,24 +104,15 @@ def test_batch_mixed(engine, oracle):
         _check(r, oracle.store_file(f, fast=True))
 
 
-@pytest.mark.parametrize("lb", ["1", "0"])
 @pytest.mark.parametrize("tile_iters", [0, 1, 3, 32, 64, 256, 1024])
-def test_tile_sizes(oracle, monkeypatch, tile_iters, lb):
-    """K1 tiles of 1..1024 iterations, with the waves' look-back exchange of
-    iteration totals (LDS tags, ring of 4 slots: tiles of 1, 3 and many
-    iterations wrap it) and, lb 0, with the barrier per iteration."""
+def test_tile_sizes(oracle, tile_iters):
     from hashbox_amd import Engine
-    monkeypatch.setenv("HBX_AB", "1")
-    monkeypatch.setenv("HBX_K1_LB", lb)
     # several tiles per file up to 256 iterations (16 MiB tiles); 1024 = one
     # tile; 0 = sized per batch (16 iterations for this one)
     n = 37 * MIN + 999 if tile_iters < 64 else (5 * tile_iters * MIN) // 2 + 999 if tile_iters <= 256 else 20 * MAXB + 5
     with Engine(0, tile_iters=tile_iters) as e:
-        assert e.knobs()["k1_lb"] == int(lb)
         x = oracle.random_bytes(n, 77)
         _check(e.chunk_hash(x), oracle.store_file(x, fast=True))
-        y = np.full(n, 0x5A, np.uint8)  # constant bytes: every cut at exactly MAX
-        _check(e.chunk_hash(y), oracle.store_file(y, fast=True))
 
 
 def test_device_resident(engine, oracle):
