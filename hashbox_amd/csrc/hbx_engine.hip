@@ -849,12 +849,15 @@ constexpr uint32_t kTileItersMin = 16, kTileItersMax = 256;
 uint32_t k1_tile_iters(const hbx_ctx* c, uint64_t total) {
   if (c->tile_iters) return c->tile_iters;
   // about two tiles per CU for large batches, four up to 4 GiB (65,536
-  // iterations): the strong-scaling shares of configs[2] (tools/gpu_tile_sweep.sh,
-  // profiles/r02n_tiles: 1 GiB 1,825 -> 1,948 GiB/s with 16 instead of 32
-  // iterations, 2 GiB 2,068 -> 2,147 with 32 instead of 64; 4 GiB equal; 8 GiB
-  // 2,231 at 256 vs 2,205 at 128)
-  const uint64_t per_cu = total <= 65536ull ? 4ull : 2ull;
-  const uint64_t t = (total + per_cu * c->md5_wgs - 1) / (per_cu * c->md5_wgs);
+  // iterations), 8/3 up to 2 GiB: the strong-scaling shares of configs[2]
+  // (tools/gpu_tile_sweep.sh, profiles/r02n_tiles: 1 GiB 1,825 -> 1,948 GiB/s
+  // with 16 instead of 32 iterations, 2 GiB 2,068 -> 2,147 with 32 instead of
+  // 64; 4 GiB equal; 8 GiB 2,231 at 256 vs 2,205 at 128).  With the K3 period
+  // (round 5) 1 GiB does best at 24 (2,141-2,150 vs 2,096-2,132 GiB/s at 16,
+  // three alternating rounds, profiles/r05s) and 2 GiB at 48 (2,275 vs 2,254)
+  const uint64_t num = total <= 32768ull ? 3ull : 1ull;
+  const uint64_t den = total <= 32768ull ? 8ull : total <= 65536ull ? 4ull : 2ull;
+  const uint64_t t = (total * num + den * c->md5_wgs - 1) / (den * c->md5_wgs);
   return (uint32_t)std::min<uint64_t>(kTileItersMax, std::max<uint64_t>(kTileItersMin, t));
 }
 
