@@ -170,13 +170,14 @@ def test_kat_block_ids_on_device(engine):
         assert engine.block_id(bytes.fromhex(r["data_hex"])).hex() == r["id"]
 
 
-@pytest.mark.parametrize("join_lag", [1, 3])
-def test_store_paths_end_to_end(oracle, tmp_path, join_lag):
+@pytest.mark.parametrize("join_lag,period", [(1, 1), (3, 1), (2, 4)])
+def test_store_paths_end_to_end(oracle, tmp_path, join_lag, period):
     """Files on disk -> pinned -> HBM -> results, in small batches so the
     two-stream double buffering and batch boundaries are exercised (the
-    arena ring is as deep as the slice schedule plus the join lag)."""
+    arena ring is as deep as the slice schedule plus the join lag, and the
+    K3 period's extra submits)."""
     from hashbox_amd import Engine
-    engine = Engine(0, md5_slice=4096, join_lag=join_lag)
+    engine = Engine(0, md5_slice=4096, join_lag=join_lag, k3_period=period)
     sizes = [0, 1, 4096, 2 * MIN + 1, 3 * MAXB + 7, 700_001, 5 * MIN, 12345, 9 * 1024 * 1024]
     paths, datas = [], []
     for i, n in enumerate(sizes * 3):

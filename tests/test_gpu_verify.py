@@ -79,11 +79,13 @@ def test_device_resident(engine, oracle):
     assert [i.tobytes() for i in ids] == expect
 
 
-@pytest.mark.parametrize("md5_slice,join_lag", [(0, 1), (3, 1), (256, 1), (256, 3), (3, 2)])
-def test_pipelined_verify_with_chunking(oracle, md5_slice, join_lag):
+@pytest.mark.parametrize("md5_slice,join_lag,period", [(0, 1, 1), (3, 1, 1), (256, 1, 1), (256, 3, 1), (3, 2, 1),
+                                                       (256, 2, 3), (3, 3, 2)])
+def test_pipelined_verify_with_chunking(oracle, md5_slice, join_lag, period):
     """hbx_verify_submit_device: verify batches share the time-sliced K3
     pipeline and the wait FIFO with chunking batches; every edge length for
-    0-9 links, blocks past 8 MiB, expected-id mismatches."""
+    0-9 links, blocks past 8 MiB, expected-id mismatches; with a K3 period
+    verify and chunking batches join one launch together."""
     import torch
     from hashbox_amd import Engine
     rng = np.random.default_rng(77 + md5_slice)
@@ -110,7 +112,7 @@ def test_pipelined_verify_with_chunking(oracle, md5_slice, join_lag):
     farena = torch.from_numpy(fhost).to("cuda:0")
     torch.cuda.synchronize()
     third = len(specs) // 3
-    with Engine(0, md5_slice=md5_slice, join_lag=join_lag) as eng:
+    with Engine(0, md5_slice=md5_slice, join_lag=join_lag, k3_period=period) as eng:
         eng.verify_submit_device(arena.data_ptr(), offs[:third], [d.size for d in datas[:third]],
                                  links[:third], expect[:third])
         eng.submit_device(farena.data_ptr(), [0, 4 << 20], [f.size for f in files])
