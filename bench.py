@@ -588,7 +588,7 @@ def residency_plan(files, file_mib, world, rank, scaling="strong", free_bytes=0,
     else:  # small per-GPU batches: the launch's fixed start-up and tail once per 4 steps
         # (profiles/r05j, r05o: 8 files 2,013 -> 2,056-2,083 GiB/s, 16 files 2,206 -> 2,183-2,249; 32
         # files P1 2,277-2,294 vs P2 2,260-2,272)
-        per = next((p for p in (4, 2) if steps <= 0 or steps % p == 0), 1) if nf < 32 else 1
+        per = next((p for p in (4, 2) if steps <= 0 or steps % p == 0), 1) if nf < 32 and not e2e else 1
     # (lead lag + P, so that the host's collect of the oldest batch never waits
     # for the launch that finalized it, measured the same or 0.5-1 % slower:
     # profiles/r05o)

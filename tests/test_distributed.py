@@ -113,6 +113,16 @@ def test_residency_plan_per_world(world, scaling):
     assert host <= 64 << 30 if scaling == "strong" else host <= world * (9 << 30)
 
 
+def test_residency_plan_e2e_small_share():
+    """--e2e at a small per-GPU share: the PCIe-bound shallow pipeline keeps
+    one K3 launch per step (a K3 period would not fit R = lead + 2)."""
+    import bench
+    free = int(FREE_GIB * (1 << 30))
+    for files in (8, 16, 64):
+        P = bench.residency_plan(files, 128, 1, 0, "strong", free, e2e=True, steps=20)
+        assert P["k3_period"] == 1 and P["need"] + P["join_lag"] <= P["R"], P
+
+
 def _bench_plan(world, extra, timeout=120):
     import subprocess
     import sys
