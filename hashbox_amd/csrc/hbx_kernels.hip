@@ -1667,9 +1667,20 @@ extern "C" __global__ __launch_bounds__(64) void hbx_k1_gate(const uint32_t* __r
 // completion signal and the next K1 ~25 us for the copy's, ~50 us per step
 // on the scan loop (profiles/r05k/scan_gaps.txt: 8 files per GPU, 500 us
 // per step); a kernel follows the previous kernel directly.  `n` 16-B words.
+// The staging buffer is reused by later batches of the same pool slot, so the
+// reads are system-scope (coherent with the host's writes, never a line a
+// cache kept from an earlier batch).
 extern "C" __global__ __launch_bounds__(256) void hbx_meta_fetch(const uint4* __restrict__ src,
                                                                  uint4* __restrict__ dst, uint32_t n) {
-  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) dst[i] = src[i];
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+    uint32_t* p = const_cast<uint32_t*>(reinterpret_cast<const uint32_t*>(src + i));
+    uint4 v;
+    v.x = __hip_atomic_load(p + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    v.y = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    v.z = __hip_atomic_load(p + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    v.w = __hip_atomic_load(p + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    dst[i] = v;
+  }
 }
 
 // ContentBlockID (store.go:187-196), one wave per file.  The file's ids are
