@@ -208,8 +208,6 @@ struct hbx_ctx {
   // the batch meta reaches the device by hbx_meta_fetch, a kernel on the scan
   // stream, instead of an SDMA copy (HBX_META_KERNEL=0 for A/B)
   uint32_t meta_kernel = 1;
-  // short K1 tiles at the end of each batch's tile list (HBX_K1_TAIL, A/B)
-  uint32_t k1_tail = 0;
   // K3Q: items per group (parts of each slice, handed out through a queue;
   // 0 = off, K3P's static groups; HBX_K3_ITEMS for A/B)
   uint32_t k3_items = 0;
@@ -840,8 +838,8 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
 // round off K1's last pass over the CUs K3 leaves free, measured slower: K1
 // 3.18 -> 3.33 ms beside K3 at 33 resident batches, from the extra halos and
 // workgroups.)
-void k1_tiles(hbx_ctx* c, uint32_t f, uint32_t from, uint32_t to, uint32_t tile) {  // iterations [from, to)
-  for (uint32_t i = from; i < to; i += tile) c->h_tiles.push_back(make_uint4(f, i, std::min(tile, to - i), 0u));
+void k1_tiles(hbx_ctx* c, uint32_t f, uint32_t iters, uint32_t tile) {
+  for (uint32_t i = 0; i < iters; i += tile) c->h_tiles.push_back(make_uint4(f, i, std::min(tile, iters - i), 0u));
 }
 
 constexpr uint32_t kTileItersMin = 16, kTileItersMax = 256;
@@ -889,7 +887,7 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
   b->cut_base.resize(n);
   c->h_slice_base.resize(n);
   c->h_tiles.clear();
-  uint64_t slices = 0, tcaps = 0, longest = 0, total_iters = 0, nscan = 0;
+  uint64_t slices = 0, tcaps = 0, longest = 0, total_iters = 0;
   for (uint64_t f = 0; f < n; f++) {
     const uint64_t iters = scan_iters(lens[f]);
     if (iters > 0xFFFFFFFFull) {
@@ -897,16 +895,8 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
       return c->fail(HBX_ERR_ARG, "file too large");
     }
     total_iters += iters;
-    nscan += iters ? 1 : 0;
   }
   const uint32_t tile = k1_tile_iters(c, total_iters);
-  // K1 tail (c->k1_tail): the last iterations of every file go into short
-  // tiles dispatched after all the long ones, about one round of them over
-  // the CUs K3 leaves, so K1 ends on short tiles instead of some CUs running
-  // a last long tile while the rest wait for the next K1
-  const uint32_t small = std::max<uint32_t>(8, tile / 3);
-  const uint64_t per_file_small =
-      c->k1_tail && !c->tile_iters && nscan ? (c->md5_wgs / 2 + nscan - 1) / nscan : 0;
   for (uint64_t f = 0; f < n; f++) {
     const uint64_t N = lens[f];
     longest = std::max(longest, N);
@@ -915,16 +905,9 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
     tcaps += max_chunks(N);
     if (const uint64_t iters = scan_iters(N)) {  // only files with split candidates scan
       slices += (N + kSlice - 1) / kSlice;
-      const uint32_t tail = (uint32_t)std::min<uint64_t>(iters / 2, per_file_small * small);
-      k1_tiles(c, (uint32_t)f, 0, (uint32_t)iters - tail, tile);
+      k1_tiles(c, (uint32_t)f, (uint32_t)iters, tile);
     }
   }
-  if (per_file_small)
-    for (uint64_t f = 0; f < n; f++)
-      if (const uint64_t iters = scan_iters(lens[f])) {
-        const uint32_t tail = (uint32_t)std::min<uint64_t>(iters / 2, per_file_small * small);
-        k1_tiles(c, (uint32_t)f, (uint32_t)iters - tail, (uint32_t)iters, small);
-      }
   b->caps = tcaps;
   // launches this batch's chains need: a chunk is <= min(longest file, MAX)
   // bytes, i.e. <= nfull full message blocks, and each launch advances it by
@@ -1314,7 +1297,6 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = ab_env("HBX_K3_PROD")) c->k3_prod = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_PLAN_CUT")) c->plan_cut = (uint32_t)std::min(2, std::max(0, std::atoi(v)));
   if (const char* v = ab_env("HBX_META_KERNEL")) c->meta_kernel = std::atoi(v) ? 1u : 0u;
-  if (const char* v = ab_env("HBX_K1_TAIL")) c->k1_tail = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_ITEMS")) c->k3_items = (uint32_t)std::min(8, std::max(0, std::atoi(v)));
   // (tests: a K3 grid of a few workgroups, so every wave takes many groups)
   if (const char* v = ab_env("HBX_K3_WGS")) c->md5_wgs = (uint32_t)std::min<int>(std::max(1, ncu), std::max(1, std::atoi(v)));
@@ -1440,11 +1422,11 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
       "{\"ab_env\": %d, \"md5_slice\": %u, \"join_lag\": %u, \"tile_iters\": %u, \"k1_gate\": %u, "
       "\"md5_wgs\": %u, \"plan_mode\": %d, \"k2_own\": %d, \"k4_window\": %u, \"k3_probe\": %d, "
       "\"lean_marks\": %u, \"k3_prod\": %u, \"k3_items\": %u, \"k3_period\": %u, \"meta_kernel\": %u, "
-      "\"plan_cut\": %u, \"k1_tail\": %u, \"k8_split_streams\": %llu, "
+      "\"plan_cut\": %u, \"k8_split_streams\": %llu, "
       "\"k8_split_fallbacks\": %llu}",
       (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_gate, c->md5_wgs,
       plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks, c->k3_prod, c->k3_items,
-      c->k3_period, c->meta_kernel, c->plan_cut, c->k1_tail,
+      c->k3_period, c->meta_kernel, c->plan_cut,
       (unsigned long long)c->k8_split_streams, (unsigned long long)c->k8_split_fallbacks);
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }

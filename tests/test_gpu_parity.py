@@ -115,25 +115,6 @@ def test_tile_sizes(oracle, tile_iters):
         _check(e.chunk_hash(x), oracle.store_file(x, fast=True))
 
 
-@pytest.mark.parametrize("tail", ["1", "0"])
-def test_k1_tail_tiles(oracle, monkeypatch, tail):
-    """HBX_K1_TAIL: each file's last iterations in short tiles listed after
-    every long tile of the batch (so a tile starts mid-file and primes from
-    its halo, and tiles of one file are not contiguous in the list): 1, 8 and
-    70 files of mixed sizes, bit-exact."""
-    from hashbox_amd import Engine
-    monkeypatch.setenv("HBX_AB", "1")
-    monkeypatch.setenv("HBX_K1_TAIL", tail)
-    g = np.random.default_rng(5)
-    with Engine(0) as e:
-        assert e.knobs()["k1_tail"] == int(tail)
-        for nf in (1, 8, 70):
-            sizes = [int(x) for x in np.exp(g.uniform(np.log(2 * MIN), np.log(40e6), nf))]
-            files = [oracle.random_bytes(n, 4000 + 10 * nf + i) for i, n in enumerate(sizes)]
-            for f, r in zip(files, e.chunk_hash_batch(files)):
-                _check(r, oracle.store_file(f, fast=True))
-
-
 def test_device_resident(engine, oracle):
     import torch
     from hashbox_amd import pack_arena_layout
