@@ -255,7 +255,7 @@ constexpr uint32_t kDmaSlot = 4096;  // bytes per wave per iteration
 extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_dma(
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
     const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ slice_base,
-    const uint4* __restrict__ tiles, uint2* __restrict__ ssum, uint64_t dummy) {
+    const uint4* __restrict__ tiles, uint2* __restrict__ ssum, uint64_t dummy, uint32_t swz) {
   __shared__ uint2 wtot[2][16];
   __shared__ __attribute__((aligned(1024))) uint8_t land[kK1Threads / 64][2][kDmaSlot];
   const uint4 td = tiles[blockIdx.x];
@@ -281,10 +281,17 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_d
   // of the piece), so the LDS slot holds the wave's 4 KiB in file order; the
   // per-lane 64-byte reads then take a 4-way bank conflict (a lane reading
   // bytes 16k.. of its own run instead makes the global access strided).
+  // swz (A/B): each DMA instruction still reads one contiguous 1 KiB, but
+  // lane i loads its 16-B unit 4 (i % 16) + i / 16, so LDS holds each 1 KiB
+  // transposed (piece p of run r at slot 16 p + r) and the per-lane reads of
+  // piece p are 16 contiguous lanes: no bank conflict
+  const uint32_t dma_lane = swz ? 64u * (l & 15u) + 16u * (l >> 4) : 16u * l;
+  const uint32_t rd_lane = swz ? 64u * (l >> 4) + (l & 15u) : 4u * l;
+  const uint32_t rd_step = swz ? 16u : 1u;
   auto issue = [&](uint32_t it, uint32_t lds) {  // 4 DMA ops, always issued
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      const uint32_t voff = w * kSlice + 1024u * k + 16u * l;
+      const uint32_t voff = w * kSlice + 1024u * k + dma_lane;
       dma16(srd, voff, it * kMinBlock, lds + 1024u * k);
     }
   };
@@ -292,7 +299,7 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_d
     const u32x4* p = reinterpret_cast<const u32x4*>(&land[w][slot][0]);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      const u32x4 t = p[4 * l + k];
+      const u32x4 t = p[rd_lane + rd_step * k];
       v[4 * k + 0] = t.x;
       v[4 * k + 1] = t.y;
       v[4 * k + 2] = t.z;

@@ -104,15 +104,23 @@ def test_batch_mixed(engine, oracle):
         _check(r, oracle.store_file(f, fast=True))
 
 
+@pytest.mark.parametrize("swz", ["0", "1"])
 @pytest.mark.parametrize("tile_iters", [0, 1, 3, 32, 64, 256, 1024])
-def test_tile_sizes(oracle, tile_iters):
+def test_tile_sizes(oracle, monkeypatch, tile_iters, swz):
+    """K1 tiles of 1..1024 iterations; swz 1: the LDS image transposed per
+    1 KiB (HBX_K1_SWZ), ragged file ends included."""
     from hashbox_amd import Engine
+    monkeypatch.setenv("HBX_AB", "1")
+    monkeypatch.setenv("HBX_K1_SWZ", swz)
     # several tiles per file up to 256 iterations (16 MiB tiles); 1024 = one
     # tile; 0 = sized per batch (16 iterations for this one)
     n = 37 * MIN + 999 if tile_iters < 64 else (5 * tile_iters * MIN) // 2 + 999 if tile_iters <= 256 else 20 * MAXB + 5
     with Engine(0, tile_iters=tile_iters) as e:
+        assert e.knobs()["k1_swz"] == int(swz)
         x = oracle.random_bytes(n, 77)
         _check(e.chunk_hash(x), oracle.store_file(x, fast=True))
+        y = oracle.random_bytes(n // 3 + 17, 78)
+        _check(e.chunk_hash(y), oracle.store_file(y, fast=True))
 
 
 def test_device_resident(engine, oracle):
