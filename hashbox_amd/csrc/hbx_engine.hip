@@ -208,8 +208,10 @@ struct hbx_ctx {
   // the batch meta reaches the device by hbx_meta_fetch, a kernel on the scan
   // stream, instead of an SDMA copy (HBX_META_KERNEL=0 for A/B)
   uint32_t meta_kernel = 1;
-  // K1's LDS image transposed per 1 KiB (conflict-free reads; HBX_K1_SWZ, A/B)
-  uint32_t k1_swz = 0;
+  // K1's LDS image transposed per 1 KiB: its per-lane reads become
+  // conflict-free (SQ_LDS_BANK_CONFLICT 1.0e8 -> 0 per launch), K1 beside K3
+  // 3.26 -> 3.19 ms per 8 GiB (profiles/r05ab); HBX_K1_SWZ=0 for the old image
+  uint32_t k1_swz = 1;
   // K3Q: items per group (parts of each slice, handed out through a queue;
   // 0 = off, K3P's static groups; HBX_K3_ITEMS for A/B)
   uint32_t k3_items = 0;

@@ -277,11 +277,12 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_d
   const s32x4 srd = make_srd(fb + q0, nbytes);
   const uint32_t lds0 = (uint32_t)(uintptr_t)&land[w][0][0];
   const uint32_t lds1 = (uint32_t)(uintptr_t)&land[w][1][0];
-  // Each DMA instruction reads 1 KiB contiguous (lane l: bytes 16l..16l+15
-  // of the piece), so the LDS slot holds the wave's 4 KiB in file order; the
-  // per-lane 64-byte reads then take a 4-way bank conflict (a lane reading
-  // bytes 16k.. of its own run instead makes the global access strided).
-  // swz (A/B): each DMA instruction still reads one contiguous 1 KiB, but
+  // Each DMA instruction reads 1 KiB contiguous; with swz 0 lane l takes
+  // bytes 16l..16l+15 of the piece, so the LDS slot holds the wave's 4 KiB in
+  // file order and the per-lane 64-byte reads take a 4-way bank conflict (a
+  // lane reading bytes 16k.. of its own run instead makes the global access
+  // strided, round 2).
+  // swz (default): each DMA instruction still reads one contiguous 1 KiB, but
   // lane i loads its 16-B unit 4 (i % 16) + i / 16, so LDS holds each 1 KiB
   // transposed (piece p of run r at slot 16 p + r) and the per-lane reads of
   // piece p are 16 contiguous lanes: no bank conflict
