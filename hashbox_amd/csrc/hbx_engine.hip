@@ -514,11 +514,6 @@ int ensure_plan_buffers(hbx_ctx* c, uint64_t extra);
 //   and the hash stream carries nothing but K3 launches.  At lag 2 the same
 //   schedule would make K1 j wait for K2 of batch j-1 (measured 1,575 GiB/s at
 //   8 files per GPU, vs 1,890 for mode 1).
-// * lag 1, mode 4 (c->plan_cut 3, K2 on its own stream; A/B): submit j plans
-//   launch j+1 at its END, on the cut stream right behind batch j's K2r, so
-//   the next launch joins batch j without the scan stream waiting for K2
-//   (with a K3 period, launches P submits apart and P x the slice: the same
-//   lead as lag 2 at period 1, the launch overhead paid once per P steps).
 // * lag 2, mode 3 (preplan on the cut stream, c->plan_cut): the same preplan
 //   as mode 2, but on the cut stream, right behind batch j-1's K2 and K2r
 //   (whose chains it adds) and before batch j's K2: neither the scan stream
@@ -531,13 +526,12 @@ uint32_t launch_budget(const hbx_ctx* c, uint32_t budget) {
 }
 
 int plan_mode_of(const hbx_ctx* c) {
-  if (c->join_lag == 1 && c->plan_cut >= 3 && c->cstream != c->stream) return 4;
   if ((c->join_lag == 2 ? c->plan_cut : c->plan_cut > 1 && c->join_lag > 2) && c->cstream != c->stream) return 3;
   return c->join_lag >= 3 ? 2 : c->join_lag == 2 ? 1 : 0;
 }
 hipStream_t plan_stream(const hbx_ctx* c) {
   const int m = plan_mode_of(c);
-  return m == 1 ? c->hstream : m >= 3 ? c->cstream : c->stream;
+  return m == 1 ? c->hstream : m == 3 ? c->cstream : c->stream;
 }
 
 // K2 + K2r get a stream of their own once the join lag allows it (or
@@ -775,14 +769,12 @@ int md5_step(hbx_ctx* c, uint32_t budget, bool drain = false) {
 // yet, hence `older` 1).  With a K3 period, only when the next submit
 // launches.  Nothing is planned when no chain would be in flight; the next
 // submit then plans inline.
-// Mode 4 (`post`): called at the end of a submit, with its batch in the FIFO
-// already (it is then 1 submit old at the next submit: `older` 0).
-int preplan(hbx_ctx* c, uint32_t budget, bool post = false) {
+int preplan(hbx_ctx* c, uint32_t budget) {
   const int mode = plan_mode_of(c);
-  if ((post ? mode != 4 : (mode != 2 && mode != 3)) || c->preplanned || c->hstream == c->stream) return HBX_OK;
+  if ((mode != 2 && mode != 3) || c->preplanned || c->hstream == c->stream) return HBX_OK;
   if (c->k3_period > 1 && c->k3_tick % c->k3_period != 0) return HBX_OK;
   budget = launch_budget(c, budget);
-  std::vector<Batch*> nbs(c->unjoined.begin(), c->unjoined.begin() + joiners(c, post ? 0 : 1, false));
+  std::vector<Batch*> nbs(c->unjoined.begin(), c->unjoined.begin() + joiners(c, 1, false));
   bool live = !nbs.empty();
   for (Batch* b : c->pending)
     if (b->joined && !b->finalized) live = true;
@@ -1047,7 +1039,7 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
     HBX_TRY(c, hipEventRecord(b->ev[2], s2));
   }
   c->unjoined.push_back(b);
-  return preplan(c, budget, true);  // mode 4: the next launch, behind this K2r
+  return HBX_OK;
 }
 
 int submit_verify_launch(hbx_ctx* c, Batch* b, const uint8_t* arena, uint64_t n, const uint64_t* offs,
@@ -1133,7 +1125,7 @@ int submit_verify_launch(hbx_ctx* c, Batch* b, const uint8_t* arena, uint64_t n,
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(b->ev[2], s));
   c->unjoined.push_back(b);
-  return preplan(c, budget, true);
+  return HBX_OK;
 }
 
 // Scatter a collected batch's pinned results into the caller's arrays.
@@ -1307,7 +1299,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = ab_env("HBX_K1_GATE")) c->k1_gate = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_LEAN_MARKS")) c->lean_marks = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_PROD")) c->k3_prod = std::atoi(v) ? 1u : 0u;
-  if (const char* v = ab_env("HBX_PLAN_CUT")) c->plan_cut = (uint32_t)std::min(3, std::max(0, std::atoi(v)));
+  if (const char* v = ab_env("HBX_PLAN_CUT")) c->plan_cut = (uint32_t)std::min(2, std::max(0, std::atoi(v)));
   if (const char* v = ab_env("HBX_META_KERNEL")) c->meta_kernel = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K1_SWZ")) c->k1_swz = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_ITEMS")) c->k3_items = (uint32_t)std::min(8, std::max(0, std::atoi(v)));
