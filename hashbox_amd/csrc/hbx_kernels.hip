@@ -1209,6 +1209,9 @@ __device__ __forceinline__ K3Group k3_group(const OrderEntry* __restrict__ order
 // The producer's side of one group: the stages S, S+1, .. of Rr blocks of the
 // wave's 64 chains, lane l's chain message stream starting at `src` (16-B
 // loads at any byte offset, as md5_coop).  Returns the group's stage count.
+// SETS register sets of loads in flight (2, or 3 for A/B: HBX_K3_PSETS=3,
+// one stage more of memory latency hidden).
+template <int SETS = 2>
 __device__ __forceinline__ uint32_t k3p_produce(uint8_t* wl, uint32_t* flags, uint32_t S, uint64_t src, uint32_t Rr) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t t = lane % 16u, sub = lane / 16u;
@@ -1220,6 +1223,23 @@ __device__ __forceinline__ uint32_t k3p_produce(uint8_t* wl, uint32_t* flags, ui
   u32x4 GA[16], GB[16];
   coop_load<16>(GA, Q, 0u, t, ngr);
   coop_load<16>(GB, Q, min(1u, nst - 1u), t, ngr);
+  if (SETS == 3) {
+    u32x4 GC[16];
+    coop_load<16>(GC, Q, min(2u, nst - 1u), t, ngr);
+    // stage x goes to LDS half x & 1 once stage x - 2 is freed (flags[1] >= S + x - 1)
+    auto put = [&](uint32_t x, u32x4 (&G)[16]) {
+      k3p_wait_ge(&flags[1], x < 2u ? S : S + x - 1u);
+      coop_write<16>(wl, wr, (S + x) & 1u, G);
+      k3p_publish(&flags[0], S + x + 1u);
+      coop_load<16>(G, Q, min(x + 3u, nst - 1u), t, ngr);
+    };
+    for (uint32_t s = 0; s < nst; s += 3u) {
+      put(s, GA);
+      if (s + 1u < nst) put(s + 1u, GB);
+      if (s + 2u < nst) put(s + 2u, GC);
+    }
+    return nst;
+  }
   for (uint32_t s = 0; s < nst; s += 2u) {
     k3p_wait_ge(&flags[1], s < 2u ? S : S + s - 1u);
     coop_write<16>(wl, wr, (S + s) & 1u, GA);
@@ -1389,6 +1409,7 @@ __device__ __forceinline__ void k3q_push(uint32_t* __restrict__ qc, uint64_t* __
 // The producer wave of pair `flags`: the same groups as its MD5 wave; for a
 // group on the cooperative path (R >= kCoopMinBudget), the stages of blocks
 // next+1 .. next+R-1 of its 64 chains, two register sets in flight.
+template <int SETS>
 __device__ void k3p_producer(uint8_t* wl, uint32_t* flags, const OrderEntry* __restrict__ order,
                              const uint32_t* __restrict__ n_order, uint32_t budget, uint32_t g0, uint32_t nwaves) {
   const uint32_t n_total = *n_order;
@@ -1397,7 +1418,7 @@ __device__ void k3p_producer(uint8_t* wl, uint32_t* flags, const OrderEntry* __r
   for (uint32_t g = g0; g < groups; g += nwaves) {
     const K3Group G = k3_group(order, n_total, g, budget);
     if (G.R < kCoopMinBudget) continue;  // wave-uniform: the MD5 wave takes the lane path
-    S += k3p_produce(wl, flags, S, G.ch.src + 64ull * (G.ch.next + 1u) - 8ull, G.R - 1u);  // from block next+1
+    S += k3p_produce<SETS>(wl, flags, S, G.ch.src + 64ull * (G.ch.next + 1u) - 8ull, G.R - 1u);  // from block next+1
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (clamped re-reads of the last stage)
 }
@@ -1608,7 +1629,7 @@ constexpr int kK3PThreads = 512;
 extern "C" __global__ __launch_bounds__(kK3PThreads, 1) void hbx_k3p_block_md5(
     const OrderEntry* __restrict__ order, const uint32_t* __restrict__ n_order, uint32_t budget,
     uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last, uint64_t* __restrict__ tslot,
-    uint64_t* __restrict__ probe) {
+    uint64_t* __restrict__ probe, uint32_t psets) {
   __shared__ __attribute__((aligned(16))) uint8_t k3_lds[4][kK3WaveLds];
   __shared__ uint32_t k3_flags[4][2];
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -1619,7 +1640,10 @@ extern "C" __global__ __launch_bounds__(kK3PThreads, 1) void hbx_k3p_block_md5(
     k3_body<true>(k3_lds[pair], order, n_order, budget, started, t_first, t_last, tslot, probe, k3_flags[pair]);
   } else {
     __builtin_amdgcn_s_setprio(2);
-    k3p_producer(k3_lds[pair], k3_flags[pair], order, n_order, budget, blockIdx.x * 4u + pair, gridDim.x * 4u);
+    if (psets == 3u)
+      k3p_producer<3>(k3_lds[pair], k3_flags[pair], order, n_order, budget, blockIdx.x * 4u + pair, gridDim.x * 4u);
+    else
+      k3p_producer<2>(k3_lds[pair], k3_flags[pair], order, n_order, budget, blockIdx.x * 4u + pair, gridDim.x * 4u);
   }
 }
 

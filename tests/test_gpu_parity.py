@@ -318,7 +318,7 @@ def test_pipelined_batches_time_sliced(oracle, md5_slice, join_lag):
         assert n[3] >= 1 and ms[3] > 0
 
 
-@pytest.mark.parametrize("prod", ["0", "1", "q2", "q4"])
+@pytest.mark.parametrize("prod", ["0", "1", "q2", "q4", "p3"])
 @pytest.mark.parametrize("md5_slice,join_lag,wgs,plan_cut", [
     (9, 1, 0, "0"), (64, 3, 0, "0"), (4096, 1, 0, "0"), (4096, 2, 0, "0"), (16384, 1, 0, "0"), (0, 1, 0, "0"),
     (64, 1, 1, "0"), (4096, 1, 2, "0"), (0, 3, 1, "0"), (4096, 2, 0, "1"), (64, 2, 0, "1"), (9, 2, 1, "1"),
@@ -339,6 +339,7 @@ def test_k3_producer_waves(oracle, monkeypatch, md5_slice, join_lag, wgs, plan_c
     from hashbox_amd import Engine
     monkeypatch.setenv("HBX_AB", "1")
     monkeypatch.setenv("HBX_K3_PROD", "0" if prod == "0" else "1")
+    monkeypatch.setenv("HBX_K3_PSETS", "3" if prod == "p3" else "2")  # p3: three producer register sets
     monkeypatch.setenv("HBX_K3_ITEMS", prod[1:] if prod.startswith("q") else "0")
     monkeypatch.setenv("HBX_PLAN_CUT", plan_cut)
     if wgs:
@@ -349,6 +350,7 @@ def test_k3_producer_waves(oracle, monkeypatch, md5_slice, join_lag, wgs, plan_c
         k = e.knobs()
         assert k["k3_prod"] == (prod != "0") and (not wgs or k["md5_wgs"] == wgs)
         assert k["k3_items"] == (int(prod[1:]) if prod.startswith("q") else 0)
+        assert k["k3_psets"] == (3 if prod == "p3" else 2)
         cut = (plan_cut == "1" and join_lag == 2) or (plan_cut == "2" and join_lag >= 2)
         assert k["plan_mode"] == (3 if cut else {1: 0, 2: 1}.get(join_lag, 2)), k
         for i in [0, 1, 2, 0, 2, 1, 1, 0, 2, 2, 0, 1]:
