@@ -200,7 +200,10 @@ struct hbx_ctx {
   // A/B): 1,435 vs 1,586 cycles per block inside the bench schedule, +1.7 %
   // (200 steps) and +2.9 % at 8 files per GPU (profiles/r05f)
   uint32_t k3_prod = 1;
-  uint32_t k3_psets = 2;  // K3P producer register sets in flight (HBX_K3_PSETS=3, A/B)
+  // K3P producer register sets in flight: 3 (a stage more of memory latency
+  // hidden) 2,297-2,318 vs 2,286-2,308 GiB/s in three alternating pairs at 64
+  // files, equal at 8 (profiles/r05af); HBX_K3_PSETS=2 for A/B
+  uint32_t k3_psets = 3;
   // at join lag 2, preplan on the cut stream (mode 3; HBX_PLAN_CUT=0: mode 1,
   // the plan on the hash stream): +2.7 % with K3P (profiles/r05e)
   // 2 (default): at lag 3 and 4 too, off the scan loop (8 files per GPU, K3

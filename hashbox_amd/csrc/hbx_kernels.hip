@@ -1209,8 +1209,8 @@ __device__ __forceinline__ K3Group k3_group(const OrderEntry* __restrict__ order
 // The producer's side of one group: the stages S, S+1, .. of Rr blocks of the
 // wave's 64 chains, lane l's chain message stream starting at `src` (16-B
 // loads at any byte offset, as md5_coop).  Returns the group's stage count.
-// SETS register sets of loads in flight (2, or 3 for A/B: HBX_K3_PSETS=3,
-// one stage more of memory latency hidden).
+// SETS register sets of loads in flight (3 by default: one stage more of
+// memory latency hidden than 2, HBX_K3_PSETS=2 for A/B).
 template <int SETS = 2>
 __device__ __forceinline__ uint32_t k3p_produce(uint8_t* wl, uint32_t* flags, uint32_t S, uint64_t src, uint32_t Rr) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -1408,7 +1408,7 @@ __device__ __forceinline__ void k3q_push(uint32_t* __restrict__ qc, uint64_t* __
 
 // The producer wave of pair `flags`: the same groups as its MD5 wave; for a
 // group on the cooperative path (R >= kCoopMinBudget), the stages of blocks
-// next+1 .. next+R-1 of its 64 chains, two register sets in flight.
+// next+1 .. next+R-1 of its 64 chains, SETS register sets in flight.
 template <int SETS>
 __device__ void k3p_producer(uint8_t* wl, uint32_t* flags, const OrderEntry* __restrict__ order,
                              const uint32_t* __restrict__ n_order, uint32_t budget, uint32_t g0, uint32_t nwaves) {
