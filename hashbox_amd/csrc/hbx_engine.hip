@@ -469,11 +469,11 @@ Batch* acquire_batch(hbx_ctx* c) {
   return b;
 }
 
+uint32_t side_lds(const hbx_ctx* c, uint32_t own);
+
 // K4 + D2H of one batch whose chains are all hashed, on the result stream
 // (after the finalizing K3's completion event), so the hash stream goes straight on with the next plan
 // and K3 launch.
-uint32_t side_lds(const hbx_ctx* c, uint32_t own);
-
 int finalize_batch(hbx_ctx* c, Batch* b) {
   hipStream_t s = c->rstream;
   b->finalized = true;
