@@ -212,7 +212,6 @@ struct hbx_ctx {
   // the batch meta reaches the device by hbx_meta_fetch, a kernel on the scan
   // stream, instead of an SDMA copy (HBX_META_KERNEL=0 for A/B)
   uint32_t meta_kernel = 1;
-  uint32_t side_pad = 0;  // side kernels kept off K3's CUs by LDS padding (HBX_SIDE_PAD, A/B)
   // K1's LDS image transposed per 1 KiB: its per-lane reads become
   // conflict-free (SQ_LDS_BANK_CONFLICT 1.0e8 -> 0 per launch), K1 beside K3
   // 3.26 -> 3.19 ms per 8 GiB (profiles/r05ab); HBX_K1_SWZ=0 for the old image
@@ -469,8 +468,6 @@ Batch* acquire_batch(hbx_ctx* c) {
   return b;
 }
 
-uint32_t side_lds(const hbx_ctx* c, uint32_t own);
-
 // K4 + D2H of one batch whose chains are all hashed, on the result stream
 // (after the finalizing K3's completion event), so the hash stream goes straight on with the next plan
 // and K3 launch.
@@ -487,7 +484,7 @@ int finalize_batch(hbx_ctx* c, Batch* b) {
     const uint64_t* d_cb = b->d_meta.as<uint64_t>() + 3 * n;
     {
       StageTimer t(c, s, 4);
-      hipLaunchKernelGGL(hbx_k4_content_id, dim3((uint32_t)n), dim3(64), side_lds(c, 0), s,
+      hipLaunchKernelGGL(hbx_k4_content_id, dim3((uint32_t)n), dim3(64), 0, s,
                          (uint32_t)n, d_cb, b->count_d(), b->ids_d(), reinterpret_cast<uint32_t*>(b->res(b->rl.cid)),
                          reinterpret_cast<int32_t*>(b->res(b->rl.ctype)), c->k4_window);
     }
@@ -526,14 +523,6 @@ int ensure_plan_buffers(hbx_ctx* c, uint64_t extra);
 //   (whose chains it adds) and before batch j's K2: neither the scan stream
 //   nor the hash stream waits for it, and the hash stream carries nothing but
 //   K3 launches.
-// Side-kernel LDS padding (c->side_pad, A/B): dynamic LDS so that K2, K2r,
-// the plan, K4 and the meta fetch (`own` bytes of static LDS) need more than
-// the 24 KiB a K3P workgroup leaves free on its CU but fit beside a K1 tile
-// (~31 KiB free): they then never share a SIMD with an MD5 wave.
-uint32_t side_lds(const hbx_ctx* c, uint32_t own) {
-  return c->side_pad ? (25u << 10) - std::min(own, 25u << 10) : 0u;
-}
-
 // The blocks per chain of one K3 launch for a per-submit slice `budget`.
 uint32_t launch_budget(const hbx_ctx* c, uint32_t budget) {
   if (budget == kBudgetAll || c->k3_period <= 1) return budget;
@@ -619,7 +608,7 @@ int plan_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
       HBX_TRY(c, hipEventRecord(t.a, s));
       if (c->plan_zeroed_on != s) HBX_TRY(c, hipMemsetAsync(c->d_plan.p, 0, 2 * kPlanBins * sizeof(uint32_t), s));
       for (uint32_t phase = 0; phase < 2; phase++)
-        hipLaunchKernelGGL(hbx_k2c_plan, dim3(kPlanGroups), dim3(kPlanThreads), side_lds(c, 8 << 10), s,
+        hipLaunchKernelGGL(hbx_k2c_plan, dim3(kPlanGroups), dim3(kPlanThreads), 0, s,
                            has_prev ? c->d_order[ps].as<OrderEntry>() : nullptr,
                            has_prev ? c->d_octl[ps].as<uint32_t>() : nullptr, c->last_budget,
                            fs, budget, c->d_order[slot].as<OrderEntry>(), c->d_octl[slot].as<uint32_t>(),
@@ -647,7 +636,7 @@ int plan_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
     StageTimer t(c, s, 2);
     HBX_TRY(c, hipMemsetAsync(c->d_plan.p, 0, 2 * kPlanBins * sizeof(uint32_t), s));
     for (uint32_t phase = 0; phase < 2; phase++)
-      hipLaunchKernelGGL(hbx_k2c_plan, dim3(kPlanGroups), dim3(kPlanThreads), side_lds(c, 8 << 10), s,
+      hipLaunchKernelGGL(hbx_k2c_plan, dim3(kPlanGroups), dim3(kPlanThreads), 0, s,
                          has_prev ? c->d_order[ps].as<OrderEntry>() : nullptr,
                          has_prev ? c->d_octl[ps].as<uint32_t>() : nullptr, c->last_budget,
                          fs, budget, c->d_order[slot].as<OrderEntry>(), c->d_octl[slot].as<uint32_t>(),
@@ -986,7 +975,7 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   if (int frc = flush_input_wait(c)) return frc;  // (no launch this submit: nothing flushed it yet)
   if (c->meta_kernel) {  // meta_bytes is a multiple of 16
     const uint32_t n16 = (uint32_t)(meta_bytes / 16);
-    hipLaunchKernelGGL(hbx_meta_fetch, dim3(std::min<uint32_t>(64, (n16 + 255) / 256)), dim3(256), side_lds(c, 0), s,
+    hipLaunchKernelGGL(hbx_meta_fetch, dim3(std::min<uint32_t>(64, (n16 + 255) / 256)), dim3(256), 0, s,
                        static_cast<const uint4*>(b->h_meta.p), b->d_meta.as<uint4>(), n16);
     HBX_TRY(c, hipGetLastError());
   } else {
@@ -1027,7 +1016,7 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   if (s2 != s) HBX_TRY(c, hipStreamWaitEvent(s2, b->ev[1], 0));
   {
     StageTimer t(c, s2, 1, !lean);
-    hipLaunchKernelGGL(hbx_k2_cut_chain, dim3((uint32_t)n), dim3(64), side_lds(c, 0), s2, arena, d_off, d_len,
+    hipLaunchKernelGGL(hbx_k2_cut_chain, dim3((uint32_t)n), dim3(64), 0, s2, arena, d_off, d_len,
                        d_sb, ssum.as<uint2>(), d_cb, b->cuts_d(), b->count_d(),
                        lean ? b->d_fcnt.as<uint32_t>() : nullptr);
   }
@@ -1041,8 +1030,7 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   c->ssum_used[slot] = true;
   // K2r: the batch's chains and their order entries (lean: K2 zeroed the count)
   if (!lean) HBX_TRY(c, hipMemsetAsync(b->d_fcnt.p, 0, 4, s2));
-  hipLaunchKernelGGL(hbx_k2r_new_chains, dim3((uint32_t)((n * kPlanLanesPerFile + 255) / 256)), dim3(256),
-                     side_lds(c, 0), s2,
+  hipLaunchKernelGGL(hbx_k2r_new_chains, dim3((uint32_t)((n * kPlanLanesPerFile + 255) / 256)), dim3(256), 0, s2,
                      (uint32_t)n, arena, d_off, d_cb, b->cuts_d(), b->count_d(), b->ids_d(), b->d_run.as<Chain>(), b->d_fresh.as<OrderEntry>(),
                      b->d_fcnt.as<uint32_t>());
   HBX_TRY(c, hipGetLastError());
@@ -1317,7 +1305,6 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = ab_env("HBX_K3_PROD")) c->k3_prod = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_PLAN_CUT")) c->plan_cut = (uint32_t)std::min(2, std::max(0, std::atoi(v)));
   if (const char* v = ab_env("HBX_META_KERNEL")) c->meta_kernel = std::atoi(v) ? 1u : 0u;
-  if (const char* v = ab_env("HBX_SIDE_PAD")) c->side_pad = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_PSETS")) c->k3_psets = std::atoi(v) == 3 ? 3u : 2u;
   if (const char* v = ab_env("HBX_K1_SWZ")) c->k1_swz = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_ITEMS")) c->k3_items = (uint32_t)std::min(8, std::max(0, std::atoi(v)));
@@ -1445,11 +1432,11 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
       "{\"ab_env\": %d, \"md5_slice\": %u, \"join_lag\": %u, \"tile_iters\": %u, \"k1_gate\": %u, "
       "\"md5_wgs\": %u, \"plan_mode\": %d, \"k2_own\": %d, \"k4_window\": %u, \"k3_probe\": %d, "
       "\"lean_marks\": %u, \"k3_prod\": %u, \"k3_items\": %u, \"k3_period\": %u, \"meta_kernel\": %u, "
-      "\"plan_cut\": %u, \"k1_swz\": %u, \"k3_psets\": %u, \"side_pad\": %u, \"k8_split_streams\": %llu, "
+      "\"plan_cut\": %u, \"k1_swz\": %u, \"k3_psets\": %u, \"k8_split_streams\": %llu, "
       "\"k8_split_fallbacks\": %llu}",
       (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_gate, c->md5_wgs,
       plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks, c->k3_prod, c->k3_items,
-      c->k3_period, c->meta_kernel, c->plan_cut, c->k1_swz, c->k3_psets, c->side_pad,
+      c->k3_period, c->meta_kernel, c->plan_cut, c->k1_swz, c->k3_psets,
       (unsigned long long)c->k8_split_streams, (unsigned long long)c->k8_split_fallbacks);
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }
