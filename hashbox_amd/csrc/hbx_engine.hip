@@ -212,12 +212,6 @@ struct hbx_ctx {
   // the batch meta reaches the device by hbx_meta_fetch, a kernel on the scan
   // stream, instead of an SDMA copy (HBX_META_KERNEL=0 for A/B)
   uint32_t meta_kernel = 1;
-  // a submit's K3 launch finalizes batches (K4 + D2H on the result stream):
-  // that host work is deferred until the submit's own scan work is enqueued
-  // (fin_q), so a launch step does not hold back the next K1 (HBX_DEFER_FIN)
-  uint32_t defer_fin_on = 1;
-  bool defer_fin = false;
-  std::vector<std::pair<Batch*, uint64_t>> fin_q;
   // K1's LDS image transposed per 1 KiB: its per-lane reads become
   // conflict-free (SQ_LDS_BANK_CONFLICT 1.0e8 -> 0 per launch), K1 beside K3
   // 3.26 -> 3.19 ms per 8 GiB (profiles/r05ab); HBX_K1_SWZ=0 for the old image
@@ -726,32 +720,10 @@ int md5_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
         forked = true;
       }
       b->final_launch = L;
-      if (c->defer_fin) {  // (complete on the device after L; results enqueued by flush_finalize)
-        b->finalized = true;
-        c->fin_q.emplace_back(b, L);
-        continue;
-      }
       int rc = finalize_batch(c, b);
       if (rc) return rc;
     }
   }
-  return HBX_OK;
-}
-
-// The finalizations a submit deferred (md5_launch with c->defer_fin), in
-// launch order: the result stream waits for each launch's completion event
-// once, then K4 + D2H per batch, as md5_launch would have enqueued them.
-int flush_finalize(hbx_ctx* c) {
-  c->defer_fin = false;
-  uint64_t forked = ~0ull;
-  for (const auto& f : c->fin_q) {
-    if (f.second != forked && c->rstream != c->hstream) {
-      HBX_TRY(c, hipStreamWaitEvent(c->rstream, c->order_free[f.second % kDoneRing], 0));
-      forked = f.second;
-    }
-    if (int rc = finalize_batch(c, f.first)) return rc;
-  }
-  c->fin_q.clear();
   return HBX_OK;
 }
 
@@ -844,8 +816,6 @@ int ensure_plan_buffers(hbx_ctx* c, uint64_t extra) {
 // in the carried order lists) and the context refuses further pipelined work.
 int submit_abort(hbx_ctx* c, Batch* b, int rc, bool enqueued) {
   const std::string keep = c->err;
-  c->defer_fin = false;  // (a failed submit's deferred finalizations are dropped: the context breaks below)
-  if (enqueued) c->fin_q.clear();
   for (auto it = c->unjoined.begin(); it != c->unjoined.end(); ++it)
     if (*it == b) {
       c->unjoined.erase(it);
@@ -982,7 +952,6 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   // enqueued (plan on the scan stream) before this batch's K1, so it never
   // waits for this batch's scan
   const uint64_t launches0 = c->launches;
-  c->defer_fin = c->defer_fin_on && c->rstream != c->hstream;
   int rc = md5_step(c, budget);
   if (!rc) rc = preplan(c, budget);
   if (rc) return rc;
@@ -991,7 +960,7 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
     for (int i = 0; i < 4; i++) HBX_TRY(c, hipEventRecord(b->ev[i], s));
     b->finalized = true;
     HBX_TRY(c, hipEventRecord(b->ev[4], s));
-    return flush_finalize(c);
+    return HBX_OK;
   }
   const uint64_t nt = c->h_tiles.size();
   uint64_t* hm = b->h_meta.as<uint64_t>();
@@ -1034,14 +1003,14 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   hipStream_t s2 = c->cstream;
   const bool lean = c->lean_marks && s2 == s;
   HBX_TRY(c, hipEventRecord(b->ev[0], s));
-  if (nt) {  // (lean: timed by ev[0] | ev[1], whichever stream K2 takes)
-    StageTimer t(c, s, 0, !c->lean_marks);
+  if (nt) {
+    StageTimer t(c, s, 0, !lean);
     hipLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3((uint32_t)nt), dim3(kK1Threads), 0, s, arena, d_off, d_len,
                        d_sb, d_tiles, ssum.as<uint2>(), slices, c->k1_swz);
   }
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(b->ev[1], s));
-  if (c->lean_marks && nt) c->open_t.push_back(TimedLaunch{b->ev[0], b->ev[1], 0, false});
+  if (lean && nt) c->open_t.push_back(TimedLaunch{b->ev[0], b->ev[1], 0, false});
   // K2 on the cut stream: the scan stream goes straight on with the next
   // batch's K1 (into the other summary slot)
   if (s2 != s) HBX_TRY(c, hipStreamWaitEvent(s2, b->ev[1], 0));
@@ -1074,7 +1043,7 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
     HBX_TRY(c, hipEventRecord(b->ev[2], s2));
   }
   c->unjoined.push_back(b);
-  return flush_finalize(c);  // the launch's K4 + D2H, now that this batch's scan is enqueued
+  return HBX_OK;
 }
 
 int submit_verify_launch(hbx_ctx* c, Batch* b, const uint8_t* arena, uint64_t n, const uint64_t* offs,
@@ -1336,7 +1305,6 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = ab_env("HBX_K3_PROD")) c->k3_prod = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_PLAN_CUT")) c->plan_cut = (uint32_t)std::min(2, std::max(0, std::atoi(v)));
   if (const char* v = ab_env("HBX_META_KERNEL")) c->meta_kernel = std::atoi(v) ? 1u : 0u;
-  if (const char* v = ab_env("HBX_DEFER_FIN")) c->defer_fin_on = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_PSETS")) c->k3_psets = std::atoi(v) == 3 ? 3u : 2u;
   if (const char* v = ab_env("HBX_K1_SWZ")) c->k1_swz = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_ITEMS")) c->k3_items = (uint32_t)std::min(8, std::max(0, std::atoi(v)));
@@ -1464,11 +1432,11 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
       "{\"ab_env\": %d, \"md5_slice\": %u, \"join_lag\": %u, \"tile_iters\": %u, \"k1_gate\": %u, "
       "\"md5_wgs\": %u, \"plan_mode\": %d, \"k2_own\": %d, \"k4_window\": %u, \"k3_probe\": %d, "
       "\"lean_marks\": %u, \"k3_prod\": %u, \"k3_items\": %u, \"k3_period\": %u, \"meta_kernel\": %u, "
-      "\"plan_cut\": %u, \"k1_swz\": %u, \"k3_psets\": %u, \"defer_fin\": %u, \"k8_split_streams\": %llu, "
+      "\"plan_cut\": %u, \"k1_swz\": %u, \"k3_psets\": %u, \"k8_split_streams\": %llu, "
       "\"k8_split_fallbacks\": %llu}",
       (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_gate, c->md5_wgs,
       plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks, c->k3_prod, c->k3_items,
-      c->k3_period, c->meta_kernel, c->plan_cut, c->k1_swz, c->k3_psets, c->defer_fin_on,
+      c->k3_period, c->meta_kernel, c->plan_cut, c->k1_swz, c->k3_psets,
       (unsigned long long)c->k8_split_streams, (unsigned long long)c->k8_split_fallbacks);
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }

@@ -405,11 +405,10 @@ def test_pipelined_steady_state(oracle, join_lag):
             _check(a, r)
 
 
-@pytest.mark.parametrize("defer", ["1", "0"])
 @pytest.mark.parametrize("period,md5_slice,join_lag,plan_cut,meta", [
     (2, 16384, 1, "1", "1"), (3, 16384, 2, "1", "1"), (4, 8192, 2, "0", "0"), (3, 4096, 3, "1", "1"),
     (4, 8192, 3, "2", "1"), (8, 9, 2, "1", "1"), (5, 3, 1, "1", "0"), (4, 0, 2, "1", "1"), (1, 4096, 3, "2", "1")])
-def test_k3_period(oracle, monkeypatch, period, md5_slice, join_lag, plan_cut, meta, defer):
+def test_k3_period(oracle, monkeypatch, period, md5_slice, join_lag, plan_cut, meta):
     """K3 period (hbx_set_k3_period): one K3 launch every `period` submits
     with period x the slice per chain, several batches joining one plan (the
     planner's fresh-list set), in a deep pipeline as bench.py drives it, then
@@ -423,7 +422,6 @@ def test_k3_period(oracle, monkeypatch, period, md5_slice, join_lag, plan_cut, m
     monkeypatch.setenv("HBX_AB", "1")
     monkeypatch.setenv("HBX_PLAN_CUT", plan_cut)
     monkeypatch.setenv("HBX_META_KERNEL", meta)
-    monkeypatch.setenv("HBX_DEFER_FIN", defer)  # 0: a launch's K4 + D2H enqueued before the submit's scan
     batches = _device_batches(oracle, 3, 83 + period)
     got, order = [], []
     with Engine(0, md5_slice=md5_slice, join_lag=join_lag, k3_period=period) as e:
