@@ -116,7 +116,7 @@ def parse():
                          "/ batch lifetime (the longest chunk's serial MD5)")
     ap.add_argument("--join-lag", type=int, default=0,
                     help="submits between a batch's own and the K3 launch its chains join "
-                         "(hbx_set_join_lag; 0 = auto: 3 below 64 files per GPU, else 1)")
+                         "(hbx_set_join_lag; 0 = auto: 2)")
     ap.add_argument("--k3-period", type=int, default=0,
                     help="one K3 launch every P submits with P x the slice (hbx_set_k3_period, 1..8; 0 = auto: "
                          "1 at 32 or more files per GPU, else 4 (or 2) if it divides --steps)")
@@ -576,13 +576,14 @@ def residency_plan(files, file_mib, world, rank, scaling="strong", free_bytes=0,
     if not lens:
         raise ValueError(f"rank {rank} has no files: --files {files} < world {world}")
     nf = len(lens)
-    # small per-GPU batches (strong scaling) are scan-latency-bound at lag 1:
-    # lag 3 plans each launch a step ahead (tools/gpu_pipe_sweep.sh: 8 files
-    # 1,576 -> 1,976 GiB/s, 16 files 1,752 -> 2,185).  At 64 files, since
-    # round 5, lag 2: with K3P the launch is shorter than the lag-1 scan loop
-    # (gate -> K1 -> K2 -> K2r -> plan), and at lag 2 the plan runs ahead on
-    # the cut stream (plan mode 3): 2,326 vs 2,280-2,292 GiB/s (profiles/r05f)
-    lag = join_lag if join_lag > 0 else (3 if nf < 64 else 2)
+    # lag 2 at every batch size (round 5): the next launch is planned ahead on
+    # the cut stream (plan mode 3), so neither loop waits for a K2.  At 64
+    # files with K3P the launch is shorter than the lag-1 scan loop (gate ->
+    # K1 -> K2 -> K2r -> plan): 2,326 vs 2,280-2,292 GiB/s (profiles/r05f);
+    # below 64 files lag 2 beat lag 3 (the round-2 choice, when lag 2 planned
+    # on the hash stream) by 0.4 % at 8 files in three pairs, 0.1-0.4 % at
+    # 16 and 0.4-0.5 % at 32 (profiles/r05ak, r05al)
+    lag = join_lag if join_lag > 0 else 2
     if k3_period > 0:
         per = k3_period
     else:  # small per-GPU batches: the launch's fixed start-up and tail once per 4 steps

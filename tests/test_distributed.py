@@ -101,7 +101,7 @@ def test_residency_plan_per_world(world, scaling):
         nf = P["files_per_gpu"]
         assert per == (1 if nf >= 32 else 4), P
         assert P["hbm_bytes"] <= 0.95 * free
-        assert P["join_lag"] == (3 if P["files_per_gpu"] < 64 else 2)
+        assert P["join_lag"] == 2
         seen.extend(P["mine"])
         host += bench.check_host_bytes(P)
     if scaling == "strong":
@@ -152,7 +152,7 @@ def test_bench_plan_world4_through_torchrun():
 def test_bench_plan_default_is_strong(world):
     """The default multi-GPU mode is BASELINE configs[2]: each step's 64 files
     split across the ranks by LPT (strong scaling), the N = 8 operating point
-    the driver's scaling run hits (8 files per rank, join lag 3)."""
+    the driver's scaling run hits (8 files per rank, join lag 2, K3 period 4)."""
     import json
     r = _bench_plan(world, [])
     assert r.returncode == 0, r.stderr[-2000:]
@@ -164,7 +164,7 @@ def test_bench_plan_default_is_strong(world):
     assert all(p["files_per_gpu"] == 64 // world for p in plans)
     assert all(p["need"] * p["k3_period"] + p["join_lag"] + p["k3_period"] - 1 <= p["R"] for p in plans)
     if world == 8:
-        assert all(p["join_lag"] == 3 and p["lead"] == 4 and p["k3_period"] == 4 for p in plans)
+        assert all(p["join_lag"] == 2 and p["lead"] == 3 and p["k3_period"] == 4 for p in plans)
 
 
 def test_bench_plan_weak_opt_in():
