@@ -686,6 +686,11 @@ def main():
     run(a, S, rank, world, local_world, dist, dev, red_dev)
 
 
+def corpus_file_ids(a, P, rank):
+    """Job file ids of this rank's files (workloads.fill_batch)."""
+    return [int(j) for j in P["mine"]] if a.scaling == "strong" else [int(j) + a.files * rank for j in P["mine"]]
+
+
 def setup(a, rank, world, local_world, ndev, dev_idx, dev):
     """Everything a rank prepares before the first barrier: its plan, arenas
     and engine (with every pipeline buffer reserved)."""
@@ -710,10 +715,12 @@ def setup(a, rank, world, local_world, ndev, dev_idx, dev):
     threads = a.cpu_threads or cores["usable"]
     if world > 1:  # ranks share the host's cores for the oracle check
         threads = max(1, threads // local_world)
-    # every rank generates its own share of the corpus from its own seed
-    # (seed + 7919 rank): strong scaling splits each step's file count, not
-    # one generated corpus
-    arenas = W.random_arenas(P["physical_arenas"], total, a.seed + 7919 * rank, dev, single=a.single_alloc)
+    # one job corpus: file j of resident batch b has bytes from seed (seed, b,
+    # j) on whichever rank holds it, so strong scaling splits the same files a
+    # one-GPU run hashes (workloads.fill_batch); weak scaling gives every rank
+    # job files of its own (j + files x rank)
+    file_ids = corpus_file_ids(a, P, rank)
+    arenas = W.corpus_arenas(P["physical_arenas"], total, offs, lens, file_ids, a.seed, dev, single=a.single_alloc)
     if a.alias_depth > 0:  # diagnostics: D in flight over the physical arenas
         arenas = [arenas[i % P["physical_arenas"]] for i in range(R)]
     ballast = torch.zeros(int(a.ballast_gib * GIB), dtype=torch.uint8, device=dev) if a.ballast_gib else None
@@ -841,9 +848,7 @@ def run(a, S, rank, world, local_world, dist, dev, red_dev):
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.e2e:
         # rebuild the random batch 0 (the arenas may hold the Zipf corpus now)
-        g = torch.Generator(device=dev)
-        g.manual_seed(a.seed)
-        arenas[0].random_(0, 256, generator=g)
+        W.fill_batch(arenas[0], 0, offs, lens, corpus_file_ids(a, P, rank), a.seed)
         k = min(a.cpu_files, nf)
         host = arenas[0][:int(offs[k - 1]) + lens[k - 1]].cpu().numpy()
         cpu = cpu_baseline([host[int(offs[i]):int(offs[i]) + lens[i]] for i in range(k)], threads, cores)
@@ -878,10 +883,11 @@ def run(a, S, rank, world, local_world, dist, dev, red_dev):
                    "scan_lead": lead, "join_lag": lag, "k3_period": per,
                    "parallelism": f"file-sharded x{world} ({a.scaling} scaling; independent HIP streams, "
                                   "no data-path collective)",
-                   "seeds": f"each rank generates its own share on its device: random arenas seed {a.seed} + "
-                            f"7919 x rank, Zipf corpus seed {a.seed + 4} + 7919 x rank"
-                            + (" (strong scaling splits each step's file count, not one corpus)"
-                               if world > 1 and a.scaling == "strong" else "")},
+                   "seeds": f"one job corpus generated on the devices: file j of resident batch b from seed "
+                            f"({a.seed}, b, j) on whichever rank holds it"
+                            + (", so the ranks split the files a one-GPU run hashes" if a.scaling == "strong"
+                               else ", j + files x rank under weak scaling")
+                            + f"; Zipf corpus seed {a.seed + 4} + 7919 x rank"},
     }
     out.update({k: v for k, v in head.items() if k not in ("value", "ms_per_step")})
     out["single_batch"] = {"ms": round(float(latency[4]), 3),

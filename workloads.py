@@ -53,6 +53,41 @@ def random_arenas(count: int, total: int, seed: int, device, single: bool = Fals
     return out
 
 
+def corpus_seed(seed: int, batch: int, file: int) -> int:
+    """Generator seed of job file `file` of resident batch `batch`."""
+    return (seed * 1_000_003 + batch * 65_537 + file) & 0x7FFFFFFFFFFFFFFF
+
+
+def fill_batch(arena, batch: int, offs: Sequence[int], lens: Sequence[int], file_ids: Sequence[int],
+               seed: int) -> None:
+    """Write the files of one resident batch: file k (job file file_ids[k])
+    gets uniform random bytes from its own generator, seeded by (seed, batch,
+    job file), so a job file's bytes do not depend on which rank holds it or
+    how many ranks share the step (strong scaling splits ONE corpus).  The
+    padding between files is left as allocated: no result depends on it."""
+    import torch
+    g = torch.Generator(device=arena.device)
+    for o, n, j in zip(offs, lens, file_ids):
+        g.manual_seed(corpus_seed(seed, batch, int(j)))
+        arena[int(o):int(o) + int(n)].random_(0, 256, generator=g)
+
+
+def corpus_arenas(count: int, total: int, offs: Sequence[int], lens: Sequence[int], file_ids: Sequence[int],
+                  seed: int, device, single: bool = False) -> list:
+    """`count` resident batches of the job corpus (fill_batch), each in an
+    arena of `total` bytes (with `single`: views of one allocation, 2 MiB-aligned)."""
+    import torch
+    if single:
+        step = (total + (2 << 20) - 1) // (2 << 20) * (2 << 20)
+        big = torch.empty(step * count, dtype=torch.uint8, device=device)
+        out = [big[i * step:i * step + total] for i in range(count)]
+    else:
+        out = [torch.empty(total, dtype=torch.uint8, device=device) for _ in range(count)]
+    for b, t in enumerate(out):
+        fill_batch(t, b, offs, lens, file_ids, seed)
+    return out
+
+
 def zipf_fill(arenas: list, used: int, seed: int, fresh_p: float = 0.5, a: float = 1.1) -> float:
     """Overwrite bytes [0, used) of every arena with one Zipf-duplicated
     stream (configs[3] scheme).  Returns the repeat fraction: bytes of
