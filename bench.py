@@ -227,7 +227,7 @@ def oracle_check(arena, offs, lens, res, threads):
     return bool(ok)
 
 
-TRAFFIC_FILE = "profiles/r05y7_traffic.json"  # PMC FETCH_SIZE pass of the round-5 final tree (tools/profile_round.sh)
+TRAFFIC_FILE = "profiles/r05y8_traffic.json"  # PMC FETCH_SIZE pass of the round-5 final tree (tools/profile_round.sh)
 
 
 def measured_traffic(kernel, per_launch_bytes, batch_bytes):
