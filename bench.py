@@ -307,7 +307,7 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
     so the host collecting later never holds an arena back.  Returns
     timings, the window's launch counts and results."""
     order = deque()  # arena index of every pending batch, oldest first
-    state = {"j": 0, "t_sub": 0.0, "t_col": 0.0}
+    state = {"j": 0, "t_sub": 0.0, "t_col": 0.0, "subs": []}
     arena_res = {}
 
     def submit():
@@ -320,7 +320,9 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
         eng.submit_device(arenas[i].data_ptr(), offs, lens)
         order.append(i)
         state["j"] += 1
-        state["t_sub"] += time.perf_counter() - t
+        dt = time.perf_counter() - t
+        state["t_sub"] += dt
+        state["subs"].append(dt)
 
     def collect():
         t = time.perf_counter()
@@ -350,8 +352,10 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
         last = collect()
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
+    subs = np.array(state["subs"][-steps:]) * 1e3
     host = {"submit_ms": state["t_sub"] / steps * 1e3, "collect_ms": state["t_col"] / steps * 1e3,
-            "in_hbx_wait_ms": eng.wait_s / steps * 1e3}
+            "in_hbx_wait_ms": eng.wait_s / steps * 1e3,
+            "submit_ms_median_max": [round(float(np.median(subs)), 4), round(float(subs.max()), 4)]}
     if dist:
         dist.barrier()
     tot_ms, tot_n = eng.stage_totals()
@@ -541,7 +545,7 @@ def run_workload(a, name, eng, arenas, offs, lens, R, B, need, lanes, dist, gpu,
         "kernel_ms_per_step": {n: round(float(v) / a.steps, 4) for n, v in zip(KNAMES, tot_ms)},
         "window_launches": {n: int(v) for n, v in zip(KNAMES, tot_n)},
         # host time per step inside the window (rank 0's): submit, and collect (incl. any wait)
-        "host_ms_per_step": {k: round(v, 4) for k, v in r["host"].items()},
+        "host_ms_per_step": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r["host"].items()},
     }
     if r["probe"] is not None:
         out["k3_probe"] = r["probe"]
