@@ -41,7 +41,6 @@ Prints ONE JSON line on rank 0.  Multi-GPU:
 from __future__ import annotations
 
 import argparse
-import gc
 import json
 import os
 import sys
@@ -346,22 +345,13 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
     eng.stage_totals(reset=True)  # everything before the window is complete and harvested
     state["t_sub"] = state["t_col"] = 0.0
     eng.wait_s = 0.0
-    # the harness's own Python garbage collection stays out of the window: a
-    # full pass over the collected results took ~7 ms once in a 9 ms window of
-    # 20 steps at 8 files per GPU (profiles/r05ap: one submit at 7.3 ms, the
-    # median at 0.1 ms); nothing in the loop forms reference cycles
-    gc.collect()
-    gc.disable()
     t0 = time.perf_counter()
     last = None
-    try:
-        for _ in range(steps):
-            submit()
-            last = collect()
-        torch.cuda.synchronize(dev)
-        t1 = time.perf_counter()
-    finally:
-        gc.enable()
+    for _ in range(steps):
+        submit()
+        last = collect()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
     subs = np.array(state["subs"][-steps:]) * 1e3
     host = {"submit_ms": state["t_sub"] / steps * 1e3, "collect_ms": state["t_col"] / steps * 1e3,
             "in_hbx_wait_ms": eng.wait_s / steps * 1e3,
