@@ -298,6 +298,20 @@ def lane_occupancy(arena_res, R, B, need, lanes, period=1):
             "occupancy_max": round(max(active) / lanes, 4)}
 
 
+def cpu_throttle():
+    """(nr_throttled, throttled_usec) of this process's cgroup, or None: a
+    CPU quota that runs out stalls the host mid-window."""
+    for path, us in (("/sys/fs/cgroup/cpu.stat", "throttled_usec"), ("/sys/fs/cgroup/cpu/cpu.stat", None),
+                     ("/sys/fs/cgroup/cpu,cpuacct/cpu.stat", None)):
+        try:
+            st = dict(line.split() for line in open(path))
+        except (OSError, ValueError):
+            continue
+        t = int(st[us]) if us else int(st.get("throttled_time", 0)) // 1000
+        return int(st.get("nr_throttled", 0)), t
+    return None
+
+
 def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=None, aliased=False):
     """Fill to R in flight, W warm-up steps, K timed steps (submit one into
     the next arena of the ring, then collect the oldest batch), then the
@@ -307,7 +321,7 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
     so the host collecting later never holds an arena back.  Returns
     timings, the window's launch counts and results."""
     order = deque()  # arena index of every pending batch, oldest first
-    state = {"j": 0, "t_sub": 0.0, "t_col": 0.0, "subs": []}
+    state = {"j": 0, "t_sub": 0.0, "t_col": 0.0, "subs": [], "cols": []}
     arena_res = {}
 
     def submit():
@@ -329,7 +343,9 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
         i = order.popleft()
         res = eng.wait()
         arena_res[i] = res
-        state["t_col"] += time.perf_counter() - t
+        dt = time.perf_counter() - t
+        state["t_col"] += dt
+        state["cols"].append(dt)
         return i, res
 
     torch.cuda.synchronize(dev)
@@ -345,6 +361,7 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
     eng.stage_totals(reset=True)  # everything before the window is complete and harvested
     state["t_sub"] = state["t_col"] = 0.0
     eng.wait_s = 0.0
+    thr0 = cpu_throttle()
     t0 = time.perf_counter()
     last = None
     for _ in range(steps):
@@ -353,9 +370,15 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     subs = np.array(state["subs"][-steps:]) * 1e3
+    cols = np.array(state["cols"][-steps:]) * 1e3
     host = {"submit_ms": state["t_sub"] / steps * 1e3, "collect_ms": state["t_col"] / steps * 1e3,
             "in_hbx_wait_ms": eng.wait_s / steps * 1e3,
-            "submit_ms_median_max": [round(float(np.median(subs)), 4), round(float(subs.max()), 4)]}
+            "submit_ms_median_max": [round(float(np.median(subs)), 4), round(float(subs.max()), 4)],
+            "submit_slowest_step": int(subs.argmax()), "collect_ms_max": round(float(cols.max()), 4),
+            "collect_slowest_step": int(cols.argmax())}
+    thr1 = cpu_throttle()
+    if thr0 and thr1:
+        host["cpu_throttled_n_ms"] = [thr1[0] - thr0[0], round((thr1[1] - thr0[1]) / 1e3, 3)]
     if dist:
         dist.barrier()
     tot_ms, tot_n = eng.stage_totals()
