@@ -321,7 +321,7 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
     so the host collecting later never holds an arena back.  Returns
     timings, the window's launch counts and results."""
     order = deque()  # arena index of every pending batch, oldest first
-    state = {"j": 0, "t_sub": 0.0, "t_col": 0.0, "subs": [], "cols": []}
+    state = {"j": 0, "t_sub": 0.0, "t_col": 0.0, "subs": [], "cols": [], "parts": []}
     arena_res = {}
 
     def submit():
@@ -329,9 +329,11 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
         i = state["j"] % R
         if len(order) >= R and not aliased:  # arena i still holds the oldest pending batch
             eng.input_after_oldest()
+        t_a = time.perf_counter()
         if before_submit:
             before_submit(i)
         eng.submit_device(arenas[i].data_ptr(), offs, lens)
+        state["parts"].append((t_a - t, time.perf_counter() - t_a))
         order.append(i)
         state["j"] += 1
         dt = time.perf_counter() - t
@@ -374,7 +376,9 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
     host = {"submit_ms": state["t_sub"] / steps * 1e3, "collect_ms": state["t_col"] / steps * 1e3,
             "in_hbx_wait_ms": eng.wait_s / steps * 1e3,
             "submit_ms_median_max": [round(float(np.median(subs)), 4), round(float(subs.max()), 4)],
-            "submit_slowest_step": int(subs.argmax()), "collect_ms_max": round(float(cols.max()), 4),
+            "submit_slowest_step": int(subs.argmax()),
+            "slowest_submit_fence_call_ms": [round(x * 1e3, 4) for x in state["parts"][len(state["parts"]) - steps + int(subs.argmax())]],
+            "collect_ms_max": round(float(cols.max()), 4),
             "collect_slowest_step": int(cols.argmax())}
     thr1 = cpu_throttle()
     if thr0 and thr1:
