@@ -333,7 +333,7 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
         if before_submit:
             before_submit(i)
         eng.submit_device(arenas[i].data_ptr(), offs, lens)
-        state["parts"].append((t_a - t, time.perf_counter() - t_a))
+        state["parts"].append((t_a - t, getattr(eng, "alloc_s", 0.0), time.perf_counter() - t_a))
         order.append(i)
         state["j"] += 1
         dt = time.perf_counter() - t
@@ -377,7 +377,7 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
             "in_hbx_wait_ms": eng.wait_s / steps * 1e3,
             "submit_ms_median_max": [round(float(np.median(subs)), 4), round(float(subs.max()), 4)],
             "submit_slowest_step": int(subs.argmax()),
-            "slowest_submit_fence_call_ms": [round(x * 1e3, 4) for x in state["parts"][len(state["parts"]) - steps + int(subs.argmax())]],
+            "slowest_submit_fence_alloc_call_ms": [round(x * 1e3, 4) for x in state["parts"][len(state["parts"]) - steps + int(subs.argmax())]],
             "collect_ms_max": round(float(cols.max()), 4),
             "collect_slowest_step": int(cols.argmax())}
     thr1 = cpu_throttle()

@@ -226,7 +226,10 @@ class Engine:
         self._after_producer()
         offs = np.ascontiguousarray(offs, np.uint64)
         lens = np.ascontiguousarray(lens, np.uint64)
+        t0 = time.perf_counter()
         caps, base, cuts, ids, sums = self._alloc_out(lens)
+        t1 = time.perf_counter()
+        self.alloc_s = t1 - t0  # (bench diagnostics: host output arrays of this submit)
         self._check(self._L.hbx_submit_device(self._ctx, ctypes.c_void_p(int(d_arena)), len(lens),
                                               _p(offs), _p(lens), _p(cuts), _p(ids), _p(base),
                                               _p(caps), sums), "hbx_submit_device")

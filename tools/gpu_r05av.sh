@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5: the slow submit at step 13 of a 20-step window at 8 files: the GPU-side fence or the submit call?
 set -o pipefail
-O=gpurun_out/r05au
+O=gpurun_out/r05av
 mkdir -p $O
 run() {
   local n=$1; shift
@@ -12,3 +12,4 @@ print('$n', d['value'], d['host_ms_per_step'])"
 }
 run w5 --steps 20 --warmup 5 || exit 1
 
+MALLOC_MMAP_THRESHOLD_=1048576 run w5mmap --steps 20 --warmup 5 || exit 1
