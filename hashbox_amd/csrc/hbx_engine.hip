@@ -877,9 +877,31 @@ inline uint64_t scan_iters(uint64_t N) {  // K1 iterations of a file (0: no spli
 // collected by wait_oldest in submission order.  Every validation and
 // allocation happens before the batch joins the FIFO; a failure after that
 // removes it again (submit_abort), so a failed submit leaves no pending batch.
+// HBX_TRACE_SLOW_SUBMIT=<ms>: a submit slower than that prints where its host
+// time went (diagnostics for one-off host stalls; off by default).
+struct SlowSubmit {
+  double limit_ms = -1.0;
+  std::chrono::steady_clock::time_point t[6];
+  SlowSubmit() {
+    if (const char* v = std::getenv("HBX_TRACE_SLOW_SUBMIT")) limit_ms = std::atof(v);
+  }
+  void mark(int i) {
+    if (limit_ms >= 0) t[i] = std::chrono::steady_clock::now();
+  }
+  void report(uint64_t launches) {
+    if (limit_ms < 0) return;
+    auto ms = [&](int a, int b) { return std::chrono::duration<double, std::milli>(t[b] - t[a]).count(); };
+    if (ms(0, 5) < limit_ms) return;
+    std::fprintf(stderr, "hbx slow submit (launch %llu): %.3f ms = setup %.3f, buffers %.3f, md5_step %.3f, preplan %.3f, scan %.3f\n",
+                 (unsigned long long)launches, ms(0, 5), ms(0, 1), ms(1, 2), ms(2, 3), ms(3, 4), ms(4, 5));
+  }
+};
+static SlowSubmit g_slow;
+
 int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* offs,
                  const uint64_t* lens, uint64_t* cut_ends, uint8_t* ids, const uint64_t* out_base,
                  const uint64_t* caps, hbx_file_summary* sums, uint32_t budget) {
+  g_slow.mark(0);
   if (c->broken) return c->fail(HBX_ERR_STATE, "context is unusable after a failed submit; destroy it");
   if (n > 0xFFFFFFFFull) return c->fail(HBX_ERR_ARG, "too many files");
   for (uint64_t f = 0; f < n; f++)
@@ -928,6 +950,7 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
   // meta block: off | len | slice_base | cut_base | tiles
   const size_t meta_bytes = n * 8 * 4 + nt * sizeof(uint4);
   const int slot = c->ssum_slot;
+  g_slow.mark(1);
   if (n) {  // every allocation first: the batch is not in the FIFO yet
     int rc = HBX_OK;
     b->rl = res_layout(n, tcaps);
@@ -941,7 +964,10 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
     if (rc) return submit_abort(c, b, rc, false);
   }
   c->pending.push_back(b);
+  g_slow.mark(2);
   const int rc = submit_batch_launch(c, b, d_arena, n, offs, lens, budget, slices, meta_bytes, slot);
+  g_slow.mark(5);
+  g_slow.report(c->launches);
   return rc ? submit_abort(c, b, rc, true) : HBX_OK;
 }
 
@@ -953,7 +979,9 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   // waits for this batch's scan
   const uint64_t launches0 = c->launches;
   int rc = md5_step(c, budget);
+  g_slow.mark(3);
   if (!rc) rc = preplan(c, budget);
+  g_slow.mark(4);
   if (rc) return rc;
   const bool gate = c->k1_gate && c->launches != launches0 && c->hstream != s;
   if (n == 0) {
