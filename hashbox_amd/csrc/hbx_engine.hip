@@ -468,6 +468,30 @@ Batch* acquire_batch(hbx_ctx* c) {
   return b;
 }
 
+// HBX_TRACE_SLOW_SUBMIT=<ms>: a submit slower than that prints where its host
+// time went (diagnostics for one-off host stalls; off by default).
+struct SlowSubmit {
+  double limit_ms = -1.0;
+  std::chrono::steady_clock::time_point t[12];
+  SlowSubmit() {
+    if (const char* v = std::getenv("HBX_TRACE_SLOW_SUBMIT")) limit_ms = std::atof(v);
+  }
+  void mark(int i) {
+    if (limit_ms >= 0) t[i] = std::chrono::steady_clock::now();
+  }
+  void report(uint64_t launches) {
+    if (limit_ms < 0) return;
+    auto ms = [&](int a, int b) { return std::chrono::duration<double, std::milli>(t[b] - t[a]).count(); };
+    if (ms(0, 5) < limit_ms) return;
+    std::fprintf(stderr, "hbx slow submit (launch %llu): %.3f ms = setup %.3f, buffers %.3f, md5_step %.3f, preplan %.3f, scan %.3f"
+                 " | md5_launch: entry %.3f, k3 launch %.3f, record %.3f, finalize %.3f\n",
+                 (unsigned long long)launches, ms(0, 5), ms(0, 1), ms(1, 2), ms(2, 3), ms(3, 4), ms(4, 5),
+                 ms(2, 6), ms(6, 7), ms(7, 8), ms(8, 9));
+    for (int i = 6; i < 10; i++) t[i] = t[2];
+  }
+};
+static SlowSubmit g_slow;
+
 // K4 + D2H of one batch whose chains are all hashed, on the result stream
 // (after the finalizing K3's completion event), so the hash stream goes straight on with the next plan
 // and K3 launch.
@@ -676,6 +700,7 @@ int md5_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
     c->k3_open.push_back(L);
   }
   const uint32_t waves = c->md5_wgs * (kK3Threads / 64);
+  g_slow.mark(6);
   const uint32_t parts = c->k3_items && budget != kBudgetAll && budget >= 64u * c->k3_items ? c->k3_items : 0u;
   if (parts && !c->h_err.p) {
     HBX_TRY(c, c->h_err.ensure(64));
@@ -697,6 +722,7 @@ int md5_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
                        c->d_order[slot].as<OrderEntry>(), static_cast<const uint32_t*>(c->d_octl[slot].as<uint32_t>()),
                        budget, c->d_gate.as<uint32_t>(), c->k3_dispatched, c->k3_waves + waves - 1u, tslot,
                        c->h_probe.p ? c->h_probe.as<uint64_t>() : nullptr);
+  g_slow.mark(7);
   HBX_TRY(c, hipGetLastError());
   c->k3_dispatched += c->md5_wgs;
   c->k3_waves += waves;
@@ -704,6 +730,7 @@ int md5_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
   // the launch's one completion event: the plan three launches on waits for
   // it, and so does the result stream for the batches it completes
   HBX_TRY(c, hipEventRecord(c->order_free[L % kDoneRing], s));
+  g_slow.mark(8);
   c->launches++;
   if (budget == kBudgetAll)  // per-batch stage times of a synchronous batch (hbx_stage_times)
     for (Batch* nb : nbs) {
@@ -724,6 +751,7 @@ int md5_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
       if (rc) return rc;
     }
   }
+  g_slow.mark(9);
   return HBX_OK;
 }
 
@@ -877,27 +905,6 @@ inline uint64_t scan_iters(uint64_t N) {  // K1 iterations of a file (0: no spli
 // collected by wait_oldest in submission order.  Every validation and
 // allocation happens before the batch joins the FIFO; a failure after that
 // removes it again (submit_abort), so a failed submit leaves no pending batch.
-// HBX_TRACE_SLOW_SUBMIT=<ms>: a submit slower than that prints where its host
-// time went (diagnostics for one-off host stalls; off by default).
-struct SlowSubmit {
-  double limit_ms = -1.0;
-  std::chrono::steady_clock::time_point t[6];
-  SlowSubmit() {
-    if (const char* v = std::getenv("HBX_TRACE_SLOW_SUBMIT")) limit_ms = std::atof(v);
-  }
-  void mark(int i) {
-    if (limit_ms >= 0) t[i] = std::chrono::steady_clock::now();
-  }
-  void report(uint64_t launches) {
-    if (limit_ms < 0) return;
-    auto ms = [&](int a, int b) { return std::chrono::duration<double, std::milli>(t[b] - t[a]).count(); };
-    if (ms(0, 5) < limit_ms) return;
-    std::fprintf(stderr, "hbx slow submit (launch %llu): %.3f ms = setup %.3f, buffers %.3f, md5_step %.3f, preplan %.3f, scan %.3f\n",
-                 (unsigned long long)launches, ms(0, 5), ms(0, 1), ms(1, 2), ms(2, 3), ms(3, 4), ms(4, 5));
-  }
-};
-static SlowSubmit g_slow;
-
 int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* offs,
                  const uint64_t* lens, uint64_t* cut_ends, uint8_t* ids, const uint64_t* out_base,
                  const uint64_t* caps, hbx_file_summary* sums, uint32_t budget) {
