@@ -472,6 +472,7 @@ Batch* acquire_batch(hbx_ctx* c) {
 // time went (diagnostics for one-off host stalls; off by default).
 struct SlowSubmit {
   double limit_ms = -1.0;
+  double fin[3] = {0, 0, 0};  // finalize: K4 (+ its timing events), D2H copy, completion record
   std::chrono::steady_clock::time_point t[12];
   SlowSubmit() {
     if (const char* v = std::getenv("HBX_TRACE_SLOW_SUBMIT")) limit_ms = std::atof(v);
@@ -487,7 +488,17 @@ struct SlowSubmit {
                  " | md5_launch: entry %.3f, k3 launch %.3f, record %.3f, finalize %.3f\n",
                  (unsigned long long)launches, ms(0, 5), ms(0, 1), ms(1, 2), ms(2, 3), ms(3, 4), ms(4, 5),
                  ms(2, 6), ms(6, 7), ms(7, 8), ms(8, 9));
-    for (int i = 6; i < 10; i++) t[i] = t[2];
+    std::fprintf(stderr, "  finalize: k4 %.3f, d2h %.3f, record %.3f\n", fin[0], fin[1], fin[2]);
+  }
+  void clear() {
+    for (int i = 6; i < 10; i++) t[i] = t[0];
+    fin[0] = fin[1] = fin[2] = 0;
+  }
+  void lap(int k, std::chrono::steady_clock::time_point& a) {
+    if (limit_ms < 0) return;
+    const auto b = std::chrono::steady_clock::now();
+    fin[k] += std::chrono::duration<double, std::milli>(b - a).count();
+    a = b;
   }
 };
 static SlowSubmit g_slow;
@@ -503,6 +514,7 @@ int finalize_batch(hbx_ctx* c, Batch* b) {
     HBX_TRY(c, hipEventRecord(b->ev[4], s));
     return HBX_OK;
   }
+  auto lap = std::chrono::steady_clock::now();
   if (b->n) {
     const uint64_t n = b->n;
     const uint64_t* d_cb = b->d_meta.as<uint64_t>() + 3 * n;
@@ -513,10 +525,13 @@ int finalize_batch(hbx_ctx* c, Batch* b) {
                          reinterpret_cast<int32_t*>(b->res(b->rl.ctype)), c->k4_window);
     }
     HBX_TRY(c, hipGetLastError());
+    g_slow.lap(0, lap);
     // one copy for every result (5 copies before: each a dispatch on this stream)
     HBX_TRY(c, hipMemcpyAsync(b->h_res.p, b->d_res.p, b->rl.total, hipMemcpyDeviceToHost, s));
+    g_slow.lap(1, lap);
   }
   HBX_TRY(c, hipEventRecord(b->ev[4], s));
+  g_slow.lap(2, lap);
   return HBX_OK;
 }
 
@@ -909,6 +924,7 @@ int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* of
                  const uint64_t* lens, uint64_t* cut_ends, uint8_t* ids, const uint64_t* out_base,
                  const uint64_t* caps, hbx_file_summary* sums, uint32_t budget) {
   g_slow.mark(0);
+  g_slow.clear();
   if (c->broken) return c->fail(HBX_ERR_STATE, "context is unusable after a failed submit; destroy it");
   if (n > 0xFFFFFFFFull) return c->fail(HBX_ERR_ARG, "too many files");
   for (uint64_t f = 0; f < n; f++)
