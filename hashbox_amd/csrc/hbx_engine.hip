@@ -212,6 +212,9 @@ struct hbx_ctx {
   // the batch meta reaches the device by hbx_meta_fetch, a kernel on the scan
   // stream, instead of an SDMA copy (HBX_META_KERNEL=0 for A/B)
   uint32_t meta_kernel = 1;
+  // a finished batch's results reach the host by hbx_result_push, a kernel
+  // on the result stream, instead of an SDMA copy (HBX_D2H_KERNEL, A/B)
+  uint32_t d2h_kernel = 0;
   // K1's LDS image transposed per 1 KiB: its per-lane reads become
   // conflict-free (SQ_LDS_BANK_CONFLICT 1.0e8 -> 0 per launch), K1 beside K3
   // 3.26 -> 3.19 ms per 8 GiB (profiles/r05ab); HBX_K1_SWZ=0 for the old image
@@ -527,7 +530,14 @@ int finalize_batch(hbx_ctx* c, Batch* b) {
     HBX_TRY(c, hipGetLastError());
     g_slow.lap(0, lap);
     // one copy for every result (5 copies before: each a dispatch on this stream)
-    HBX_TRY(c, hipMemcpyAsync(b->h_res.p, b->d_res.p, b->rl.total, hipMemcpyDeviceToHost, s));
+    if (c->d2h_kernel && b->rl.total % 16 == 0) {
+      const uint64_t n16 = b->rl.total / 16;
+      hipLaunchKernelGGL(hbx_result_push, dim3((uint32_t)std::min<uint64_t>(c->d2h_kernel, (n16 + 255) / 256)),
+                         dim3(256), 0, s, b->d_res.as<uint4>(), static_cast<uint4*>(b->h_res.p), n16);
+      HBX_TRY(c, hipGetLastError());
+    } else {
+      HBX_TRY(c, hipMemcpyAsync(b->h_res.p, b->d_res.p, b->rl.total, hipMemcpyDeviceToHost, s));
+    }
     g_slow.lap(1, lap);
   }
   HBX_TRY(c, hipEventRecord(b->ev[4], s));
@@ -1353,6 +1363,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = ab_env("HBX_MD5_SLICE")) c->md5_slice = (uint32_t)std::max(0, std::atoi(v));
   if (const char* v = ab_env("HBX_K1_GATE")) c->k1_gate = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_LEAN_MARKS")) c->lean_marks = std::atoi(v) ? 1u : 0u;
+  if (const char* v = ab_env("HBX_D2H_KERNEL")) c->d2h_kernel = (uint32_t)std::min(std::max(std::atoi(v), 0), 1024);
   if (const char* v = ab_env("HBX_K3_PROD")) c->k3_prod = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_PLAN_CUT")) c->plan_cut = (uint32_t)std::min(2, std::max(0, std::atoi(v)));
   if (const char* v = ab_env("HBX_META_KERNEL")) c->meta_kernel = std::atoi(v) ? 1u : 0u;
@@ -1483,11 +1494,11 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
       "{\"ab_env\": %d, \"md5_slice\": %u, \"join_lag\": %u, \"tile_iters\": %u, \"k1_gate\": %u, "
       "\"md5_wgs\": %u, \"plan_mode\": %d, \"k2_own\": %d, \"k4_window\": %u, \"k3_probe\": %d, "
       "\"lean_marks\": %u, \"k3_prod\": %u, \"k3_items\": %u, \"k3_period\": %u, \"meta_kernel\": %u, "
-      "\"plan_cut\": %u, \"k1_swz\": %u, \"k3_psets\": %u, \"k8_split_streams\": %llu, "
+      "\"plan_cut\": %u, \"k1_swz\": %u, \"k3_psets\": %u, \"d2h_kernel\": %u, \"k8_split_streams\": %llu, "
       "\"k8_split_fallbacks\": %llu}",
       (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_gate, c->md5_wgs,
       plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks, c->k3_prod, c->k3_items,
-      c->k3_period, c->meta_kernel, c->plan_cut, c->k1_swz, c->k3_psets,
+      c->k3_period, c->meta_kernel, c->plan_cut, c->k1_swz, c->k3_psets, c->d2h_kernel,
       (unsigned long long)c->k8_split_streams, (unsigned long long)c->k8_split_fallbacks);
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }

@@ -1715,6 +1715,19 @@ extern "C" __global__ __launch_bounds__(256) void hbx_meta_fetch(const uint4* __
   }
 }
 
+// A finished batch's results (d_res) into its pinned host buffer, written by
+// this kernel on the result stream in place of hipMemcpyAsync (c->d2h_kernel):
+// an SDMA copy call held the submitting host thread ~7 ms once in a while
+// (profiles/r05ay: the D2H call inside finalize_batch).  `n` 16-B words; the
+// stores go over PCIe and are made visible to the host before the completion
+// event by a system-scope fence.
+extern "C" __global__ __launch_bounds__(256) void hbx_result_push(const uint4* __restrict__ src,
+                                                                  uint4* __restrict__ dst, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u)
+    __builtin_nontemporal_store(src[i], dst + i);
+  __threadfence_system();
+}
+
 // ContentBlockID (store.go:187-196), one wave per file.  The file's ids are
 // staged into LDS by all 64 lanes at once (kK4Window per round trip) and the
 // chain-block message is generated from there: the ids are read twice
