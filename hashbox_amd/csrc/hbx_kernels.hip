@@ -1724,7 +1724,7 @@ extern "C" __global__ __launch_bounds__(256) void hbx_meta_fetch(const uint4* __
 extern "C" __global__ __launch_bounds__(256) void hbx_result_push(const uint4* __restrict__ src,
                                                                   uint4* __restrict__ dst, uint64_t n) {
   for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u)
-    __builtin_nontemporal_store(src[i], dst + i);
+    dst[i] = src[i];
   __threadfence_system();
 }
 
