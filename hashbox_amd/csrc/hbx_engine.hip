@@ -213,8 +213,10 @@ struct hbx_ctx {
   // stream, instead of an SDMA copy (HBX_META_KERNEL=0 for A/B)
   uint32_t meta_kernel = 1;
   // a finished batch's results reach the host by hbx_result_push, a kernel
-  // on the result stream, instead of an SDMA copy (HBX_D2H_KERNEL, A/B)
-  uint32_t d2h_kernel = 0;
+  // on the result stream, instead of an SDMA copy (HBX_D2H_KERNEL=0 for A/B):
+  // the copy call held the host ~7 ms once per ~16 submits after a drain
+  // (profiles/r05az: 8-file 20-step window 1,395 -> 1,994-2,033 GiB/s)
+  uint32_t d2h_kernel = 64;  // workgroups (0 = SDMA copy)
   // K1's LDS image transposed per 1 KiB: its per-lane reads become
   // conflict-free (SQ_LDS_BANK_CONFLICT 1.0e8 -> 0 per launch), K1 beside K3
   // 3.26 -> 3.19 ms per 8 GiB (profiles/r05ab); HBX_K1_SWZ=0 for the old image
