@@ -587,17 +587,16 @@ ARENA_SLACK = 64 << 20  # per resident batch beyond its packed bytes (allocator 
 def residency_plan(files, file_mib, world, rank, scaling="strong", free_bytes=0, hbm_frac=0.95,
                    ranks_per_device=1, arenas=0, md5_slice=-1, join_lag=0, lead=-1, e2e=False,
                    alias_depth=0, k3_period=0, steps=0):
-    """The pipeline each rank runs, a pure function so the
-    CPU tests can check it for N = 1..8.  Files of the job: `files` x
-    `file_mib` MiB; strong scaling gives this rank its LPT share of each
-    step's files (independent files, store.go:84-199), weak a whole batch.
-    R batches stay resident (as many as `hbm_frac` of the free HBM holds),
-    each K3 launch advances every chain by B blocks, a batch needs `need`
-    launches and its chains join `lag` submits after its own:
-    need + lag <= R keeps the window free of forced drains.  With a K3 period
-    P (one launch every P submits, P x B blocks per chain each) a batch waits
-    up to lag + P - 1 submits to join and its launches are P submits apart:
-    need x P + lead + P - 1 <= R."""
+    """The pipeline each rank runs.  Files of the job:
+    `files` x `file_mib` MiB; strong scaling gives this rank its LPT share of
+    each step's files (independent files, store.go:84-199), weak a whole
+    batch.  The schedule itself (R resident batches, slice B, join lag, lead,
+    K3 period, launches per batch `need`) comes from the library's planner,
+    hbx_plan_pipeline (include/hbxgpu.h), so a cgo caller gets exactly the
+    plan this bench runs; tests/test_plan.py checks it against the round-5
+    Python planner at N = 1..8.  Pure host arithmetic (no GPU) for a given
+    free_bytes."""
+    from hashbox_amd import plan_pipeline
     from hashbox_amd.shard import lpt_assign
     import workloads as W
     fbytes = file_mib << 20
@@ -607,50 +606,22 @@ def residency_plan(files, file_mib, world, rank, scaling="strong", free_bytes=0,
     if not lens:
         raise ValueError(f"rank {rank} has no files: --files {files} < world {world}")
     nf = len(lens)
-    # lag 2 at every batch size (round 5): the next launch is planned ahead on
-    # the cut stream (plan mode 3), so neither loop waits for a K2.  At 64
-    # files with K3P the launch is shorter than the lag-1 scan loop (gate ->
-    # K1 -> K2 -> K2r -> plan): 2,326 vs 2,280-2,292 GiB/s (profiles/r05f);
-    # below 64 files lag 2 beat lag 3 (the round-2 choice, when lag 2 planned
-    # on the hash stream) by 0.4 % at 8 files in three pairs, 0.1-0.4 % at
-    # 16 and 0.4-0.5 % at 32 (profiles/r05ak, r05al)
-    lag = join_lag if join_lag > 0 else 2
-    if k3_period > 0:
-        per = k3_period
-    else:  # small per-GPU batches: the launch's fixed start-up and tail once per 4 steps
-        # (profiles/r05j, r05o: 8 files 2,013 -> 2,056-2,083 GiB/s, 16 files 2,206 -> 2,183-2,249; 32
-        # files P1 2,277-2,294 vs P2 2,260-2,272)
-        per = next((p for p in (4, 2) if steps <= 0 or steps % p == 0), 1) if nf < 32 and not e2e else 1
-    # (lead lag + P, so that the host's collect of the oldest batch never waits
-    # for the launch that finalized it, measured the same or 0.5-1 % slower:
-    # profiles/r05o)
-    ld = lead if lead >= 0 else lag + 1
     offs, total = W.pack_layout(lens)
-    # launches a batch needs before its chains are all hashed
-    nfull = (min(fbytes, 8 << 20) + 8) >> 6
-    r_fit = max(ld + 1, int(free_bytes * hbm_frac / max(1, ranks_per_device)) // (total + ARENA_SLACK))
-    if e2e:
-        r_fit = min(r_fit, ld + 2)  # PCIe-bound: a shallow pipeline suffices
-    def slice_for(R):  # launches of P x B blocks, P submits apart, within R - lead - (P - 1) submits
-        launches = max(1, (R - ld - per + 1) // per)
-        return -(-nfull // (launches * per))
-    if md5_slice < 0:
-        R = arenas if arenas > 0 else r_fit
-        B = slice_for(R)
+    req = dict(n_files=nf, arena_bytes=total, longest_file=max(lens), free_bytes=free_bytes, hbm_frac=hbm_frac,
+               ranks_per_device=ranks_per_device, steps=steps, arenas=arenas, md5_slice=md5_slice,
+               join_lag=join_lag, lead=lead, k3_period=k3_period, host_input=e2e)
+    if alias_depth > 0:  # diagnostics: D in flight over the physical arenas
+        p = plan_pipeline(**dict(req, arenas=alias_depth))
+        try:
+            physical = plan_pipeline(**req)["resident"]
+        except ValueError:  # too few physical arenas for a plan of their own
+            physical = arenas
     else:
-        B = md5_slice
-        R = arenas if arenas > 0 else min((1 if B == 0 else -(-nfull // (B * per))) * per + ld + per - 1, r_fit)
-    physical = R
-    if alias_depth > 0:  # diagnostics: D in flight over the R physical arenas
-        R = alias_depth
-        if md5_slice < 0:
-            B = slice_for(R)
-    need = 1 if B == 0 else -(-nfull // (B * per))  # K3 launches per batch
-    if need * per + lag + per - 1 > R:
-        raise ValueError(f"pipeline depth {R} < launches per batch {need} x period {per} + join lag {lag} + "
-                         f"{per - 1}: raise --arenas or the slice")
-    return {"mine": mine, "lens": lens, "files_per_gpu": nf, "join_lag": lag, "lead": ld, "offs": offs,
-            "arena_bytes": total, "R": R, "physical_arenas": physical, "B": B, "need": need, "k3_period": per,
+        p = plan_pipeline(**req)
+        physical = p["resident"]
+    return {"lib_plan": p, "mine": mine, "lens": lens, "files_per_gpu": nf, "join_lag": p["join_lag"], "lead": p["lead"],
+            "offs": offs, "arena_bytes": total, "R": p["resident"], "physical_arenas": physical,
+            "B": p["md5_slice"], "need": p["launches_per_batch"], "k3_period": p["k3_period"],
             "hbm_bytes": physical * (total + ARENA_SLACK), "file_bytes": fbytes}
 
 
@@ -756,12 +727,15 @@ def setup(a, rank, world, local_world, ndev, dev_idx, dev):
         arenas = [arenas[i % P["physical_arenas"]] for i in range(R)]
     ballast = torch.zeros(int(a.ballast_gib * GIB), dtype=torch.uint8, device=dev) if a.ballast_gib else None
     torch.cuda.synchronize(dev)
-    eng = Engine(dev_idx, md5_slice=B, join_lag=lag, k3_period=P["k3_period"])
+    eng = Engine(dev_idx)
     if a.k3_probe:  # the probe alone (hbx_set_k3_probe), no other HBX_* switch
         eng.set_k3_probe(True)
-    # every batch slot, chain table and summary buffer of the pipeline is
-    # allocated now: an allocation inside the timed region would drain the streams
-    eng.reserve(R + 2, len(lens), sum(lens))
+    # the library's plan (hbx_apply_plan): slice, join lag, K3 period, and every
+    # batch slot, chain table and summary buffer of the pipeline allocated now
+    # (an allocation inside the timed region would drain the streams)
+    eng.apply_plan(P["lib_plan"], len(lens), sum(lens))
+    k = eng.knobs()
+    assert (k["md5_slice"], k["join_lag"], k["k3_period"]) == (B, lag, P["k3_period"]), k
     for _ in range(2):  # single-batch latency (one batch alone, synchronous call), untimed
         eng.chunk_hash_device(arenas[0].data_ptr(), offs, lens)
     latency = eng.stage_times()

@@ -34,7 +34,7 @@ EXPORTS = [
     "hbx_wire_encode_id", "hbx_wire_encode_block_header", "hbx_wire_parse",
     "hbx_verify_submit_device", "hbx_inflate_blocks_device", "hbx_store_paths_zcb", "hbx_after_stream",
     "hbx_set_join_lag", "hbx_set_k3_period", "hbx_k3_wave_times", "hbx_input_after_oldest", "hbx_knobs",
-    "hbx_input_fence", "hbx_set_k3_probe", "hbx_store_paths_status",
+    "hbx_input_fence", "hbx_set_k3_probe", "hbx_store_paths_status", "hbx_plan_pipeline", "hbx_apply_plan",
 ]
 # Functions returning something other than an int status.
 _NON_STATUS = ("hbx_ctx_destroy", "hbx_last_error", "hbx_max_chunks", "hbx_file_entry_size",
@@ -62,6 +62,25 @@ class FileSummary(ctypes.Structure):
     _fields_ = [("content_id", ctypes.c_uint8 * 16), ("content_type", ctypes.c_int32),
                 ("n_chunks", ctypes.c_uint32)]
 
+
+class PlanRequest(ctypes.Structure):
+    """hbx_plan_request (include/hbxgpu.h)."""
+    _fields_ = [("n_files", ctypes.c_uint64), ("arena_bytes", ctypes.c_uint64), ("longest_file", ctypes.c_uint64),
+                ("free_bytes", ctypes.c_uint64), ("hbm_frac", ctypes.c_double),
+                ("ranks_per_device", ctypes.c_uint32), ("steps", ctypes.c_uint32), ("arenas", ctypes.c_int32),
+                ("md5_slice", ctypes.c_int32), ("join_lag", ctypes.c_int32), ("lead", ctypes.c_int32),
+                ("k3_period", ctypes.c_int32), ("flags", ctypes.c_uint32)]
+
+
+class PipelinePlan(ctypes.Structure):
+    """hbx_pipeline_plan (include/hbxgpu.h)."""
+    _fields_ = [("resident", ctypes.c_uint32), ("md5_slice", ctypes.c_uint32), ("join_lag", ctypes.c_uint32),
+                ("lead", ctypes.c_uint32), ("k3_period", ctypes.c_uint32), ("launches_per_batch", ctypes.c_uint32),
+                ("hbm_bytes", ctypes.c_uint64)]
+
+
+PLAN_HOST_INPUT = 1
+PLAN_ARENA_SLACK = 64 << 20
 
 # hbx_batch_ready_fn (include/hbxgpu.h)
 BATCH_READY = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64)
@@ -164,6 +183,8 @@ def load() -> ctypes.CDLL:
     L.hbx_verify_submit_device.argtypes = [P, P, U64, P, P, P, P, P, P, P, P, PU64]
     L.hbx_store_paths_z.argtypes = [P, U64, P, P, P, P, P, P, P, ctypes.c_uint32, U64, P, P, P, P]
     L.hbx_store_paths_status.argtypes = [P, U64, P, P, P, P, P, P, P, P, ctypes.c_uint32, U64, P, P, P, P, P, P]
+    L.hbx_plan_pipeline.argtypes = [P, ctypes.POINTER(PlanRequest), ctypes.POINTER(PipelinePlan)]
+    L.hbx_apply_plan.argtypes = [P, ctypes.POINTER(PipelinePlan), U64, U64]
     for name in EXPORTS:
         if name not in _NON_STATUS:
             getattr(L, name).restype = I

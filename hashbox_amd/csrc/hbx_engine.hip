@@ -1458,7 +1458,12 @@ void hbx_ctx_destroy(hbx_ctx* c) {
   delete c;
 }
 
-const char* hbx_last_error(const hbx_ctx* c) { return c ? c->err.c_str() : "null context"; }
+// Failures of calls made without a context (hbx_plan_pipeline with ctx NULL)
+// are described per thread.
+static thread_local std::string g_noctx_err;
+const char* hbx_last_error(const hbx_ctx* c) {
+  return c ? c->err.c_str() : g_noctx_err.empty() ? "null context" : g_noctx_err.c_str();
+}
 
 int hbx_set_tile_iters(hbx_ctx* c, uint32_t iters) {
   if (!c || iters > 1024) return HBX_ERR_ARG;
@@ -1485,6 +1490,90 @@ int hbx_set_k3_period(hbx_ctx* c, uint32_t period) {
   c->k3_period = period;
   c->k3_tick = 0;
   return HBX_OK;
+}
+
+// The pipeline's operating point (DESIGN.md §3 "Throughput model", §7):
+// throughput ~ bytes resident / a batch's lifetime, so R = as many arenas as
+// hbm_frac of the free memory holds; a batch holds its arena for its `need`
+// launches (period P apart) plus the join lag and lead, so the slice is the
+// longest chain's blocks over the launches that fit in R - lead - (P - 1)
+// submits.  bench.py takes every plan from here (tests/test_plan.py checks
+// it against the round-5 Python planner at N = 1..8).
+int hbx_plan_pipeline(hbx_ctx* c, const hbx_plan_request* q, hbx_pipeline_plan* p) {
+  if (!q || !p) return HBX_ERR_ARG;
+  auto bad = [&](const std::string& m) {
+    if (c) return c->fail(HBX_ERR_ARG, m);
+    g_noctx_err = m;
+    return HBX_ERR_ARG;
+  };
+  if (q->n_files == 0) return bad("hbx_plan_pipeline: no files");
+  if (q->join_lag > 4) return bad("hbx_plan_pipeline: join lag must be 1..4");
+  if (q->k3_period > kMaxFresh) return bad("hbx_plan_pipeline: K3 period must be 1..8");
+  uint64_t free_b = q->free_bytes;
+  if (free_b == 0) {
+    if (!c) return bad("hbx_plan_pipeline: free_bytes 0 needs a context");
+    std::lock_guard<std::mutex> g(c->mu);
+    size_t fr = 0, tot = 0;
+    HBX_TRY(c, hipSetDevice(c->device));
+    HBX_TRY(c, hipMemGetInfo(&fr, &tot));
+    free_b = fr;
+  }
+  const int64_t lag = q->join_lag > 0 ? q->join_lag : 2;
+  const bool host_in = (q->flags & HBX_PLAN_HOST_INPUT) != 0;
+  int64_t per = 1;
+  if (q->k3_period > 0) {
+    per = q->k3_period;
+  } else if (q->n_files < 32 && !host_in) {
+    // small per-GPU batches: the launch's start-up and tail once per 4 steps
+    // (profiles/r05j, r05o: 8 files 2,013 -> 2,056-2,083 GiB/s; 32 files P1
+    // 2,277-2,294 vs P2 2,260-2,272)
+    per = (q->steps == 0 || q->steps % 4 == 0) ? 4 : (q->steps % 2 == 0) ? 2 : 1;
+  }
+  const int64_t ld = q->lead >= 0 ? q->lead : lag + 1;
+  const uint64_t nfull = (std::min<uint64_t>(q->longest_file, HBX_MAX_BLOCK_SIZE) + 8u) >> 6;
+  const double frac = q->hbm_frac > 0.0 ? q->hbm_frac : 0.95;
+  const uint64_t share = (uint64_t)((double)free_b * frac / (double)std::max<uint32_t>(1u, q->ranks_per_device));
+  const uint64_t stride = q->arena_bytes + HBX_PLAN_ARENA_SLACK;
+  int64_t r_fit = std::max<int64_t>(ld + 1, (int64_t)(share / stride));
+  if (host_in) r_fit = std::min<int64_t>(r_fit, ld + 2);  // PCIe-bound: a shallow pipeline suffices
+  auto cdiv = [](uint64_t a, uint64_t b) { return (a + b - 1) / b; };
+  auto slice_for = [&](int64_t R) {  // launches of P x B blocks, P submits apart, within R - lead - (P - 1)
+    const int64_t launches = std::max<int64_t>(1, (R - ld - per + 1) / per);
+    return cdiv(nfull, (uint64_t)(launches * per));
+  };
+  int64_t R;
+  uint64_t B;
+  if (q->md5_slice < 0) {
+    R = q->arenas > 0 ? q->arenas : r_fit;
+    B = slice_for(R);
+  } else {
+    B = (uint64_t)q->md5_slice;
+    R = q->arenas > 0 ? q->arenas
+                      : std::min<int64_t>((B == 0 ? 1 : (int64_t)cdiv(nfull, B * per)) * per + ld + per - 1, r_fit);
+  }
+  const int64_t need = B == 0 ? 1 : (int64_t)cdiv(nfull, B * per);  // K3 launches per batch
+  if (need * per + lag + per - 1 > R)
+    return bad("hbx_plan_pipeline: pipeline depth " + std::to_string(R) + " < launches per batch " +
+               std::to_string(need) + " x period " + std::to_string(per) + " + join lag " + std::to_string(lag) +
+               " + " + std::to_string(per - 1) + ": more arenas or a larger slice");
+  if (B > 0xFFFFFFFFull || R > 0xFFFFFFFFll) return bad("hbx_plan_pipeline: plan out of range");
+  p->resident = (uint32_t)R;
+  p->md5_slice = (uint32_t)B;
+  p->join_lag = (uint32_t)lag;
+  p->lead = (uint32_t)ld;
+  p->k3_period = (uint32_t)per;
+  p->launches_per_batch = (uint32_t)need;
+  p->hbm_bytes = (uint64_t)R * stride;
+  return HBX_OK;
+}
+
+int hbx_apply_plan(hbx_ctx* c, const hbx_pipeline_plan* p, uint64_t files, uint64_t bytes) {
+  if (!c || !p || p->resident == 0) return HBX_ERR_ARG;
+  int rc = hbx_set_md5_slice(c, p->md5_slice);
+  if (!rc) rc = hbx_set_join_lag(c, p->join_lag);
+  if (!rc) rc = hbx_set_k3_period(c, p->k3_period);
+  if (!rc) rc = hbx_reserve(c, p->resident + 2u, files, bytes);
+  return rc;
 }
 
 int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {

@@ -900,10 +900,6 @@ struct alignas(16) Chain {
 constexpr uint32_t kChainDone = 0xFFFFFFFFu;
 constexpr uint32_t kBudgetAll = 0xFFFFFFFFu;
 
-__device__ __forceinline__ uint32_t chain_cnt(uint32_t len, uint32_t next, uint32_t budget) {
-  const uint32_t nfull = (len + 8u) >> 6;
-  return min(nfull - next, budget);
-}
 // ------------------------------------------------------- chain schedule --
 // A batch's chains live in the batch's own array for their whole life (K2r
 // writes them; K3 updates `next` and the MD5 state in place).  What changes
@@ -1180,11 +1176,18 @@ __device__ __forceinline__ void k3p_consume(uint8_t* wl, uint32_t* flags, uint32
   }
 }
 
-// The group's wave-minimum count and the chain of this lane, exactly as the
-// MD5 wave computes them (both roles walk the same groups).
+// The group's wave-minimum count and the chain position of this lane, exactly
+// as the MD5 wave computes them (both roles walk the same groups).  Only what
+// cannot change during the launch is read: the order entry's rem (the
+// planner's) and the chain's src and len.  The chain's `next` and state are
+// the MD5 wave's to rewrite, and for a group on the lane path it does so
+// without waiting for the producer, so a producer that read them after that
+// rewrite would see another count (advisor r05: a wrapped kChainDone count
+// turned a lane-path group into a cooperative one and put the pair's stage
+// counters out of step).
 struct K3Group {
-  const Chain* chp;
-  Chain ch;
+  uint64_t src;     // chain bytes
+  uint32_t next;    // first full block this launch hashes
   uint32_t cnt, R;
   bool active;
 };
@@ -1196,11 +1199,12 @@ __device__ __forceinline__ K3Group k3_group(const OrderEntry* __restrict__ order
   G.active = k < n_total;
   // idle lanes stay alive for the wave-wide loop bound: they run an empty
   // slice over the group's first chain and store nothing
-  G.chp = reinterpret_cast<const Chain*>(order[G.active ? k : 64u * g].chain);
-  G.ch = *G.chp;
-  const uint32_t len = G.active ? G.ch.len : 0u;
-  const uint32_t b0 = G.active ? G.ch.next : 0u;
-  G.cnt = G.active ? chain_cnt(len, b0, budget) : 0u;
+  const OrderEntry o = order[G.active ? k : 64u * g];
+  const Chain* chp = reinterpret_cast<const Chain*>(o.chain);
+  G.src = chp->src;
+  const uint32_t left = o.rem - 1u;  // listed entries have rem >= 1
+  G.next = ((chp->len + 8u) >> 6) - left;
+  G.cnt = G.active ? min(left, budget) : 0u;
   // R = the wave's smallest count: all 64 chains advance R blocks together
   G.R = ~wave_max_all(G.active ? ~G.cnt : 0u);
   return G;
@@ -1293,15 +1297,20 @@ __device__ __forceinline__ K3Lane k3_lane(const OrderEntry* __restrict__ order, 
   if constexpr (!ITEMS) {
     // idle lanes stay alive for the wave-wide loop bound: they run an empty
     // slice over the group's first chain and store nothing
-    L.chp = reinterpret_cast<Chain*>(order[active ? k : 64u * g].chain);
+    // counts from the order entry, as the producer wave computes them
+    // (k3_group): the chain's own `next` agrees with it by the planner's
+    // invariant (rem = 1 + full blocks left), but only rem is read by both
+    const OrderEntry o = order[active ? k : 64u * g];
+    L.chp = reinterpret_cast<Chain*>(o.chain);
     const Chain ch = *L.chp;
+    const uint32_t left = o.rem - 1u;
+    L.next = ((ch.len + 8u) >> 6) - left;
     L.len = active ? ch.len : 0u;
-    L.b0 = active ? ch.next : 0u;
-    L.cnt = active ? chain_cnt(L.len, L.b0, budget) : 0u;
-    L.finish = active && L.b0 + L.cnt == ((L.len + 8u) >> 6);
+    L.b0 = active ? L.next : 0u;
+    L.cnt = active ? min(left, budget) : 0u;
+    L.finish = active && left <= budget;
     L.live = active;
     L.src = reinterpret_cast<const uint8_t*>(ch.src);
-    L.next = ch.next;
     L.h[0] = ch.h[0];
     L.h[1] = ch.h[1];
     L.h[2] = ch.h[2];
@@ -1418,7 +1427,7 @@ __device__ void k3p_producer(uint8_t* wl, uint32_t* flags, const OrderEntry* __r
   for (uint32_t g = g0; g < groups; g += nwaves) {
     const K3Group G = k3_group(order, n_total, g, budget);
     if (G.R < kCoopMinBudget) continue;  // wave-uniform: the MD5 wave takes the lane path
-    S += k3p_produce<SETS>(wl, flags, S, G.ch.src + 64ull * (G.ch.next + 1u) - 8ull, G.R - 1u);  // from block next+1
+    S += k3p_produce<SETS>(wl, flags, S, G.src + 64ull * (G.next + 1u) - 8ull, G.R - 1u);  // from block next+1
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (clamped re-reads of the last stage)
 }

@@ -344,6 +344,17 @@ class Engine:
         self._check(self._L.hbx_reserve(self._ctx, int(batches), int(files), int(nbytes)),
                     "hbx_reserve")
 
+    def plan_pipeline(self, **kw) -> dict:
+        """hbx_plan_pipeline on this context (free_bytes=0: the device's free
+        memory now); see the module function :func:`plan_pipeline`."""
+        return plan_pipeline(engine=self, **kw)
+
+    def apply_plan(self, plan: dict, files: int, nbytes: int):
+        """hbx_apply_plan: the plan's slice, join lag and K3 period, and R + 2
+        reserved batches of up to `files` files and `nbytes` bytes."""
+        pp = _lib.PipelinePlan(**{k: int(plan[k]) for k in _PLAN_KEYS})
+        self._check(self._L.hbx_apply_plan(self._ctx, ctypes.byref(pp), int(files), int(nbytes)), "hbx_apply_plan")
+
     def stage_totals(self, reset: bool = False):
         """Cumulative device ms and launch counts per kernel: K1, K2, plan, K3, K4."""
         ms = (ctypes.c_double * 5)()
@@ -639,6 +650,34 @@ class Engine:
         ms = (ctypes.c_float * 5)()
         self._check(self._L.hbx_stage_times(self._ctx, ms), "hbx_stage_times")
         return np.array(list(ms), np.float64)
+
+
+_PLAN_KEYS = ("resident", "md5_slice", "join_lag", "lead", "k3_period", "launches_per_batch", "hbm_bytes")
+
+
+def plan_pipeline(n_files: int, arena_bytes: int, longest_file: int, free_bytes: int = 0, hbm_frac: float = 0.95,
+                  ranks_per_device: int = 1, steps: int = 0, arenas: int = 0, md5_slice: int = -1,
+                  join_lag: int = 0, lead: int = -1, k3_period: int = 0, host_input: bool = False,
+                  engine: Optional["Engine"] = None) -> dict:
+    """The pipeline's operating point from the library (hbx_plan_pipeline,
+    include/hbxgpu.h): resident batches R, MD5 slice, join lag, lead, K3
+    period, launches per batch and the HBM the arenas take.  Pure host
+    arithmetic when free_bytes > 0 (no GPU needed); with free_bytes=0 an
+    engine must be given (its device's free memory).  Raises ValueError for
+    an impossible request."""
+    L = _lib.load()
+    q = _lib.PlanRequest(n_files=int(n_files), arena_bytes=int(arena_bytes), longest_file=int(longest_file),
+                         free_bytes=int(free_bytes), hbm_frac=float(hbm_frac),
+                         ranks_per_device=int(ranks_per_device), steps=int(steps), arenas=int(arenas),
+                         md5_slice=int(md5_slice), join_lag=int(join_lag), lead=int(lead),
+                         k3_period=int(k3_period), flags=_lib.PLAN_HOST_INPUT if host_input else 0)
+    p = _lib.PipelinePlan()
+    ctx = engine._ctx if engine is not None else None
+    rc = L.hbx_plan_pipeline(ctx, ctypes.byref(q), ctypes.byref(p))
+    if rc != 0:
+        msg = L.hbx_last_error(ctx).decode()
+        raise ValueError(f"hbx_plan_pipeline: {_lib.ERRORS.get(rc, rc)}: {msg}")
+    return {k: int(getattr(p, k)) for k in _PLAN_KEYS}
 
 
 def device_count() -> int:

@@ -519,6 +519,55 @@ int hbx_set_join_lag(hbx_ctx *ctx, uint32_t lag);
  * HBX_ERR_STATE while batches are pending. */
 int hbx_set_k3_period(hbx_ctx *ctx, uint32_t period);
 
+/* ---- Pipeline operating point ---------------------------------------------
+ * Hashback calls storeFile once per file from its tree walk
+ * (hashback/store.go:356 -> :84); a caller that batches those files for
+ * hbx_submit_device reaches the engine's measured rate only with the
+ * schedule below: R batches resident in device memory,
+ * each MD5 launch advancing every chain by the slice, a join lag of 2, a
+ * lead of 3 and, below 32 files per batch, one MD5 launch every 4 submits.
+ * hbx_plan_pipeline computes that schedule (bench.py runs exactly this plan)
+ * and hbx_apply_plan sets it on a context.  Request fields <= 0 (md5_slice:
+ * < 0) are "auto"; a positive value overrides that knob. */
+#define HBX_PLAN_HOST_INPUT 1u /* each batch is copied in from host memory per step: shallow pipeline */
+#define HBX_PLAN_ARENA_SLACK (64ull << 20) /* planned per resident arena beyond its bytes (allocator rounding) */
+typedef struct {
+  uint64_t n_files;          /* files per batch on this device */
+  uint64_t arena_bytes;      /* one batch's arena: last offset + last length + HBX_ARENA_SLACK (or more) */
+  uint64_t longest_file;     /* bytes of the batch's longest file (its longest MD5 chain: min(this, 8 MiB)) */
+  uint64_t free_bytes;       /* device memory to plan for; 0 = the context's device, free now */
+  double hbm_frac;           /* share of free_bytes for resident arenas (<= 0: 0.95) */
+  uint32_t ranks_per_device; /* processes sharing the device's memory (0: 1) */
+  uint32_t steps;            /* submits the caller runs between drains (0: open-ended); an auto
+                                period divides it */
+  int32_t arenas;            /* resident batches R (<= 0: as many as hbm_frac of free_bytes holds) */
+  int32_t md5_slice;         /* blocks per chain per submit (< 0: sized from R; 0: unlimited) */
+  int32_t join_lag;          /* 1..4 (<= 0: 2) */
+  int32_t lead;              /* steps an arena stays resident beyond its batch's launches (< 0: lag + 1) */
+  int32_t k3_period;         /* 1..8 (<= 0: 4, or 2 if 4 does not divide steps, below 32 files; else 1) */
+  uint32_t flags;            /* HBX_PLAN_HOST_INPUT */
+} hbx_plan_request;
+typedef struct {
+  uint32_t resident;           /* R: batches in flight, one device arena each */
+  uint32_t md5_slice;          /* for hbx_set_md5_slice (blocks per chain per submit; 0 = unlimited) */
+  uint32_t join_lag;           /* for hbx_set_join_lag */
+  uint32_t lead;               /* the arena of batch j is refilled for batch j + R (hbx_input_after_oldest) */
+  uint32_t k3_period;          /* for hbx_set_k3_period */
+  uint32_t launches_per_batch; /* MD5 launches a batch's longest chain needs */
+  uint64_t hbm_bytes;          /* R x (arena_bytes + HBX_PLAN_ARENA_SLACK) */
+} hbx_pipeline_plan;
+/* Fill *plan from *req.  ctx may be NULL when req->free_bytes > 0 (pure
+ * host arithmetic, no device call).  HBX_ERR_ARG for an impossible request
+ * (no files, a knob out of range, or R too small for the launches a batch
+ * needs: then hbx_last_error(ctx) says which; with ctx NULL,
+ * hbx_last_error(NULL) describes the calling thread's last such failure). */
+int hbx_plan_pipeline(hbx_ctx *ctx, const hbx_plan_request *req, hbx_pipeline_plan *plan);
+/* Set the plan's slice, join lag and period on ctx and reserve R + 2 batches
+ * of up to `files` files and `bytes` bytes (hbx_reserve).  The caller keeps R
+ * arenas and, from the (R+1)-th submit on, calls hbx_input_after_oldest
+ * before refilling the oldest one.  HBX_ERR_STATE while batches are pending. */
+int hbx_apply_plan(hbx_ctx *ctx, const hbx_pipeline_plan *plan, uint64_t files, uint64_t bytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -375,6 +375,60 @@ def test_k3_producer_waves(oracle, monkeypatch, md5_slice, join_lag, wgs, plan_c
             _check(a, r)
 
 
+@pytest.mark.parametrize("prod", ["1", "p3"])
+@pytest.mark.parametrize("md5_slice,join_lag", [(9, 1), (9, 2), (16384, 1), (0, 2)])
+def test_k3_lane_path_groups_between_cooperative_ones(oracle, monkeypatch, md5_slice, join_lag, prod):
+    """Advisor r05 (high): with a producer wave per MD5 wave, a group on the
+    lane path (fewer than 8 blocks for some lane) is hashed without waiting
+    for the producer, and the MD5 wave rewrites its chains' `next`.  Both
+    waves must still agree on every group's count, so the producer derives it
+    from the order entry (immutable during the launch), never from the chain
+    table.  Here most groups are on the lane path and sit between cooperative
+    ones in each wave's walk: thousands of tiny files (0-2 full blocks) and
+    files of 8-15 full blocks in one bin (at slice 16,384 the last bin spans
+    counts 0-15), blocks of 64 of each so that one wave of a 1-workgroup grid
+    (HBX_K3_WGS=1, four MD5 waves) walks lane, lane, cooperative, ..; plus a
+    few long files; bit-exact over several pipelined batches."""
+    import torch
+    from hashbox_amd import Engine, pack_arena_layout
+    monkeypatch.setenv("HBX_AB", "1")
+    monkeypatch.setenv("HBX_K3_PROD", "1")
+    monkeypatch.setenv("HBX_K3_PSETS", "3" if prod == "p3" else "2")
+    monkeypatch.setenv("HBX_K3_ITEMS", "0")
+    monkeypatch.setenv("HBX_K3_WGS", "1")
+    rng = np.random.default_rng(977 + md5_slice % 13)
+    batches = []
+    for b in range(3):
+        sizes = []
+        for blk in range(36):
+            lo, hi = [(0, 120), (0, 120), (504, 1016)][(blk + b) % 3]
+            sizes += [int(v) for v in rng.integers(lo, hi, 64)]
+        sizes += [3 * MIN + 5, MAXB + 123, 40_000]
+        files = [oracle.random_bytes(n, 5000 + 7919 * b + i) for i, n in enumerate(sizes)]
+        offs, total = pack_arena_layout(sizes)
+        host = np.zeros(total, np.uint8)
+        for o, f in zip(offs, files):
+            host[int(o):int(o) + f.size] = f
+        batches.append((torch.from_numpy(host).to("cuda:0"), offs, sizes,
+                        [oracle.store_file(f, fast=True) for f in files]))
+    torch.cuda.synchronize()
+    got, order = [], []
+    with Engine(0, md5_slice=md5_slice, join_lag=join_lag) as e:
+        k = e.knobs()
+        assert k["k3_prod"] and k["md5_wgs"] == 1
+        for i in [0, 1, 2, 1, 0, 2]:
+            dev, offs, sizes, _ = batches[i]
+            e.submit_device(dev.data_ptr(), offs, sizes)
+            order.append(i)
+            if e.pending() >= 4:
+                got.append(e.wait())
+        while e.pending():
+            got.append(e.wait())
+    for i, g in zip(order, got):
+        for a, r in zip(g, batches[i][3]):
+            _check(a, r)
+
+
 @pytest.mark.parametrize("join_lag", [1, 2, 3, 4])
 def test_pipelined_steady_state(oracle, join_lag):
     """A deep pipeline as bench.py drives it: submit, and wait only once
