@@ -633,6 +633,9 @@ def check_host_bytes(plan, world_on_host=1):
 
 def main():
     a = parse()
+    if a.k3_period > 0 and a.steps % a.k3_period:  # advisor r05: the window must hold whole K3 periods
+        sys.exit(f"--k3-period {a.k3_period} must divide --steps {a.steps} (one K3 launch per period; the "
+                 "timed window's launch count is asserted)")
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -496,6 +496,7 @@ struct SlowSubmit {
     std::fprintf(stderr, "  finalize: k4 %.3f, d2h %.3f, record %.3f\n", fin[0], fin[1], fin[2]);
   }
   void clear() {
+    if (limit_ms < 0) return;
     for (int i = 6; i < 10; i++) t[i] = t[0];
     fin[0] = fin[1] = fin[2] = 0;
   }
@@ -506,7 +507,10 @@ struct SlowSubmit {
     a = b;
   }
 };
-static SlowSubmit g_slow;
+// Per thread (advisor r05): a context's calls are serialised by its own lock
+// only, so contexts submitting from different threads must not share it; two
+// contexts on one thread never overlap.
+static thread_local SlowSubmit g_slow;
 
 // K4 + D2H of one batch whose chains are all hashed, on the result stream
 // (after the finalizing K3's completion event), so the hash stream goes straight on with the next plan

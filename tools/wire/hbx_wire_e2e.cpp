@@ -9,12 +9,18 @@
 //                                   ACKN(id)   if it does (dedup)
 //   client  writ(block)       sink  ACKN(id)   after re-verifying the block
 //
-// The sink re-verifies every k-th written block the way the server does
-// (inflate, then HashData, block.go:152-174), with zlib and the CPU oracle's
-// MD5 (oracle/hbx_oracle.c: the checker, not the thing measured).  Framing is
-// the library's (hbx_wire_*).  Prints one JSON line.
+// The sink re-verifies every written block before it acknowledges it, as the
+// server does (server.go:180-182: VerifyBlock = inflate, then HashData,
+// block.go:152-174), with zlib and the CPU oracle's MD5 (oracle/hbx_oracle.c:
+// the checker, not the thing measured), on `verify_threads` verifier threads
+// (the server verifies inline in the connection's goroutine; a pool keeps one
+// core's inflate + MD5 rate from standing in for the GPU path's).  An ACKN is
+// sent only once its block verified; a block that fails gets ERRS ("Unable to
+// verify blockID", server.go:200-201).  verify_every > 1 samples every k-th
+// write instead (a labelled second figure only).  Framing is the library's
+// (hbx_wire_*).  Prints one JSON line.
 //
-// usage: hbx_wire_e2e <file-list> [io_threads] [window] [verify_every]
+// usage: hbx_wire_e2e <file-list> [io_threads] [window] [verify_every=1] [verify_threads=8]
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -115,52 +121,113 @@ struct SinkStats {
   uint64_t allocs = 0, reads = 0, acks_dedup = 0, writes = 0, verified = 0, bad = 0, bytes = 0;
 };
 
-void sink(int fd, uint32_t verify_every, SinkStats* st) {
+// One written block waiting for its VerifyBlock (a copy: the reader's buffer
+// moves on).
+struct WriteJob {
+  uint16_t num;
+  uint8_t id[16];
+  std::vector<uint8_t> links, data;
+  uint32_t n_links;
+  bool verify;
+};
+
+void sink(int fd, uint32_t verify_every, uint32_t verify_threads, SinkStats* st) {
   Reader r{fd};
   std::set<std::string> have;
-  std::vector<uint8_t> raw;
   hbx_wire_msg m;
   uint8_t out[22];
+  std::mutex send_mu, q_mu;
+  std::condition_variable q_cv;
+  std::deque<WriteJob> q;
+  bool closing = false, dead = false;
+  std::atomic<uint64_t> verified{0}, bad{0};
+  auto reply = [&](uint16_t num, uint32_t type, const uint8_t* id) {
+    uint8_t o[22];
+    hbx_wire_encode_id(num, type & HBX_SERVER_MASK, id, o);
+    std::lock_guard<std::mutex> g(send_mu);
+    return send_all(fd, o, 22);
+  };
+  auto verifier = [&] {
+    std::vector<uint8_t> raw(8u << 20);
+    for (;;) {
+      WriteJob j;
+      {
+        std::unique_lock<std::mutex> g(q_mu);
+        q_cv.wait(g, [&] { return closing || !q.empty(); });
+        if (q.empty()) return;
+        j = std::move(q.front());
+        q.pop_front();
+      }
+      q_cv.notify_all();  // room in the queue
+      bool ok = true;
+      if (j.verify) {  // server.go:182 -> VerifyBlock (block.go:152-166): inflate, HashData, compare
+        uLongf n = raw.size();
+        uint8_t id[16];
+        const int zr = ::uncompress(raw.data(), &n, j.data.data(), j.data.size());
+        hbxo_block_id(j.links.data(), j.n_links, raw.data(), n, id);
+        ok = zr == Z_OK && std::memcmp(id, j.id, 16) == 0;
+        verified++;
+        if (!ok) bad++;
+      }
+      // ACKN after the verify; a failed one gets the server's error type
+      if (!reply(j.num, ok ? HBX_MSG_ACKNOWLEDGE : HBX_MSG_ERROR, j.id)) {
+        std::lock_guard<std::mutex> g(q_mu);
+        dead = true;
+      }
+    }
+  };
+  std::vector<std::thread> pool;
+  for (uint32_t t = 0; t < std::max(1u, verify_threads); t++) pool.emplace_back(verifier);
   while (r.next(m)) {
     if (m.type == HBX_MSG_GOODBYE) break;
     if (m.type == HBX_MSG_ALLOCATE) {
       st->allocs++;
       const bool known = have.count(std::string((const char*)m.id, 16)) != 0;
-      const uint32_t t = (known ? HBX_MSG_ACKNOWLEDGE : HBX_MSG_READ) & HBX_SERVER_MASK;
       if (known) st->acks_dedup++; else st->reads++;
-      hbx_wire_encode_id(m.num, t, m.id, out);
-      if (!send_all(fd, out, 22)) break;
+      if (!reply(m.num, known ? HBX_MSG_ACKNOWLEDGE : HBX_MSG_READ, m.id)) break;
     } else if (m.type == HBX_MSG_WRITE) {
       st->writes++;
       st->bytes += m.data_len;
-      if (verify_every && st->writes % verify_every == 1) {  // server.go:182 -> VerifyBlock
-        raw.resize(8u << 20);
-        uLongf n = raw.size();
-        uint8_t id[16];
-        const int zr = ::uncompress(raw.data(), &n, m.data, m.data_len);
-        hbxo_block_id(m.links, m.n_links, raw.data(), n, id);
-        st->verified++;
-        if (zr != Z_OK || std::memcmp(id, m.id, 16) != 0) st->bad++;
-      }
+      WriteJob j;
+      j.num = m.num;
+      std::memcpy(j.id, m.id, 16);
+      j.n_links = m.n_links;
+      j.links.assign(m.links, m.links + 16u * m.n_links);
+      j.data.assign(m.data, m.data + m.data_len);
+      j.verify = verify_every != 0 && (st->writes - 1) % verify_every == 0;
       have.insert(std::string((const char*)m.id, 16));
-      hbx_wire_encode_id(m.num, HBX_MSG_ACKNOWLEDGE & HBX_SERVER_MASK, m.id, out);
-      if (!send_all(fd, out, 22)) break;
+      std::unique_lock<std::mutex> g(q_mu);
+      q_cv.wait(g, [&] { return q.size() < 4u * pool.size() || dead; });  // bounded: the reader backs up
+      if (dead) break;
+      q.push_back(std::move(j));
+      g.unlock();
+      q_cv.notify_all();
     } else {
       break;
     }
   }
+  {
+    std::lock_guard<std::mutex> g(q_mu);
+    closing = true;
+  }
+  q_cv.notify_all();
+  for (auto& t : pool) t.join();
+  st->verified = verified;
+  st->bad = bad;
+  (void)out;
 }
 
 }  // namespace
 
 int main(int argc, char** argv) {
   if (argc < 2) {
-    std::fprintf(stderr, "usage: %s <file-list> [io_threads] [window] [verify_every]\n", argv[0]);
+    std::fprintf(stderr, "usage: %s <file-list> [io_threads] [window] [verify_every=1] [verify_threads=8]\n", argv[0]);
     return 2;
   }
   const uint32_t io_threads = argc > 2 ? (uint32_t)std::atoi(argv[2]) : 16u;
   const uint32_t window = argc > 3 ? (uint32_t)std::atoi(argv[3]) : 4096u;
-  const uint32_t verify_every = argc > 4 ? (uint32_t)std::atoi(argv[4]) : 64u;
+  const uint32_t verify_every = argc > 4 ? (uint32_t)std::atoi(argv[4]) : 1u;  // server.go:182: every write
+  const uint32_t verify_threads = argc > 5 ? (uint32_t)std::atoi(argv[5]) : 8u;
   std::vector<std::string> names;
   {
     std::ifstream in(argv[1]);
@@ -211,7 +278,7 @@ int main(int argc, char** argv) {
   std::thread srv([&] {
     const int fd = ::accept(ls, nullptr, nullptr);
     if (fd >= 0) {
-      sink(fd, verify_every, &st);
+      sink(fd, verify_every, verify_threads, &st);
       ::close(fd);
     }
   });
@@ -346,11 +413,13 @@ int main(int argc, char** argv) {
       "\"files\": %llu, \"bytes\": %llu, \"chunks\": %llu, \"compressed_bytes\": %llu, "
       "\"store_seconds\": %.3f, \"store_gibs\": %.3f, \"end_to_end_seconds\": %.3f, "
       "\"wire_tail_after_store_seconds\": %.3f, \"end_to_end_gibs\": %.3f, \"window\": %u, "
+      "\"verify_every\": %u, \"verify_threads\": %u, "
       "\"sink\": {\"allocs\": %llu, \"reads\": %llu, \"dedup_acks\": %llu, \"writes\": %llu, "
       "\"verified\": %llu, \"verify_failures\": %llu}, \"client_writes\": %llu, \"acked\": %llu, "
       "\"failed\": %s}\n",
       (unsigned long long)n, (unsigned long long)total, (unsigned long long)nb, (unsigned long long)zbytes,
       t1 - t0, total / (t1 - t0) / (1 << 30), t3 - t0, t3 - t1, total / (t3 - t0) / (1 << 30), window,
+      verify_every, verify_threads,
       (unsigned long long)st.allocs, (unsigned long long)st.reads, (unsigned long long)dedup,
       (unsigned long long)st.writes, (unsigned long long)st.verified, (unsigned long long)st.bad,
       (unsigned long long)written, (unsigned long long)acked, failed ? "true" : "false");
