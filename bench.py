@@ -135,6 +135,9 @@ def parse():
                     help="skip the probed lifetime decomposition after the timed window (key 'lifetime')")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the oracle check of the last collected and the last drained batch")
+    ap.add_argument("--check-batches", type=int, default=1,
+                    help="batches collected in the timed window checked file by file against the oracle "
+                         "(the last K, each its own arena; default 1), besides the last drained one")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPUs; gloo for tests")
     ap.add_argument("--dist-always", action="store_true",
                     help="join a process group even at world 1 (exercises the RCCL barriers and reductions "
@@ -366,9 +369,11 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
     thr0 = cpu_throttle()
     t0 = time.perf_counter()
     last = None
+    window = []
     for _ in range(steps):
         submit()
         last = collect()
+        window.append(last)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     subs = np.array(state["subs"][-steps:]) * 1e3
@@ -396,7 +401,7 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
     t2 = time.perf_counter()
     return {"el": t1 - t0, "drain": t2 - t_d, "fill_to_drained": t2 - t_fill,
             "batches_total": state["j"], "tot_ms": tot_ms, "tot_n": tot_n,
-            "last": last, "drained": drained, "arena_res": arena_res, "host": host, "probe": probe,
+            "last": last, "window": window, "drained": drained, "arena_res": arena_res, "host": host, "probe": probe,
             "probe_raw": probe_raw}
 
 
@@ -523,11 +528,17 @@ def run_workload(a, name, eng, arenas, offs, lens, R, B, need, lanes, dist, gpu,
     longest = max((int(np.max(np.diff(np.concatenate([[0], x.cut_ends]).astype(np.int64))))
                    for x in res if x.n_chunks), default=0)
     check = None
-    if not a.no_check:  # outside the timer: the last batch collected in the window, and the
-        # last one drained (completed by the forced drain launch)
-        ok = oracle_check(arenas[r["last"][0]], offs, lens, res, check_threads)
+    n_checked = 0
+    if not a.no_check:  # outside the timer: the last K batches collected in the window (each
+        # its own arena while K <= R: the arenas are read-only inputs), and the last one
+        # drained (completed by the forced drain launch); every file of each
+        ok = True
+        for i, got in r["window"][-max(1, min(a.check_batches, R)):]:
+            ok = ok and oracle_check(arenas[i], offs, lens, got, check_threads)
+            n_checked += 1
         if r["drained"] is not None:
             ok = ok and oracle_check(arenas[r["drained"][0]], offs, lens, r["drained"][1], check_threads)
+            n_checked += 1
         check = bool(max_over_ranks(1.0 if ok else 0.0, dist, dev, op="min") == 1.0)
     value = a.steps * job_batch_bytes / el / GIB
     drain = max_over_ranks(r["drain"], dist, dev)
@@ -578,6 +589,7 @@ def run_workload(a, name, eng, arenas, offs, lens, R, B, need, lanes, dist, gpu,
         out["k3_probe"] = r["probe"]
     if check is not None:
         out["check_vs_oracle"] = check
+        out["checked_batches_per_gpu"] = n_checked
     return out
 
 
