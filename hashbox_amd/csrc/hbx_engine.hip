@@ -212,6 +212,9 @@ struct hbx_ctx {
   // the batch meta reaches the device by hbx_meta_fetch, a kernel on the scan
   // stream, instead of an SDMA copy (HBX_META_KERNEL=0 for A/B)
   uint32_t meta_kernel = 1;
+  // round 6: the meta copy inside the K1 gate kernel (hbx_k1_gate_meta), one
+  // scan-stream kernel fewer per step (HBX_GATE_META=0: separate kernels)
+  uint32_t gate_meta = 1;
   // a finished batch's results reach the host by hbx_result_push, a kernel
   // on the result stream, instead of an SDMA copy (HBX_D2H_KERNEL=0 for A/B):
   // the copy call held the host ~7 ms once per ~16 submits after a drain
@@ -499,6 +502,13 @@ struct SlowSubmit {
     if (limit_ms < 0) return;
     for (int i = 6; i < 10; i++) t[i] = t[0];
     fin[0] = fin[1] = fin[2] = 0;
+  }
+  // one host call outside submit (e.g. the H2D copy call), reported alone
+  void call(const char* what, std::chrono::steady_clock::time_point a, uint64_t launches) {
+    if (limit_ms < 0) return;
+    const double d = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+    if (d >= limit_ms)
+      std::fprintf(stderr, "hbx slow call (launch %llu): %s %.3f ms\n", (unsigned long long)launches, what, d);
   }
   void lap(int k, std::chrono::steady_clock::time_point& a) {
     if (limit_ms < 0) return;
@@ -1040,7 +1050,15 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   DevBuf& ssum = c->d_ssum[slot];
 
   if (int frc = flush_input_wait(c)) return frc;  // (no launch this submit: nothing flushed it yet)
-  if (c->meta_kernel) {  // meta_bytes is a multiple of 16
+  const bool gate_meta = c->meta_kernel && c->gate_meta && c->k1_gate;
+  if (gate_meta) {  // one kernel: the meta copy, then (if a K3 launch was issued) the gate
+    if (c->ssum_used[slot] && c->cstream != s) HBX_TRY(c, hipStreamWaitEvent(s, c->ssum_free[slot], 0));
+    const uint32_t n16 = (uint32_t)(meta_bytes / 16);
+    hipLaunchKernelGGL(hbx_k1_gate_meta, dim3(std::min<uint32_t>(16, (n16 + 255) / 256)), dim3(256), 0, s,
+                       static_cast<const uint32_t*>(c->d_gate.as<uint32_t>()), c->k3_dispatched, 1000000u,
+                       gate ? 1u : 0u, static_cast<const uint4*>(b->h_meta.p), b->d_meta.as<uint4>(), n16);
+    HBX_TRY(c, hipGetLastError());
+  } else if (c->meta_kernel) {  // meta_bytes is a multiple of 16
     const uint32_t n16 = (uint32_t)(meta_bytes / 16);
     hipLaunchKernelGGL(hbx_meta_fetch, dim3(std::min<uint32_t>(64, (n16 + 255) / 256)), dim3(256), 0, s,
                        static_cast<const uint4*>(b->h_meta.p), b->d_meta.as<uint4>(), n16);
@@ -1056,8 +1074,8 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   const uint8_t* arena = static_cast<const uint8_t*>(d_arena);
 
   // the K2 that last read this summary slot (two batches back) must be done
-  if (c->ssum_used[slot] && c->cstream != s) HBX_TRY(c, hipStreamWaitEvent(s, c->ssum_free[slot], 0));
-  if (gate) {  // K1 after the K3 launch above has all its workgroups on CUs (<= 10 ms)
+  if (!gate_meta && c->ssum_used[slot] && c->cstream != s) HBX_TRY(c, hipStreamWaitEvent(s, c->ssum_free[slot], 0));
+  if (gate && !gate_meta) {  // K1 after the K3 launch above has all its workgroups on CUs (<= 10 ms)
     hipLaunchKernelGGL(hbx_k1_gate, dim3(1), dim3(64), 0, s, static_cast<const uint32_t*>(c->d_gate.as<uint32_t>()),
                        c->k3_dispatched, 1000000u);
     HBX_TRY(c, hipGetLastError());
@@ -1373,6 +1391,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = ab_env("HBX_K3_PROD")) c->k3_prod = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_PLAN_CUT")) c->plan_cut = (uint32_t)std::min(2, std::max(0, std::atoi(v)));
   if (const char* v = ab_env("HBX_META_KERNEL")) c->meta_kernel = std::atoi(v) ? 1u : 0u;
+  if (const char* v = ab_env("HBX_GATE_META")) c->gate_meta = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_PSETS")) c->k3_psets = std::atoi(v) == 3 ? 3u : 2u;
   if (const char* v = ab_env("HBX_K1_SWZ")) c->k1_swz = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_ITEMS")) c->k3_items = (uint32_t)std::min(8, std::max(0, std::atoi(v)));
@@ -1590,11 +1609,11 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
       "\"md5_wgs\": %u, \"plan_mode\": %d, \"k2_own\": %d, \"k4_window\": %u, \"k3_probe\": %d, "
       "\"lean_marks\": %u, \"k3_prod\": %u, \"k3_items\": %u, \"k3_period\": %u, \"meta_kernel\": %u, "
       "\"plan_cut\": %u, \"k1_swz\": %u, \"k3_psets\": %u, \"d2h_kernel\": %u, \"k8_split_streams\": %llu, "
-      "\"k8_split_fallbacks\": %llu}",
+      "\"k8_split_fallbacks\": %llu, \"gate_meta\": %u}",
       (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_gate, c->md5_wgs,
       plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks, c->k3_prod, c->k3_items,
       c->k3_period, c->meta_kernel, c->plan_cut, c->k1_swz, c->k3_psets, c->d2h_kernel,
-      (unsigned long long)c->k8_split_streams, (unsigned long long)c->k8_split_fallbacks);
+      (unsigned long long)c->k8_split_streams, (unsigned long long)c->k8_split_fallbacks, c->gate_meta);
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }
 
@@ -2406,8 +2425,12 @@ int hbx_memcpy_h2d_async(hbx_ctx* c, void* d, const void* h, uint64_t n) {
   if (!c || (n && (!d || !h))) return HBX_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   HBX_TRY(c, hipSetDevice(c->device));
+  const auto t0 = std::chrono::steady_clock::now();
   if (int frc = flush_input_wait(c)) return frc;
+  g_slow.call("h2d: input wait", t0, c->launches);
+  const auto t1 = std::chrono::steady_clock::now();
   HBX_TRY(c, hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, c->stream));
+  g_slow.call("h2d: hipMemcpyAsync", t1, c->launches);
   return HBX_OK;
 }
 

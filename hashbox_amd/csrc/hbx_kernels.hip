@@ -1689,6 +1689,36 @@ extern "C" __global__ __launch_bounds__(kK3PThreads, 1) void hbx_k3q_block_md5(
 // fills the CUs K3 leaves free.  One wave; lane 0 polls with vector loads.
 // The wait is bounded (limit in 100 MHz ticks of s_memrealtime): a gate
 // that times out only delays its K1.
+// With meta (round 6, c->gate_meta): the kernel first copies the batch's
+// meta block from its pinned staging buffer (hbx_meta_fetch's loads, below),
+// so the scan stream runs one kernel fewer per step (one hand-off less before
+// K1: the scan loop sets the step at 8 files per GPU); only workgroup 0's
+// first lane polls, and only if `poll`.
+__device__ __forceinline__ void meta_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, uint32_t n) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    uint32_t* p = const_cast<uint32_t*>(reinterpret_cast<const uint32_t*>(src + i));
+    uint4 v;
+    v.x = __hip_atomic_load(p + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    v.y = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    v.z = __hip_atomic_load(p + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    v.w = __hip_atomic_load(p + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    dst[i] = v;
+  }
+}
+extern "C" __global__ __launch_bounds__(256) void hbx_k1_gate_meta(const uint32_t* __restrict__ started,
+                                                                   uint32_t target, uint32_t limit,
+                                                                   uint32_t poll, const uint4* __restrict__ msrc,
+                                                                   uint4* __restrict__ mdst, uint32_t n16) {
+  meta_copy(msrc, mdst, n16);
+  if (!poll || blockIdx.x != 0 || threadIdx.x != 0) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    const uint32_t v = __hip_atomic_load(started, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if ((int32_t)(v - target) >= 0) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)limit) break;
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
 extern "C" __global__ __launch_bounds__(64) void hbx_k1_gate(const uint32_t* __restrict__ started,
                                                               uint32_t target, uint32_t limit) {
   if (threadIdx.x != 0) return;

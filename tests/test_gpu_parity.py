@@ -461,7 +461,8 @@ def test_pipelined_steady_state(oracle, join_lag):
 
 @pytest.mark.parametrize("period,md5_slice,join_lag,plan_cut,meta", [
     (2, 16384, 1, "1", "1"), (3, 16384, 2, "1", "1"), (4, 8192, 2, "0", "0"), (3, 4096, 3, "1", "1"),
-    (4, 8192, 3, "2", "1"), (8, 9, 2, "1", "1"), (5, 3, 1, "1", "0"), (4, 0, 2, "1", "1"), (1, 4096, 3, "2", "1")])
+    (4, 8192, 3, "2", "1"), (8, 9, 2, "1", "1"), (5, 3, 1, "1", "0"), (4, 0, 2, "1", "1"), (1, 4096, 3, "2", "1"),
+    (4, 8192, 2, "1", "2"), (2, 64, 1, "0", "2")])
 def test_k3_period(oracle, monkeypatch, period, md5_slice, join_lag, plan_cut, meta):
     """K3 period (hbx_set_k3_period): one K3 launch every `period` submits
     with period x the slice per chain, several batches joining one plan (the
@@ -470,17 +471,21 @@ def test_k3_period(oracle, monkeypatch, period, md5_slice, join_lag, plan_cut, m
     (hbx_input_after_oldest).  Every batch bit-exact; the launch count follows
     the period; the period is fixed while batches are pending.  plan_cut 2:
     the preplan on the cut stream at lag 3 too; meta 0: the batch meta by
-    SDMA copy instead of hbx_meta_fetch."""
+    SDMA copy instead of hbx_meta_fetch; meta 1: the meta copy inside the
+    K1 gate kernel (hbx_k1_gate_meta, the default); meta 2: hbx_meta_fetch and
+    the gate as two kernels."""
     import torch
     from hashbox_amd import Engine, HbxError
     monkeypatch.setenv("HBX_AB", "1")
     monkeypatch.setenv("HBX_PLAN_CUT", plan_cut)
-    monkeypatch.setenv("HBX_META_KERNEL", meta)
+    monkeypatch.setenv("HBX_META_KERNEL", "0" if meta == "0" else "1")
+    monkeypatch.setenv("HBX_GATE_META", "1" if meta == "1" else "0")
     batches = _device_batches(oracle, 3, 83 + period)
     got, order = [], []
     with Engine(0, md5_slice=md5_slice, join_lag=join_lag, k3_period=period) as e:
         k = e.knobs()
-        assert k["k3_period"] == period and k["meta_kernel"] == int(meta) and k["plan_cut"] == int(plan_cut)
+        assert k["k3_period"] == period and k["meta_kernel"] == (meta != "0") and k["plan_cut"] == int(plan_cut)
+        assert k["gate_meta"] == (meta == "1")
         e.stage_totals(reset=True)
         nfull = ((8 << 20) + 8) >> 6
         lb = md5_slice * period if md5_slice else nfull
