@@ -37,6 +37,26 @@ int main(int argc, char **argv) {
     if (hbx_chunk_hash(NULL, NULL, 0, NULL, NULL, 0, NULL) != HBX_ERR_ARG) return 4;
     if (hbx_max_chunks(131072) != 3) return 5;
     if (hbx_set_join_lag(NULL, 1) != HBX_ERR_ARG) return 6;
+    /* the operating point is host arithmetic: planned without a device (the
+     * N = 8 share of configs[2]: 8 x 128 MiB per GPU, 282 GiB free) */
+    hbx_plan_request q;
+    memset(&q, 0, sizeof q);
+    q.n_files = 8;
+    q.arena_bytes = 8ull * (128ull << 20) + (64u << 10);
+    q.longest_file = 128ull << 20;
+    q.free_bytes = 282ull << 30;
+    q.steps = 20;
+    q.md5_slice = -1;
+    q.lead = -1;
+    hbx_pipeline_plan pl;
+    if (hbx_plan_pipeline(NULL, &q, &pl) != HBX_OK) return 7;
+    if (pl.join_lag != 2 || pl.lead != 3 || pl.k3_period != 4 || pl.resident < 200 ||
+        (uint64_t)pl.md5_slice * pl.k3_period * pl.launches_per_batch < 131073u)
+      return 8;
+    q.join_lag = 9; /* refused, described by hbx_last_error(NULL) */
+    if (hbx_plan_pipeline(NULL, &q, &pl) != HBX_ERR_ARG || !strstr(hbx_last_error(NULL), "join lag")) return 9;
+    printf("plan R=%u slice=%u lag=%u lead=%u period=%u launches=%u\n", pl.resident, pl.md5_slice, pl.join_lag,
+           pl.lead, pl.k3_period, pl.launches_per_batch);
     printf("nodev ok\n");
     return 0;
   }

@@ -93,4 +93,5 @@ def test_plain_c_driver_links_and_reports_no_device(tmp_path):
     f = tmp_path / "in.bin"
     f.write_bytes(b"hello")
     r = subprocess.run([str(tmp_path / "abi_driver"), str(f), "--expect-nodev"], capture_output=True, text=True)
-    assert r.returncode == 0 and r.stdout.strip() == "nodev ok", (r.returncode, r.stdout, r.stderr)
+    assert r.returncode == 0 and r.stdout.strip().splitlines()[-1] == "nodev ok", (r.returncode, r.stdout, r.stderr)
+    assert r.stdout.startswith("plan R=") and " lag=2 lead=3 period=4 " in r.stdout
