@@ -16,6 +16,8 @@
 #   wire         tools/bench_wire.py (config 5 to the verifying loopback sink)
 #   config5      tools/bench_config5.py (100 k files from tmpfs, end to end)
 #   ab=ENV       bench.py with HBX_AB=1 and ENV (e.g. ab=HBX_K3_PSETS=2) -> ab_<ENV>.json
+#   b=NAME,[VAR=VAL,..],--arg,val,..   bench.py with that environment and those arguments -> NAME.json
+#   copystall, env=VAR=VAL   the e2e leg with the slow-submit trace (+ HIP runtime log / one runtime variable)
 set -o pipefail
 TAG=$1
 shift
@@ -51,7 +53,7 @@ for step in "$@"; do
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${step#testsk=}" > $O/gpu_tests_k.log 2>&1 \
         || { tail -40 $O/gpu_tests_k.log; exit 1; }
       tail -3 $O/gpu_tests_k.log ;;
-    bench) run_bench bench20 300 ;;
+    bench) run_bench bench20 300 --gpus 1 --steps 20 --warmup 5 ;;  # the driver's command
     bench200) run_bench bench200 400 --steps 200 ;;
     f8) run_bench f8 300 --files 8 --steps 20 --warmup 5 --e2e-steps 0 --no-cpu-baseline --no-lifetime ;;
     f16) run_bench f16 300 --files 16 --steps 20 --warmup 5 --e2e-steps 0 --no-cpu-baseline --no-lifetime ;;
@@ -74,6 +76,17 @@ for step in "$@"; do
       env HBX_TRACE_SLOW_SUBMIT=1 "$kv" timeout -k 10 300 python bench.py --e2e --steps 60 --warmup 5 --no-cpu-baseline \
         --no-check > $O/env_$kv.json 2> $O/env_$kv.err || { tail -20 $O/env_$kv.err; exit 1; }
       grep -E "hbx slow" $O/env_$kv.err | head -20; summ $O/env_$kv.json ;;
+    b=*)  # b=NAME,[VAR=VAL,...],--bench-arg,value,... -> NAME.json (VAR=VAL: environment; HBX_* need HBX_AB=1)
+      IFS=, read -ra toks <<< "${step#b=}"
+      name=${toks[0]}
+      envs=()
+      args=()
+      for t in "${toks[@]:1}"; do
+        if [[ $t == --* || ${#args[@]} -gt 0 ]]; then args+=("$t"); else envs+=("$t"); fi
+      done
+      env "${envs[@]}" timeout -k 10 400 python bench.py "${args[@]}" > $O/$name.json 2> $O/$name.err \
+        || { echo "FAIL $step"; tail -20 $O/$name.err; exit 1; }
+      summ $O/$name.json ;;
     ab=*)
       kv=${step#ab=}
       env HBX_AB=1 "$kv" timeout -k 10 300 python bench.py --e2e-steps 0 --no-cpu-baseline > $O/ab_$kv.json 2> $O/ab_$kv.err \
