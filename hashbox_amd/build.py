@@ -30,7 +30,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return LIB
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           os.path.join(CSRC, "hbx_engine.hip"), "-o", LIB + ".tmp"]
+           os.path.join(CSRC, "hbx_engine.hip"), "-lhsa-runtime64", "-o", LIB + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=CSRC)

@@ -12,6 +12,8 @@
 // 556-560 + block.go:96-111 (StoreData -> HashData).
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 
 #include <fcntl.h>
 #include <unistd.h>
@@ -301,6 +303,12 @@ struct hbx_ctx {
   DevBuf d_idesc, d_ires;                                  // hbx_inflate_blocks_device
   DevBuf d_sreg, d_sstart, d_sres, d_sscratch, d_smeta;    // its split path (K8s)
   uint64_t k8_split_streams = 0, k8_split_fallbacks = 0;   // (hbx_knobs: how often the split path resolved)
+  // SDMA engines warmed at context creation (warm_sdma_engines): H2D and D2H
+  // engine masks, and the milliseconds this context spent on it (0 once the
+  // process has done it for the device)
+  uint32_t sdma_h2d = 0, sdma_d2h = 0;
+  double sdma_warm_ms = 0.0;
+  uint32_t sdma_warm = 1;
   PinBuf h_read[2];         // hbx_store_paths: pinned landing slots for file reads
   PinBuf h_zstage;          // hbx_store_paths_z: compressed streams of one batch (synchronous form)
   // hbx_store_paths_z: compression stages in flight, each on its own stream
@@ -1368,6 +1376,72 @@ static hipError_t make_stream(hipStream_t* s, const char* env, int ncu, const ch
   return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
 }
 
+// SDMA engine warm-up (verdict r05 item 2: the ~7 ms host stall in the copy
+// call).  The HSA runtime creates an SDMA engine's queue the first time a
+// copy is put on that engine, and hipMemcpyAsync puts a copy on the first
+// engine that is free at the call: with one 8 GiB H2D copy still running the
+// next goes to the next engine, so the first copies of a pipeline each met a
+// fresh engine and the call held the host 7.2-7.6 ms while the runtime
+// built its queue (AMD_LOG_LEVEL=4 of the e2e leg: only the first 8 GiB copy on
+// engines 0x2, 0x4, 0x8 and 0x10 was slow, every later one on the same engine
+// took 17-34 us; HSA_ENABLE_SDMA=0 removed the stall with blit kernels,
+// ROC_SIGNAL_POOL_SIZE and HSA_ENABLE_SDMA_GANG did not move it;
+// profiles/r06c).  So every engine the runtime reports for H2D and D2H gets
+// one 64-byte copy here, once per device per process, before any pipeline
+// runs.  HBX_SDMA_WARM=0 (A/B) leaves the engines cold.
+static hsa_status_t first_cpu_agent(hsa_agent_t a, void* data) {
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
+    *static_cast<hsa_agent_t*>(data) = a;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+static void warm_sdma_engines(hbx_ctx* c) {
+  static std::mutex mu;
+  static uint64_t done = 0;  // devices warmed in this process (bit per device)
+  std::lock_guard<std::mutex> g(mu);
+  if (c->device >= 64 || (done >> c->device) & 1u) return;
+  const auto t0 = std::chrono::steady_clock::now();
+  void* d = nullptr;
+  void* h = nullptr;
+  if (hipMalloc(&d, 4096) != hipSuccess || hipHostMalloc(&h, 4096, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    if (d) (void)hipFree(d);
+    return;  // no warm-up: correct, only the first copies per engine are slow
+  }
+  std::memset(h, 0, 4096);
+  hsa_amd_pointer_info_t pi;
+  std::memset(&pi, 0, sizeof(pi));
+  pi.size = sizeof(pi);
+  hsa_agent_t cpu{0};
+  hsa_signal_t sig{0};
+  if (hsa_amd_pointer_info(d, &pi, nullptr, nullptr, nullptr) == HSA_STATUS_SUCCESS && pi.agentOwner.handle &&
+      hsa_iterate_agents(first_cpu_agent, &cpu) != HSA_STATUS_ERROR && cpu.handle &&
+      hsa_signal_create(1, 0, nullptr, &sig) == HSA_STATUS_SUCCESS) {
+    const hsa_agent_t gpu = pi.agentOwner;
+    for (int dir = 0; dir < 2; dir++) {
+      const hsa_agent_t dst = dir ? cpu : gpu, src = dir ? gpu : cpu;
+      uint32_t mask = 0;
+      if (hsa_amd_memory_copy_engine_status(dst, src, &mask) != HSA_STATUS_SUCCESS) continue;
+      (dir ? c->sdma_d2h : c->sdma_h2d) = mask;
+      for (uint32_t bit = 1; bit && bit <= mask; bit <<= 1) {
+        if (!(mask & bit)) continue;
+        hsa_signal_store_screlease(sig, 1);
+        if (hsa_amd_memory_async_copy_on_engine(dir ? h : d, dst, dir ? d : h, src, 64, 0, nullptr, sig,
+                                                (hsa_amd_sdma_engine_id_t)bit, true) != HSA_STATUS_SUCCESS)
+          continue;
+        (void)hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+      }
+    }
+    hsa_signal_destroy(sig);
+  }
+  (void)hipHostFree(h);
+  (void)hipFree(d);
+  done |= 1ull << c->device;
+  c->sdma_warm_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
 int hbx_ctx_create(int device, hbx_ctx** out) {
   if (!out) return HBX_ERR_ARG;
   *out = nullptr;
@@ -1392,6 +1466,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = ab_env("HBX_PLAN_CUT")) c->plan_cut = (uint32_t)std::min(2, std::max(0, std::atoi(v)));
   if (const char* v = ab_env("HBX_META_KERNEL")) c->meta_kernel = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_GATE_META")) c->gate_meta = std::atoi(v) ? 1u : 0u;
+  if (const char* v = ab_env("HBX_SDMA_WARM")) c->sdma_warm = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_PSETS")) c->k3_psets = std::atoi(v) == 3 ? 3u : 2u;
   if (const char* v = ab_env("HBX_K1_SWZ")) c->k1_swz = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_ITEMS")) c->k3_items = (uint32_t)std::min(8, std::max(0, std::atoi(v)));
@@ -1422,6 +1497,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
     hbx_ctx_destroy(c);
     return HBX_ERR_HIP;
   }
+  if (c->sdma_warm) warm_sdma_engines(c);
   *out = c;
   return HBX_OK;
 }
@@ -1609,11 +1685,13 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
       "\"md5_wgs\": %u, \"plan_mode\": %d, \"k2_own\": %d, \"k4_window\": %u, \"k3_probe\": %d, "
       "\"lean_marks\": %u, \"k3_prod\": %u, \"k3_items\": %u, \"k3_period\": %u, \"meta_kernel\": %u, "
       "\"plan_cut\": %u, \"k1_swz\": %u, \"k3_psets\": %u, \"d2h_kernel\": %u, \"k8_split_streams\": %llu, "
-      "\"k8_split_fallbacks\": %llu, \"gate_meta\": %u}",
+      "\"k8_split_fallbacks\": %llu, \"gate_meta\": %u, \"sdma_warm\": %u, \"sdma_h2d_mask\": %u, "
+      "\"sdma_d2h_mask\": %u, \"sdma_warm_ms\": %.3f}",
       (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_gate, c->md5_wgs,
       plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks, c->k3_prod, c->k3_items,
       c->k3_period, c->meta_kernel, c->plan_cut, c->k1_swz, c->k3_psets, c->d2h_kernel,
-      (unsigned long long)c->k8_split_streams, (unsigned long long)c->k8_split_fallbacks, c->gate_meta);
+      (unsigned long long)c->k8_split_streams, (unsigned long long)c->k8_split_fallbacks, c->gate_meta,
+      c->sdma_warm, c->sdma_h2d, c->sdma_d2h, c->sdma_warm_ms);
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }
 

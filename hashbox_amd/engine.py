@@ -333,7 +333,7 @@ class Engine:
         """The context's effective pipeline knobs (hbx_knobs), including
         whether HBX_* A/B switches were honoured (only with HBX_AB=1)."""
         import json
-        buf = ctypes.create_string_buffer(1024)
+        buf = ctypes.create_string_buffer(4096)
         self._check(self._L.hbx_knobs(self._ctx, buf, len(buf)), "hbx_knobs")
         return json.loads(buf.value.decode())
 

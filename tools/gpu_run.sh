@@ -68,7 +68,7 @@ for step in "$@"; do
       timeout -k 10 700 python tools/bench_config5.py > $O/config5.json 2> $O/config5.err || { tail -20 $O/config5.err; exit 1; }
       cat $O/config5.json ;;
     copystall)  # the host stall in the SDMA copy call (verdict r05 item 2): trace + HIP runtime wait/signal log
-      HBX_TRACE_SLOW_SUBMIT=1 AMD_LOG_LEVEL=4 AMD_LOG_MASK=0x24 timeout -k 10 300 python bench.py --e2e --steps 60 --warmup 5 \
+      HBX_TRACE_SLOW_SUBMIT=1 AMD_LOG_LEVEL=4 timeout -k 10 300 python bench.py --e2e --steps 25 --warmup 5 \
         --no-cpu-baseline --no-check > $O/copystall.json 2> $O/copystall.err || { tail -20 $O/copystall.err; exit 1; }
       grep -E "hbx slow" $O/copystall.err | head -20; summ $O/copystall.json ;;
     env=*)  # bench.py --e2e with one runtime environment variable (e.g. env=ROC_SIGNAL_POOL_SIZE=256)
