@@ -364,6 +364,7 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
         dist.barrier()
     torch.cuda.synchronize(dev)
     eng.stage_totals(reset=True)  # everything before the window is complete and harvested
+    eng.host_call_max(reset=True)
     state["t_sub"] = state["t_col"] = 0.0
     eng.wait_s = 0.0
     thr0 = cpu_throttle()
@@ -385,6 +386,8 @@ def steady(eng, arenas, offs, lens, R, steps, warmup, dist, dev, before_submit=N
             "slowest_submit_fence_alloc_call_ms": [round(x * 1e3, 4) for x in state["parts"][len(state["parts"]) - steps + int(subs.argmax())]],
             "collect_ms_max": round(float(cols.max()), 4),
             "collect_slowest_step": int(cols.argmax())}
+    hc = eng.host_call_max()
+    host["library_slowest_call_ms"] = {"h2d_copy": round(float(hc[0]), 4), "submit": round(float(hc[1]), 4)}
     thr1 = cpu_throttle()
     if thr0 and thr1:
         host["cpu_throttled_n_ms"] = [thr1[0] - thr0[0], round((thr1[1] - thr0[1]) / 1e3, 3)]

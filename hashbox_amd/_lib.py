@@ -35,6 +35,7 @@ EXPORTS = [
     "hbx_verify_submit_device", "hbx_inflate_blocks_device", "hbx_store_paths_zcb", "hbx_after_stream",
     "hbx_set_join_lag", "hbx_set_k3_period", "hbx_k3_wave_times", "hbx_input_after_oldest", "hbx_knobs",
     "hbx_input_fence", "hbx_set_k3_probe", "hbx_store_paths_status", "hbx_plan_pipeline", "hbx_apply_plan",
+    "hbx_host_call_max",
 ]
 # Functions returning something other than an int status.
 _NON_STATUS = ("hbx_ctx_destroy", "hbx_last_error", "hbx_max_chunks", "hbx_file_entry_size",
@@ -152,6 +153,7 @@ def load() -> ctypes.CDLL:
     L.hbx_knobs.argtypes = [P, ctypes.c_char_p, U64]
     L.hbx_stage_totals.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64), I]
     L.hbx_io_times.argtypes = [P, ctypes.POINTER(ctypes.c_double), I]
+    L.hbx_host_call_max.argtypes = [P, ctypes.POINTER(ctypes.c_double), I]
     L.hbx_reserve.argtypes = [P, ctypes.c_uint32, U64, U64]
     L.hbx_verify_blocks.argtypes = [P, U64, P, P, P, P, P, P, P, P, ctypes.POINTER(U64)]
     L.hbx_verify_blocks_device.argtypes = [P, P, U64, P, P, P, P, P, P, P, P, ctypes.POINTER(U64)]

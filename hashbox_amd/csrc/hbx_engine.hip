@@ -308,6 +308,10 @@ struct hbx_ctx {
   // process has done it for the device)
   uint32_t sdma_h2d = 0, sdma_d2h = 0;
   double sdma_warm_ms = 0.0;
+  // hbx_host_call_max: the longest host time of one H2D copy call and of one
+  // batch submit since the last reset (hbx_memcpy_h2d_async, the disk path's
+  // copies, submit_batch), ms
+  double max_copy_ms = 0.0, max_submit_ms = 0.0;
   uint32_t sdma_warm = 1;
   PinBuf h_read[2];         // hbx_store_paths: pinned landing slots for file reads
   PinBuf h_zstage;          // hbx_store_paths_z: compressed streams of one batch (synchronous form)
@@ -482,6 +486,10 @@ Batch* acquire_batch(hbx_ctx* c) {
   b->v_ok = nullptr;
   b->v_nbad = nullptr;
   return b;
+}
+
+static double ms_since(std::chrono::steady_clock::time_point t) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
 }
 
 // HBX_TRACE_SLOW_SUBMIT=<ms>: a submit slower than that prints where its host
@@ -954,9 +962,20 @@ inline uint64_t scan_iters(uint64_t N) {  // K1 iterations of a file (0: no spli
 // collected by wait_oldest in submission order.  Every validation and
 // allocation happens before the batch joins the FIFO; a failure after that
 // removes it again (submit_abort), so a failed submit leaves no pending batch.
+int submit_batch_timed(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* offs,
+                       const uint64_t* lens, uint64_t* cut_ends, uint8_t* ids, const uint64_t* out_base,
+                       const uint64_t* caps, hbx_file_summary* sums, uint32_t budget);
 int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* offs,
                  const uint64_t* lens, uint64_t* cut_ends, uint8_t* ids, const uint64_t* out_base,
                  const uint64_t* caps, hbx_file_summary* sums, uint32_t budget) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = submit_batch_timed(c, d_arena, n, offs, lens, cut_ends, ids, out_base, caps, sums, budget);
+  c->max_submit_ms = std::max(c->max_submit_ms, ms_since(t0));
+  return rc;
+}
+int submit_batch_timed(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* offs,
+                       const uint64_t* lens, uint64_t* cut_ends, uint8_t* ids, const uint64_t* out_base,
+                       const uint64_t* caps, hbx_file_summary* sums, uint32_t budget) {
   g_slow.mark(0);
   g_slow.clear();
   if (c->broken) return c->fail(HBX_ERR_STATE, "context is unusable after a failed submit; destroy it");
@@ -2442,9 +2461,12 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
         (rc = c->hip(hipStreamWaitEvent(c->stream, c->zs[arena_zstage].done, 0), "hipStreamWaitEvent")))
       break;
     arena_zstage = -1;
+    const auto tc = std::chrono::steady_clock::now();
     if ((rc = c->hip(hipMemcpyAsync(arena.p, c->h_read[p].p, tot, hipMemcpyHostToDevice, c->stream),
                      "hipMemcpyAsync")))
       break;
+    c->max_copy_ms = std::max(c->max_copy_ms, ms_since(tc));
+    g_slow.call("store_paths h2d: hipMemcpyAsync", tc, c->launches);
     if ((rc = c->hip(hipEventRecord(c->h2d_done[p], c->stream), "hipEventRecord"))) break;
     slot_used[p] = true;
     // a skipped file (status != 0) goes in as an empty file: no chunks
@@ -2489,6 +2511,15 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
 }
 }  // namespace
 
+int hbx_host_call_max(hbx_ctx* c, double ms[2], int reset) {
+  if (!c || !ms) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  ms[0] = c->max_copy_ms;
+  ms[1] = c->max_submit_ms;
+  if (reset) c->max_copy_ms = c->max_submit_ms = 0.0;
+  return HBX_OK;
+}
+
 int hbx_io_times(hbx_ctx* c, double s[3], int reset) {
   if (!c || !s) return HBX_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
@@ -2508,6 +2539,7 @@ int hbx_memcpy_h2d_async(hbx_ctx* c, void* d, const void* h, uint64_t n) {
   g_slow.call("h2d: input wait", t0, c->launches);
   const auto t1 = std::chrono::steady_clock::now();
   HBX_TRY(c, hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, c->stream));
+  c->max_copy_ms = std::max(c->max_copy_ms, ms_since(t1));
   g_slow.call("h2d: hipMemcpyAsync", t1, c->launches);
   return HBX_OK;
 }

@@ -629,6 +629,13 @@ class Engine:
                           for i in range(r.n_chunks)]
         return res
 
+    def host_call_max(self, reset: bool = False) -> np.ndarray:
+        """hbx_host_call_max: ms of the slowest single H2D copy call and the
+        slowest single submit since the last reset."""
+        a = (ctypes.c_double * 2)()
+        self._check(self._L.hbx_host_call_max(self._ctx, a, int(reset)), "hbx_host_call_max")
+        return np.array(list(a))
+
     def io_times(self, reset: bool = False) -> np.ndarray:
         """store_paths host seconds: reading files, waiting for batches to be
         collected (arena reuse and the final drain), waiting for a pinned

@@ -185,6 +185,13 @@ int hbx_store_paths(hbx_ctx *ctx, uint64_t n_files, const char *const *paths,
  * arena's reuse, and the drain at the end of the call), [2] waiting for a
  * pinned slot's H2D copy.  reset != 0 zeroes them. */
 int hbx_io_times(hbx_ctx *ctx, double s[3], int reset);
+/* Host time of the slowest single call since the last reset, ms: [0] one H2D
+ * copy call (hbx_memcpy_h2d_async and the disk path's copies), [1] one batch
+ * submit (hbx_submit_device and the disk path's submits).  reset != 0 zeroes
+ * them after reading.  No reference counterpart: diagnostics (the copy call
+ * once held the host ~7 ms while the runtime created an SDMA engine's queue,
+ * DESIGN.md §8). */
+int hbx_host_call_max(hbx_ctx *ctx, double ms[2], int reset);
 
 /* MD5(BE32(n_links) || links || BE32(len) || data) on the device. */
 int hbx_block_id(hbx_ctx *ctx, const uint8_t *links, uint32_t n_links, const uint8_t *data,

@@ -89,13 +89,15 @@ def main():
         passes = []
         for _ in range(a.passes):
             eng.io_times(reset=True)
+            eng.host_call_max(reset=True)
             c0 = cpu_state()
             t0 = time.time()
             res = eng.store_paths(paths, a.io_threads, a.batch_mib << 20, sizes=sizes)
             t_gpu = time.time() - t0
             c1 = cpu_state()
             io = eng.io_times()
-            passes.append({"e2e_seconds": round(t_gpu, 3), "e2e_gibs": round(total / t_gpu / (1 << 30), 3),
+            hc = eng.host_call_max()
+            passes.append({"slowest_h2d_call_ms": round(float(hc[0]), 3), "slowest_submit_ms": round(float(hc[1]), 3),"e2e_seconds": round(t_gpu, 3), "e2e_gibs": round(total / t_gpu / (1 << 30), 3),
                            "library_seconds": round(eng.last_call_s, 3),
                            "library_gibs": round(total / eng.last_call_s / (1 << 30), 3),
                            "read_files_seconds": round(float(io[0]), 3),
