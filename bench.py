@@ -464,14 +464,28 @@ def lifetime_leg(eng, arenas, offs, lens, R, B, lead, nfull, head, dist, gpu, pe
         w = steady(eng, arenas, offs, lens, R, max(3, period), max(3, period), dist, gpu)["probe_raw"].astype(np.int64)
     finally:
         eng.set_k3_probe(False)
-    coop = w[w[:, 7] > 0]
+    blocks = w[:, 7] & 0xffffffff
+    polls = w[:, 7] >> 32  # the wave's polls that found its producer's stage not yet written
+    keep = blocks > 0
+    coop, blocks, polls = w[keep], blocks[keep], polls[keep]
     if not len(coop):
         return None
     R_w = coop[:, 3] & 0xffff
-    full = coop[R_w == R_w.max()]
+    sel = R_w == R_w.max()
+    full, fblocks, fpolls = coop[sel], blocks[sel], polls[sel]
     cyc = (full[:, 5] - full[:, 4]).astype(np.float64)
     ticks = (full[:, 6] - (full[:, 1] & ((1 << 56) - 1))).astype(np.float64)
-    cpb = float(np.median(cyc / full[:, 7]))
+    cpb = float(np.median(cyc / fblocks))
+    # the slowest tenth of the full-slice waves (by cycles per block) against the
+    # rest: do they wait for their producer (polls), or issue slower?
+    per = cyc / fblocks
+    slow = per >= np.quantile(per, 0.9)
+    stage_wait = {"polls_per_wave_min_med_max": [int(fpolls.min()), float(np.median(fpolls)), int(fpolls.max())],
+                  "polls_per_1000_blocks_median": round(float(np.median(fpolls / fblocks * 1000)), 3),
+                  "slowest_tenth_cycles_per_block_median": round(float(np.median(per[slow])), 1),
+                  "slowest_tenth_polls_median": float(np.median(fpolls[slow])),
+                  "rest_polls_median": float(np.median(fpolls[~slow])) if (~slow).any() else None,
+                  "poll_sleep_cycles": 64}
     ghz = float(np.median(cyc / np.maximum(ticks, 1) * 0.1))
     launch_ms = float(head["roofline"]["avg_launch_ms"])
     hashing_ms = B * cpb / ghz * 1e-6
@@ -490,6 +504,7 @@ def lifetime_leg(eng, arenas, offs, lens, R, B, lead, nfull, head, dist, gpu, pe
         "lifetime_ms": round(R * step_ms, 2), "serial_floor_ms": round(floor_ms, 2),
         "lifetime_over_floor": round(R * step_ms / floor_ms, 4),
         "k3_busy_waves": busy,
+        "stage_wait": stage_wait,
     }
 
 

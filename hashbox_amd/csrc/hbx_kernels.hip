@@ -1091,6 +1091,17 @@ __device__ __forceinline__ void k3p_wait_ge(uint32_t* p, uint32_t want) {
   }
   asm volatile("" ::: "memory");  // no LDS access of the stage moves above the wait
 }
+// The same, counting the polls that found the stage not yet written (the MD5
+// wave's waits for its producer; reported by the K3 probe, verdict r05 item 1)
+__device__ __forceinline__ void k3p_wait_ge(uint32_t* p, uint32_t want, uint32_t& polls) {
+  for (;;) {
+    const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane((int)k3p_flag(p));
+    if ((int32_t)(v - want) >= 0) break;
+    polls++;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");
+}
 __device__ __forceinline__ void k3p_publish(uint32_t* p, uint32_t v) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the stage's LDS writes (or reads) are done
   if ((threadIdx.x & 63u) == 0u) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1116,7 +1127,8 @@ __device__ __forceinline__ void k3p_publish(uint32_t* p, uint32_t v) {
 // A stage is freed once its last block is hashed (its reads have landed: the
 // block waited for them), except the group's last stage (freed by the caller
 // once the group is done).
-__device__ __forceinline__ void k3p_consume(uint8_t* wl, uint32_t* flags, uint32_t S, uint32_t Rr, uint32_t (&h)[4]) {
+__device__ __forceinline__ void k3p_consume(uint8_t* wl, uint32_t* flags, uint32_t S, uint32_t Rr, uint32_t (&h)[4],
+                                            uint32_t& polls) {
   const uint32_t row = (uint32_t)(uintptr_t)(wl + (threadIdx.x & 63u) * Coop<16>::Row);  // LDS address
   auto stage_at = [&](uint32_t k) { return row + ((S + k) & 1u) * Coop<16>::Half; };
   // the 4 reads of a block into N, then wait until only those are outstanding:
@@ -1139,7 +1151,7 @@ __device__ __forceinline__ void k3p_consume(uint8_t* wl, uint32_t* flags, uint32
   };
   const uint32_t nst = (4u * Rr + 15u) / 16u;  // >= 2 (Rr >= kCoopMinBudget - 1)
   u32x4 WA[4], WB[4];
-  k3p_wait_ge(&flags[0], S + 1u);
+  k3p_wait_ge(&flags[0], S + 1u, polls);
   asm volatile(
       "ds_read_b128 %0, %4\n\t"
       "ds_read_b128 %1, %4 offset:16\n\t"
@@ -1158,7 +1170,7 @@ __device__ __forceinline__ void k3p_consume(uint8_t* wl, uint32_t* flags, uint32
     hash(WB);
     next_wait(a0 + 192u, WB, WA);
     hash(WA);
-    k3p_wait_ge(&flags[0], S + k + 2u);
+    k3p_wait_ge(&flags[0], S + k + 2u, polls);
     next_wait(stage_at(k + 1u), WA, WB);
     hash(WB);
     asm volatile("" ::: "memory");  // stage k is done (its reads have landed: the blocks waited for them)
@@ -1503,6 +1515,7 @@ __device__ __forceinline__ void k3_body(
   uint32_t pR = 0u, pmax = 0u;
   uint32_t S = 0;  // PROD: stages of this launch so far (the producer counts the same)
   uint32_t seq = 0;  // ITEMS: items announced to the producer
+  uint32_t polls = 0;  // PROD: polls that found the producer's stage not yet written
   bool first = true;
   for (uint32_t g = g0;; g += nwaves) {
     uint32_t part = 0u, item = 0u;
@@ -1533,7 +1546,7 @@ __device__ __forceinline__ void k3_body(
         pmax = wave_max_all(cnt);
       }
       if constexpr (PROD) {  // stages from the producer wave; the group's last is freed at its end
-        k3p_consume(wl, flags, S, R - 1u, h);
+        k3p_consume(wl, flags, S, R - 1u, h, polls);
         S += (4u * (R - 1u) + 15u) / 16u;
       } else {
         md5_coop<16>(wl, src, h, L.next + 1u, R - 1u);
@@ -1611,7 +1624,7 @@ __device__ __forceinline__ void k3_body(
     p[4] = pc1;
     p[5] = pc2;
     p[6] = pt2;
-    p[7] = pR ? pR - 1u : 0u;
+    p[7] = (pR ? pR - 1u : 0u) | ((uint64_t)polls << 32);  // + the launch's stage-wait polls (s_sleep 1 each)
   }
   if (started && tslot && (threadIdx.x & 63u) == 0u) {
     const uint32_t tk = __hip_atomic_fetch_add(started + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);

@@ -499,7 +499,9 @@ int hbx_set_k3_probe(hbx_ctx *ctx, int on);
  * group's loads and prologue block) | XCC id << 56, end, R | max count << 16
  * | HW_ID << 32, s_memtime (shader cycles) at the start and the end of the
  * first group's cooperative phase, s_memrealtime at its end, the blocks of
- * each chain it hashed (R - 1)} (times in s_memrealtime ticks, 100 MHz; R and
+ * each chain it hashed (R - 1) | the polls (s_sleep 1 each) in which the wave
+ * found its producer's next stage not yet written, over the launch, << 32}
+ * (times in s_memrealtime ticks, 100 MHz; R and
  * the count saturate at 65535; the last four are 0 for a wave whose first
  * group took the lane path).  Copies the latest launch's records (8 x u64 per
  * wave, up to max_waves) after the hash stream drains; *n_waves = waves per

@@ -63,16 +63,19 @@ def main():
         # (s_memtime cycles over s_memrealtime ticks), slowest waves vs median
         cyc = (busy[:, 5] - busy[:, 4]).astype(np.float64)
         ticks = (busy[:, 6] - (busy[:, 1] & low56)).astype(np.float64)
-        nb = busy[:, 7].astype(np.float64)
+        nb = (busy[:, 7] & 0xffffffff).astype(np.float64)
+        polls = (busy[:, 7] >> 32).astype(np.int64)  # stage-wait polls over the launch (s_sleep 1 each)
         ok = nb > 0
         cpb = np.where(ok, cyc / np.maximum(nb, 1), np.nan)
         ghz = np.where(ok, cyc / np.maximum(ticks, 1) * 0.1, np.nan)
         rows.append({"step": step, "median_full_end_us": round(float(np.median(end[full])), 1),
                      "span_us": round(float(end.max()), 1),
                      "median_cpb": round(float(np.nanmedian(cpb)), 1), "median_ghz": round(float(np.nanmedian(ghz)), 3),
+                     "median_polls": float(np.median(polls[full])),
                      "slowest": [{"cu": cu[i], "end_us": round(float(end[i]), 1),
                                   "cpb": None if np.isnan(cpb[i]) else round(float(cpb[i]), 1),
-                                  "ghz": None if np.isnan(ghz[i]) else round(float(ghz[i]), 3)} for i in order[:6]]})
+                                  "ghz": None if np.isnan(ghz[i]) else round(float(ghz[i]), 3),
+                                  "polls": int(polls[i])} for i in order[:6]]})
         print(json.dumps(rows[-1]), flush=True)
     while eng.pending():
         eng.wait()

@@ -87,6 +87,9 @@ for step in "$@"; do
       env "${envs[@]}" timeout -k 10 400 python bench.py "${args[@]}" > $O/$name.json 2> $O/$name.err \
         || { echo "FAIL $step"; tail -20 $O/$name.err; exit 1; }
       summ $O/$name.json ;;
+    slowcu)  # per-launch K3 probe: slowest CUs, their cycles per block and stage-wait polls
+      timeout -k 10 300 python tools/diag_slow_cu.py > $O/slow_cu.txt 2> $O/slow_cu.err || { tail -20 $O/slow_cu.err; exit 1; }
+      tail -4 $O/slow_cu.txt | cut -c1-600 ;;
     ab=*)
       kv=${step#ab=}
       env HBX_AB=1 "$kv" timeout -k 10 300 python bench.py --e2e-steps 0 --no-cpu-baseline > $O/ab_$kv.json 2> $O/ab_$kv.err \
