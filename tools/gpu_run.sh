@@ -67,6 +67,9 @@ for step in "$@"; do
     config5)
       timeout -k 10 700 python tools/bench_config5.py > $O/config5.json 2> $O/config5.err || { tail -20 $O/config5.err; exit 1; }
       cat $O/config5.json ;;
+    config5t)  # config 5 with the slow-submit trace (every submit or copy call over 1 ms prints its phases)
+      HBX_TRACE_SLOW_SUBMIT=1 timeout -k 10 700 python tools/bench_config5.py > $O/config5t.json 2> $O/config5t.err || { tail -20 $O/config5t.err; exit 1; }
+      grep -c "hbx slow" $O/config5t.err; grep -A1 "hbx slow submit" $O/config5t.err | head -40 | cut -c1-400 ;;
     copystall)  # the host stall in the SDMA copy call (verdict r05 item 2): trace + HIP runtime wait/signal log
       HBX_TRACE_SLOW_SUBMIT=1 AMD_LOG_LEVEL=4 timeout -k 10 300 python bench.py --e2e --steps 25 --warmup 5 \
         --no-cpu-baseline --no-check > $O/copystall.json 2> $O/copystall.err || { tail -20 $O/copystall.err; exit 1; }
