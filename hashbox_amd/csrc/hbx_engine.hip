@@ -965,6 +965,12 @@ inline uint64_t scan_iters(uint64_t N) {  // K1 iterations of a file (0: no spli
 int submit_batch_timed(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* offs,
                        const uint64_t* lens, uint64_t* cut_ends, uint8_t* ids, const uint64_t* out_base,
                        const uint64_t* caps, hbx_file_summary* sums, uint32_t budget);
+}  // namespace
+// hbx_reserve with the context's lock already held (defined beside it, inside
+// the C-ABI block; not exported)
+extern "C" __attribute__((visibility("hidden"))) int reserve_locked(hbx_ctx* c, uint32_t batches, uint64_t files,
+                                                                    uint64_t bytes);
+namespace {
 int submit_batch(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64_t* offs,
                  const uint64_t* lens, uint64_t* cut_ends, uint8_t* ids, const uint64_t* out_base,
                  const uint64_t* caps, hbx_file_summary* sums, uint32_t budget) {
@@ -1765,6 +1771,10 @@ int hbx_set_md5_slice(hbx_ctx* c, uint32_t blocks) {
 int hbx_reserve(hbx_ctx* c, uint32_t batches, uint64_t files, uint64_t bytes) {
   if (!c || files > 0xFFFFFFFFull) return HBX_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
+  return reserve_locked(c, batches, files, bytes);
+}
+
+int reserve_locked(hbx_ctx* c, uint32_t batches, uint64_t files, uint64_t bytes) {
   if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
   HBX_TRY(c, hipSetDevice(c->device));
   const uint64_t caps = bytes / HBX_MIN_BLOCK_SIZE + files;  // >= sum of max_chunks over the files
@@ -2332,7 +2342,7 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
   if (c->d_ring.size() < depth) c->d_ring.resize(depth);
   // size every staging buffer once, for the largest batch this call forms
   // (growing one later would re-pin host memory or drain the streams)
-  uint64_t biggest = 0, zbytes = 0, zchunks = 0, zsegs = 0;
+  uint64_t biggest = 0, zbytes = 0, zchunks = 0, zsegs = 0, most_files = 0;
   for (uint64_t i = 0; i < n;) {
     uint64_t tot = 0, cnt = 0;
     while (i < n && (cnt == 0 || tot + lens[i] <= batch_bytes) && cnt < 65536) {
@@ -2341,6 +2351,7 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
       cnt++;
     }
     biggest = std::max(biggest, tot);
+    most_files = std::max(most_files, cnt);
     // compression stage bounds of this batch: chunks <= a file's
     // max_chunks, a chunk's stream <= hbx_deflate_bound rounded to 16 B
     const uint64_t nch = tot / HBX_MIN_BLOCK_SIZE + cnt;
@@ -2365,6 +2376,11 @@ int store_paths_impl(hbx_ctx* c, uint64_t n, const char* const* paths, const uin
     int r0 = ensure_shared(c, c->d_ring[i], biggest + 65536);
     if (r0) return r0;
   }
+  // every batch slot of the pipeline sized for the largest batch up front: a
+  // pooled batch that met a larger batch later reallocated its pinned meta and
+  // result buffers inside that submit (19-28 ms per submit of config 5,
+  // HBX_TRACE_SLOW_SUBMIT "buffers", profiles/r06e)
+  if (int r0 = reserve_locked(c, (uint32_t)depth + 2u, most_files, biggest)) return r0;
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   bool slot_used[2] = {false, false};
   std::vector<uint64_t> offs, skip_lens;
