@@ -1093,12 +1093,13 @@ __device__ __forceinline__ void k3p_wait_ge(uint32_t* p, uint32_t want) {
 }
 // The same, counting the polls that found the stage not yet written (the MD5
 // wave's waits for its producer; reported by the K3 probe, verdict r05 item 1)
-__device__ __forceinline__ void k3p_wait_ge(uint32_t* p, uint32_t want, uint32_t& polls) {
+// spin (HBX_K3_SPIN, A/B): re-poll at once instead of after s_sleep 1 (64 cycles)
+__device__ __forceinline__ void k3p_wait_ge(uint32_t* p, uint32_t want, uint32_t& polls, bool spin) {
   for (;;) {
     const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane((int)k3p_flag(p));
     if ((int32_t)(v - want) >= 0) break;
     polls++;
-    __builtin_amdgcn_s_sleep(1);
+    if (!spin) __builtin_amdgcn_s_sleep(1);
   }
   asm volatile("" ::: "memory");
 }
@@ -1128,7 +1129,7 @@ __device__ __forceinline__ void k3p_publish(uint32_t* p, uint32_t v) {
 // block waited for them), except the group's last stage (freed by the caller
 // once the group is done).
 __device__ __forceinline__ void k3p_consume(uint8_t* wl, uint32_t* flags, uint32_t S, uint32_t Rr, uint32_t (&h)[4],
-                                            uint32_t& polls) {
+                                            uint32_t& polls, bool spin) {
   const uint32_t row = (uint32_t)(uintptr_t)(wl + (threadIdx.x & 63u) * Coop<16>::Row);  // LDS address
   auto stage_at = [&](uint32_t k) { return row + ((S + k) & 1u) * Coop<16>::Half; };
   // the 4 reads of a block into N, then wait until only those are outstanding:
@@ -1151,7 +1152,7 @@ __device__ __forceinline__ void k3p_consume(uint8_t* wl, uint32_t* flags, uint32
   };
   const uint32_t nst = (4u * Rr + 15u) / 16u;  // >= 2 (Rr >= kCoopMinBudget - 1)
   u32x4 WA[4], WB[4];
-  k3p_wait_ge(&flags[0], S + 1u, polls);
+  k3p_wait_ge(&flags[0], S + 1u, polls, spin);
   asm volatile(
       "ds_read_b128 %0, %4\n\t"
       "ds_read_b128 %1, %4 offset:16\n\t"
@@ -1170,7 +1171,7 @@ __device__ __forceinline__ void k3p_consume(uint8_t* wl, uint32_t* flags, uint32
     hash(WB);
     next_wait(a0 + 192u, WB, WA);
     hash(WA);
-    k3p_wait_ge(&flags[0], S + k + 2u, polls);
+    k3p_wait_ge(&flags[0], S + k + 2u, polls, spin);
     next_wait(stage_at(k + 1u), WA, WB);
     hash(WB);
     asm volatile("" ::: "memory");  // stage k is done (its reads have landed: the blocks waited for them)
@@ -1479,7 +1480,7 @@ template <bool PROD, bool ITEMS = false>
 __device__ __forceinline__ void k3_body(
     uint8_t* wl, const OrderEntry* __restrict__ order, const uint32_t* __restrict__ n_order, uint32_t budget,
     uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last, uint64_t* __restrict__ tslot,
-    uint64_t* __restrict__ probe, uint32_t* flags = nullptr, K3Queue Q = K3Queue{}) {
+    uint64_t* __restrict__ probe, uint32_t* flags = nullptr, K3Queue Q = K3Queue{}, bool spin = false) {
   static_assert(PROD || !ITEMS, "items need the producer waves");
   // the MD5 chains are issue-bound: win the SIMD's issue arbitration against
   // co-resident waves of other kernels
@@ -1546,7 +1547,7 @@ __device__ __forceinline__ void k3_body(
         pmax = wave_max_all(cnt);
       }
       if constexpr (PROD) {  // stages from the producer wave; the group's last is freed at its end
-        k3p_consume(wl, flags, S, R - 1u, h, polls);
+        k3p_consume(wl, flags, S, R - 1u, h, polls, spin);
         S += (4u * (R - 1u) + 15u) / 16u;
       } else {
         md5_coop<16>(wl, src, h, L.next + 1u, R - 1u);
@@ -1652,6 +1653,9 @@ extern "C" __global__ __launch_bounds__(kK3PThreads, 1) void hbx_k3p_block_md5(
     const OrderEntry* __restrict__ order, const uint32_t* __restrict__ n_order, uint32_t budget,
     uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last, uint64_t* __restrict__ tslot,
     uint64_t* __restrict__ probe, uint32_t psets) {
+  // psets: producer register sets (2 or 3) | 0x100 for the spinning stage wait
+  const bool spin = (psets & 0x100u) != 0u;
+  psets &= 0xffu;
   __shared__ __attribute__((aligned(16))) uint8_t k3_lds[4][kK3WaveLds];
   __shared__ uint32_t k3_flags[4][2];
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -1659,7 +1663,8 @@ extern "C" __global__ __launch_bounds__(kK3PThreads, 1) void hbx_k3p_block_md5(
   if (threadIdx.x < 8u) k3_flags[threadIdx.x >> 1][threadIdx.x & 1u] = 0u;
   __syncthreads();
   if (wave < 4u) {
-    k3_body<true>(k3_lds[pair], order, n_order, budget, started, t_first, t_last, tslot, probe, k3_flags[pair]);
+    k3_body<true>(k3_lds[pair], order, n_order, budget, started, t_first, t_last, tslot, probe, k3_flags[pair],
+                  K3Queue{}, spin);
   } else {
     __builtin_amdgcn_s_setprio(2);
     if (psets == 3u)

@@ -375,7 +375,7 @@ def test_k3_producer_waves(oracle, monkeypatch, md5_slice, join_lag, wgs, plan_c
             _check(a, r)
 
 
-@pytest.mark.parametrize("prod", ["1", "p3"])
+@pytest.mark.parametrize("prod", ["1", "p3", "s"])
 @pytest.mark.parametrize("md5_slice,join_lag", [(9, 1), (9, 2), (16384, 1), (0, 2)])
 def test_k3_lane_path_groups_between_cooperative_ones(oracle, monkeypatch, md5_slice, join_lag, prod):
     """Advisor r05 (high): with a producer wave per MD5 wave, a group on the
@@ -396,6 +396,7 @@ def test_k3_lane_path_groups_between_cooperative_ones(oracle, monkeypatch, md5_s
     monkeypatch.setenv("HBX_K3_PSETS", "3" if prod == "p3" else "2")
     monkeypatch.setenv("HBX_K3_ITEMS", "0")
     monkeypatch.setenv("HBX_K3_WGS", "1")
+    monkeypatch.setenv("HBX_K3_SPIN", "1" if prod == "s" else "0")  # s: stage waits without s_sleep
     rng = np.random.default_rng(977 + md5_slice % 13)
     batches = []
     for b in range(3):
@@ -415,7 +416,7 @@ def test_k3_lane_path_groups_between_cooperative_ones(oracle, monkeypatch, md5_s
     got, order = [], []
     with Engine(0, md5_slice=md5_slice, join_lag=join_lag) as e:
         k = e.knobs()
-        assert k["k3_prod"] and k["md5_wgs"] == 1
+        assert k["k3_prod"] and k["md5_wgs"] == 1 and k["k3_spin"] == (prod == "s")
         for i in [0, 1, 2, 1, 0, 2]:
             dev, offs, sizes, _ = batches[i]
             e.submit_device(dev.data_ptr(), offs, sizes)
