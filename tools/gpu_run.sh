@@ -90,6 +90,12 @@ for step in "$@"; do
       env "${envs[@]}" timeout -k 10 400 python bench.py "${args[@]}" > $O/$name.json 2> $O/$name.err \
         || { echo "FAIL $step"; tail -20 $O/$name.err; exit 1; }
       summ $O/$name.json ;;
+    hbms=*)  # tools/ubench/hbm_streams cases by name (comma-separated), chains alone
+      IFS=, read -ra cs <<< "${step#hbms=}"
+      for cn in "${cs[@]}"; do
+        timeout -k 10 120 tools/ubench/hbm_streams 128 $cn >> $O/hbm_streams.txt 2>&1 || { tail -5 $O/hbm_streams.txt; exit 1; }
+      done
+      grep -v "^#" $O/hbm_streams.txt ;;
     slowcu)  # per-launch K3 probe: slowest CUs, their cycles per block and stage-wait polls
       timeout -k 10 300 python tools/diag_slow_cu.py > $O/slow_cu.txt 2> $O/slow_cu.err || { tail -20 $O/slow_cu.err; exit 1; }
       tail -4 $O/slow_cu.txt | cut -c1-600 ;;

@@ -221,7 +221,10 @@ int main(int argc, char** argv) {
   // stages each): few translations per wave like "local", but every chain's
   // 256 B in a DRAM row of its own like "rand" (TLB reach vs DRAM locality);
   // "rand128" is "rand" over the same 128 stages.
-  struct Case { const char* name; int sets; bool lds; int place; uint32_t S; int cpw = 64; };
+  // "win<M>" (round 6): the 64 chains of a wave at random byte offsets inside a
+  // window of M MiB of its own (random, 2 MiB aligned): the translation reach
+  // a wave's chains need, between "page" (one 2 MiB page) and "rand" (128 GiB)
+  struct Case { const char* name; int sets; bool lds; int place; uint32_t S; int cpw = 64; uint32_t win_mib = 0; };
   // default: round 4, K3's 32,768 chains at 64 per wave (128 CUs, the
   // streamer on the other 128) vs 32 per wave (all 256 CUs, the streamer
   // sharing them with 64 KiB of LDS)
@@ -237,6 +240,9 @@ int main(int argc, char** argv) {
       {"coop_lds2_local", 2, true, 1, 32768u},  {"coop_lds3_local", 3, true, 1, 32768u},
       {"coop_lds2_page", 2, true, 2, 32768u},   {"coop_lds2_rand128", 2, true, 0, 32768u},
       {"coop8_rand", 8, true, 0, 32768u},        {"coop8_rand", 8, true, 0, 16384u},
+      {"coop_lds2_win2", 2, true, 3, 32768u, 64, 2},     {"coop_lds2_win8", 2, true, 3, 32768u, 64, 8},
+      {"coop_lds2_win32", 2, true, 3, 32768u, 64, 32},   {"coop_lds2_win128", 2, true, 3, 32768u, 64, 128},
+      {"coop_lds2_win512", 2, true, 3, 32768u, 64, 512}, {"coop_lds2_win2048", 2, true, 3, 32768u, 64, 2048},
   };
   // cases_full: the round-3 table (profiles/r03hbms/hbm_streams_sets_local.txt), run by name (argv[2])
   // argv[2] (optional): run only the cases named exactly so, argv[3] only that
@@ -257,6 +263,11 @@ int main(int argc, char** argv) {
     for (uint32_t i = 0; i < S; i++) {
       if (k.place == 2) {  // wave w: its own 2 MiB page, chain c at 32 KiB * c
         h[i] = (uint64_t)d_big + (uint64_t)(i / 64u) * (2ull << 20) + 32768ull * (i % 64u) + 8ull;
+      } else if (k.place == 3) {  // wave w: a window of win_mib MiB, chains at random offsets in it
+        static uint64_t wbase = 0;
+        const uint64_t W = (uint64_t)k.win_mib << 20;
+        if (i % 64u == 0u) wbase = (rng() % ((big - W - span) >> 21)) << 21;
+        h[i] = (uint64_t)d_big + wbase + rng() % (W > span ? W - span : 1ull);
       } else if (local) {  // wave w: chains side by side; stage st of chain c at w*64*span' + 16 KiB*st + 256*c
         const uint64_t w = i / 64u, c = i % 64u;
         h[i] = (uint64_t)d_big + w * 64ull * 256ull * (stages + 8u) + 256ull * c + 8ull;  // (16 KiB per stage: see kernel)
