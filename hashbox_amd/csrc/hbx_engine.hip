@@ -206,7 +206,10 @@ struct hbx_ctx {
   // hidden) 2,297-2,318 vs 2,286-2,308 GiB/s in three alternating pairs at 64
   // files, equal at 8 (profiles/r05af); HBX_K3_PSETS=2 for A/B
   uint32_t k3_psets = 3;
-  uint32_t k3_spin = 0;  // HBX_K3_SPIN=1 (A/B): the MD5 wave re-polls a late stage without s_sleep
+  uint32_t k3_spin = 0;
+  // HBX_PLAN_ADDR=<bins> (A/B, 0..512): full-slice chains ordered by data
+  // address in that many 512 MiB granules (plan_bin)
+  uint32_t plan_addr = 0;  // HBX_K3_SPIN=1 (A/B): the MD5 wave re-polls a late stage without s_sleep
   // at join lag 2, preplan on the cut stream (mode 3; HBX_PLAN_CUT=0: mode 1,
   // the plan on the hash stream): +2.7 % with K3P (profiles/r05e)
   // 2 (default): at lag 3 and 4 too, off the scan loop (8 files per GPU, K3
@@ -694,7 +697,7 @@ int plan_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
                            has_prev ? c->d_order[ps].as<OrderEntry>() : nullptr,
                            has_prev ? c->d_octl[ps].as<uint32_t>() : nullptr, c->last_budget,
                            fs, budget, c->d_order[slot].as<OrderEntry>(), c->d_octl[slot].as<uint32_t>(),
-                           c->d_plan.as<uint32_t>(), phase);
+                           c->d_plan.as<uint32_t>(), phase | (c->plan_addr << 8));
       HBX_TRY(c, hipGetLastError());
       HBX_TRY(c, hipEventRecord(t.b, s));
       // K3 waits on the timing end itself; the pair is queued for harvest
@@ -722,7 +725,7 @@ int plan_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
                          has_prev ? c->d_order[ps].as<OrderEntry>() : nullptr,
                          has_prev ? c->d_octl[ps].as<uint32_t>() : nullptr, c->last_budget,
                          fs, budget, c->d_order[slot].as<OrderEntry>(), c->d_octl[slot].as<uint32_t>(),
-                         c->d_plan.as<uint32_t>(), phase);
+                         c->d_plan.as<uint32_t>(), phase | (c->plan_addr << 8));
   }
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(c->plan_done[slot], s));
@@ -1495,6 +1498,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = ab_env("HBX_SDMA_WARM")) c->sdma_warm = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_PSETS")) c->k3_psets = std::atoi(v) == 3 ? 3u : 2u;
   if (const char* v = ab_env("HBX_K3_SPIN")) c->k3_spin = std::atoi(v) ? 1u : 0u;
+  if (const char* v = ab_env("HBX_PLAN_ADDR")) c->plan_addr = (uint32_t)std::min(512, std::max(0, std::atoi(v)));
   if (const char* v = ab_env("HBX_K1_SWZ")) c->k1_swz = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_ITEMS")) c->k3_items = (uint32_t)std::min(8, std::max(0, std::atoi(v)));
   // (tests: a K3 grid of a few workgroups, so every wave takes many groups)
@@ -1713,12 +1717,12 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
       "\"lean_marks\": %u, \"k3_prod\": %u, \"k3_items\": %u, \"k3_period\": %u, \"meta_kernel\": %u, "
       "\"plan_cut\": %u, \"k1_swz\": %u, \"k3_psets\": %u, \"d2h_kernel\": %u, \"k8_split_streams\": %llu, "
       "\"k8_split_fallbacks\": %llu, \"gate_meta\": %u, \"sdma_warm\": %u, \"sdma_h2d_mask\": %u, "
-      "\"sdma_d2h_mask\": %u, \"sdma_warm_ms\": %.3f, \"k3_spin\": %u}",
+      "\"sdma_d2h_mask\": %u, \"sdma_warm_ms\": %.3f, \"k3_spin\": %u, \"plan_addr\": %u}",
       (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_gate, c->md5_wgs,
       plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks, c->k3_prod, c->k3_items,
       c->k3_period, c->meta_kernel, c->plan_cut, c->k1_swz, c->k3_psets, c->d2h_kernel,
       (unsigned long long)c->k8_split_streams, (unsigned long long)c->k8_split_fallbacks, c->gate_meta,
-      c->sdma_warm, c->sdma_h2d, c->sdma_d2h, c->sdma_warm_ms, c->k3_spin);
+      c->sdma_warm, c->sdma_h2d, c->sdma_d2h, c->sdma_warm_ms, c->k3_spin, c->plan_addr);
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }
 

@@ -923,6 +923,23 @@ __device__ __forceinline__ uint32_t order_bin(uint32_t cnt, uint32_t budget) {
   const uint32_t c = min(cnt, ref);
   return (ref - c) * (kPlanBins - 1u) / ref;
 }
+// Address-ordered full slices (round 6, HBX_PLAN_ADDR, A/B): the entries that
+// hash a full slice (count == budget: most of a steady-state launch) go to
+// bins [0, abins) by their chain's data address in 512 MiB granules (mod
+// abins), so a wave's 64 chains, and a CU's four waves (dense placement), read
+// a few windows of memory instead of 64 pages anywhere in the resident
+// arenas (tools/ubench/hbm_streams: chains within 512 MiB windows 3.41 vs
+// 3.10 TB/s spread over 128 GiB, profiles/r06g); the rest by descending
+// count in bins [abins, 1024).  Every group of the full-slice region still
+// has count == budget, so the K3 walk is unchanged.
+__device__ __forceinline__ uint32_t plan_bin(const OrderEntry& o, uint32_t budget, uint32_t abins) {
+  const uint32_t cnt = min(o.rem - 1u, budget);
+  if (!abins) return order_bin(cnt, budget);
+  if (cnt == budget) return (uint32_t)((reinterpret_cast<const Chain*>(o.chain)->src >> 29) % abins);
+  const uint32_t ref = min(budget, (uint32_t)(kMaxBlock >> 6) + 1u);
+  const uint32_t c = min(cnt, ref);
+  return abins + (ref - c) * (kPlanBins - 1u - abins) / ref;
+}
 
 // ------------------------------------------------------- K2r new chains --
 // One chain per chunk of a new batch, in any order, into the batch's array;
@@ -992,6 +1009,8 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
     const OrderEntry* __restrict__ prev, const uint32_t* __restrict__ n_prev_p, uint32_t bprev,
     FreshSet fs, uint32_t budget, OrderEntry* __restrict__ out, uint32_t* __restrict__ n_out,
     uint32_t* __restrict__ gh, uint32_t phase) {
+  const uint32_t abins = phase >> 8;  // address bins for full slices (plan_bin), 0 = off
+  phase &= 0xffu;
   __shared__ uint32_t hist[kPlanBins], pos[kPlanBins], wsum[kPlanThreads / 64];
   const uint32_t tid = threadIdx.x;
   const uint32_t gt = blockIdx.x * kPlanThreads + tid, gn = gridDim.x * kPlanThreads;
@@ -1026,7 +1045,7 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
   __syncthreads();
   for (uint32_t e = gt; e < n_all; e += gn) {
     const OrderEntry o = entry(e);
-    if (o.rem) atomicAdd(&hist[order_bin(min(o.rem - 1u, budget), budget)], 1u);
+    if (o.rem) atomicAdd(&hist[plan_bin(o, budget, abins)], 1u);
   }
   __syncthreads();
   if (phase == 0u) {
@@ -1052,7 +1071,7 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
   __syncthreads();
   for (uint32_t e = gt; e < n_all; e += gn) {
     const OrderEntry o = entry(e);
-    if (o.rem) out[atomicAdd(&pos[order_bin(min(o.rem - 1u, budget), budget)], 1u)] = o;
+    if (o.rem) out[atomicAdd(&pos[plan_bin(o, budget, abins)], 1u)] = o;
   }
 }
 

@@ -375,7 +375,7 @@ def test_k3_producer_waves(oracle, monkeypatch, md5_slice, join_lag, wgs, plan_c
             _check(a, r)
 
 
-@pytest.mark.parametrize("prod", ["1", "p3", "s"])
+@pytest.mark.parametrize("prod", ["1", "p3", "s", "a"])
 @pytest.mark.parametrize("md5_slice,join_lag", [(9, 1), (9, 2), (16384, 1), (0, 2)])
 def test_k3_lane_path_groups_between_cooperative_ones(oracle, monkeypatch, md5_slice, join_lag, prod):
     """Advisor r05 (high): with a producer wave per MD5 wave, a group on the
@@ -397,6 +397,7 @@ def test_k3_lane_path_groups_between_cooperative_ones(oracle, monkeypatch, md5_s
     monkeypatch.setenv("HBX_K3_ITEMS", "0")
     monkeypatch.setenv("HBX_K3_WGS", "1")
     monkeypatch.setenv("HBX_K3_SPIN", "1" if prod == "s" else "0")  # s: stage waits without s_sleep
+    monkeypatch.setenv("HBX_PLAN_ADDR", "512" if prod == "a" else "0")  # a: full slices ordered by address
     rng = np.random.default_rng(977 + md5_slice % 13)
     batches = []
     for b in range(3):
@@ -417,6 +418,7 @@ def test_k3_lane_path_groups_between_cooperative_ones(oracle, monkeypatch, md5_s
     with Engine(0, md5_slice=md5_slice, join_lag=join_lag) as e:
         k = e.knobs()
         assert k["k3_prod"] and k["md5_wgs"] == 1 and k["k3_spin"] == (prod == "s")
+        assert k["plan_addr"] == (512 if prod == "a" else 0)
         for i in [0, 1, 2, 1, 0, 2]:
             dev, offs, sizes, _ = batches[i]
             e.submit_device(dev.data_ptr(), offs, sizes)
@@ -430,17 +432,20 @@ def test_k3_lane_path_groups_between_cooperative_ones(oracle, monkeypatch, md5_s
             _check(a, r)
 
 
-@pytest.mark.parametrize("join_lag", [1, 2, 3, 4])
-def test_pipelined_steady_state(oracle, join_lag):
+@pytest.mark.parametrize("join_lag,plan_addr", [(1, 0), (2, 0), (3, 0), (4, 0), (2, 512), (1, 7)])
+def test_pipelined_steady_state(oracle, monkeypatch, join_lag, plan_addr):
     """A deep pipeline as bench.py drives it: submit, and wait only once
     `depth` batches are pending, so batches complete through the slice
     schedule rather than a forced drain.  Join lags 1-4: the plan inline on
     the scan stream (lag 1), on the hash stream (lag 2), one launch ahead on
     the scan stream (lag >= 3)."""
     from hashbox_amd import Engine
+    monkeypatch.setenv("HBX_AB", "1")
+    monkeypatch.setenv("HBX_PLAN_ADDR", str(plan_addr))  # full slices ordered by data address (plan_bin)
     batches = _device_batches(oracle, 3, 57)
     got = []
     with Engine(0, md5_slice=4096, join_lag=join_lag) as e:  # 256 KiB per chain per launch: 32 per 8 MiB
+        assert e.knobs()["plan_addr"] == plan_addr
         order = [i % 3 for i in range(40)]
         for i in order:
             dev, offs, sizes, _ = batches[i]
