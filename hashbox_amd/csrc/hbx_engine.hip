@@ -207,9 +207,10 @@ struct hbx_ctx {
   // files, equal at 8 (profiles/r05af); HBX_K3_PSETS=2 for A/B
   uint32_t k3_psets = 3;
   uint32_t k3_spin = 0;
-  // HBX_PLAN_ADDR=<bins> (A/B, 0..512): full-slice chains ordered by data
-  // address in that many 512 MiB granules (plan_bin)
-  uint32_t plan_addr = 0;
+  // full-slice chains ordered by data address in plan_addr granules of
+  // 2^plan_addr_shift bytes (plan_bin; HBX_PLAN_ADDR=0..512, 0 = by count
+  // only as before round 6; HBX_PLAN_ADDR_SHIFT=20..40)
+  uint32_t plan_addr = 512, plan_addr_shift = 29;
   // K1 launched with its batch's ev[0]/ev[1] as hipExtLaunchKernel start/stop
   // events instead of marker packets around it (HBX_K1_EXT=0: markers)
   uint32_t k1_ext = 1;  // HBX_K3_SPIN=1 (A/B): the MD5 wave re-polls a late stage without s_sleep
@@ -700,7 +701,7 @@ int plan_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
                            has_prev ? c->d_order[ps].as<OrderEntry>() : nullptr,
                            has_prev ? c->d_octl[ps].as<uint32_t>() : nullptr, c->last_budget,
                            fs, budget, c->d_order[slot].as<OrderEntry>(), c->d_octl[slot].as<uint32_t>(),
-                           c->d_plan.as<uint32_t>(), phase | (c->plan_addr << 8));
+                           c->d_plan.as<uint32_t>(), phase | (c->plan_addr << 8) | (c->plan_addr_shift << 24));
       HBX_TRY(c, hipGetLastError());
       HBX_TRY(c, hipEventRecord(t.b, s));
       // K3 waits on the timing end itself; the pair is queued for harvest
@@ -728,7 +729,7 @@ int plan_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
                          has_prev ? c->d_order[ps].as<OrderEntry>() : nullptr,
                          has_prev ? c->d_octl[ps].as<uint32_t>() : nullptr, c->last_budget,
                          fs, budget, c->d_order[slot].as<OrderEntry>(), c->d_octl[slot].as<uint32_t>(),
-                         c->d_plan.as<uint32_t>(), phase | (c->plan_addr << 8));
+                         c->d_plan.as<uint32_t>(), phase | (c->plan_addr << 8) | (c->plan_addr_shift << 24));
   }
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(c->plan_done[slot], s));
@@ -1513,6 +1514,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = ab_env("HBX_K3_PSETS")) c->k3_psets = std::atoi(v) == 3 ? 3u : 2u;
   if (const char* v = ab_env("HBX_K3_SPIN")) c->k3_spin = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_PLAN_ADDR")) c->plan_addr = (uint32_t)std::min(512, std::max(0, std::atoi(v)));
+  if (const char* v = ab_env("HBX_PLAN_ADDR_SHIFT")) c->plan_addr_shift = (uint32_t)std::min(40, std::max(20, std::atoi(v)));
   if (const char* v = ab_env("HBX_K1_EXT")) c->k1_ext = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K1_SWZ")) c->k1_swz = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_ITEMS")) c->k3_items = (uint32_t)std::min(8, std::max(0, std::atoi(v)));
@@ -1732,12 +1734,12 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
       "\"lean_marks\": %u, \"k3_prod\": %u, \"k3_items\": %u, \"k3_period\": %u, \"meta_kernel\": %u, "
       "\"plan_cut\": %u, \"k1_swz\": %u, \"k3_psets\": %u, \"d2h_kernel\": %u, \"k8_split_streams\": %llu, "
       "\"k8_split_fallbacks\": %llu, \"gate_meta\": %u, \"sdma_warm\": %u, \"sdma_h2d_mask\": %u, "
-      "\"sdma_d2h_mask\": %u, \"sdma_warm_ms\": %.3f, \"k3_spin\": %u, \"plan_addr\": %u, \"k1_ext\": %u}",
+      "\"sdma_d2h_mask\": %u, \"sdma_warm_ms\": %.3f, \"k3_spin\": %u, \"plan_addr\": %u, \"plan_addr_shift\": %u, \"k1_ext\": %u}",
       (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_gate, c->md5_wgs,
       plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks, c->k3_prod, c->k3_items,
       c->k3_period, c->meta_kernel, c->plan_cut, c->k1_swz, c->k3_psets, c->d2h_kernel,
       (unsigned long long)c->k8_split_streams, (unsigned long long)c->k8_split_fallbacks, c->gate_meta,
-      c->sdma_warm, c->sdma_h2d, c->sdma_d2h, c->sdma_warm_ms, c->k3_spin, c->plan_addr, c->k1_ext);
+      c->sdma_warm, c->sdma_h2d, c->sdma_d2h, c->sdma_warm_ms, c->k3_spin, c->plan_addr, c->plan_addr_shift, c->k1_ext);
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }
 

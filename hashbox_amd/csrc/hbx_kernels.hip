@@ -923,19 +923,21 @@ __device__ __forceinline__ uint32_t order_bin(uint32_t cnt, uint32_t budget) {
   const uint32_t c = min(cnt, ref);
   return (ref - c) * (kPlanBins - 1u) / ref;
 }
-// Address-ordered full slices (round 6, HBX_PLAN_ADDR, A/B): the entries that
-// hash a full slice (count == budget: most of a steady-state launch) go to
-// bins [0, abins) by their chain's data address in 512 MiB granules (mod
+// Address-ordered full slices (round 6, the default: 512 bins of 512 MiB
+// granules; HBX_PLAN_ADDR / HBX_PLAN_ADDR_SHIFT for A/B): the entries that hash
+// a full slice (count == budget: most of a steady-state launch) go to bins
+// [0, abins) by their chain's data address in 2^ashift-byte granules (mod
 // abins), so a wave's 64 chains, and a CU's four waves (dense placement), read
 // a few windows of memory instead of 64 pages anywhere in the resident
 // arenas (tools/ubench/hbm_streams: chains within 512 MiB windows 3.41 vs
-// 3.10 TB/s spread over 128 GiB, profiles/r06g); the rest by descending
-// count in bins [abins, 1024).  Every group of the full-slice region still
-// has count == budget, so the K3 walk is unchanged.
-__device__ __forceinline__ uint32_t plan_bin(const OrderEntry& o, uint32_t budget, uint32_t abins) {
+// 3.10 TB/s spread over 128 GiB, profiles/r06g; K3 3.47-3.49 -> 3.41-3.43 ms,
+// launch overhead 1.084-1.089 -> 1.040-1.050, profiles/r06h); the rest by
+// descending count in bins [abins, 1024).  Every group of the full-slice
+// region still has count == budget, so the K3 walk is unchanged.
+__device__ __forceinline__ uint32_t plan_bin(const OrderEntry& o, uint32_t budget, uint32_t abins, uint32_t ashift) {
   const uint32_t cnt = min(o.rem - 1u, budget);
   if (!abins) return order_bin(cnt, budget);
-  if (cnt == budget) return (uint32_t)((reinterpret_cast<const Chain*>(o.chain)->src >> 29) % abins);
+  if (cnt == budget) return (uint32_t)((reinterpret_cast<const Chain*>(o.chain)->src >> ashift) % abins);
   const uint32_t ref = min(budget, (uint32_t)(kMaxBlock >> 6) + 1u);
   const uint32_t c = min(cnt, ref);
   return abins + (ref - c) * (kPlanBins - 1u - abins) / ref;
@@ -1009,7 +1011,8 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
     const OrderEntry* __restrict__ prev, const uint32_t* __restrict__ n_prev_p, uint32_t bprev,
     FreshSet fs, uint32_t budget, OrderEntry* __restrict__ out, uint32_t* __restrict__ n_out,
     uint32_t* __restrict__ gh, uint32_t phase) {
-  const uint32_t abins = phase >> 8;  // address bins for full slices (plan_bin), 0 = off
+  const uint32_t abins = (phase >> 8) & 0xfffu;  // address bins for full slices (plan_bin), 0 = off
+  const uint32_t ashift = phase >> 24;            // their granule: 2^ashift bytes
   phase &= 0xffu;
   __shared__ uint32_t hist[kPlanBins], pos[kPlanBins], wsum[kPlanThreads / 64];
   const uint32_t tid = threadIdx.x;
@@ -1045,7 +1048,7 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
   __syncthreads();
   for (uint32_t e = gt; e < n_all; e += gn) {
     const OrderEntry o = entry(e);
-    if (o.rem) atomicAdd(&hist[plan_bin(o, budget, abins)], 1u);
+    if (o.rem) atomicAdd(&hist[plan_bin(o, budget, abins, ashift)], 1u);
   }
   __syncthreads();
   if (phase == 0u) {
@@ -1071,7 +1074,7 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
   __syncthreads();
   for (uint32_t e = gt; e < n_all; e += gn) {
     const OrderEntry o = entry(e);
-    if (o.rem) out[atomicAdd(&pos[plan_bin(o, budget, abins)], 1u)] = o;
+    if (o.rem) out[atomicAdd(&pos[plan_bin(o, budget, abins, ashift)], 1u)] = o;
   }
 }
 

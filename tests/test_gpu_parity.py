@@ -397,7 +397,7 @@ def test_k3_lane_path_groups_between_cooperative_ones(oracle, monkeypatch, md5_s
     monkeypatch.setenv("HBX_K3_ITEMS", "0")
     monkeypatch.setenv("HBX_K3_WGS", "1")
     monkeypatch.setenv("HBX_K3_SPIN", "1" if prod == "s" else "0")  # s: stage waits without s_sleep
-    monkeypatch.setenv("HBX_PLAN_ADDR", "512" if prod == "a" else "0")  # a: full slices ordered by address
+    monkeypatch.setenv("HBX_PLAN_ADDR", "0" if prod == "a" else "512")  # a: by count only (round-5 order)
     rng = np.random.default_rng(977 + md5_slice % 13)
     batches = []
     for b in range(3):
@@ -418,7 +418,7 @@ def test_k3_lane_path_groups_between_cooperative_ones(oracle, monkeypatch, md5_s
     with Engine(0, md5_slice=md5_slice, join_lag=join_lag) as e:
         k = e.knobs()
         assert k["k3_prod"] and k["md5_wgs"] == 1 and k["k3_spin"] == (prod == "s")
-        assert k["plan_addr"] == (512 if prod == "a" else 0)
+        assert k["plan_addr"] == (0 if prod == "a" else 512)
         for i in [0, 1, 2, 1, 0, 2]:
             dev, offs, sizes, _ = batches[i]
             e.submit_device(dev.data_ptr(), offs, sizes)
@@ -432,7 +432,7 @@ def test_k3_lane_path_groups_between_cooperative_ones(oracle, monkeypatch, md5_s
             _check(a, r)
 
 
-@pytest.mark.parametrize("join_lag,plan_addr", [(1, 0), (2, 0), (3, 0), (4, 0), (2, 512), (1, 7)])
+@pytest.mark.parametrize("join_lag,plan_addr", [(1, 512), (2, 512), (3, 512), (4, 512), (2, 0), (1, 7)])
 def test_pipelined_steady_state(oracle, monkeypatch, join_lag, plan_addr):
     """A deep pipeline as bench.py drives it: submit, and wait only once
     `depth` batches are pending, so batches complete through the slice
