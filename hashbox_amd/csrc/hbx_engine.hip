@@ -213,7 +213,8 @@ struct hbx_ctx {
   uint32_t plan_addr = 512, plan_addr_shift = 29;
   // K1 launched with its batch's ev[0]/ev[1] as hipExtLaunchKernel start/stop
   // events instead of marker packets around it (HBX_K1_EXT=0: markers)
-  uint32_t k1_ext = 1;  // HBX_K3_SPIN=1 (A/B): the MD5 wave re-polls a late stage without s_sleep
+  uint32_t k1_ext = 1;
+  uint32_t k1_dma4 = 1;  // K1's four LDS-DMA pieces in one statement (HBX_K1_DMA4=0: one per piece)  // HBX_K3_SPIN=1 (A/B): the MD5 wave re-polls a late stage without s_sleep
   // at join lag 2, preplan on the cut stream (mode 3; HBX_PLAN_CUT=0: mode 1,
   // the plan on the hash stream): +2.7 % with K3P (profiles/r05e)
   // 2 (default): at lag 3 and 4 too, off the scan loop (8 files per GPU, K3
@@ -1134,7 +1135,8 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
     // join lag >= 2 K1 had four (ev[0], its timer's pair, ev[1]) between the
     // scan loop's kernels.  They double as K1's timer and K2's dependency.
     hipExtLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3((uint32_t)nt), dim3(kK1Threads), 0, s, b->ev[0], b->ev[1], 0,
-                          arena, d_off, d_len, d_sb, d_tiles, ssum.as<uint2>(), slices, c->k1_swz);
+                          arena, d_off, d_len, d_sb, d_tiles, ssum.as<uint2>(), slices,
+                          c->k1_swz | (c->k1_dma4 ? 0u : 2u));
     HBX_TRY(c, hipGetLastError());
     c->open_t.push_back(TimedLaunch{b->ev[0], b->ev[1], 0, false});
   } else {
@@ -1142,7 +1144,7 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
     if (nt) {
       StageTimer t(c, s, 0, !lean);
       hipLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3((uint32_t)nt), dim3(kK1Threads), 0, s, arena, d_off, d_len,
-                         d_sb, d_tiles, ssum.as<uint2>(), slices, c->k1_swz);
+                         d_sb, d_tiles, ssum.as<uint2>(), slices, c->k1_swz | (c->k1_dma4 ? 0u : 2u));
     }
     HBX_TRY(c, hipGetLastError());
     HBX_TRY(c, hipEventRecord(b->ev[1], s));
@@ -1516,6 +1518,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = ab_env("HBX_PLAN_ADDR")) c->plan_addr = (uint32_t)std::min(512, std::max(0, std::atoi(v)));
   if (const char* v = ab_env("HBX_PLAN_ADDR_SHIFT")) c->plan_addr_shift = (uint32_t)std::min(40, std::max(20, std::atoi(v)));
   if (const char* v = ab_env("HBX_K1_EXT")) c->k1_ext = std::atoi(v) ? 1u : 0u;
+  if (const char* v = ab_env("HBX_K1_DMA4")) c->k1_dma4 = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K1_SWZ")) c->k1_swz = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_ITEMS")) c->k3_items = (uint32_t)std::min(8, std::max(0, std::atoi(v)));
   // (tests: a K3 grid of a few workgroups, so every wave takes many groups)
@@ -1734,12 +1737,12 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
       "\"lean_marks\": %u, \"k3_prod\": %u, \"k3_items\": %u, \"k3_period\": %u, \"meta_kernel\": %u, "
       "\"plan_cut\": %u, \"k1_swz\": %u, \"k3_psets\": %u, \"d2h_kernel\": %u, \"k8_split_streams\": %llu, "
       "\"k8_split_fallbacks\": %llu, \"gate_meta\": %u, \"sdma_warm\": %u, \"sdma_h2d_mask\": %u, "
-      "\"sdma_d2h_mask\": %u, \"sdma_warm_ms\": %.3f, \"k3_spin\": %u, \"plan_addr\": %u, \"plan_addr_shift\": %u, \"k1_ext\": %u}",
+      "\"sdma_d2h_mask\": %u, \"sdma_warm_ms\": %.3f, \"k3_spin\": %u, \"plan_addr\": %u, \"plan_addr_shift\": %u, \"k1_ext\": %u, \"k1_dma4\": %u}",
       (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_gate, c->md5_wgs,
       plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks, c->k3_prod, c->k3_items,
       c->k3_period, c->meta_kernel, c->plan_cut, c->k1_swz, c->k3_psets, c->d2h_kernel,
       (unsigned long long)c->k8_split_streams, (unsigned long long)c->k8_split_fallbacks, c->gate_meta,
-      c->sdma_warm, c->sdma_h2d, c->sdma_d2h, c->sdma_warm_ms, c->k3_spin, c->plan_addr, c->plan_addr_shift, c->k1_ext);
+      c->sdma_warm, c->sdma_h2d, c->sdma_d2h, c->sdma_warm_ms, c->k3_spin, c->plan_addr, c->plan_addr_shift, c->k1_ext, c->k1_dma4);
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }
 

@@ -243,6 +243,28 @@ __device__ __forceinline__ void dma16(s32x4 srd, uint32_t voff, uint32_t soff, u
       : "memory");
 }
 
+// The four 1 KiB pieces of a wave's iteration in ONE statement (round 6): M0
+// set once, the pieces 1 KiB apart through the instruction offset, which the
+// LDS-DMA adds to both the memory and the LDS address (LDS = M0 + offset +
+// 16 * lane); the per-piece form paid s_nop 4 + 3 s_mov + s_nop 0 per piece,
+// 15 issue slots more per iteration (hbx_k1 ISA, -S).
+__device__ __forceinline__ void dma16x4(s32x4 srd, uint32_t voff, uint32_t soff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen" HBX_K1_CPOL " lds\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen offset:1024" HBX_K1_CPOL " lds\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen offset:2048" HBX_K1_CPOL " lds\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen offset:3072" HBX_K1_CPOL " lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(srd), "s"(lds), "s"(soff)
+      : "memory");
+}
+
 constexpr uint32_t kDmaSlot = 4096;  // bytes per wave per iteration
 
 // One workgroup per tile.  Equal tiles finish in whole rounds over the CUs K3
@@ -256,6 +278,9 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_d
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
     const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ slice_base,
     const uint4* __restrict__ tiles, uint2* __restrict__ ssum, uint64_t dummy, uint32_t swz) {
+  // swz bit 1 (HBX_K1_DMA4=0, A/B): one statement per piece instead of dma16x4
+  const bool dma4 = !(swz & 2u);
+  swz &= 1u;
   __shared__ uint2 wtot[2][16];
   __shared__ __attribute__((aligned(1024))) uint8_t land[kK1Threads / 64][2][kDmaSlot];
   const uint4 td = tiles[blockIdx.x];
@@ -290,6 +315,10 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_d
   const uint32_t rd_lane = swz ? 64u * (l >> 4) + (l & 15u) : 4u * l;
   const uint32_t rd_step = swz ? 16u : 1u;
   auto issue = [&](uint32_t it, uint32_t lds) {  // 4 DMA ops, always issued
+    if (dma4) {
+      dma16x4(srd, w * kSlice + dma_lane, it * kMinBlock, lds);
+      return;
+    }
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const uint32_t voff = w * kSlice + 1024u * k + dma_lane;
