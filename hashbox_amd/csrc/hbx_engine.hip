@@ -206,6 +206,12 @@ struct hbx_ctx {
   // hidden) 2,297-2,318 vs 2,286-2,308 GiB/s in three alternating pairs at 64
   // files, equal at 8 (profiles/r05af); HBX_K3_PSETS=2 for A/B
   uint32_t k3_psets = 3;
+  // HBX_K3_HAND=1 (A/B): the producer's loads as inline asm with hand-counted
+  // waits (the compiler waits for all three register sets at every third
+  // stage); bit-exact but no faster: 2,251/2,254 vs 2,275/2,339 GiB/s, 8 files
+  // 2,077 vs 2,122 (profiles/r06j), so the producer's lead is not what stalls
+  // the MD5 wave
+  uint32_t k3_hand = 0;
   uint32_t k3_spin = 0;
   // full-slice chains ordered by data address in plan_addr granules of
   // 2^plan_addr_shift bytes (plan_bin; HBX_PLAN_ADDR=0..512, 0 = by count
@@ -782,7 +788,7 @@ int md5_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
     hipLaunchKernelGGL(hbx_k3p_block_md5, dim3(c->md5_wgs), dim3(kK3PThreads), 0, s,
                        c->d_order[slot].as<OrderEntry>(), static_cast<const uint32_t*>(c->d_octl[slot].as<uint32_t>()),
                        budget, c->d_gate.as<uint32_t>(), c->k3_dispatched, c->k3_waves + waves - 1u, tslot,
-                       c->h_probe.p ? c->h_probe.as<uint64_t>() : nullptr, c->k3_psets | (c->k3_spin ? 0x100u : 0u));
+                       c->h_probe.p ? c->h_probe.as<uint64_t>() : nullptr, c->k3_psets | (c->k3_spin ? 0x100u : 0u) | (c->k3_hand ? 0x200u : 0u));
   else
     hipLaunchKernelGGL(hbx_k3_block_md5, dim3(c->md5_wgs), dim3(kK3Threads), 0, s,
                        c->d_order[slot].as<OrderEntry>(), static_cast<const uint32_t*>(c->d_octl[slot].as<uint32_t>()),
@@ -1514,6 +1520,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = ab_env("HBX_GATE_META")) c->gate_meta = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_SDMA_WARM")) c->sdma_warm = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_PSETS")) c->k3_psets = std::atoi(v) == 3 ? 3u : 2u;
+  if (const char* v = ab_env("HBX_K3_HAND")) c->k3_hand = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_SPIN")) c->k3_spin = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_PLAN_ADDR")) c->plan_addr = (uint32_t)std::min(512, std::max(0, std::atoi(v)));
   if (const char* v = ab_env("HBX_PLAN_ADDR_SHIFT")) c->plan_addr_shift = (uint32_t)std::min(40, std::max(20, std::atoi(v)));
@@ -1737,12 +1744,12 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
       "\"lean_marks\": %u, \"k3_prod\": %u, \"k3_items\": %u, \"k3_period\": %u, \"meta_kernel\": %u, "
       "\"plan_cut\": %u, \"k1_swz\": %u, \"k3_psets\": %u, \"d2h_kernel\": %u, \"k8_split_streams\": %llu, "
       "\"k8_split_fallbacks\": %llu, \"gate_meta\": %u, \"sdma_warm\": %u, \"sdma_h2d_mask\": %u, "
-      "\"sdma_d2h_mask\": %u, \"sdma_warm_ms\": %.3f, \"k3_spin\": %u, \"plan_addr\": %u, \"plan_addr_shift\": %u, \"k1_ext\": %u, \"k1_dma4\": %u}",
+      "\"sdma_d2h_mask\": %u, \"sdma_warm_ms\": %.3f, \"k3_spin\": %u, \"plan_addr\": %u, \"plan_addr_shift\": %u, \"k1_ext\": %u, \"k1_dma4\": %u, \"k3_hand\": %u}",
       (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_gate, c->md5_wgs,
       plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks, c->k3_prod, c->k3_items,
       c->k3_period, c->meta_kernel, c->plan_cut, c->k1_swz, c->k3_psets, c->d2h_kernel,
       (unsigned long long)c->k8_split_streams, (unsigned long long)c->k8_split_fallbacks, c->gate_meta,
-      c->sdma_warm, c->sdma_h2d, c->sdma_d2h, c->sdma_warm_ms, c->k3_spin, c->plan_addr, c->plan_addr_shift, c->k1_ext, c->k1_dma4);
+      c->sdma_warm, c->sdma_h2d, c->sdma_d2h, c->sdma_warm_ms, c->k3_spin, c->plan_addr, c->plan_addr_shift, c->k1_ext, c->k1_dma4, c->k3_hand);
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }
 

@@ -1279,7 +1279,37 @@ __device__ __forceinline__ K3Group k3_group(const OrderEntry* __restrict__ order
 // loads at any byte offset, as md5_coop).  Returns the group's stage count.
 // SETS register sets of loads in flight (3 by default: one stage more of
 // memory latency hidden than 2, HBX_K3_PSETS=2 for A/B).
-template <int SETS = 2>
+// Hand-counted producer loads (round 6, HBX_K3_HAND=1, A/B only: bit-exact,
+// measured no faster, profiles/r06j; tools/check_asm_loads.py lists the ISA
+// accesses to registers of loads still in flight): the compiler placed
+// `s_waitcnt vmcnt(0)` before the first coop_write of every three stages (its
+// count is lost across the conditional puts and the flag-wait loops), so the
+// producer waited for all three register sets in flight, not the oldest one,
+// and a stage's loads had about one stage of lead instead of three.  Here the
+// 16 loads of a set are inline asm (the compiler inserts no wait for them),
+// every put issues exactly one set (clamped re-reads past the group's last
+// stage, as coop_load), so at each put the oldest set is followed by exactly
+// 2 x 16 newer loads: `s_waitcnt vmcnt(32)` (vmcnt(16) with two sets), bound
+// to the set's registers, lands it.  Loads the compiler issues itself (the
+// order entries at a group's start) only make its own waits stricter.
+__device__ __forceinline__ void coop_load_asm(u32x4 (&Gs)[16], const uint64_t (&Q)[16], uint32_t st, uint32_t t,
+                                              uint32_t ngr) {
+  const uint32_t g = min(16u * st + t, ngr - 1u);
+  const uint64_t off = 16ull * (g - t);
+#pragma unroll
+  for (int q = 0; q < 16; q++)
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(Gs[q]) : "v"(Q[q] + off));
+}
+template <int N>
+__device__ __forceinline__ void coop_vmwait(u32x4 (&G)[16]) {
+  asm volatile("s_waitcnt vmcnt(%16)"
+               : "+v"(G[0]), "+v"(G[1]), "+v"(G[2]), "+v"(G[3]), "+v"(G[4]), "+v"(G[5]), "+v"(G[6]), "+v"(G[7]),
+                 "+v"(G[8]), "+v"(G[9]), "+v"(G[10]), "+v"(G[11]), "+v"(G[12]), "+v"(G[13]), "+v"(G[14]), "+v"(G[15])
+               : "n"(N)
+               : "memory");
+}
+
+template <int SETS = 2, bool HAND = false>
 __device__ __forceinline__ uint32_t k3p_produce(uint8_t* wl, uint32_t* flags, uint32_t S, uint64_t src, uint32_t Rr) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t t = lane % 16u, sub = lane / 16u;
@@ -1288,6 +1318,33 @@ __device__ __forceinline__ uint32_t k3p_produce(uint8_t* wl, uint32_t* flags, ui
   uint64_t Q[16];
 #pragma unroll
   for (int q = 0; q < 16; q++) Q[q] = shfl64(src, 4u * (uint32_t)q + sub) + 16ull * t;
+  if constexpr (HAND) {
+    u32x4 GA[16], GB[16], GC[16];
+    coop_load_asm(GA, Q, 0u, t, ngr);
+    coop_load_asm(GB, Q, min(1u, nst - 1u), t, ngr);
+    if (SETS == 3) coop_load_asm(GC, Q, min(2u, nst - 1u), t, ngr);
+    // stage x goes to LDS half x & 1 once stage x - 2 is freed (flags[1] >= S + x - 1)
+    auto put = [&](uint32_t x, u32x4(&G)[16]) {
+      k3p_wait_ge(&flags[1], x < 2u ? S : S + x - 1u);
+      coop_vmwait<16 * (SETS - 1)>(G);
+      coop_write<16>(wl, wr, (S + x) & 1u, G);
+      k3p_publish(&flags[0], S + x + 1u);
+      coop_load_asm(G, Q, min(x + (uint32_t)SETS, nst - 1u), t, ngr);
+    };
+    if (SETS == 3) {
+      for (uint32_t s = 0; s < nst; s += 3u) {
+        put(s, GA);
+        if (s + 1u < nst) put(s + 1u, GB);
+        if (s + 2u < nst) put(s + 2u, GC);
+      }
+    } else {
+      for (uint32_t s = 0; s < nst; s += 2u) {
+        put(s, GA);
+        if (s + 1u < nst) put(s + 1u, GB);
+      }
+    }
+    return nst;
+  }
   u32x4 GA[16], GB[16];
   coop_load<16>(GA, Q, 0u, t, ngr);
   coop_load<16>(GB, Q, min(1u, nst - 1u), t, ngr);
@@ -1482,7 +1539,7 @@ __device__ __forceinline__ void k3q_push(uint32_t* __restrict__ qc, uint64_t* __
 // The producer wave of pair `flags`: the same groups as its MD5 wave; for a
 // group on the cooperative path (R >= kCoopMinBudget), the stages of blocks
 // next+1 .. next+R-1 of its 64 chains, SETS register sets in flight.
-template <int SETS>
+template <int SETS, bool HAND = false>
 __device__ void k3p_producer(uint8_t* wl, uint32_t* flags, const OrderEntry* __restrict__ order,
                              const uint32_t* __restrict__ n_order, uint32_t budget, uint32_t g0, uint32_t nwaves) {
   const uint32_t n_total = *n_order;
@@ -1491,7 +1548,7 @@ __device__ void k3p_producer(uint8_t* wl, uint32_t* flags, const OrderEntry* __r
   for (uint32_t g = g0; g < groups; g += nwaves) {
     const K3Group G = k3_group(order, n_total, g, budget);
     if (G.R < kCoopMinBudget) continue;  // wave-uniform: the MD5 wave takes the lane path
-    S += k3p_produce<SETS>(wl, flags, S, G.src + 64ull * (G.next + 1u) - 8ull, G.R - 1u);  // from block next+1
+    S += k3p_produce<SETS, HAND>(wl, flags, S, G.src + 64ull * (G.next + 1u) - 8ull, G.R - 1u);  // from block next+1
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (clamped re-reads of the last stage)
 }
@@ -1705,7 +1762,9 @@ extern "C" __global__ __launch_bounds__(kK3PThreads, 1) void hbx_k3p_block_md5(
     uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last, uint64_t* __restrict__ tslot,
     uint64_t* __restrict__ probe, uint32_t psets) {
   // psets: producer register sets (2 or 3) | 0x100 for the spinning stage wait
+  // | 0x200 for the hand-counted producer loads (k3p_produce HAND)
   const bool spin = (psets & 0x100u) != 0u;
+  const bool hand = (psets & 0x200u) != 0u;
   psets &= 0xffu;
   __shared__ __attribute__((aligned(16))) uint8_t k3_lds[4][kK3WaveLds];
   __shared__ uint32_t k3_flags[4][2];
@@ -1718,10 +1777,17 @@ extern "C" __global__ __launch_bounds__(kK3PThreads, 1) void hbx_k3p_block_md5(
                   K3Queue{}, spin);
   } else {
     __builtin_amdgcn_s_setprio(2);
-    if (psets == 3u)
-      k3p_producer<3>(k3_lds[pair], k3_flags[pair], order, n_order, budget, blockIdx.x * 4u + pair, gridDim.x * 4u);
-    else
-      k3p_producer<2>(k3_lds[pair], k3_flags[pair], order, n_order, budget, blockIdx.x * 4u + pair, gridDim.x * 4u);
+    const uint32_t g0 = blockIdx.x * 4u + pair, nw = gridDim.x * 4u;
+    if (hand) {
+      if (psets == 3u)
+        k3p_producer<3, true>(k3_lds[pair], k3_flags[pair], order, n_order, budget, g0, nw);
+      else
+        k3p_producer<2, true>(k3_lds[pair], k3_flags[pair], order, n_order, budget, g0, nw);
+    } else if (psets == 3u) {
+      k3p_producer<3>(k3_lds[pair], k3_flags[pair], order, n_order, budget, g0, nw);
+    } else {
+      k3p_producer<2>(k3_lds[pair], k3_flags[pair], order, n_order, budget, g0, nw);
+    }
   }
 }
 
