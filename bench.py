@@ -84,7 +84,7 @@ HBM_PROBE_GBS = 6580.0
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md), GB/s
 GIB = 1 << 30
 KNAMES = ["k1_digest_scan", "k2_cut_chain", "k2c_chain_plan", "k3_block_md5", "k4_content_id"]
-KERNEL_OF = {"k1_digest_scan": "hbx_k1_digest_scan_dma", "k2_cut_chain": "hbx_k2_cut_chain",
+KERNEL_OF = {"k1_digest_scan": ("hbx_k1d_digest_scan", "hbx_k1_digest_scan_dma"), "k2_cut_chain": "hbx_k2_cut_chain",
              "k2c_chain_plan": "hbx_k2c_plan", "k3_block_md5": "hbx_k3p_block_md5",  # K3P, the default since round 5
              "k4_content_id": "hbx_k4_content_id"}
 
@@ -248,7 +248,9 @@ def measured_traffic(kernel, per_launch_bytes, batch_bytes):
     if not files or batch_bytes != 64 * (128 << 20):
         return None, None
     d = json.load(open(files[-1]))
-    k = d.get("kernels", {}).get(kernel)
+    kk = d.get("kernels", {})
+    # K1 has two kernels (K1D, round 6, and the one-workgroup-per-tile form)
+    k = next((kk[n] for n in ((kernel,) if isinstance(kernel, str) else kernel) if n in kk), None)
     if not k:
         return None, None
     return int(k["hbm_bytes"]), os.path.relpath(files[-1], ROOT)

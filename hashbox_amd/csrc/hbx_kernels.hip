@@ -129,7 +129,7 @@ struct K1State {
 // virtual zeros.
 __device__ __forceinline__ K1State k1_prime(const uint32_t (&halo)[16], bool at_start,
                                             uint2 (&wtot)[2][16], uint32_t w, uint32_t l,
-                                            uint32_t e_l) {
+                                            uint32_t e_l, uint32_t wb = 1u) {
   K1State st;
   if (at_start) {
     st.pa = RunAgg{0u, 0u, 0u, 0u};
@@ -140,9 +140,9 @@ __device__ __forceinline__ K1State k1_prime(const uint32_t (&halo)[16], bool at_
   st.pa = run_aggregates(halo);
   const uint32_t iA = wave_incl_sum(st.pa.af);
   const uint32_t iC = wave_incl_sum(e_l * st.pa.af + st.pa.jf);
-  if (l == 63u) wtot[1][w] = make_uint2(iA, iC);
+  if (l == 63u) wtot[wb][w] = make_uint2(iA, iC);
   __syncthreads();
-  const uint2 t = (l < 16u) ? wtot[1][l] : make_uint2(0u, 0u);
+  const uint2 t = (l < 16u) ? wtot[wb][l] : make_uint2(0u, 0u);
   const uint32_t sA = row_incl_sum(t.x), sC = row_incl_sum(t.y);
   st.S1c = readlane(sA, 15);
   st.s2c = 0x8000u - readlane(sC, 15);  // virtual-zero start: s2 = 2^15 - sum k*x_k
@@ -369,6 +369,175 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_d
   for (uint32_t it = 0; it < n_it; it += 2u) {
     step(it, run_b, out);
     if (it + 1u < n_it) step(it + 1u, out, run_b);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup exits
+}
+
+// ------------------------------------------------------- K1D (round 6) --
+// The same scan with the tiles handed out at run time.  hbx_k1_digest_scan_dma
+// runs one workgroup per tile, all tiles of a batch equally long, so the
+// tiles finish in whole rounds over the CUs K3 leaves free and one CU fewer
+// costs a round (the residency cliff; and at 8 files per GPU
+// 683 tiles over ~128 CUs end in a part-filled sixth round).  K1D launches
+// about as many workgroups as there are free CUs; each takes the next tile
+// from a counter (one vector atomic by thread 0), and the host lists the
+// tiles in decreasing length (guided: about the work left over twice the
+// workgroups), so the last ones are short and the CUs finish together.
+//
+// A workgroup's DMA stream runs on across its tiles: a tile is its units
+// [halo, iteration 0, .., iteration n-1], the halo being the MIN bytes before
+// the tile (or zeros at a file's start, read past the end of the descriptor)
+// that primes the rollsum state.  The next tile is claimed three units before
+// the current one ends, so its halo and first iteration are in flight while
+// the current tile's last two iterations compute: no per-tile start-up
+// latency.  Every unit issues exactly 4 DMA + 1 store per wave (the halo's
+// store goes to the dummy slot), so the hand-counted waits of the per-tile
+// kernel hold across tiles.  The claim (wave 0, lane 0): the atomic after the
+// store of unit m-4 (m = the tile's units), `vmcnt(0)` for wave 0 at unit m-3
+// (it waits early for DMA(m-2), issued a whole unit before), the index to LDS
+// before that unit's barrier, read by every wave after it; the tile's
+// descriptor comes by scalar loads, waited for by the next unit's lgkmcnt(0).
+// Tiles are at least 3 iterations (m >= 4; the host guarantees it).
+struct K1Chunk {
+  const uint8_t* fb;   // file start
+  uint64_t N, q0, sb;  // file bytes, the tile's first position, the file's slice base
+  uint32_t m;          // units: the halo + the tile's iterations
+  uint32_t hb;         // halo bytes at the descriptor's start (0 at a file's start)
+  s32x4 srd;           // [fb + q0 - hb, + hb + the tile's bytes)
+  bool valid;
+};
+__device__ __forceinline__ K1Chunk k1_chunk(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
+                                            const uint64_t* __restrict__ file_len,
+                                            const uint64_t* __restrict__ slice_base, const uint4* __restrict__ tiles,
+                                            uint32_t n_tiles, uint32_t t) {
+  K1Chunk c;
+  c.valid = t < n_tiles;
+  const uint4 td = tiles[c.valid ? t : 0u];
+  const uint32_t f = td.x;
+  c.N = file_len[f];
+  c.fb = arena + file_off[f];
+  c.sb = slice_base[f];
+  c.q0 = (uint64_t)td.y * kMinBlock;
+  const uint64_t rem = c.N - c.q0;
+  const uint32_t n_it = (uint32_t)umin64(td.z, (rem + kMinBlock - 1) / kMinBlock);
+  c.m = n_it + 1u;
+  c.hb = c.q0 ? kMinBlock : 0u;
+  const uint32_t nbytes = c.hb + (uint32_t)((umin64(rem, (uint64_t)n_it * kMinBlock) + 15ull) & ~15ull);
+  c.srd = make_srd(c.fb + c.q0 - c.hb, nbytes);
+  return c;
+}
+// Descriptor offset of unit k of tile c; past the tile (k >= m) and the halo
+// at a file's start read past the descriptor's end: zeros.
+__device__ __forceinline__ uint32_t k1_unit_soff(const K1Chunk& c, uint32_t k) {
+  const uint32_t past = c.hb + (c.m - 1u) * kMinBlock;
+  if (k == 0u) return c.hb ? 0u : past;
+  return k < c.m ? c.hb + (k - 1u) * kMinBlock : past;
+}
+
+extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1d_digest_scan(
+    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
+    const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ slice_base,
+    const uint4* __restrict__ tiles, uint32_t n_tiles, uint32_t* __restrict__ ctr, uint2* __restrict__ ssum,
+    uint64_t dummy) {
+  __shared__ uint2 wtot[2][16];
+  __shared__ uint32_t claim0, claim;  // the first tile's index; the later ones'
+  __shared__ __attribute__((aligned(1024))) uint8_t land[kK1Threads / 64][2][kDmaSlot];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t l = tid & 63u;
+  const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+  const uint32_t e_l = w * kSlice + l * 64u;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)&land[w][0][0];
+  const uint32_t lds1 = (uint32_t)(uintptr_t)&land[w][1][0];
+  // the transposed (conflict-free) LDS image of hbx_k1_digest_scan_dma, swz 1
+  const uint32_t dma_lane = 64u * (l & 15u) + 16u * (l >> 4);
+  const uint32_t rd_lane = 64u * (l >> 4) + (l & 15u);
+  auto land_read = [&](uint32_t slot, uint32_t (&v)[16]) {
+    const u32x4* p = reinterpret_cast<const u32x4*>(&land[w][slot][0]);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const u32x4 t = p[rd_lane + 16u * k];
+      v[4 * k + 0] = t.x;
+      v[4 * k + 1] = t.y;
+      v[4 * k + 2] = t.z;
+      v[4 * k + 3] = t.w;
+    }
+  };
+  if (tid == 0u) claim0 = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  K1Chunk cur = k1_chunk(arena, file_off, file_len, slice_base, tiles, n_tiles,
+                         (uint32_t)__builtin_amdgcn_readfirstlane((int)claim0));
+  if (!cur.valid) return;
+  K1Chunk nxt = cur;
+  nxt.valid = false;
+  // stream position k of the current tile (k >= m: the next tile's unit k - m,
+  // or past the current tile's end when there is none)
+  auto issue = [&](uint32_t k, uint32_t lds) {
+    const bool use_n = k >= cur.m && nxt.valid;
+    const s32x4 srd = use_n ? nxt.srd : cur.srd;
+    const uint32_t soff = use_n ? k1_unit_soff(nxt, k - cur.m) : k1_unit_soff(cur, k);
+    dma16x4(srd, w * kSlice + dma_lane, soff, lds);
+  };
+  issue(0u, lds0);
+  issue(1u, lds1);
+  uint32_t run_a[16], run_b[16];
+  K1State st{0u, 0u, RunAgg{0u, 0u, 0u, 0u}};
+  uint32_t u = 0u, k = 0u, v_claim = 0u;
+  const uint64_t ctr64 = reinterpret_cast<uint64_t>(ctr);
+  bool done = false;
+  auto step = [&](uint32_t (&cv)[16], const uint32_t (&pv)[16]) {
+    const bool claim_now = k + 3u == cur.m;  // the claim issued after unit m-4's store lands
+    // outstanding per wave, oldest first: DMA(u), store(u-2), DMA(u+1),
+    // store(u-1) (+ wave 0's claim atomic after store(u-1) at a claim unit)
+    if (claim_now && w == 0u)
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(v_claim) : : "memory");  // (binds the claim's register)
+    else if (u == 0u)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (u == 1u)
+      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    land_read(u & 1u, cv);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot consumed before it is refilled
+    if (claim_now && tid == 0u) claim = v_claim;         // published by this unit's barrier
+    issue(k + 2u, (u & 1u) ? lds1 : lds0);
+    if (k == 0u) {  // the halo: prime the rollsum state
+      // one barrier per unit, also at a file's start (k1_prime has none
+      // there): unit u+1 writes wave totals into wtot[u & 1] only after every
+      // wave has read unit u-1's
+      if (cur.q0 == 0u) __syncthreads();
+      st = k1_prime(cv, cur.q0 == 0u, wtot, w, l, e_l, u & 1u);
+      k1_store_slice(ssum, dummy, l, 0u, 0u);
+    } else {
+      const uint64_t qs = cur.q0 + (uint64_t)(k - 1u) * kMinBlock;
+      uint32_t smax, sprev;
+      k1_iteration(cv, pv, st, wtot, u, w, l, e_l, qs, cur.N, smax, sprev);
+      const bool ok = qs + (uint64_t)w * kSlice < cur.N;
+      k1_store_slice(ssum, ok ? cur.sb + ((qs >> kSliceShift) + w) : dummy, l, smax, sprev);
+    }
+    // inline asm: a compiler-issued atomic got a vmcnt(0) right behind it in
+    // every wave (draining the DMA just issued); this one is waited for by
+    // wave 0's vmcnt(0) at the next unit, which names its register
+    if (k + 4u == cur.m && tid == 0u)
+      asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=&v"(v_claim) : "v"(ctr64), "v"(1u) : "memory");
+    if (claim_now)
+      nxt = k1_chunk(arena, file_off, file_len, slice_base, tiles, n_tiles,
+                     (uint32_t)__builtin_amdgcn_readfirstlane((int)claim));
+    u++;
+    if (++k == cur.m) {
+      if (nxt.valid) {
+        cur = nxt;
+        nxt.valid = false;
+        k = 0u;
+      } else {
+        done = true;
+      }
+    }
+  };
+  for (;;) {
+    step(run_a, run_b);
+    if (done) break;
+    step(run_b, run_a);
+    if (done) break;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup exits
 }

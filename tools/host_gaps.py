@@ -21,7 +21,7 @@ krows = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Na
                for r in csv.DictReader(open(kt)))
 hrows = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Function", r.get("Operation", "?")))
                for r in csv.DictReader(open(ht[0]))) if ht else []
-k1 = [e for e in krows if e[2] == "hbx_k1_digest_scan_dma"]
+k1 = [e for e in krows if e[2] in ("hbx_k1_digest_scan_dma", "hbx_k1d_digest_scan")]
 shown = 0
 for i in range(len(k1) - 1, 0, -1):
     a, b = k1[i - 1][1], k1[i][0]

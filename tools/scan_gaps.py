@@ -25,7 +25,7 @@ if mc:
     for r in csv.DictReader(open(mc[0])):
         copies.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
                        f"copy {r.get('Direction', '')} {r.get('Bytes', r.get('Size', ''))}B", "dma"))
-k1 = [e for e in ev if e[2] == "hbx_k1_digest_scan_dma"][-n:]
+k1 = [e for e in ev if e[2] in ("hbx_k1_digest_scan_dma", "hbx_k1d_digest_scan")][-n:]
 gaps = np.array([(k1[i + 1][0] - k1[i][1]) / 1e3 for i in range(len(k1) - 1)])
 dur = np.array([(e - s) / 1e3 for s, e, _, _ in k1])
 print(f"K1 launches {len(k1)}: duration us mean {dur.mean():.1f} median {np.median(dur):.1f}; "

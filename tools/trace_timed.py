@@ -17,7 +17,7 @@ bench = None
 for line in open(sys.argv[2]):
     if line.startswith("{") and '"metric"' in line:
         bench = json.loads(line)
-names = {"k1_digest_scan": "hbx_k1_digest_scan_dma", "k2_cut_chain": "hbx_k2_cut_chain",
+names = {"k1_digest_scan": ("hbx_k1_digest_scan_dma", "hbx_k1d_digest_scan"), "k2_cut_chain": "hbx_k2_cut_chain",
          "k2c_chain_plan": "hbx_k2c_plan", "k3_block_md5": ("hbx_k3_block_md5", "hbx_k3p_block_md5", "hbx_k3q_block_md5"),
          "k4_content_id": "hbx_k4_content_id"}
 # after the window, one drain launch per join-lag step (a preplanned launch

@@ -26,7 +26,7 @@ def spans(*names):
 LAG = next((int(a.split("=", 1)[1]) for a in sys.argv if a.startswith("--lag=")), 1)  # drain launches after the window
 k3 = spans("hbx_k3_block_md5", "hbx_k3p_block_md5", "hbx_k3q_block_md5")
 k2 = spans("hbx_k2_cut_chain")
-k1 = spans("hbx_k1_digest_scan_dma", "hbx_k1_digest_scan_lite", "hbx_k1_digest_scan")
+k1 = spans("hbx_k1_digest_scan_dma", "hbx_k1d_digest_scan", "hbx_k1_digest_scan_lite", "hbx_k1_digest_scan")
 w3 = k3[-(K + LAG):-LAG]
 w1 = k1[-K:]
 w2 = k2[-K:]
