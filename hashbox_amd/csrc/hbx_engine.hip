@@ -212,6 +212,14 @@ struct hbx_ctx {
   // 2,077 vs 2,122 (profiles/r06j), so the producer's lead is not what stalls
   // the MD5 wave
   uint32_t k3_hand = 0;
+  // HBX_K3_XT=1 (A/B): round 1's constants added to the staged words by K3P's
+  // producer wave, 16 VALU per block off the MD5 wave.  Bit-exact, slower:
+  // 1,518-1,520 vs 1,454-1,459 cycles per block with the adds in the
+  // producer's registers or as LDS atomics alike, 2,349-2,353 vs 2,380-2,382
+  // GiB/s (profiles/r06q, r06r): the MD5 wave is not held by its own
+  // off-path adds (they fill its dependent chain's gaps), and the producer's
+  // added work lands on the same SIMD or the same LDS path
+  uint32_t k3_xt = 0;
   uint32_t k3_spin = 0;
   // full-slice chains ordered by data address in plan_addr granules of
   // 2^plan_addr_shift bytes (plan_bin; HBX_PLAN_ADDR=0..512, 0 = by count
@@ -797,7 +805,7 @@ int md5_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
     hipLaunchKernelGGL(hbx_k3p_block_md5, dim3(c->md5_wgs), dim3(kK3PThreads), 0, s,
                        c->d_order[slot].as<OrderEntry>(), static_cast<const uint32_t*>(c->d_octl[slot].as<uint32_t>()),
                        budget, c->d_gate.as<uint32_t>(), c->k3_dispatched, c->k3_waves + waves - 1u, tslot,
-                       c->h_probe.p ? c->h_probe.as<uint64_t>() : nullptr, c->k3_psets | (c->k3_spin ? 0x100u : 0u) | (c->k3_hand ? 0x200u : 0u));
+                       c->h_probe.p ? c->h_probe.as<uint64_t>() : nullptr, c->k3_psets | (c->k3_spin ? 0x100u : 0u) | (c->k3_hand ? 0x200u : 0u) | (c->k3_xt ? 0x400u : 0u));
   else
     hipLaunchKernelGGL(hbx_k3_block_md5, dim3(c->md5_wgs), dim3(kK3Threads), 0, s,
                        c->d_order[slot].as<OrderEntry>(), static_cast<const uint32_t*>(c->d_octl[slot].as<uint32_t>()),
@@ -1565,6 +1573,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = ab_env("HBX_SDMA_WARM")) c->sdma_warm = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_PSETS")) c->k3_psets = std::atoi(v) == 3 ? 3u : 2u;
   if (const char* v = ab_env("HBX_K3_HAND")) c->k3_hand = std::atoi(v) ? 1u : 0u;
+  if (const char* v = ab_env("HBX_K3_XT")) c->k3_xt = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_SPIN")) c->k3_spin = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_PLAN_ADDR")) c->plan_addr = (uint32_t)std::min(512, std::max(0, std::atoi(v)));
   if (const char* v = ab_env("HBX_PLAN_ADDR_SHIFT")) c->plan_addr_shift = (uint32_t)std::min(40, std::max(20, std::atoi(v)));
@@ -1733,7 +1742,14 @@ int hbx_plan_pipeline(hbx_ctx* c, const hbx_plan_request* q, hbx_pipeline_plan* 
     // 2,277-2,294 vs P2 2,260-2,272)
     per = (q->steps == 0 || q->steps % 4 == 0) ? 4 : (q->steps % 2 == 0) ? 2 : 1;
   }
-  const int64_t ld = q->lead >= 0 ? q->lead : lag + 1;
+  // lead (steps an arena stays resident beyond its batch's launches): the join
+  // lag at 32 or more files per GPU (round 6: the next batch's K1 follows the
+  // launch that finishes the old one through hbx_input_after_oldest; R = 33 at
+  // 64 files then holds 31 launches instead of 30: 2,380-2,391 vs 2,303-2,350
+  // GiB/s in three alternating pairs, profiles/r06p), lag + 1 below (8 files:
+  // 2,045 vs 2,082, where R ~ 256 makes the lead's share negligible) and for
+  // host input
+  const int64_t ld = q->lead >= 0 ? q->lead : lag + ((q->n_files >= 32 && !host_in) ? 0 : 1);
   const uint64_t nfull = (std::min<uint64_t>(q->longest_file, HBX_MAX_BLOCK_SIZE) + 8u) >> 6;
   const double frac = q->hbm_frac > 0.0 ? q->hbm_frac : 0.95;
   const uint64_t share = (uint64_t)((double)free_b * frac / (double)std::max<uint32_t>(1u, q->ranks_per_device));
@@ -1791,12 +1807,12 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
       "\"lean_marks\": %u, \"k3_prod\": %u, \"k3_items\": %u, \"k3_period\": %u, \"meta_kernel\": %u, "
       "\"plan_cut\": %u, \"k1_swz\": %u, \"k3_psets\": %u, \"d2h_kernel\": %u, \"k8_split_streams\": %llu, "
       "\"k8_split_fallbacks\": %llu, \"gate_meta\": %u, \"sdma_warm\": %u, \"sdma_h2d_mask\": %u, "
-      "\"sdma_d2h_mask\": %u, \"sdma_warm_ms\": %.3f, \"k3_spin\": %u, \"plan_addr\": %u, \"plan_addr_shift\": %u, \"k1_ext\": %u, \"k1_dma4\": %u, \"k3_hand\": %u, \"k1d\": %u, \"k1d_par\": %u, \"k1d_grid\": %u}",
+      "\"sdma_d2h_mask\": %u, \"sdma_warm_ms\": %.3f, \"k3_spin\": %u, \"plan_addr\": %u, \"plan_addr_shift\": %u, \"k1_ext\": %u, \"k1_dma4\": %u, \"k3_hand\": %u, \"k3_xt\": %u, \"k1d\": %u, \"k1d_par\": %u, \"k1d_grid\": %u}",
       (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_gate, c->md5_wgs,
       plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks, c->k3_prod, c->k3_items,
       c->k3_period, c->meta_kernel, c->plan_cut, c->k1_swz, c->k3_psets, c->d2h_kernel,
       (unsigned long long)c->k8_split_streams, (unsigned long long)c->k8_split_fallbacks, c->gate_meta,
-      c->sdma_warm, c->sdma_h2d, c->sdma_d2h, c->sdma_warm_ms, c->k3_spin, c->plan_addr, c->plan_addr_shift, c->k1_ext, c->k1_dma4, c->k3_hand, c->k1d, c->k1d_par, c->k1d_grid);
+      c->sdma_warm, c->sdma_h2d, c->sdma_d2h, c->sdma_warm_ms, c->k3_spin, c->plan_addr, c->plan_addr_shift, c->k1_ext, c->k1_dma4, c->k3_hand, c->k3_xt, c->k1d, c->k1d_par, c->k1d_grid);
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }
 

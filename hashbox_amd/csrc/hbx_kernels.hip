@@ -719,76 +719,89 @@ __device__ __forceinline__ uint32_t xad(uint32_t b, uint32_t cd, uint32_t t1) { 
     a = (b) + rotl(xad((b), cd_, (a) + (x) + (t)), s);     \
   }
 
-__device__ __forceinline__ void md5_compress(uint32_t (&h)[4], const uint32_t (&m)[16]) {
+// Round 1's additive constants (RFC 1321 T[1..16]): with XT the message words
+// arrive with them already added (x_j + T_j, written by K3P's producer wave
+// through LDS atomics, k3p_produce), so a round-1 step is F -> add3(a, F,
+// x_j + T_j) -> rotate -> add, one VALU fewer, and the later rounds, which
+// read x_j again, add T_k - T_j instead of T_k (folded constants): 16 of the
+// block's 320 VALU leave the MD5 wave's stream (round 6, HBX_K3_XT).
+constexpr uint32_t kR1[16] = {0xd76aa478u, 0xe8c7b756u, 0x242070dbu, 0xc1bdceeeu, 0xf57c0fafu, 0x4787c62au,
+                              0xa8304613u, 0xfd469501u, 0x698098d8u, 0x8b44f7afu, 0xffff5bb1u, 0x895cd7beu,
+                              0x6b901122u, 0xfd987193u, 0xa679438eu, 0x49b40821u};
+template <bool XT>
+__device__ __forceinline__ void md5_compress_t(uint32_t (&h)[4], const uint32_t (&m)[16]) {
   uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
-  HBX_STEP(HBX_F, a, b, c, d, m[0], 0xd76aa478u, 7);
-  HBX_STEP(HBX_F, d, a, b, c, m[1], 0xe8c7b756u, 12);
-  HBX_STEP(HBX_F, c, d, a, b, m[2], 0x242070dbu, 17);
-  HBX_STEP(HBX_F, b, c, d, a, m[3], 0xc1bdceeeu, 22);
-  HBX_STEP(HBX_F, a, b, c, d, m[4], 0xf57c0fafu, 7);
-  HBX_STEP(HBX_F, d, a, b, c, m[5], 0x4787c62au, 12);
-  HBX_STEP(HBX_F, c, d, a, b, m[6], 0xa8304613u, 17);
-  HBX_STEP(HBX_F, b, c, d, a, m[7], 0xfd469501u, 22);
-  HBX_STEP(HBX_F, a, b, c, d, m[8], 0x698098d8u, 7);
-  HBX_STEP(HBX_F, d, a, b, c, m[9], 0x8b44f7afu, 12);
-  HBX_STEP(HBX_F, c, d, a, b, m[10], 0xffff5bb1u, 17);
-  HBX_STEP(HBX_F, b, c, d, a, m[11], 0x895cd7beu, 22);
-  HBX_STEP(HBX_F, a, b, c, d, m[12], 0x6b901122u, 7);
-  HBX_STEP(HBX_F, d, a, b, c, m[13], 0xfd987193u, 12);
-  HBX_STEP(HBX_F, c, d, a, b, m[14], 0xa679438eu, 17);
-  HBX_STEP(HBX_F, b, c, d, a, m[15], 0x49b40821u, 22);
-  HBX_STEP(HBX_G, a, b, c, d, m[1], 0xf61e2562u, 5);
-  HBX_STEP(HBX_G, d, a, b, c, m[6], 0xc040b340u, 9);
-  HBX_STEP(HBX_G, c, d, a, b, m[11], 0x265e5a51u, 14);
-  HBX_STEP(HBX_G, b, c, d, a, m[0], 0xe9b6c7aau, 20);
-  HBX_STEP(HBX_G, a, b, c, d, m[5], 0xd62f105du, 5);
-  HBX_STEP(HBX_G, d, a, b, c, m[10], 0x02441453u, 9);
-  HBX_STEP(HBX_G, c, d, a, b, m[15], 0xd8a1e681u, 14);
-  HBX_STEP(HBX_G, b, c, d, a, m[4], 0xe7d3fbc8u, 20);
-  HBX_STEP(HBX_G, a, b, c, d, m[9], 0x21e1cde6u, 5);
-  HBX_STEP(HBX_G, d, a, b, c, m[14], 0xc33707d6u, 9);
-  HBX_STEP(HBX_G, c, d, a, b, m[3], 0xf4d50d87u, 14);
-  HBX_STEP(HBX_G, b, c, d, a, m[8], 0x455a14edu, 20);
-  HBX_STEP(HBX_G, a, b, c, d, m[13], 0xa9e3e905u, 5);
-  HBX_STEP(HBX_G, d, a, b, c, m[2], 0xfcefa3f8u, 9);
-  HBX_STEP(HBX_G, c, d, a, b, m[7], 0x676f02d9u, 14);
-  HBX_STEP(HBX_G, b, c, d, a, m[12], 0x8d2a4c8au, 20);
-  HBX_STEP_H(a, b, c, d, m[5], 0xfffa3942u, 4);
-  HBX_STEP_H(d, a, b, c, m[8], 0x8771f681u, 11);
-  HBX_STEP_H(c, d, a, b, m[11], 0x6d9d6122u, 16);
-  HBX_STEP_H(b, c, d, a, m[14], 0xfde5380cu, 23);
-  HBX_STEP_H(a, b, c, d, m[1], 0xa4beea44u, 4);
-  HBX_STEP_H(d, a, b, c, m[4], 0x4bdecfa9u, 11);
-  HBX_STEP_H(c, d, a, b, m[7], 0xf6bb4b60u, 16);
-  HBX_STEP_H(b, c, d, a, m[10], 0xbebfbc70u, 23);
-  HBX_STEP_H(a, b, c, d, m[13], 0x289b7ec6u, 4);
-  HBX_STEP_H(d, a, b, c, m[0], 0xeaa127fau, 11);
-  HBX_STEP_H(c, d, a, b, m[3], 0xd4ef3085u, 16);
-  HBX_STEP_H(b, c, d, a, m[6], 0x04881d05u, 23);
-  HBX_STEP_H(a, b, c, d, m[9], 0xd9d4d039u, 4);
-  HBX_STEP_H(d, a, b, c, m[12], 0xe6db99e5u, 11);
-  HBX_STEP_H(c, d, a, b, m[15], 0x1fa27cf8u, 16);
-  HBX_STEP_H(b, c, d, a, m[2], 0xc4ac5665u, 23);
-  HBX_STEP(HBX_I, a, b, c, d, m[0], 0xf4292244u, 6);
-  HBX_STEP(HBX_I, d, a, b, c, m[7], 0x432aff97u, 10);
-  HBX_STEP(HBX_I, c, d, a, b, m[14], 0xab9423a7u, 15);
-  HBX_STEP(HBX_I, b, c, d, a, m[5], 0xfc93a039u, 21);
-  HBX_STEP(HBX_I, a, b, c, d, m[12], 0x655b59c3u, 6);
-  HBX_STEP(HBX_I, d, a, b, c, m[3], 0x8f0ccc92u, 10);
-  HBX_STEP(HBX_I, c, d, a, b, m[10], 0xffeff47du, 15);
-  HBX_STEP(HBX_I, b, c, d, a, m[1], 0x85845dd1u, 21);
-  HBX_STEP(HBX_I, a, b, c, d, m[8], 0x6fa87e4fu, 6);
-  HBX_STEP(HBX_I, d, a, b, c, m[15], 0xfe2ce6e0u, 10);
-  HBX_STEP(HBX_I, c, d, a, b, m[6], 0xa3014314u, 15);
-  HBX_STEP(HBX_I, b, c, d, a, m[13], 0x4e0811a1u, 21);
-  HBX_STEP(HBX_I, a, b, c, d, m[4], 0xf7537e82u, 6);
-  HBX_STEP(HBX_I, d, a, b, c, m[11], 0xbd3af235u, 10);
-  HBX_STEP(HBX_I, c, d, a, b, m[2], 0x2ad7d2bbu, 15);
-  HBX_STEP(HBX_I, b, c, d, a, m[9], 0xeb86d391u, 21);
+  HBX_STEP(HBX_F, a, b, c, d, m[0], (XT ? 0u : 0xd76aa478u), 7);
+  HBX_STEP(HBX_F, d, a, b, c, m[1], (XT ? 0u : 0xe8c7b756u), 12);
+  HBX_STEP(HBX_F, c, d, a, b, m[2], (XT ? 0u : 0x242070dbu), 17);
+  HBX_STEP(HBX_F, b, c, d, a, m[3], (XT ? 0u : 0xc1bdceeeu), 22);
+  HBX_STEP(HBX_F, a, b, c, d, m[4], (XT ? 0u : 0xf57c0fafu), 7);
+  HBX_STEP(HBX_F, d, a, b, c, m[5], (XT ? 0u : 0x4787c62au), 12);
+  HBX_STEP(HBX_F, c, d, a, b, m[6], (XT ? 0u : 0xa8304613u), 17);
+  HBX_STEP(HBX_F, b, c, d, a, m[7], (XT ? 0u : 0xfd469501u), 22);
+  HBX_STEP(HBX_F, a, b, c, d, m[8], (XT ? 0u : 0x698098d8u), 7);
+  HBX_STEP(HBX_F, d, a, b, c, m[9], (XT ? 0u : 0x8b44f7afu), 12);
+  HBX_STEP(HBX_F, c, d, a, b, m[10], (XT ? 0u : 0xffff5bb1u), 17);
+  HBX_STEP(HBX_F, b, c, d, a, m[11], (XT ? 0u : 0x895cd7beu), 22);
+  HBX_STEP(HBX_F, a, b, c, d, m[12], (XT ? 0u : 0x6b901122u), 7);
+  HBX_STEP(HBX_F, d, a, b, c, m[13], (XT ? 0u : 0xfd987193u), 12);
+  HBX_STEP(HBX_F, c, d, a, b, m[14], (XT ? 0u : 0xa679438eu), 17);
+  HBX_STEP(HBX_F, b, c, d, a, m[15], (XT ? 0u : 0x49b40821u), 22);
+  HBX_STEP(HBX_G, a, b, c, d, m[1], (XT ? 0xf61e2562u - kR1[1] : 0xf61e2562u), 5);
+  HBX_STEP(HBX_G, d, a, b, c, m[6], (XT ? 0xc040b340u - kR1[6] : 0xc040b340u), 9);
+  HBX_STEP(HBX_G, c, d, a, b, m[11], (XT ? 0x265e5a51u - kR1[11] : 0x265e5a51u), 14);
+  HBX_STEP(HBX_G, b, c, d, a, m[0], (XT ? 0xe9b6c7aau - kR1[0] : 0xe9b6c7aau), 20);
+  HBX_STEP(HBX_G, a, b, c, d, m[5], (XT ? 0xd62f105du - kR1[5] : 0xd62f105du), 5);
+  HBX_STEP(HBX_G, d, a, b, c, m[10], (XT ? 0x02441453u - kR1[10] : 0x02441453u), 9);
+  HBX_STEP(HBX_G, c, d, a, b, m[15], (XT ? 0xd8a1e681u - kR1[15] : 0xd8a1e681u), 14);
+  HBX_STEP(HBX_G, b, c, d, a, m[4], (XT ? 0xe7d3fbc8u - kR1[4] : 0xe7d3fbc8u), 20);
+  HBX_STEP(HBX_G, a, b, c, d, m[9], (XT ? 0x21e1cde6u - kR1[9] : 0x21e1cde6u), 5);
+  HBX_STEP(HBX_G, d, a, b, c, m[14], (XT ? 0xc33707d6u - kR1[14] : 0xc33707d6u), 9);
+  HBX_STEP(HBX_G, c, d, a, b, m[3], (XT ? 0xf4d50d87u - kR1[3] : 0xf4d50d87u), 14);
+  HBX_STEP(HBX_G, b, c, d, a, m[8], (XT ? 0x455a14edu - kR1[8] : 0x455a14edu), 20);
+  HBX_STEP(HBX_G, a, b, c, d, m[13], (XT ? 0xa9e3e905u - kR1[13] : 0xa9e3e905u), 5);
+  HBX_STEP(HBX_G, d, a, b, c, m[2], (XT ? 0xfcefa3f8u - kR1[2] : 0xfcefa3f8u), 9);
+  HBX_STEP(HBX_G, c, d, a, b, m[7], (XT ? 0x676f02d9u - kR1[7] : 0x676f02d9u), 14);
+  HBX_STEP(HBX_G, b, c, d, a, m[12], (XT ? 0x8d2a4c8au - kR1[12] : 0x8d2a4c8au), 20);
+  HBX_STEP_H(a, b, c, d, m[5], (XT ? 0xfffa3942u - kR1[5] : 0xfffa3942u), 4);
+  HBX_STEP_H(d, a, b, c, m[8], (XT ? 0x8771f681u - kR1[8] : 0x8771f681u), 11);
+  HBX_STEP_H(c, d, a, b, m[11], (XT ? 0x6d9d6122u - kR1[11] : 0x6d9d6122u), 16);
+  HBX_STEP_H(b, c, d, a, m[14], (XT ? 0xfde5380cu - kR1[14] : 0xfde5380cu), 23);
+  HBX_STEP_H(a, b, c, d, m[1], (XT ? 0xa4beea44u - kR1[1] : 0xa4beea44u), 4);
+  HBX_STEP_H(d, a, b, c, m[4], (XT ? 0x4bdecfa9u - kR1[4] : 0x4bdecfa9u), 11);
+  HBX_STEP_H(c, d, a, b, m[7], (XT ? 0xf6bb4b60u - kR1[7] : 0xf6bb4b60u), 16);
+  HBX_STEP_H(b, c, d, a, m[10], (XT ? 0xbebfbc70u - kR1[10] : 0xbebfbc70u), 23);
+  HBX_STEP_H(a, b, c, d, m[13], (XT ? 0x289b7ec6u - kR1[13] : 0x289b7ec6u), 4);
+  HBX_STEP_H(d, a, b, c, m[0], (XT ? 0xeaa127fau - kR1[0] : 0xeaa127fau), 11);
+  HBX_STEP_H(c, d, a, b, m[3], (XT ? 0xd4ef3085u - kR1[3] : 0xd4ef3085u), 16);
+  HBX_STEP_H(b, c, d, a, m[6], (XT ? 0x04881d05u - kR1[6] : 0x04881d05u), 23);
+  HBX_STEP_H(a, b, c, d, m[9], (XT ? 0xd9d4d039u - kR1[9] : 0xd9d4d039u), 4);
+  HBX_STEP_H(d, a, b, c, m[12], (XT ? 0xe6db99e5u - kR1[12] : 0xe6db99e5u), 11);
+  HBX_STEP_H(c, d, a, b, m[15], (XT ? 0x1fa27cf8u - kR1[15] : 0x1fa27cf8u), 16);
+  HBX_STEP_H(b, c, d, a, m[2], (XT ? 0xc4ac5665u - kR1[2] : 0xc4ac5665u), 23);
+  HBX_STEP(HBX_I, a, b, c, d, m[0], (XT ? 0xf4292244u - kR1[0] : 0xf4292244u), 6);
+  HBX_STEP(HBX_I, d, a, b, c, m[7], (XT ? 0x432aff97u - kR1[7] : 0x432aff97u), 10);
+  HBX_STEP(HBX_I, c, d, a, b, m[14], (XT ? 0xab9423a7u - kR1[14] : 0xab9423a7u), 15);
+  HBX_STEP(HBX_I, b, c, d, a, m[5], (XT ? 0xfc93a039u - kR1[5] : 0xfc93a039u), 21);
+  HBX_STEP(HBX_I, a, b, c, d, m[12], (XT ? 0x655b59c3u - kR1[12] : 0x655b59c3u), 6);
+  HBX_STEP(HBX_I, d, a, b, c, m[3], (XT ? 0x8f0ccc92u - kR1[3] : 0x8f0ccc92u), 10);
+  HBX_STEP(HBX_I, c, d, a, b, m[10], (XT ? 0xffeff47du - kR1[10] : 0xffeff47du), 15);
+  HBX_STEP(HBX_I, b, c, d, a, m[1], (XT ? 0x85845dd1u - kR1[1] : 0x85845dd1u), 21);
+  HBX_STEP(HBX_I, a, b, c, d, m[8], (XT ? 0x6fa87e4fu - kR1[8] : 0x6fa87e4fu), 6);
+  HBX_STEP(HBX_I, d, a, b, c, m[15], (XT ? 0xfe2ce6e0u - kR1[15] : 0xfe2ce6e0u), 10);
+  HBX_STEP(HBX_I, c, d, a, b, m[6], (XT ? 0xa3014314u - kR1[6] : 0xa3014314u), 15);
+  HBX_STEP(HBX_I, b, c, d, a, m[13], (XT ? 0x4e0811a1u - kR1[13] : 0x4e0811a1u), 21);
+  HBX_STEP(HBX_I, a, b, c, d, m[4], (XT ? 0xf7537e82u - kR1[4] : 0xf7537e82u), 6);
+  HBX_STEP(HBX_I, d, a, b, c, m[11], (XT ? 0xbd3af235u - kR1[11] : 0xbd3af235u), 10);
+  HBX_STEP(HBX_I, c, d, a, b, m[2], (XT ? 0x2ad7d2bbu - kR1[2] : 0x2ad7d2bbu), 15);
+  HBX_STEP(HBX_I, b, c, d, a, m[9], (XT ? 0xeb86d391u - kR1[9] : 0xeb86d391u), 21);
   h[0] += a;
   h[1] += b;
   h[2] += c;
   h[3] += d;
+}
+__device__ __forceinline__ void md5_compress(uint32_t (&h)[4], const uint32_t (&m)[16]) {
+  md5_compress_t<false>(h, m);
 }
 
 __device__ __forceinline__ void md5_init(uint32_t (&h)[4]) {
@@ -1348,6 +1361,7 @@ __device__ __forceinline__ void k3p_publish(uint32_t* p, uint32_t v) {
 // A stage is freed once its last block is hashed (its reads have landed: the
 // block waited for them), except the group's last stage (freed by the caller
 // once the group is done).
+template <bool XT = false>
 __device__ __forceinline__ void k3p_consume(uint8_t* wl, uint32_t* flags, uint32_t S, uint32_t Rr, uint32_t (&h)[4],
                                             uint32_t& polls, bool spin) {
   const uint32_t row = (uint32_t)(uintptr_t)(wl + (threadIdx.x & 63u) * Coop<16>::Row);  // LDS address
@@ -1368,7 +1382,7 @@ __device__ __forceinline__ void k3p_consume(uint8_t* wl, uint32_t* flags, uint32
   auto hash = [&](const u32x4(&W)[4]) {
     const uint32_t m[16] = {W[0].x, W[0].y, W[0].z, W[0].w, W[1].x, W[1].y, W[1].z, W[1].w,
                             W[2].x, W[2].y, W[2].z, W[2].w, W[3].x, W[3].y, W[3].z, W[3].w};
-    md5_compress(h, m);
+    md5_compress_t<XT>(h, m);  // XT: the producer added round 1's constants
   };
   const uint32_t nst = (4u * Rr + 15u) / 16u;  // >= 2 (Rr >= kCoopMinBudget - 1)
   u32x4 WA[4], WB[4];
@@ -1478,11 +1492,41 @@ __device__ __forceinline__ void coop_vmwait(u32x4 (&G)[16]) {
                : "memory");
 }
 
-template <int SETS = 2, bool HAND = false>
+// XT (round 6): the producer adds round 1's constants to the words of a stage
+// in its registers before writing the rows (granule t of a chain's stage holds
+// words 4 (t % 4) .. +3 of a block), 64 v_add_u32 per stage.  They share the
+// SIMD with the MD5 wave, but at a lower priority (s_setprio 2 vs 3) they
+// issue only in the MD5 wave's bubbles (~30 VALU slots per block at 1,450
+// cycles).  (The same adds as LDS atomics after the writes, 64 ds_add_u32 per
+// stage, kept the VALU free but the rows' atomics, 2-3-way bank-conflicted,
+// held the LDS path the MD5 wave reads through: 1,512-1,520 vs 1,454-1,456
+// cycles per block, profiles/r06q.)
+__device__ __forceinline__ void coop_write_k(uint8_t* wl, uint32_t wr, uint32_t half, const u32x4 (&Gs)[16],
+                                             const uint32_t (&kc)[4]) {
+#pragma unroll
+  for (int q = 0; q < 16; q++) {
+    const u32x4 v = {Gs[q].x + kc[0], Gs[q].y + kc[1], Gs[q].z + kc[2], Gs[q].w + kc[3]};
+    *reinterpret_cast<u32x4*>(wl + wr + half * Coop<16>::Half + Coop<16>::C * Coop<16>::Row * (uint32_t)q) = v;
+  }
+}
+__device__ __forceinline__ void k3_lane_r1(uint32_t (&kc)[4]) {  // this producer lane's 4 round-1 constants
+  const uint32_t j0 = 4u * ((threadIdx.x & 63u) % 4u);
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    uint32_t v = 0u;
+#pragma unroll
+    for (int j = 0; j < 16; j += 4) v = j0 == (uint32_t)j ? kR1[j + w] : v;
+    kc[w] = v;
+  }
+}
+
+template <int SETS = 2, bool HAND = false, bool XT = false>
 __device__ __forceinline__ uint32_t k3p_produce(uint8_t* wl, uint32_t* flags, uint32_t S, uint64_t src, uint32_t Rr) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t t = lane % 16u, sub = lane / 16u;
   const uint32_t wr = sub * Coop<16>::Row + 16u * t;
+  uint32_t kc[4];
+  if constexpr (XT) k3_lane_r1(kc);
   const uint32_t ngr = 4u * Rr, nst = (ngr + 15u) / 16u;
   uint64_t Q[16];
 #pragma unroll
@@ -1496,7 +1540,10 @@ __device__ __forceinline__ uint32_t k3p_produce(uint8_t* wl, uint32_t* flags, ui
     auto put = [&](uint32_t x, u32x4(&G)[16]) {
       k3p_wait_ge(&flags[1], x < 2u ? S : S + x - 1u);
       coop_vmwait<16 * (SETS - 1)>(G);
-      coop_write<16>(wl, wr, (S + x) & 1u, G);
+      if constexpr (XT)
+        coop_write_k(wl, wr, (S + x) & 1u, G, kc);
+      else
+        coop_write<16>(wl, wr, (S + x) & 1u, G);
       k3p_publish(&flags[0], S + x + 1u);
       coop_load_asm(G, Q, min(x + (uint32_t)SETS, nst - 1u), t, ngr);
     };
@@ -1523,7 +1570,10 @@ __device__ __forceinline__ uint32_t k3p_produce(uint8_t* wl, uint32_t* flags, ui
     // stage x goes to LDS half x & 1 once stage x - 2 is freed (flags[1] >= S + x - 1)
     auto put = [&](uint32_t x, u32x4 (&G)[16]) {
       k3p_wait_ge(&flags[1], x < 2u ? S : S + x - 1u);
-      coop_write<16>(wl, wr, (S + x) & 1u, G);
+      if constexpr (XT)
+        coop_write_k(wl, wr, (S + x) & 1u, G, kc);
+      else
+        coop_write<16>(wl, wr, (S + x) & 1u, G);
       k3p_publish(&flags[0], S + x + 1u);
       coop_load<16>(G, Q, min(x + 3u, nst - 1u), t, ngr);
     };
@@ -1536,12 +1586,18 @@ __device__ __forceinline__ uint32_t k3p_produce(uint8_t* wl, uint32_t* flags, ui
   }
   for (uint32_t s = 0; s < nst; s += 2u) {
     k3p_wait_ge(&flags[1], s < 2u ? S : S + s - 1u);
-    coop_write<16>(wl, wr, (S + s) & 1u, GA);
+    if constexpr (XT)
+      coop_write_k(wl, wr, (S + s) & 1u, GA, kc);
+    else
+      coop_write<16>(wl, wr, (S + s) & 1u, GA);
     k3p_publish(&flags[0], S + s + 1u);
     coop_load<16>(GA, Q, min(s + 2u, nst - 1u), t, ngr);
     if (s + 1u < nst) {
       k3p_wait_ge(&flags[1], s + 1u < 2u ? S : S + s);
-      coop_write<16>(wl, wr, (S + s + 1u) & 1u, GB);
+      if constexpr (XT)
+        coop_write_k(wl, wr, (S + s + 1u) & 1u, GB, kc);
+      else
+        coop_write<16>(wl, wr, (S + s + 1u) & 1u, GB);
       k3p_publish(&flags[0], S + s + 2u);
       coop_load<16>(GB, Q, min(s + 3u, nst - 1u), t, ngr);
     }
@@ -1708,7 +1764,7 @@ __device__ __forceinline__ void k3q_push(uint32_t* __restrict__ qc, uint64_t* __
 // The producer wave of pair `flags`: the same groups as its MD5 wave; for a
 // group on the cooperative path (R >= kCoopMinBudget), the stages of blocks
 // next+1 .. next+R-1 of its 64 chains, SETS register sets in flight.
-template <int SETS, bool HAND = false>
+template <int SETS, bool HAND = false, bool XT = false>
 __device__ void k3p_producer(uint8_t* wl, uint32_t* flags, const OrderEntry* __restrict__ order,
                              const uint32_t* __restrict__ n_order, uint32_t budget, uint32_t g0, uint32_t nwaves) {
   const uint32_t n_total = *n_order;
@@ -1717,7 +1773,7 @@ __device__ void k3p_producer(uint8_t* wl, uint32_t* flags, const OrderEntry* __r
   for (uint32_t g = g0; g < groups; g += nwaves) {
     const K3Group G = k3_group(order, n_total, g, budget);
     if (G.R < kCoopMinBudget) continue;  // wave-uniform: the MD5 wave takes the lane path
-    S += k3p_produce<SETS, HAND>(wl, flags, S, G.src + 64ull * (G.next + 1u) - 8ull, G.R - 1u);  // from block next+1
+    S += k3p_produce<SETS, HAND, XT>(wl, flags, S, G.src + 64ull * (G.next + 1u) - 8ull, G.R - 1u);  // from block next+1
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (clamped re-reads of the last stage)
 }
@@ -1753,7 +1809,7 @@ struct K3Queue {
   uint32_t tag, parts;
   uint32_t* err;
 };
-template <bool PROD, bool ITEMS = false>
+template <bool PROD, bool ITEMS = false, bool XT = false>
 __device__ __forceinline__ void k3_body(
     uint8_t* wl, const OrderEntry* __restrict__ order, const uint32_t* __restrict__ n_order, uint32_t budget,
     uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last, uint64_t* __restrict__ tslot,
@@ -1824,7 +1880,7 @@ __device__ __forceinline__ void k3_body(
         pmax = wave_max_all(cnt);
       }
       if constexpr (PROD) {  // stages from the producer wave; the group's last is freed at its end
-        k3p_consume(wl, flags, S, R - 1u, h, polls, spin);
+        k3p_consume<XT>(wl, flags, S, R - 1u, h, polls, spin);
         S += (4u * (R - 1u) + 15u) / 16u;
       } else {
         md5_coop<16>(wl, src, h, L.next + 1u, R - 1u);
@@ -1932,8 +1988,10 @@ extern "C" __global__ __launch_bounds__(kK3PThreads, 1) void hbx_k3p_block_md5(
     uint64_t* __restrict__ probe, uint32_t psets) {
   // psets: producer register sets (2 or 3) | 0x100 for the spinning stage wait
   // | 0x200 for the hand-counted producer loads (k3p_produce HAND)
+  // | 0x400 for round 1's constants added by the producer (XT)
   const bool spin = (psets & 0x100u) != 0u;
   const bool hand = (psets & 0x200u) != 0u;
+  const bool xt = (psets & 0x400u) != 0u && !hand;  // (the hand-counted producer has no XT form)
   psets &= 0xffu;
   __shared__ __attribute__((aligned(16))) uint8_t k3_lds[4][kK3WaveLds];
   __shared__ uint32_t k3_flags[4][2];
@@ -1942,8 +2000,12 @@ extern "C" __global__ __launch_bounds__(kK3PThreads, 1) void hbx_k3p_block_md5(
   if (threadIdx.x < 8u) k3_flags[threadIdx.x >> 1][threadIdx.x & 1u] = 0u;
   __syncthreads();
   if (wave < 4u) {
-    k3_body<true>(k3_lds[pair], order, n_order, budget, started, t_first, t_last, tslot, probe, k3_flags[pair],
-                  K3Queue{}, spin);
+    if (xt)
+      k3_body<true, false, true>(k3_lds[pair], order, n_order, budget, started, t_first, t_last, tslot, probe,
+                                 k3_flags[pair], K3Queue{}, spin);
+    else
+      k3_body<true>(k3_lds[pair], order, n_order, budget, started, t_first, t_last, tslot, probe, k3_flags[pair],
+                    K3Queue{}, spin);
   } else {
     __builtin_amdgcn_s_setprio(2);
     const uint32_t g0 = blockIdx.x * 4u + pair, nw = gridDim.x * 4u;
@@ -1952,6 +2014,11 @@ extern "C" __global__ __launch_bounds__(kK3PThreads, 1) void hbx_k3p_block_md5(
         k3p_producer<3, true>(k3_lds[pair], k3_flags[pair], order, n_order, budget, g0, nw);
       else
         k3p_producer<2, true>(k3_lds[pair], k3_flags[pair], order, n_order, budget, g0, nw);
+    } else if (xt) {
+      if (psets == 3u)
+        k3p_producer<3, false, true>(k3_lds[pair], k3_flags[pair], order, n_order, budget, g0, nw);
+      else
+        k3p_producer<2, false, true>(k3_lds[pair], k3_flags[pair], order, n_order, budget, g0, nw);
     } else if (psets == 3u) {
       k3p_producer<3>(k3_lds[pair], k3_flags[pair], order, n_order, budget, g0, nw);
     } else {
