@@ -720,11 +720,12 @@ __device__ __forceinline__ uint32_t xad(uint32_t b, uint32_t cd, uint32_t t1) { 
   }
 
 // Round 1's additive constants (RFC 1321 T[1..16]): with XT the message words
-// arrive with them already added (x_j + T_j, written by K3P's producer wave
-// through LDS atomics, k3p_produce), so a round-1 step is F -> add3(a, F,
-// x_j + T_j) -> rotate -> add, one VALU fewer, and the later rounds, which
-// read x_j again, add T_k - T_j instead of T_k (folded constants): 16 of the
-// block's 320 VALU leave the MD5 wave's stream (round 6, HBX_K3_XT).
+// arrive with them already added (x_j + T_j, added by K3P's producer wave,
+// k3p_produce XT), so a round-1 step is F -> add3(a, F, x_j + T_j) -> rotate
+// -> add, one VALU fewer, and the later rounds, which read x_j again, add
+// T_k - T_j instead of T_k (folded constants): 16 of the block's 320 VALU
+// leave the MD5 wave's stream (round 6, HBX_K3_XT=1, A/B only: measured
+// slower, see hbx_engine.hip k3_xt).
 constexpr uint32_t kR1[16] = {0xd76aa478u, 0xe8c7b756u, 0x242070dbu, 0xc1bdceeeu, 0xf57c0fafu, 0x4787c62au,
                               0xa8304613u, 0xfd469501u, 0x698098d8u, 0x8b44f7afu, 0xffff5bb1u, 0x895cd7beu,
                               0x6b901122u, 0xfd987193u, 0xa679438eu, 0x49b40821u};
