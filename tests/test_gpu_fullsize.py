@@ -1,12 +1,12 @@
 """GPU: the benchmark's operating point, bit-exact.  configs[1] (64 x 128 MiB
 random per batch) and a Zipf-duplicated 8 GiB corpus (configs[3] scheme, ~50 %
 repeats) run through exactly bench.py's pipelined schedule — hbx_reserve, the
-slice sized for 33 resident batches with the default join lag 2 and lead 3
-(4,370 blocks per chain per launch; K3P and plan mode 3, the engine's
-defaults), fill to 33 in flight, then collect-one/submit-one — and every
+slice sized for 33 resident batches with the default join lag 2 and lead 2
+(4,229 blocks per chain per launch; K3P and plan mode 3, the engine's
+defaults), fill to 33 in flight, then submit-one/collect-one — and every
 file of every collected batch is compared with the oracle's literal
-storeFile loop (store.go:111-196) on all host cores; configs[1] also at join
-lag 1, lead 2 (4,229 blocks).  In-flight batches share three read-only
+storeFile loop (store.go:111-196) on all host cores; configs[1] also at lead
+3 (round 5's default, 4,370 blocks) and at join lag 1, lead 2.  In-flight batches share three read-only
 arenas, so the exact steady-state schedule runs in 24 GiB of HBM."""
 import os
 from collections import deque
@@ -36,24 +36,32 @@ def _oracle_of(oracle, arena, offs, lens):
     return refs
 
 
-def _run_schedule(arenas, offs, lens, steps, R=33, lag=2):
-    """bench.py's steady(): R submitted before any collect, then collect the
-    oldest + submit one; drain at the end.  Returns [(arena index, results)]."""
+def _run_schedule(arenas, offs, lens, steps, R=33, lag=2, lead=None):
+    """R batches in flight, the slice for `lead` (default lag + 1): collect
+    the oldest, then submit one; with lead == lag (bench.py's default at 64
+    files since round 6) bench's own order instead: submit into the arena
+    whose batch is in its last launch (hbx_input_after_oldest), then collect.
+    Drain at the end.  Returns [(arena index, results)]."""
     import torch
     from hashbox_amd import Engine
+    lead = lag + 1 if lead is None else lead
     nfull = ((8 << 20) + 8) >> 6
-    B = -(-nfull // (R - (lag + 1)))
+    B = -(-nfull // (R - lead))
     out, order = [], deque()
     with Engine(0, md5_slice=B, join_lag=lag) as e:
         k = e.knobs()
         assert k["k3_prod"] == 1 and k["plan_mode"] == {1: 0, 2: 3}[lag], k
-        e.reserve(R + 1, len(lens), int(sum(lens)))
+        e.reserve(R + 2, len(lens), int(sum(lens)))
         for j in range(steps):
-            if len(order) >= R:
+            if len(order) >= R and lead > lag:
                 out.append((order.popleft(), e.wait()))
+            elif len(order) >= R:
+                e.input_after_oldest()
             i = j % len(arenas)
             e.submit_device(arenas[i].data_ptr(), offs, lens)
             order.append(i)
+            if len(order) > R:
+                out.append((order.popleft(), e.wait()))
         torch.cuda.synchronize()  # every launch so far is complete and counted
         ms, n = e.stage_totals()
         while order:
@@ -77,15 +85,16 @@ def _check(results, refs):
             assert g.content_type == (3 if r.n_chunks > 1 else 2)
 
 
-@pytest.mark.parametrize("lag", [2, 1])
-def test_configs1_full_size_steady_state(oracle, lag):
+@pytest.mark.parametrize("lag,lead", [(2, 2), (2, 3), (1, 2)])
+def test_configs1_full_size_steady_state(oracle, lag, lead):
+    """(2, 2) is bench.py's default schedule at 64 files (4,229 blocks)."""
     import torch
     import workloads as W
     lens = [128 << 20] * 64
     offs, total = W.pack_layout(lens)
     arenas = W.random_arenas(3, total, 1000, torch.device("cuda", 0))
     refs = [_oracle_of(oracle, a, offs, lens) for a in arenas]
-    results = _run_schedule(arenas, offs, lens, steps=40, lag=lag)
+    results = _run_schedule(arenas, offs, lens, steps=40, lag=lag, lead=lead)
     assert len(results) == 40
     _check(results, refs)
     del arenas
@@ -101,7 +110,7 @@ def test_zipf_full_size_steady_state(oracle):
     rep = W.zipf_fill(arenas, int(offs[-1]) + lens[-1], seed=4)
     assert 0.4 < rep < 0.6, rep
     refs = [_oracle_of(oracle, arenas[0], offs, lens)]
-    results = _run_schedule(arenas, offs, lens, steps=36)
+    results = _run_schedule(arenas, offs, lens, steps=36, lead=2)
     _check(results, refs)
     del arenas
     torch.cuda.empty_cache()
