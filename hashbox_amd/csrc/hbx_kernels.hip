@@ -342,7 +342,11 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_d
   for (int k = 0; k < 16; k++) out[k] = 0u;
   if (q0 != 0) load_run64(make_rsrc_u(fb + q0 - kMinBlock, kMinBlock), e_l, 0u, out);
   K1State st = k1_prime(out, q0 == 0, wtot, w, l, e_l);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // vmcnt(0) through the builtin, which the compiler's wait pass sees (an asm
+  // one it does not): with the asm form it added its own vmcnt(0) after the
+  // first two iterations' DMA, so every tile's first iteration waited for
+  // both (round 6, tests/test_isa.py)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt/lgkmcnt not waited
 
   issue(0u, lds0);
   issue(1u, lds1);  // past the tile end: out-of-range reads land zeros, never read
