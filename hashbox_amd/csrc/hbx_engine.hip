@@ -229,6 +229,11 @@ struct hbx_ctx {
   // events instead of marker packets around it (HBX_K1_EXT=0: markers)
   uint32_t k1_ext = 1;
   uint32_t k1_dma4 = 1;
+  // K1's first two DMA iterations issued before the halo's loads (HBX_K1_EARLY=0:
+  // after the prime); one memory round trip per tile fewer in principle,
+  // neutral in measurement (64 files 2,328/2,329 vs 2,337/2,351, 8 files
+  // 2,075/2,082 vs 2,041/2,062 GiB/s, profiles/r06u)
+  uint32_t k1_early = 1;
   // K1D (round 6, A/B: HBX_K1D=1): tiles handed out at run time
   // (hbx_k1d_digest_scan), in decreasing length for about k1d_par workgroups
   // at once, on a grid of k1d_grid persistent workgroups.  Bit-exact, not
@@ -1190,7 +1195,7 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
     // scan loop's kernels.  They double as K1's timer and K2's dependency.
     hipExtLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3((uint32_t)nt), dim3(kK1Threads), 0, s, b->ev[0], b->ev[1], 0,
                           arena, d_off, d_len, d_sb, d_tiles, ssum.as<uint2>(), slices,
-                          c->k1_swz | (c->k1_dma4 ? 0u : 2u));
+                          c->k1_swz | (c->k1_dma4 ? 0u : 2u) | (c->k1_early ? 0u : 4u));
     HBX_TRY(c, hipGetLastError());
     c->open_t.push_back(TimedLaunch{b->ev[0], b->ev[1], 0, false});
   } else {
@@ -1202,7 +1207,7 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
                            d_tiles, (uint32_t)nt, d_k1ctr, ssum.as<uint2>(), slices);
       else
         hipLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3((uint32_t)nt), dim3(kK1Threads), 0, s, arena, d_off, d_len,
-                           d_sb, d_tiles, ssum.as<uint2>(), slices, c->k1_swz | (c->k1_dma4 ? 0u : 2u));
+                           d_sb, d_tiles, ssum.as<uint2>(), slices, c->k1_swz | (c->k1_dma4 ? 0u : 2u) | (c->k1_early ? 0u : 4u));
     }
     HBX_TRY(c, hipGetLastError());
     HBX_TRY(c, hipEventRecord(b->ev[1], s));
@@ -1580,6 +1585,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = ab_env("HBX_K1_EXT")) c->k1_ext = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K1_DMA4")) c->k1_dma4 = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K1D")) c->k1d = std::atoi(v) ? 1u : 0u;
+  if (const char* v = ab_env("HBX_K1_EARLY")) c->k1_early = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K1D_PAR")) c->k1d_par = (uint32_t)std::min(1024, std::max(1, std::atoi(v)));
   if (const char* v = ab_env("HBX_K1D_GRID")) c->k1d_grid = (uint32_t)std::min(4096, std::max(1, std::atoi(v)));
   if (const char* v = ab_env("HBX_K1_SWZ")) c->k1_swz = std::atoi(v) ? 1u : 0u;
@@ -1807,12 +1813,12 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
       "\"lean_marks\": %u, \"k3_prod\": %u, \"k3_items\": %u, \"k3_period\": %u, \"meta_kernel\": %u, "
       "\"plan_cut\": %u, \"k1_swz\": %u, \"k3_psets\": %u, \"d2h_kernel\": %u, \"k8_split_streams\": %llu, "
       "\"k8_split_fallbacks\": %llu, \"gate_meta\": %u, \"sdma_warm\": %u, \"sdma_h2d_mask\": %u, "
-      "\"sdma_d2h_mask\": %u, \"sdma_warm_ms\": %.3f, \"k3_spin\": %u, \"plan_addr\": %u, \"plan_addr_shift\": %u, \"k1_ext\": %u, \"k1_dma4\": %u, \"k3_hand\": %u, \"k3_xt\": %u, \"k1d\": %u, \"k1d_par\": %u, \"k1d_grid\": %u}",
+      "\"sdma_d2h_mask\": %u, \"sdma_warm_ms\": %.3f, \"k3_spin\": %u, \"plan_addr\": %u, \"plan_addr_shift\": %u, \"k1_ext\": %u, \"k1_dma4\": %u, \"k3_hand\": %u, \"k3_xt\": %u, \"k1_early\": %u, \"k1d\": %u, \"k1d_par\": %u, \"k1d_grid\": %u}",
       (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_gate, c->md5_wgs,
       plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks, c->k3_prod, c->k3_items,
       c->k3_period, c->meta_kernel, c->plan_cut, c->k1_swz, c->k3_psets, c->d2h_kernel,
       (unsigned long long)c->k8_split_streams, (unsigned long long)c->k8_split_fallbacks, c->gate_meta,
-      c->sdma_warm, c->sdma_h2d, c->sdma_d2h, c->sdma_warm_ms, c->k3_spin, c->plan_addr, c->plan_addr_shift, c->k1_ext, c->k1_dma4, c->k3_hand, c->k3_xt, c->k1d, c->k1d_par, c->k1d_grid);
+      c->sdma_warm, c->sdma_h2d, c->sdma_d2h, c->sdma_warm_ms, c->k3_spin, c->plan_addr, c->plan_addr_shift, c->k1_ext, c->k1_dma4, c->k3_hand, c->k3_xt, c->k1_early, c->k1d, c->k1d_par, c->k1d_grid);
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }
 

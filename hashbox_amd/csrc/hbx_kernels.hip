@@ -278,8 +278,10 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_d
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
     const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ slice_base,
     const uint4* __restrict__ tiles, uint2* __restrict__ ssum, uint64_t dummy, uint32_t swz) {
-  // swz bit 1 (HBX_K1_DMA4=0, A/B): one statement per piece instead of dma16x4
+  // swz bit 1 (HBX_K1_DMA4=0, A/B): one statement per piece instead of dma16x4;
+  // bit 2 (HBX_K1_EARLY=0, A/B): the first DMA after the halo's loads
   const bool dma4 = !(swz & 2u);
+  const bool early = !(swz & 4u);
   swz &= 1u;
   __shared__ uint2 wtot[2][16];
   __shared__ __attribute__((aligned(1024))) uint8_t land[kK1Threads / 64][2][kDmaSlot];
@@ -337,6 +339,14 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_d
     }
   };
 
+  // the first two iterations' DMA goes out before the halo's loads, so their
+  // latency and the halo's overlap (round 6: one memory round trip per tile
+  // fewer; loads complete in order, so the wait for the halo inside k1_prime
+  // lands the DMA too)
+  if (early) {
+    issue(0u, lds0);
+    issue(1u, lds1);  // past the tile end: out-of-range reads land zeros, never read
+  }
   uint32_t out[16];
 #pragma unroll
   for (int k = 0; k < 16; k++) out[k] = 0u;
@@ -346,10 +356,11 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_d
   // one it does not): with the asm form it added its own vmcnt(0) after the
   // first two iterations' DMA, so every tile's first iteration waited for
   // both (round 6, tests/test_isa.py)
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt/lgkmcnt not waited
-
-  issue(0u, lds0);
-  issue(1u, lds1);  // past the tile end: out-of-range reads land zeros, never read
+  if (!early) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt/lgkmcnt not waited
+    issue(0u, lds0);
+    issue(1u, lds1);
+  }
   // two register sets swap roles each iteration (this run / the run MIN
   // earlier), so no 16-register copy per iteration
   uint32_t run_b[16];
