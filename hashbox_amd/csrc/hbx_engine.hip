@@ -225,6 +225,12 @@ struct hbx_ctx {
   // 2^plan_addr_shift bytes (plan_bin; HBX_PLAN_ADDR=0..512, 0 = by count
   // only as before round 6; HBX_PLAN_ADDR_SHIFT=20..40)
   uint32_t plan_addr = 512, plan_addr_shift = 29;
+  // HBX_PLAN_NEAR=n (A/B): chains in their last launch with >= (1 - n/64) of
+  // the slice left go to the address bins too.  Bit-exact, slower: n = 8
+  // 2,213-2,280 vs 2,298-2,324 GiB/s, n = 16 1,991 (profiles/r06x): the
+  // full-slice waves that take one pay a self-staged remainder round, and
+  // the launch tail grows (launch overhead 1.08-1.23)
+  uint32_t plan_near = 0;
   // K1 launched with its batch's ev[0]/ev[1] as hipExtLaunchKernel start/stop
   // events instead of marker packets around it (HBX_K1_EXT=0: markers)
   uint32_t k1_ext = 1;
@@ -730,7 +736,7 @@ int plan_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
                            has_prev ? c->d_order[ps].as<OrderEntry>() : nullptr,
                            has_prev ? c->d_octl[ps].as<uint32_t>() : nullptr, c->last_budget,
                            fs, budget, c->d_order[slot].as<OrderEntry>(), c->d_octl[slot].as<uint32_t>(),
-                           c->d_plan.as<uint32_t>(), phase | (c->plan_addr << 8) | (c->plan_addr_shift << 24));
+                           c->d_plan.as<uint32_t>(), phase | (c->plan_near << 1) | (c->plan_addr << 8) | (c->plan_addr_shift << 24));
       HBX_TRY(c, hipGetLastError());
       HBX_TRY(c, hipEventRecord(t.b, s));
       // K3 waits on the timing end itself; the pair is queued for harvest
@@ -758,7 +764,7 @@ int plan_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
                          has_prev ? c->d_order[ps].as<OrderEntry>() : nullptr,
                          has_prev ? c->d_octl[ps].as<uint32_t>() : nullptr, c->last_budget,
                          fs, budget, c->d_order[slot].as<OrderEntry>(), c->d_octl[slot].as<uint32_t>(),
-                         c->d_plan.as<uint32_t>(), phase | (c->plan_addr << 8) | (c->plan_addr_shift << 24));
+                         c->d_plan.as<uint32_t>(), phase | (c->plan_near << 1) | (c->plan_addr << 8) | (c->plan_addr_shift << 24));
   }
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(c->plan_done[slot], s));
@@ -1581,6 +1587,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = ab_env("HBX_K3_XT")) c->k3_xt = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_SPIN")) c->k3_spin = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_PLAN_ADDR")) c->plan_addr = (uint32_t)std::min(512, std::max(0, std::atoi(v)));
+  if (const char* v = ab_env("HBX_PLAN_NEAR")) c->plan_near = (uint32_t)std::min(64, std::max(0, std::atoi(v)));
   if (const char* v = ab_env("HBX_PLAN_ADDR_SHIFT")) c->plan_addr_shift = (uint32_t)std::min(40, std::max(20, std::atoi(v)));
   if (const char* v = ab_env("HBX_K1_EXT")) c->k1_ext = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K1_DMA4")) c->k1_dma4 = std::atoi(v) ? 1u : 0u;
@@ -1813,12 +1820,12 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
       "\"lean_marks\": %u, \"k3_prod\": %u, \"k3_items\": %u, \"k3_period\": %u, \"meta_kernel\": %u, "
       "\"plan_cut\": %u, \"k1_swz\": %u, \"k3_psets\": %u, \"d2h_kernel\": %u, \"k8_split_streams\": %llu, "
       "\"k8_split_fallbacks\": %llu, \"gate_meta\": %u, \"sdma_warm\": %u, \"sdma_h2d_mask\": %u, "
-      "\"sdma_d2h_mask\": %u, \"sdma_warm_ms\": %.3f, \"k3_spin\": %u, \"plan_addr\": %u, \"plan_addr_shift\": %u, \"k1_ext\": %u, \"k1_dma4\": %u, \"k3_hand\": %u, \"k3_xt\": %u, \"k1_early\": %u, \"k1d\": %u, \"k1d_par\": %u, \"k1d_grid\": %u}",
+      "\"sdma_d2h_mask\": %u, \"sdma_warm_ms\": %.3f, \"k3_spin\": %u, \"plan_addr\": %u, \"plan_addr_shift\": %u, \"plan_near\": %u, \"k1_ext\": %u, \"k1_dma4\": %u, \"k3_hand\": %u, \"k3_xt\": %u, \"k1_early\": %u, \"k1d\": %u, \"k1d_par\": %u, \"k1d_grid\": %u}",
       (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_gate, c->md5_wgs,
       plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks, c->k3_prod, c->k3_items,
       c->k3_period, c->meta_kernel, c->plan_cut, c->k1_swz, c->k3_psets, c->d2h_kernel,
       (unsigned long long)c->k8_split_streams, (unsigned long long)c->k8_split_fallbacks, c->gate_meta,
-      c->sdma_warm, c->sdma_h2d, c->sdma_d2h, c->sdma_warm_ms, c->k3_spin, c->plan_addr, c->plan_addr_shift, c->k1_ext, c->k1_dma4, c->k3_hand, c->k3_xt, c->k1_early, c->k1d, c->k1d_par, c->k1d_grid);
+      c->sdma_warm, c->sdma_h2d, c->sdma_d2h, c->sdma_warm_ms, c->k3_spin, c->plan_addr, c->plan_addr_shift, c->plan_near, c->k1_ext, c->k1_dma4, c->k3_hand, c->k3_xt, c->k1_early, c->k1d, c->k1d_par, c->k1d_grid);
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }
 

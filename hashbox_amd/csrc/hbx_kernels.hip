@@ -1161,10 +1161,22 @@ __device__ __forceinline__ uint32_t order_bin(uint32_t cnt, uint32_t budget) {
 // launch overhead 1.084-1.089 -> 1.040-1.050, profiles/r06h); the rest by
 // descending count in bins [abins, 1024).  Every group of the full-slice
 // region still has count == budget, so the K3 walk is unchanged.
-__device__ __forceinline__ uint32_t plan_bin(const OrderEntry& o, uint32_t budget, uint32_t abins, uint32_t ashift) {
+// Near-full chains too (round 6, `near` in 64ths of the slice, HBX_PLAN_NEAR;
+// A/B only, measured slower, hbx_engine.hip plan_near):
+// a chain in its last launch with at least budget (1 - near/64) blocks left
+// goes to its address bin beside the full slices instead of a count bin.  In
+// a count bin its wave's 64 chains lie anywhere in the resident arenas, and
+// such a wave, nearly a full slice long, ended most launches last with its
+// CU's three other waves (tools/diag_slow_cu.py: 22 of 30 launches,
+// profiles/r06w); among full slices it costs its wave one self-staged round
+// of the remaining (budget - count) blocks for the other lanes.
+__device__ __forceinline__ uint32_t plan_bin(const OrderEntry& o, uint32_t budget, uint32_t abins, uint32_t ashift,
+                                             uint32_t near = 0u) {
   const uint32_t cnt = min(o.rem - 1u, budget);
   if (!abins) return order_bin(cnt, budget);
-  if (cnt == budget) return (uint32_t)((reinterpret_cast<const Chain*>(o.chain)->src >> ashift) % abins);
+  const uint64_t thr = (uint64_t)budget - (uint64_t)budget * near / 64u;
+  if (cnt == budget || (uint64_t)cnt >= thr)
+    return (uint32_t)((reinterpret_cast<const Chain*>(o.chain)->src >> ashift) % abins);
   const uint32_t ref = min(budget, (uint32_t)(kMaxBlock >> 6) + 1u);
   const uint32_t c = min(cnt, ref);
   return abins + (ref - c) * (kPlanBins - 1u - abins) / ref;
@@ -1240,7 +1252,8 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
     uint32_t* __restrict__ gh, uint32_t phase) {
   const uint32_t abins = (phase >> 8) & 0xfffu;  // address bins for full slices (plan_bin), 0 = off
   const uint32_t ashift = phase >> 24;            // their granule: 2^ashift bytes
-  phase &= 0xffu;
+  const uint32_t near = (phase >> 1) & 0x7fu;     // near-full chains to the address bins (plan_bin)
+  phase &= 1u;
   __shared__ uint32_t hist[kPlanBins], pos[kPlanBins], wsum[kPlanThreads / 64];
   const uint32_t tid = threadIdx.x;
   const uint32_t gt = blockIdx.x * kPlanThreads + tid, gn = gridDim.x * kPlanThreads;
@@ -1275,7 +1288,7 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
   __syncthreads();
   for (uint32_t e = gt; e < n_all; e += gn) {
     const OrderEntry o = entry(e);
-    if (o.rem) atomicAdd(&hist[plan_bin(o, budget, abins, ashift)], 1u);
+    if (o.rem) atomicAdd(&hist[plan_bin(o, budget, abins, ashift, near)], 1u);
   }
   __syncthreads();
   if (phase == 0u) {
@@ -1301,7 +1314,7 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
   __syncthreads();
   for (uint32_t e = gt; e < n_all; e += gn) {
     const OrderEntry o = entry(e);
-    if (o.rem) out[atomicAdd(&pos[plan_bin(o, budget, abins, ashift)], 1u)] = o;
+    if (o.rem) out[atomicAdd(&pos[plan_bin(o, budget, abins, ashift, near)], 1u)] = o;
   }
 }
 

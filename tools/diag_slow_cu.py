@@ -36,6 +36,7 @@ def main():
     eng.reserve(R + 2, len(lens), sum(lens))
     eng.set_k3_probe(True)
     count = collections.Counter()
+    slowest_partial = collections.Counter()  # is each launch's last wave a partial (R < B) group?
     rows = []
     j = 0
     for _ in range(R):
@@ -75,11 +76,15 @@ def main():
                      "slowest": [{"cu": cu[i], "end_us": round(float(end[i]), 1),
                                   "cpb": None if np.isnan(cpb[i]) else round(float(cpb[i]), 1),
                                   "ghz": None if np.isnan(ghz[i]) else round(float(ghz[i]), 3),
-                                  "polls": int(polls[i])} for i in order[:6]]})
+                                  "polls": int(polls[i]), "R": int(Rw[i]), "full": bool(full[i])}
+                                 for i in order[:6]]})
+        slowest_partial[bool(not full[order[0]])] += 1
         print(json.dumps(rows[-1]), flush=True)
     while eng.pending():
         eng.wait()
-    print(json.dumps({"cu_in_slowest8_count": {str(k): v for k, v in count.most_common(12)}}))
+    print(json.dumps({"cu_in_slowest8_count": {str(k): v for k, v in count.most_common(12)},
+                      "last_wave_partial_launches": slowest_partial[True],
+                      "last_wave_full_launches": slowest_partial[False]}))
     eng.close()
 
 
