@@ -220,6 +220,12 @@ struct hbx_ctx {
   // off-path adds (they fill its dependent chain's gaps), and the producer's
   // added work lands on the same SIMD or the same LDS path
   uint32_t k3_xt = 0;
+  // HBX_K3_PAIR=1 (A/B): K3 placement with the full-slice groups dense, then
+  // one long partial group with three short ones per workgroup (k3_slots).
+  // Bit-exact, slower at 64 files: 2,314-2,359 vs 2,385-2,406 GiB/s, launch
+  // overhead 1.09-1.13 vs 1.02-1.04 (profiles/r06y): a workgroup whose short
+  // groups are done keeps its CU from K1 while the long one runs alone
+  uint32_t k3_pair = 0;
   uint32_t k3_spin = 0;
   // full-slice chains ordered by data address in plan_addr granules of
   // 2^plan_addr_shift bytes (plan_bin; HBX_PLAN_ADDR=0..512, 0 = by count
@@ -816,7 +822,7 @@ int md5_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
     hipLaunchKernelGGL(hbx_k3p_block_md5, dim3(c->md5_wgs), dim3(kK3PThreads), 0, s,
                        c->d_order[slot].as<OrderEntry>(), static_cast<const uint32_t*>(c->d_octl[slot].as<uint32_t>()),
                        budget, c->d_gate.as<uint32_t>(), c->k3_dispatched, c->k3_waves + waves - 1u, tslot,
-                       c->h_probe.p ? c->h_probe.as<uint64_t>() : nullptr, c->k3_psets | (c->k3_spin ? 0x100u : 0u) | (c->k3_hand ? 0x200u : 0u) | (c->k3_xt ? 0x400u : 0u));
+                       c->h_probe.p ? c->h_probe.as<uint64_t>() : nullptr, c->k3_psets | (c->k3_spin ? 0x100u : 0u) | (c->k3_hand ? 0x200u : 0u) | (c->k3_xt ? 0x400u : 0u) | (c->k3_pair ? 0x800u : 0u));
   else
     hipLaunchKernelGGL(hbx_k3_block_md5, dim3(c->md5_wgs), dim3(kK3Threads), 0, s,
                        c->d_order[slot].as<OrderEntry>(), static_cast<const uint32_t*>(c->d_octl[slot].as<uint32_t>()),
@@ -1585,6 +1591,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = ab_env("HBX_K3_PSETS")) c->k3_psets = std::atoi(v) == 3 ? 3u : 2u;
   if (const char* v = ab_env("HBX_K3_HAND")) c->k3_hand = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_XT")) c->k3_xt = std::atoi(v) ? 1u : 0u;
+  if (const char* v = ab_env("HBX_K3_PAIR")) c->k3_pair = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_SPIN")) c->k3_spin = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_PLAN_ADDR")) c->plan_addr = (uint32_t)std::min(512, std::max(0, std::atoi(v)));
   if (const char* v = ab_env("HBX_PLAN_NEAR")) c->plan_near = (uint32_t)std::min(64, std::max(0, std::atoi(v)));
@@ -1820,12 +1827,12 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
       "\"lean_marks\": %u, \"k3_prod\": %u, \"k3_items\": %u, \"k3_period\": %u, \"meta_kernel\": %u, "
       "\"plan_cut\": %u, \"k1_swz\": %u, \"k3_psets\": %u, \"d2h_kernel\": %u, \"k8_split_streams\": %llu, "
       "\"k8_split_fallbacks\": %llu, \"gate_meta\": %u, \"sdma_warm\": %u, \"sdma_h2d_mask\": %u, "
-      "\"sdma_d2h_mask\": %u, \"sdma_warm_ms\": %.3f, \"k3_spin\": %u, \"plan_addr\": %u, \"plan_addr_shift\": %u, \"plan_near\": %u, \"k1_ext\": %u, \"k1_dma4\": %u, \"k3_hand\": %u, \"k3_xt\": %u, \"k1_early\": %u, \"k1d\": %u, \"k1d_par\": %u, \"k1d_grid\": %u}",
+      "\"sdma_d2h_mask\": %u, \"sdma_warm_ms\": %.3f, \"k3_spin\": %u, \"plan_addr\": %u, \"plan_addr_shift\": %u, \"plan_near\": %u, \"k1_ext\": %u, \"k1_dma4\": %u, \"k3_hand\": %u, \"k3_xt\": %u, \"k3_pair\": %u, \"k1_early\": %u, \"k1d\": %u, \"k1d_par\": %u, \"k1d_grid\": %u}",
       (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_gate, c->md5_wgs,
       plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks, c->k3_prod, c->k3_items,
       c->k3_period, c->meta_kernel, c->plan_cut, c->k1_swz, c->k3_psets, c->d2h_kernel,
       (unsigned long long)c->k8_split_streams, (unsigned long long)c->k8_split_fallbacks, c->gate_meta,
-      c->sdma_warm, c->sdma_h2d, c->sdma_d2h, c->sdma_warm_ms, c->k3_spin, c->plan_addr, c->plan_addr_shift, c->plan_near, c->k1_ext, c->k1_dma4, c->k3_hand, c->k3_xt, c->k1_early, c->k1d, c->k1d_par, c->k1d_grid);
+      c->sdma_warm, c->sdma_h2d, c->sdma_d2h, c->sdma_warm_ms, c->k3_spin, c->plan_addr, c->plan_addr_shift, c->plan_near, c->k1_ext, c->k1_dma4, c->k3_hand, c->k3_xt, c->k3_pair, c->k1_early, c->k1d, c->k1d_par, c->k1d_grid);
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }
 

@@ -1309,7 +1309,10 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
       *n_out = before + inc;
       n_out[1] = 0u;  // K3Q's item queue head and tail for this order slot
       n_out[2] = 0u;
+      if (!abins) n_out[3] = 0xFFFFFFFFu;  // no address bins: K3 places groups densely (k3_slots)
     }
+    // entries in the address (full-slice) bins, for K3's placement (k3_slots)
+    if (blockIdx.x == 0 && abins && tid == abins) n_out[3] = before + inc - v;
   }
   __syncthreads();
   for (uint32_t e = gt; e < n_all; e += gn) {
@@ -1793,13 +1796,53 @@ __device__ __forceinline__ void k3q_push(uint32_t* __restrict__ qc, uint64_t* __
 // The producer wave of pair `flags`: the same groups as its MD5 wave; for a
 // group on the cooperative path (R >= kCoopMinBudget), the stages of blocks
 // next+1 .. next+R-1 of its 64 chains, SETS register sets in flight.
+// Placement of the groups on the waves (round 6, K3 `pair`, HBX_K3_PAIR=1;
+// A/B only, measured slower, hbx_engine.hip k3_pair; default dense).  The groups come in the planner's order: the full slices (address
+// bins) first, then the partial ones (chains in their last launch) by
+// descending count.  A partial group's 64 chains lie anywhere in the resident
+// arenas, and the longest of them ended most launches last, together with
+// their CU's other waves (tools/diag_slow_cu.py, profiles/r06w).  So the full
+// slices fill whole workgroups densely, as before, and each workgroup after
+// them pairs one long partial group with three of the shortest: those finish
+// early and leave the long one the CU's memory path.  Wave slot v of the
+// launch (blockIdx * 4 + wave, then + nwaves ...) takes group
+// k3_slot_group(v); a hole takes none.  Any slot map that is a bijection onto
+// the groups gives the same results.
+constexpr uint32_t kNoGroup = 0xFFFFFFFFu;
+struct K3Slots {
+  uint32_t F, F4, P, K, S;  // full groups, padded to a workgroup; partial groups, their workgroups; slots
+};
+__device__ __forceinline__ K3Slots k3_slots(uint32_t groups, uint32_t nfull_entries, bool pair) {
+  K3Slots s;
+  s.F = pair ? min(nfull_entries / 64u, groups) : groups;
+  s.F4 = pair ? (s.F + 3u) & ~3u : s.F;
+  s.P = groups - s.F;
+  s.K = (s.P + 3u) / 4u;
+  s.S = s.F4 + 4u * s.K;
+  return s;
+}
+__device__ __forceinline__ uint32_t k3_slot_group(const K3Slots& s, uint32_t v) {
+  if (v < s.F) return v;
+  if (v < s.F4) return kNoGroup;
+  const uint32_t k = (v - s.F4) >> 2, j = (v - s.F4) & 3u;
+  if (j == 0u) return s.F + k;          // the k-th longest partial group
+  const uint32_t d = 3u * k + (j - 1u);  // the d-th shortest
+  if (d >= s.P) return kNoGroup;
+  const uint32_t q = s.P - 1u - d;
+  return q >= s.K ? s.F + q : kNoGroup;
+}
+
 template <int SETS, bool HAND = false, bool XT = false>
 __device__ void k3p_producer(uint8_t* wl, uint32_t* flags, const OrderEntry* __restrict__ order,
-                             const uint32_t* __restrict__ n_order, uint32_t budget, uint32_t g0, uint32_t nwaves) {
+                             const uint32_t* __restrict__ n_order, uint32_t budget, uint32_t g0, uint32_t nwaves,
+                             bool pair = false) {
   const uint32_t n_total = *n_order;
   const uint32_t groups = (n_total + 63u) / 64u;
+  const K3Slots sl = k3_slots(groups, n_order[3], pair);
   uint32_t S = 0;  // stages of this launch so far
-  for (uint32_t g = g0; g < groups; g += nwaves) {
+  for (uint32_t v = g0; v < sl.S; v += nwaves) {
+    const uint32_t g = k3_slot_group(sl, v);
+    if (g == kNoGroup) continue;
     const K3Group G = k3_group(order, n_total, g, budget);
     if (G.R < kCoopMinBudget) continue;  // wave-uniform: the MD5 wave takes the lane path
     S += k3p_produce<SETS, HAND, XT>(wl, flags, S, G.src + 64ull * (G.next + 1u) - 8ull, G.R - 1u);  // from block next+1
@@ -1842,7 +1885,8 @@ template <bool PROD, bool ITEMS = false, bool XT = false>
 __device__ __forceinline__ void k3_body(
     uint8_t* wl, const OrderEntry* __restrict__ order, const uint32_t* __restrict__ n_order, uint32_t budget,
     uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last, uint64_t* __restrict__ tslot,
-    uint64_t* __restrict__ probe, uint32_t* flags = nullptr, K3Queue Q = K3Queue{}, bool spin = false) {
+    uint64_t* __restrict__ probe, uint32_t* flags = nullptr, K3Queue Q = K3Queue{}, bool spin = false,
+    bool pair = false) {
   static_assert(PROD || !ITEMS, "items need the producer waves");
   // the MD5 chains are issue-bound: win the SIMD's issue arbitration against
   // co-resident waves of other kernels
@@ -1880,8 +1924,9 @@ __device__ __forceinline__ void k3_body(
   uint32_t seq = 0;  // ITEMS: items announced to the producer
   uint32_t polls = 0;  // PROD: polls that found the producer's stage not yet written
   bool first = true;
-  for (uint32_t g = g0;; g += nwaves) {
-    uint32_t part = 0u, item = 0u;
+  const K3Slots sl = k3_slots(groups, ITEMS ? kNoGroup : n_order[3], pair && !ITEMS);
+  for (uint32_t v = g0;; v += nwaves) {
+    uint32_t part = 0u, item = 0u, g = v;
     if constexpr (ITEMS) {
       item = g0 < groups ? k3q_pop(Q.qc, Q.q, groups, groups * Q.parts, Q.tag, Q.err) : kItemExit;
       if ((threadIdx.x & 63u) == 0u) {  // announce it to the producer (kItemExit: it stops too)
@@ -1892,7 +1937,9 @@ __device__ __forceinline__ void k3_body(
       g = item % groups;
       part = item / groups;
     } else {
-      if (g >= groups) break;
+      if (v >= sl.S) break;
+      g = k3_slot_group(sl, v);
+      if (g == kNoGroup) continue;
     }
     K3Lane L = k3_lane<ITEMS>(order, n_total, g, part, budget, per_part);
     uint32_t(&h)[4] = L.h;
@@ -2021,37 +2068,38 @@ extern "C" __global__ __launch_bounds__(kK3PThreads, 1) void hbx_k3p_block_md5(
   const bool spin = (psets & 0x100u) != 0u;
   const bool hand = (psets & 0x200u) != 0u;
   const bool xt = (psets & 0x400u) != 0u && !hand;  // (the hand-counted producer has no XT form)
+  const bool pairing = (psets & 0x800u) != 0u;      // long/short partial groups per CU (k3_slots)
   psets &= 0xffu;
   __shared__ __attribute__((aligned(16))) uint8_t k3_lds[4][kK3WaveLds];
   __shared__ uint32_t k3_flags[4][2];
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const uint32_t pair = wave & 3u;
+  const uint32_t wp = wave & 3u;  // the MD5 / producer pair
   if (threadIdx.x < 8u) k3_flags[threadIdx.x >> 1][threadIdx.x & 1u] = 0u;
   __syncthreads();
   if (wave < 4u) {
     if (xt)
-      k3_body<true, false, true>(k3_lds[pair], order, n_order, budget, started, t_first, t_last, tslot, probe,
-                                 k3_flags[pair], K3Queue{}, spin);
+      k3_body<true, false, true>(k3_lds[wp], order, n_order, budget, started, t_first, t_last, tslot, probe,
+                                 k3_flags[wp], K3Queue{}, spin, pairing);
     else
-      k3_body<true>(k3_lds[pair], order, n_order, budget, started, t_first, t_last, tslot, probe, k3_flags[pair],
-                    K3Queue{}, spin);
+      k3_body<true>(k3_lds[wp], order, n_order, budget, started, t_first, t_last, tslot, probe, k3_flags[wp],
+                    K3Queue{}, spin, pairing);
   } else {
     __builtin_amdgcn_s_setprio(2);
-    const uint32_t g0 = blockIdx.x * 4u + pair, nw = gridDim.x * 4u;
+    const uint32_t g0 = blockIdx.x * 4u + wp, nw = gridDim.x * 4u;
     if (hand) {
       if (psets == 3u)
-        k3p_producer<3, true>(k3_lds[pair], k3_flags[pair], order, n_order, budget, g0, nw);
+        k3p_producer<3, true>(k3_lds[wp], k3_flags[wp], order, n_order, budget, g0, nw, pairing);
       else
-        k3p_producer<2, true>(k3_lds[pair], k3_flags[pair], order, n_order, budget, g0, nw);
+        k3p_producer<2, true>(k3_lds[wp], k3_flags[wp], order, n_order, budget, g0, nw, pairing);
     } else if (xt) {
       if (psets == 3u)
-        k3p_producer<3, false, true>(k3_lds[pair], k3_flags[pair], order, n_order, budget, g0, nw);
+        k3p_producer<3, false, true>(k3_lds[wp], k3_flags[wp], order, n_order, budget, g0, nw, pairing);
       else
-        k3p_producer<2, false, true>(k3_lds[pair], k3_flags[pair], order, n_order, budget, g0, nw);
+        k3p_producer<2, false, true>(k3_lds[wp], k3_flags[wp], order, n_order, budget, g0, nw, pairing);
     } else if (psets == 3u) {
-      k3p_producer<3>(k3_lds[pair], k3_flags[pair], order, n_order, budget, g0, nw);
+      k3p_producer<3>(k3_lds[wp], k3_flags[wp], order, n_order, budget, g0, nw, pairing);
     } else {
-      k3p_producer<2>(k3_lds[pair], k3_flags[pair], order, n_order, budget, g0, nw);
+      k3p_producer<2>(k3_lds[wp], k3_flags[wp], order, n_order, budget, g0, nw, pairing);
     }
   }
 }
