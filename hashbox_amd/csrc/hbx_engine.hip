@@ -206,55 +206,20 @@ struct hbx_ctx {
   // hidden) 2,297-2,318 vs 2,286-2,308 GiB/s in three alternating pairs at 64
   // files, equal at 8 (profiles/r05af); HBX_K3_PSETS=2 for A/B
   uint32_t k3_psets = 3;
-  // HBX_K3_HAND=1 (A/B): the producer's loads as inline asm with hand-counted
-  // waits (the compiler waits for all three register sets at every third
-  // stage); bit-exact but no faster: 2,251/2,254 vs 2,275/2,339 GiB/s, 8 files
-  // 2,077 vs 2,122 (profiles/r06j), so the producer's lead is not what stalls
-  // the MD5 wave
-  uint32_t k3_hand = 0;
-  // HBX_K3_XT=1 (A/B): round 1's constants added to the staged words by K3P's
-  // producer wave, 16 VALU per block off the MD5 wave.  Bit-exact, slower:
-  // 1,518-1,520 vs 1,454-1,459 cycles per block with the adds in the
-  // producer's registers or as LDS atomics alike, 2,349-2,353 vs 2,380-2,382
-  // GiB/s (profiles/r06q, r06r): the MD5 wave is not held by its own
-  // off-path adds (they fill its dependent chain's gaps), and the producer's
-  // added work lands on the same SIMD or the same LDS path
-  uint32_t k3_xt = 0;
-  // HBX_K3_PAIR=1 (A/B): K3 placement with the full-slice groups dense, then
-  // one long partial group with three short ones per workgroup (k3_slots).
-  // Bit-exact, slower at 64 files: 2,314-2,359 vs 2,385-2,406 GiB/s, launch
-  // overhead 1.09-1.13 vs 1.02-1.04 (profiles/r06y): a workgroup whose short
-  // groups are done keeps its CU from K1 while the long one runs alone
-  uint32_t k3_pair = 0;
   uint32_t k3_spin = 0;
   // full-slice chains ordered by data address in plan_addr granules of
   // 2^plan_addr_shift bytes (plan_bin; HBX_PLAN_ADDR=0..512, 0 = by count
   // only as before round 6; HBX_PLAN_ADDR_SHIFT=20..40)
   uint32_t plan_addr = 512, plan_addr_shift = 29;
-  // HBX_PLAN_NEAR=n (A/B): chains in their last launch with >= (1 - n/64) of
-  // the slice left go to the address bins too.  Bit-exact, slower: n = 8
-  // 2,213-2,280 vs 2,298-2,324 GiB/s, n = 16 1,991 (profiles/r06x): the
-  // full-slice waves that take one pay a self-staged remainder round, and
-  // the launch tail grows (launch overhead 1.08-1.23)
-  uint32_t plan_near = 0;
   // K1 launched with its batch's ev[0]/ev[1] as hipExtLaunchKernel start/stop
   // events instead of marker packets around it (HBX_K1_EXT=0: markers)
   uint32_t k1_ext = 1;
-  uint32_t k1_dma4 = 1;
+  uint32_t k1_dma4 = 1;  // K1's four LDS-DMA pieces in one statement (HBX_K1_DMA4=0: one per piece)
   // K1's first two DMA iterations issued before the halo's loads (HBX_K1_EARLY=0:
   // after the prime); one memory round trip per tile fewer in principle,
   // neutral in measurement (64 files 2,328/2,329 vs 2,337/2,351, 8 files
   // 2,075/2,082 vs 2,041/2,062 GiB/s, profiles/r06u)
   uint32_t k1_early = 1;
-  // K1D (round 6, A/B: HBX_K1D=1): tiles handed out at run time
-  // (hbx_k1d_digest_scan), in decreasing length for about k1d_par workgroups
-  // at once, on a grid of k1d_grid persistent workgroups.  Bit-exact, not
-  // faster: 64 files 2,259-2,338 vs 2,310-2,344 GiB/s, 8 files 1,898-2,042
-  // vs 2,057-2,099 (profiles/r06k, r06l): the persistent workgroups hold
-  // every CU K3 leaves, so the cut and result streams' small kernels wait for
-  // the whole K1 (the plan of the next K3 launch among them), and each tile's
-  // halo unit costs what the shorter tail saves
-  uint32_t k1d = 0, k1d_par = 128, k1d_grid = 132;  // K1's four LDS-DMA pieces in one statement (HBX_K1_DMA4=0: one per piece)  // HBX_K3_SPIN=1 (A/B): the MD5 wave re-polls a late stage without s_sleep
   // at join lag 2, preplan on the cut stream (mode 3; HBX_PLAN_CUT=0: mode 1,
   // the plan on the hash stream): +2.7 % with K3P (profiles/r05e)
   // 2 (default): at lag 3 and 4 too, off the scan loop (8 files per GPU, K3
@@ -742,7 +707,7 @@ int plan_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
                            has_prev ? c->d_order[ps].as<OrderEntry>() : nullptr,
                            has_prev ? c->d_octl[ps].as<uint32_t>() : nullptr, c->last_budget,
                            fs, budget, c->d_order[slot].as<OrderEntry>(), c->d_octl[slot].as<uint32_t>(),
-                           c->d_plan.as<uint32_t>(), phase | (c->plan_near << 1) | (c->plan_addr << 8) | (c->plan_addr_shift << 24));
+                           c->d_plan.as<uint32_t>(), phase | (c->plan_addr << 8) | (c->plan_addr_shift << 24));
       HBX_TRY(c, hipGetLastError());
       HBX_TRY(c, hipEventRecord(t.b, s));
       // K3 waits on the timing end itself; the pair is queued for harvest
@@ -770,7 +735,7 @@ int plan_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
                          has_prev ? c->d_order[ps].as<OrderEntry>() : nullptr,
                          has_prev ? c->d_octl[ps].as<uint32_t>() : nullptr, c->last_budget,
                          fs, budget, c->d_order[slot].as<OrderEntry>(), c->d_octl[slot].as<uint32_t>(),
-                         c->d_plan.as<uint32_t>(), phase | (c->plan_near << 1) | (c->plan_addr << 8) | (c->plan_addr_shift << 24));
+                         c->d_plan.as<uint32_t>(), phase | (c->plan_addr << 8) | (c->plan_addr_shift << 24));
   }
   HBX_TRY(c, hipGetLastError());
   HBX_TRY(c, hipEventRecord(c->plan_done[slot], s));
@@ -822,7 +787,7 @@ int md5_launch(hbx_ctx* c, const std::vector<Batch*>& nbs, uint32_t budget) {
     hipLaunchKernelGGL(hbx_k3p_block_md5, dim3(c->md5_wgs), dim3(kK3PThreads), 0, s,
                        c->d_order[slot].as<OrderEntry>(), static_cast<const uint32_t*>(c->d_octl[slot].as<uint32_t>()),
                        budget, c->d_gate.as<uint32_t>(), c->k3_dispatched, c->k3_waves + waves - 1u, tslot,
-                       c->h_probe.p ? c->h_probe.as<uint64_t>() : nullptr, c->k3_psets | (c->k3_spin ? 0x100u : 0u) | (c->k3_hand ? 0x200u : 0u) | (c->k3_xt ? 0x400u : 0u) | (c->k3_pair ? 0x800u : 0u));
+                       c->h_probe.p ? c->h_probe.as<uint64_t>() : nullptr, c->k3_psets | (c->k3_spin ? 0x100u : 0u));
   else
     hipLaunchKernelGGL(hbx_k3_block_md5, dim3(c->md5_wgs), dim3(kK3Threads), 0, s,
                        c->d_order[slot].as<OrderEntry>(), static_cast<const uint32_t*>(c->d_octl[slot].as<uint32_t>()),
@@ -986,24 +951,6 @@ void k1_tiles(hbx_ctx* c, uint32_t f, uint32_t iters, uint32_t tile) {
 
 constexpr uint32_t kTileItersMin = 16, kTileItersMax = 256;
 
-// K1D's tiles of one file (guided): each about the iterations still left over
-// twice the workgroups that run at once (c->k1d_par), 4..256, so the last ones
-// are short; never a piece under 3 iterations (the kernel claims the next
-// tile three units before the end of the current one).  `left` counts down
-// over the batch.
-constexpr uint32_t kK1dTileMin = 4, kK1dPieceMin = 3;
-void k1d_tiles(hbx_ctx* c, uint32_t f, uint32_t iters, uint64_t& left) {
-  const uint64_t two_g = 2ull * c->k1d_par;
-  for (uint32_t i = 0; i < iters;) {
-    const uint64_t want = std::min<uint64_t>(kTileItersMax, std::max<uint64_t>(kK1dTileMin, (left + two_g - 1) / two_g));
-    uint32_t take = (uint32_t)std::min<uint64_t>(want, iters - i);
-    if (iters - i - take < kK1dPieceMin) take = iters - i;
-    c->h_tiles.push_back(make_uint4(f, i, take, 0u));
-    i += take;
-    left -= take;
-  }
-}
-
 // K1 tile length for a batch of `total` iterations (c->tile_iters, or about
 // two or four tiles per CU when that is 0)
 uint32_t k1_tile_iters(const hbx_ctx* c, uint64_t total) {
@@ -1076,7 +1023,6 @@ int submit_batch_timed(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64
     total_iters += iters;
   }
   const uint32_t tile = k1_tile_iters(c, total_iters);
-  uint64_t left = total_iters;  // K1D: iterations not yet in a tile
   for (uint64_t f = 0; f < n; f++) {
     const uint64_t N = lens[f];
     longest = std::max(longest, N);
@@ -1085,10 +1031,7 @@ int submit_batch_timed(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64
     tcaps += max_chunks(N);
     if (const uint64_t iters = scan_iters(N)) {  // only files with split candidates scan
       slices += (N + kSlice - 1) / kSlice;
-      if (c->k1d)
-        k1d_tiles(c, (uint32_t)f, (uint32_t)iters, left);
-      else
-        k1_tiles(c, (uint32_t)f, (uint32_t)iters, tile);
+      k1_tiles(c, (uint32_t)f, (uint32_t)iters, tile);
     }
   }
   b->caps = tcaps;
@@ -1100,9 +1043,8 @@ int submit_batch_timed(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64
   const uint64_t lb = launch_budget(c, budget);  // a K3 period multiplies the slice
   b->need = budget == kBudgetAll ? 1u : (uint32_t)std::max<uint64_t>(1, (nfull + lb - 1) / lb);
   const uint64_t nt = c->h_tiles.size();
-  // meta block: off | len | slice_base | cut_base | tiles | K1D's tile
-  // counter (16 zero bytes, reset by the meta copy every batch)
-  const size_t meta_bytes = n * 8 * 4 + (nt + 1) * sizeof(uint4);
+  // meta block: off | len | slice_base | cut_base | tiles
+  const size_t meta_bytes = n * 8 * 4 + nt * sizeof(uint4);
   const int slot = c->ssum_slot;
   g_slow.mark(1);
   if (n) {  // every allocation first: the batch is not in the FIFO yet
@@ -1151,7 +1093,6 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   std::memcpy(hm + 2 * n, c->h_slice_base.data(), n * 8);
   std::memcpy(hm + 3 * n, b->cut_base.data(), n * 8);
   if (nt) std::memcpy(hm + 4 * n, c->h_tiles.data(), nt * sizeof(uint4));
-  std::memset(hm + 4 * n + 2 * nt, 0, sizeof(uint4));  // K1D's tile counter
   c->ssum_slot ^= 1;
   DevBuf& ssum = c->d_ssum[slot];
 
@@ -1193,14 +1134,7 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
   // after its collect, long after both completed)
   hipStream_t s2 = c->cstream;
   const bool lean = c->lean_marks && s2 == s;
-  uint32_t* d_k1ctr = reinterpret_cast<uint32_t*>(const_cast<uint4*>(d_tiles + nt));
-  const uint32_t k1_grid = c->k1d ? (uint32_t)std::min<uint64_t>(nt, c->k1d_grid) : (uint32_t)nt;
-  if (nt && c->k1d && c->k1_ext) {
-    hipExtLaunchKernelGGL(hbx_k1d_digest_scan, dim3(k1_grid), dim3(kK1Threads), 0, s, b->ev[0], b->ev[1], 0, arena,
-                          d_off, d_len, d_sb, d_tiles, (uint32_t)nt, d_k1ctr, ssum.as<uint2>(), slices);
-    HBX_TRY(c, hipGetLastError());
-    c->open_t.push_back(TimedLaunch{b->ev[0], b->ev[1], 0, false});
-  } else if (nt && c->k1_ext) {
+  if (nt && c->k1_ext) {
     // round 6: ev[0] / ev[1] bound to K1's own dispatch (hipExtLaunchKernel's
     // start and stop events), not recorded as marker packets around it: at
     // join lag >= 2 K1 had four (ev[0], its timer's pair, ev[1]) between the
@@ -1214,12 +1148,8 @@ int submit_batch_launch(hbx_ctx* c, Batch* b, const void* d_arena, uint64_t n, c
     HBX_TRY(c, hipEventRecord(b->ev[0], s));
     if (nt) {
       StageTimer t(c, s, 0, !lean);
-      if (c->k1d)
-        hipLaunchKernelGGL(hbx_k1d_digest_scan, dim3(k1_grid), dim3(kK1Threads), 0, s, arena, d_off, d_len, d_sb,
-                           d_tiles, (uint32_t)nt, d_k1ctr, ssum.as<uint2>(), slices);
-      else
-        hipLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3((uint32_t)nt), dim3(kK1Threads), 0, s, arena, d_off, d_len,
-                           d_sb, d_tiles, ssum.as<uint2>(), slices, c->k1_swz | (c->k1_dma4 ? 0u : 2u) | (c->k1_early ? 0u : 4u));
+      hipLaunchKernelGGL(hbx_k1_digest_scan_dma, dim3((uint32_t)nt), dim3(kK1Threads), 0, s, arena, d_off, d_len,
+                         d_sb, d_tiles, ssum.as<uint2>(), slices, c->k1_swz | (c->k1_dma4 ? 0u : 2u) | (c->k1_early ? 0u : 4u));
     }
     HBX_TRY(c, hipGetLastError());
     HBX_TRY(c, hipEventRecord(b->ev[1], s));
@@ -1589,19 +1519,12 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
   if (const char* v = ab_env("HBX_GATE_META")) c->gate_meta = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_SDMA_WARM")) c->sdma_warm = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_PSETS")) c->k3_psets = std::atoi(v) == 3 ? 3u : 2u;
-  if (const char* v = ab_env("HBX_K3_HAND")) c->k3_hand = std::atoi(v) ? 1u : 0u;
-  if (const char* v = ab_env("HBX_K3_XT")) c->k3_xt = std::atoi(v) ? 1u : 0u;
-  if (const char* v = ab_env("HBX_K3_PAIR")) c->k3_pair = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_SPIN")) c->k3_spin = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_PLAN_ADDR")) c->plan_addr = (uint32_t)std::min(512, std::max(0, std::atoi(v)));
-  if (const char* v = ab_env("HBX_PLAN_NEAR")) c->plan_near = (uint32_t)std::min(64, std::max(0, std::atoi(v)));
   if (const char* v = ab_env("HBX_PLAN_ADDR_SHIFT")) c->plan_addr_shift = (uint32_t)std::min(40, std::max(20, std::atoi(v)));
   if (const char* v = ab_env("HBX_K1_EXT")) c->k1_ext = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K1_DMA4")) c->k1_dma4 = std::atoi(v) ? 1u : 0u;
-  if (const char* v = ab_env("HBX_K1D")) c->k1d = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K1_EARLY")) c->k1_early = std::atoi(v) ? 1u : 0u;
-  if (const char* v = ab_env("HBX_K1D_PAR")) c->k1d_par = (uint32_t)std::min(1024, std::max(1, std::atoi(v)));
-  if (const char* v = ab_env("HBX_K1D_GRID")) c->k1d_grid = (uint32_t)std::min(4096, std::max(1, std::atoi(v)));
   if (const char* v = ab_env("HBX_K1_SWZ")) c->k1_swz = std::atoi(v) ? 1u : 0u;
   if (const char* v = ab_env("HBX_K3_ITEMS")) c->k3_items = (uint32_t)std::min(8, std::max(0, std::atoi(v)));
   // (tests: a K3 grid of a few workgroups, so every wave takes many groups)
@@ -1827,12 +1750,12 @@ int hbx_knobs(hbx_ctx* c, char* out, uint64_t cap) {
       "\"lean_marks\": %u, \"k3_prod\": %u, \"k3_items\": %u, \"k3_period\": %u, \"meta_kernel\": %u, "
       "\"plan_cut\": %u, \"k1_swz\": %u, \"k3_psets\": %u, \"d2h_kernel\": %u, \"k8_split_streams\": %llu, "
       "\"k8_split_fallbacks\": %llu, \"gate_meta\": %u, \"sdma_warm\": %u, \"sdma_h2d_mask\": %u, "
-      "\"sdma_d2h_mask\": %u, \"sdma_warm_ms\": %.3f, \"k3_spin\": %u, \"plan_addr\": %u, \"plan_addr_shift\": %u, \"plan_near\": %u, \"k1_ext\": %u, \"k1_dma4\": %u, \"k3_hand\": %u, \"k3_xt\": %u, \"k3_pair\": %u, \"k1_early\": %u, \"k1d\": %u, \"k1d_par\": %u, \"k1d_grid\": %u}",
+      "\"sdma_d2h_mask\": %u, \"sdma_warm_ms\": %.3f, \"k3_spin\": %u, \"plan_addr\": %u, \"plan_addr_shift\": %u, \"k1_ext\": %u, \"k1_dma4\": %u, \"k1_early\": %u}",
       (ab && std::atoi(ab) != 0) ? 1 : 0, c->md5_slice, c->join_lag, c->tile_iters, c->k1_gate, c->md5_wgs,
       plan_mode_of(c), c->k2_own, c->k4_window, c->h_probe.p ? 1 : 0, c->lean_marks, c->k3_prod, c->k3_items,
       c->k3_period, c->meta_kernel, c->plan_cut, c->k1_swz, c->k3_psets, c->d2h_kernel,
       (unsigned long long)c->k8_split_streams, (unsigned long long)c->k8_split_fallbacks, c->gate_meta,
-      c->sdma_warm, c->sdma_h2d, c->sdma_d2h, c->sdma_warm_ms, c->k3_spin, c->plan_addr, c->plan_addr_shift, c->plan_near, c->k1_ext, c->k1_dma4, c->k3_hand, c->k3_xt, c->k3_pair, c->k1_early, c->k1d, c->k1d_par, c->k1d_grid);
+      c->sdma_warm, c->sdma_h2d, c->sdma_d2h, c->sdma_warm_ms, c->k3_spin, c->plan_addr, c->plan_addr_shift, c->k1_ext, c->k1_dma4, c->k1_early);
   return (n > 0 && (uint64_t)n < cap) ? HBX_OK : HBX_ERR_ARG;
 }
 
@@ -1894,10 +1817,9 @@ int reserve_locked(hbx_ctx* c, uint32_t batches, uint64_t files, uint64_t bytes)
   if (!c->pending.empty()) return c->fail(HBX_ERR_STATE, "submitted batches are still pending");
   HBX_TRY(c, hipSetDevice(c->device));
   const uint64_t caps = bytes / HBX_MIN_BLOCK_SIZE + files;  // >= sum of max_chunks over the files
-  const uint64_t tmin = c->k1d ? kK1dTileMin : (c->tile_iters ? c->tile_iters : kTileItersMin);
-  const uint64_t tiles = bytes / (tmin * HBX_MIN_BLOCK_SIZE) + files;
+  const uint64_t tiles = bytes / ((uint64_t)(c->tile_iters ? c->tile_iters : kTileItersMin) * HBX_MIN_BLOCK_SIZE) + files;
   const uint64_t slices = bytes / kSlice + files;
-  const size_t meta_bytes = files * 8 * 4 + (tiles + 1) * sizeof(uint4);
+  const size_t meta_bytes = files * 8 * 4 + tiles * sizeof(uint4);
   int rc = HBX_OK;
   for (int t = 0; t < 2 && !rc; t++) rc = ensure_shared(c, c->d_ssum[t], (slices + 1) * sizeof(uint2));
   if (!rc) rc = ensure_shared(c, c->d_plan, 2 * kPlanBins * sizeof(uint32_t));

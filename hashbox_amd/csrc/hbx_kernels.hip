@@ -129,7 +129,7 @@ struct K1State {
 // virtual zeros.
 __device__ __forceinline__ K1State k1_prime(const uint32_t (&halo)[16], bool at_start,
                                             uint2 (&wtot)[2][16], uint32_t w, uint32_t l,
-                                            uint32_t e_l, uint32_t wb = 1u) {
+                                            uint32_t e_l) {
   K1State st;
   if (at_start) {
     st.pa = RunAgg{0u, 0u, 0u, 0u};
@@ -140,9 +140,9 @@ __device__ __forceinline__ K1State k1_prime(const uint32_t (&halo)[16], bool at_
   st.pa = run_aggregates(halo);
   const uint32_t iA = wave_incl_sum(st.pa.af);
   const uint32_t iC = wave_incl_sum(e_l * st.pa.af + st.pa.jf);
-  if (l == 63u) wtot[wb][w] = make_uint2(iA, iC);
+  if (l == 63u) wtot[1][w] = make_uint2(iA, iC);
   __syncthreads();
-  const uint2 t = (l < 16u) ? wtot[wb][l] : make_uint2(0u, 0u);
+  const uint2 t = (l < 16u) ? wtot[1][l] : make_uint2(0u, 0u);
   const uint32_t sA = row_incl_sum(t.x), sC = row_incl_sum(t.y);
   st.S1c = readlane(sA, 15);
   st.s2c = 0x8000u - readlane(sC, 15);  // virtual-zero start: s2 = 2^15 - sum k*x_k
@@ -388,175 +388,6 @@ extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1_digest_scan_d
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup exits
 }
 
-// ------------------------------------------------------- K1D (round 6) --
-// The same scan with the tiles handed out at run time.  hbx_k1_digest_scan_dma
-// runs one workgroup per tile, all tiles of a batch equally long, so the
-// tiles finish in whole rounds over the CUs K3 leaves free and one CU fewer
-// costs a round (the residency cliff; and at 8 files per GPU
-// 683 tiles over ~128 CUs end in a part-filled sixth round).  K1D launches
-// about as many workgroups as there are free CUs; each takes the next tile
-// from a counter (one vector atomic by thread 0), and the host lists the
-// tiles in decreasing length (guided: about the work left over twice the
-// workgroups), so the last ones are short and the CUs finish together.
-//
-// A workgroup's DMA stream runs on across its tiles: a tile is its units
-// [halo, iteration 0, .., iteration n-1], the halo being the MIN bytes before
-// the tile (or zeros at a file's start, read past the end of the descriptor)
-// that primes the rollsum state.  The next tile is claimed three units before
-// the current one ends, so its halo and first iteration are in flight while
-// the current tile's last two iterations compute: no per-tile start-up
-// latency.  Every unit issues exactly 4 DMA + 1 store per wave (the halo's
-// store goes to the dummy slot), so the hand-counted waits of the per-tile
-// kernel hold across tiles.  The claim (wave 0, lane 0): the atomic after the
-// store of unit m-4 (m = the tile's units), `vmcnt(0)` for wave 0 at unit m-3
-// (it waits early for DMA(m-2), issued a whole unit before), the index to LDS
-// before that unit's barrier, read by every wave after it; the tile's
-// descriptor comes by scalar loads, waited for by the next unit's lgkmcnt(0).
-// Tiles are at least 3 iterations (m >= 4; the host guarantees it).
-struct K1Chunk {
-  const uint8_t* fb;   // file start
-  uint64_t N, q0, sb;  // file bytes, the tile's first position, the file's slice base
-  uint32_t m;          // units: the halo + the tile's iterations
-  uint32_t hb;         // halo bytes at the descriptor's start (0 at a file's start)
-  s32x4 srd;           // [fb + q0 - hb, + hb + the tile's bytes)
-  bool valid;
-};
-__device__ __forceinline__ K1Chunk k1_chunk(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
-                                            const uint64_t* __restrict__ file_len,
-                                            const uint64_t* __restrict__ slice_base, const uint4* __restrict__ tiles,
-                                            uint32_t n_tiles, uint32_t t) {
-  K1Chunk c;
-  c.valid = t < n_tiles;
-  const uint4 td = tiles[c.valid ? t : 0u];
-  const uint32_t f = td.x;
-  c.N = file_len[f];
-  c.fb = arena + file_off[f];
-  c.sb = slice_base[f];
-  c.q0 = (uint64_t)td.y * kMinBlock;
-  const uint64_t rem = c.N - c.q0;
-  const uint32_t n_it = (uint32_t)umin64(td.z, (rem + kMinBlock - 1) / kMinBlock);
-  c.m = n_it + 1u;
-  c.hb = c.q0 ? kMinBlock : 0u;
-  const uint32_t nbytes = c.hb + (uint32_t)((umin64(rem, (uint64_t)n_it * kMinBlock) + 15ull) & ~15ull);
-  c.srd = make_srd(c.fb + c.q0 - c.hb, nbytes);
-  return c;
-}
-// Descriptor offset of unit k of tile c; past the tile (k >= m) and the halo
-// at a file's start read past the descriptor's end: zeros.
-__device__ __forceinline__ uint32_t k1_unit_soff(const K1Chunk& c, uint32_t k) {
-  const uint32_t past = c.hb + (c.m - 1u) * kMinBlock;
-  if (k == 0u) return c.hb ? 0u : past;
-  return k < c.m ? c.hb + (k - 1u) * kMinBlock : past;
-}
-
-extern "C" __global__ __launch_bounds__(kK1Threads, 1) void hbx_k1d_digest_scan(
-    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ file_off,
-    const uint64_t* __restrict__ file_len, const uint64_t* __restrict__ slice_base,
-    const uint4* __restrict__ tiles, uint32_t n_tiles, uint32_t* __restrict__ ctr, uint2* __restrict__ ssum,
-    uint64_t dummy) {
-  __shared__ uint2 wtot[2][16];
-  __shared__ uint32_t claim0, claim;  // the first tile's index; the later ones'
-  __shared__ __attribute__((aligned(1024))) uint8_t land[kK1Threads / 64][2][kDmaSlot];
-  const uint32_t tid = threadIdx.x;
-  const uint32_t l = tid & 63u;
-  const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
-  const uint32_t e_l = w * kSlice + l * 64u;
-  const uint32_t lds0 = (uint32_t)(uintptr_t)&land[w][0][0];
-  const uint32_t lds1 = (uint32_t)(uintptr_t)&land[w][1][0];
-  // the transposed (conflict-free) LDS image of hbx_k1_digest_scan_dma, swz 1
-  const uint32_t dma_lane = 64u * (l & 15u) + 16u * (l >> 4);
-  const uint32_t rd_lane = 64u * (l >> 4) + (l & 15u);
-  auto land_read = [&](uint32_t slot, uint32_t (&v)[16]) {
-    const u32x4* p = reinterpret_cast<const u32x4*>(&land[w][slot][0]);
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const u32x4 t = p[rd_lane + 16u * k];
-      v[4 * k + 0] = t.x;
-      v[4 * k + 1] = t.y;
-      v[4 * k + 2] = t.z;
-      v[4 * k + 3] = t.w;
-    }
-  };
-  if (tid == 0u) claim0 = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  K1Chunk cur = k1_chunk(arena, file_off, file_len, slice_base, tiles, n_tiles,
-                         (uint32_t)__builtin_amdgcn_readfirstlane((int)claim0));
-  if (!cur.valid) return;
-  K1Chunk nxt = cur;
-  nxt.valid = false;
-  // stream position k of the current tile (k >= m: the next tile's unit k - m,
-  // or past the current tile's end when there is none)
-  auto issue = [&](uint32_t k, uint32_t lds) {
-    const bool use_n = k >= cur.m && nxt.valid;
-    const s32x4 srd = use_n ? nxt.srd : cur.srd;
-    const uint32_t soff = use_n ? k1_unit_soff(nxt, k - cur.m) : k1_unit_soff(cur, k);
-    dma16x4(srd, w * kSlice + dma_lane, soff, lds);
-  };
-  issue(0u, lds0);
-  issue(1u, lds1);
-  uint32_t run_a[16], run_b[16];
-  K1State st{0u, 0u, RunAgg{0u, 0u, 0u, 0u}};
-  uint32_t u = 0u, k = 0u, v_claim = 0u;
-  const uint64_t ctr64 = reinterpret_cast<uint64_t>(ctr);
-  bool done = false;
-  auto step = [&](uint32_t (&cv)[16], const uint32_t (&pv)[16]) {
-    const bool claim_now = k + 3u == cur.m;  // the claim issued after unit m-4's store lands
-    // outstanding per wave, oldest first: DMA(u), store(u-2), DMA(u+1),
-    // store(u-1) (+ wave 0's claim atomic after store(u-1) at a claim unit)
-    if (claim_now && w == 0u)
-      asm volatile("s_waitcnt vmcnt(0)" : "+v"(v_claim) : : "memory");  // (binds the claim's register)
-    else if (u == 0u)
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if (u == 1u)
-      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    land_read(u & 1u, cv);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot consumed before it is refilled
-    if (claim_now && tid == 0u) claim = v_claim;         // published by this unit's barrier
-    issue(k + 2u, (u & 1u) ? lds1 : lds0);
-    if (k == 0u) {  // the halo: prime the rollsum state
-      // one barrier per unit, also at a file's start (k1_prime has none
-      // there): unit u+1 writes wave totals into wtot[u & 1] only after every
-      // wave has read unit u-1's
-      if (cur.q0 == 0u) __syncthreads();
-      st = k1_prime(cv, cur.q0 == 0u, wtot, w, l, e_l, u & 1u);
-      k1_store_slice(ssum, dummy, l, 0u, 0u);
-    } else {
-      const uint64_t qs = cur.q0 + (uint64_t)(k - 1u) * kMinBlock;
-      uint32_t smax, sprev;
-      k1_iteration(cv, pv, st, wtot, u, w, l, e_l, qs, cur.N, smax, sprev);
-      const bool ok = qs + (uint64_t)w * kSlice < cur.N;
-      k1_store_slice(ssum, ok ? cur.sb + ((qs >> kSliceShift) + w) : dummy, l, smax, sprev);
-    }
-    // inline asm: a compiler-issued atomic got a vmcnt(0) right behind it in
-    // every wave (draining the DMA just issued); this one is waited for by
-    // wave 0's vmcnt(0) at the next unit, which names its register
-    if (k + 4u == cur.m && tid == 0u)
-      asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=&v"(v_claim) : "v"(ctr64), "v"(1u) : "memory");
-    if (claim_now)
-      nxt = k1_chunk(arena, file_off, file_len, slice_base, tiles, n_tiles,
-                     (uint32_t)__builtin_amdgcn_readfirstlane((int)claim));
-    u++;
-    if (++k == cur.m) {
-      if (nxt.valid) {
-        cur = nxt;
-        nxt.valid = false;
-        k = 0u;
-      } else {
-        done = true;
-      }
-    }
-  };
-  for (;;) {
-    step(run_a, run_b);
-    if (done) break;
-    step(run_b, run_a);
-    if (done) break;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup exits
-}
-
 // ------------------------------------------------------------------ K2 --
 namespace {
 
@@ -734,90 +565,76 @@ __device__ __forceinline__ uint32_t xad(uint32_t b, uint32_t cd, uint32_t t1) { 
     a = (b) + rotl(xad((b), cd_, (a) + (x) + (t)), s);     \
   }
 
-// Round 1's additive constants (RFC 1321 T[1..16]): with XT the message words
-// arrive with them already added (x_j + T_j, added by K3P's producer wave,
-// k3p_produce XT), so a round-1 step is F -> add3(a, F, x_j + T_j) -> rotate
-// -> add, one VALU fewer, and the later rounds, which read x_j again, add
-// T_k - T_j instead of T_k (folded constants): 16 of the block's 320 VALU
-// leave the MD5 wave's stream (round 6, HBX_K3_XT=1, A/B only: measured
-// slower, see hbx_engine.hip k3_xt).
-constexpr uint32_t kR1[16] = {0xd76aa478u, 0xe8c7b756u, 0x242070dbu, 0xc1bdceeeu, 0xf57c0fafu, 0x4787c62au,
-                              0xa8304613u, 0xfd469501u, 0x698098d8u, 0x8b44f7afu, 0xffff5bb1u, 0x895cd7beu,
-                              0x6b901122u, 0xfd987193u, 0xa679438eu, 0x49b40821u};
-template <bool XT>
-__device__ __forceinline__ void md5_compress_t(uint32_t (&h)[4], const uint32_t (&m)[16]) {
+__device__ __forceinline__ void md5_compress(uint32_t (&h)[4], const uint32_t (&m)[16]) {
   uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
-  HBX_STEP(HBX_F, a, b, c, d, m[0], (XT ? 0u : 0xd76aa478u), 7);
-  HBX_STEP(HBX_F, d, a, b, c, m[1], (XT ? 0u : 0xe8c7b756u), 12);
-  HBX_STEP(HBX_F, c, d, a, b, m[2], (XT ? 0u : 0x242070dbu), 17);
-  HBX_STEP(HBX_F, b, c, d, a, m[3], (XT ? 0u : 0xc1bdceeeu), 22);
-  HBX_STEP(HBX_F, a, b, c, d, m[4], (XT ? 0u : 0xf57c0fafu), 7);
-  HBX_STEP(HBX_F, d, a, b, c, m[5], (XT ? 0u : 0x4787c62au), 12);
-  HBX_STEP(HBX_F, c, d, a, b, m[6], (XT ? 0u : 0xa8304613u), 17);
-  HBX_STEP(HBX_F, b, c, d, a, m[7], (XT ? 0u : 0xfd469501u), 22);
-  HBX_STEP(HBX_F, a, b, c, d, m[8], (XT ? 0u : 0x698098d8u), 7);
-  HBX_STEP(HBX_F, d, a, b, c, m[9], (XT ? 0u : 0x8b44f7afu), 12);
-  HBX_STEP(HBX_F, c, d, a, b, m[10], (XT ? 0u : 0xffff5bb1u), 17);
-  HBX_STEP(HBX_F, b, c, d, a, m[11], (XT ? 0u : 0x895cd7beu), 22);
-  HBX_STEP(HBX_F, a, b, c, d, m[12], (XT ? 0u : 0x6b901122u), 7);
-  HBX_STEP(HBX_F, d, a, b, c, m[13], (XT ? 0u : 0xfd987193u), 12);
-  HBX_STEP(HBX_F, c, d, a, b, m[14], (XT ? 0u : 0xa679438eu), 17);
-  HBX_STEP(HBX_F, b, c, d, a, m[15], (XT ? 0u : 0x49b40821u), 22);
-  HBX_STEP(HBX_G, a, b, c, d, m[1], (XT ? 0xf61e2562u - kR1[1] : 0xf61e2562u), 5);
-  HBX_STEP(HBX_G, d, a, b, c, m[6], (XT ? 0xc040b340u - kR1[6] : 0xc040b340u), 9);
-  HBX_STEP(HBX_G, c, d, a, b, m[11], (XT ? 0x265e5a51u - kR1[11] : 0x265e5a51u), 14);
-  HBX_STEP(HBX_G, b, c, d, a, m[0], (XT ? 0xe9b6c7aau - kR1[0] : 0xe9b6c7aau), 20);
-  HBX_STEP(HBX_G, a, b, c, d, m[5], (XT ? 0xd62f105du - kR1[5] : 0xd62f105du), 5);
-  HBX_STEP(HBX_G, d, a, b, c, m[10], (XT ? 0x02441453u - kR1[10] : 0x02441453u), 9);
-  HBX_STEP(HBX_G, c, d, a, b, m[15], (XT ? 0xd8a1e681u - kR1[15] : 0xd8a1e681u), 14);
-  HBX_STEP(HBX_G, b, c, d, a, m[4], (XT ? 0xe7d3fbc8u - kR1[4] : 0xe7d3fbc8u), 20);
-  HBX_STEP(HBX_G, a, b, c, d, m[9], (XT ? 0x21e1cde6u - kR1[9] : 0x21e1cde6u), 5);
-  HBX_STEP(HBX_G, d, a, b, c, m[14], (XT ? 0xc33707d6u - kR1[14] : 0xc33707d6u), 9);
-  HBX_STEP(HBX_G, c, d, a, b, m[3], (XT ? 0xf4d50d87u - kR1[3] : 0xf4d50d87u), 14);
-  HBX_STEP(HBX_G, b, c, d, a, m[8], (XT ? 0x455a14edu - kR1[8] : 0x455a14edu), 20);
-  HBX_STEP(HBX_G, a, b, c, d, m[13], (XT ? 0xa9e3e905u - kR1[13] : 0xa9e3e905u), 5);
-  HBX_STEP(HBX_G, d, a, b, c, m[2], (XT ? 0xfcefa3f8u - kR1[2] : 0xfcefa3f8u), 9);
-  HBX_STEP(HBX_G, c, d, a, b, m[7], (XT ? 0x676f02d9u - kR1[7] : 0x676f02d9u), 14);
-  HBX_STEP(HBX_G, b, c, d, a, m[12], (XT ? 0x8d2a4c8au - kR1[12] : 0x8d2a4c8au), 20);
-  HBX_STEP_H(a, b, c, d, m[5], (XT ? 0xfffa3942u - kR1[5] : 0xfffa3942u), 4);
-  HBX_STEP_H(d, a, b, c, m[8], (XT ? 0x8771f681u - kR1[8] : 0x8771f681u), 11);
-  HBX_STEP_H(c, d, a, b, m[11], (XT ? 0x6d9d6122u - kR1[11] : 0x6d9d6122u), 16);
-  HBX_STEP_H(b, c, d, a, m[14], (XT ? 0xfde5380cu - kR1[14] : 0xfde5380cu), 23);
-  HBX_STEP_H(a, b, c, d, m[1], (XT ? 0xa4beea44u - kR1[1] : 0xa4beea44u), 4);
-  HBX_STEP_H(d, a, b, c, m[4], (XT ? 0x4bdecfa9u - kR1[4] : 0x4bdecfa9u), 11);
-  HBX_STEP_H(c, d, a, b, m[7], (XT ? 0xf6bb4b60u - kR1[7] : 0xf6bb4b60u), 16);
-  HBX_STEP_H(b, c, d, a, m[10], (XT ? 0xbebfbc70u - kR1[10] : 0xbebfbc70u), 23);
-  HBX_STEP_H(a, b, c, d, m[13], (XT ? 0x289b7ec6u - kR1[13] : 0x289b7ec6u), 4);
-  HBX_STEP_H(d, a, b, c, m[0], (XT ? 0xeaa127fau - kR1[0] : 0xeaa127fau), 11);
-  HBX_STEP_H(c, d, a, b, m[3], (XT ? 0xd4ef3085u - kR1[3] : 0xd4ef3085u), 16);
-  HBX_STEP_H(b, c, d, a, m[6], (XT ? 0x04881d05u - kR1[6] : 0x04881d05u), 23);
-  HBX_STEP_H(a, b, c, d, m[9], (XT ? 0xd9d4d039u - kR1[9] : 0xd9d4d039u), 4);
-  HBX_STEP_H(d, a, b, c, m[12], (XT ? 0xe6db99e5u - kR1[12] : 0xe6db99e5u), 11);
-  HBX_STEP_H(c, d, a, b, m[15], (XT ? 0x1fa27cf8u - kR1[15] : 0x1fa27cf8u), 16);
-  HBX_STEP_H(b, c, d, a, m[2], (XT ? 0xc4ac5665u - kR1[2] : 0xc4ac5665u), 23);
-  HBX_STEP(HBX_I, a, b, c, d, m[0], (XT ? 0xf4292244u - kR1[0] : 0xf4292244u), 6);
-  HBX_STEP(HBX_I, d, a, b, c, m[7], (XT ? 0x432aff97u - kR1[7] : 0x432aff97u), 10);
-  HBX_STEP(HBX_I, c, d, a, b, m[14], (XT ? 0xab9423a7u - kR1[14] : 0xab9423a7u), 15);
-  HBX_STEP(HBX_I, b, c, d, a, m[5], (XT ? 0xfc93a039u - kR1[5] : 0xfc93a039u), 21);
-  HBX_STEP(HBX_I, a, b, c, d, m[12], (XT ? 0x655b59c3u - kR1[12] : 0x655b59c3u), 6);
-  HBX_STEP(HBX_I, d, a, b, c, m[3], (XT ? 0x8f0ccc92u - kR1[3] : 0x8f0ccc92u), 10);
-  HBX_STEP(HBX_I, c, d, a, b, m[10], (XT ? 0xffeff47du - kR1[10] : 0xffeff47du), 15);
-  HBX_STEP(HBX_I, b, c, d, a, m[1], (XT ? 0x85845dd1u - kR1[1] : 0x85845dd1u), 21);
-  HBX_STEP(HBX_I, a, b, c, d, m[8], (XT ? 0x6fa87e4fu - kR1[8] : 0x6fa87e4fu), 6);
-  HBX_STEP(HBX_I, d, a, b, c, m[15], (XT ? 0xfe2ce6e0u - kR1[15] : 0xfe2ce6e0u), 10);
-  HBX_STEP(HBX_I, c, d, a, b, m[6], (XT ? 0xa3014314u - kR1[6] : 0xa3014314u), 15);
-  HBX_STEP(HBX_I, b, c, d, a, m[13], (XT ? 0x4e0811a1u - kR1[13] : 0x4e0811a1u), 21);
-  HBX_STEP(HBX_I, a, b, c, d, m[4], (XT ? 0xf7537e82u - kR1[4] : 0xf7537e82u), 6);
-  HBX_STEP(HBX_I, d, a, b, c, m[11], (XT ? 0xbd3af235u - kR1[11] : 0xbd3af235u), 10);
-  HBX_STEP(HBX_I, c, d, a, b, m[2], (XT ? 0x2ad7d2bbu - kR1[2] : 0x2ad7d2bbu), 15);
-  HBX_STEP(HBX_I, b, c, d, a, m[9], (XT ? 0xeb86d391u - kR1[9] : 0xeb86d391u), 21);
+  HBX_STEP(HBX_F, a, b, c, d, m[0], 0xd76aa478u, 7);
+  HBX_STEP(HBX_F, d, a, b, c, m[1], 0xe8c7b756u, 12);
+  HBX_STEP(HBX_F, c, d, a, b, m[2], 0x242070dbu, 17);
+  HBX_STEP(HBX_F, b, c, d, a, m[3], 0xc1bdceeeu, 22);
+  HBX_STEP(HBX_F, a, b, c, d, m[4], 0xf57c0fafu, 7);
+  HBX_STEP(HBX_F, d, a, b, c, m[5], 0x4787c62au, 12);
+  HBX_STEP(HBX_F, c, d, a, b, m[6], 0xa8304613u, 17);
+  HBX_STEP(HBX_F, b, c, d, a, m[7], 0xfd469501u, 22);
+  HBX_STEP(HBX_F, a, b, c, d, m[8], 0x698098d8u, 7);
+  HBX_STEP(HBX_F, d, a, b, c, m[9], 0x8b44f7afu, 12);
+  HBX_STEP(HBX_F, c, d, a, b, m[10], 0xffff5bb1u, 17);
+  HBX_STEP(HBX_F, b, c, d, a, m[11], 0x895cd7beu, 22);
+  HBX_STEP(HBX_F, a, b, c, d, m[12], 0x6b901122u, 7);
+  HBX_STEP(HBX_F, d, a, b, c, m[13], 0xfd987193u, 12);
+  HBX_STEP(HBX_F, c, d, a, b, m[14], 0xa679438eu, 17);
+  HBX_STEP(HBX_F, b, c, d, a, m[15], 0x49b40821u, 22);
+  HBX_STEP(HBX_G, a, b, c, d, m[1], 0xf61e2562u, 5);
+  HBX_STEP(HBX_G, d, a, b, c, m[6], 0xc040b340u, 9);
+  HBX_STEP(HBX_G, c, d, a, b, m[11], 0x265e5a51u, 14);
+  HBX_STEP(HBX_G, b, c, d, a, m[0], 0xe9b6c7aau, 20);
+  HBX_STEP(HBX_G, a, b, c, d, m[5], 0xd62f105du, 5);
+  HBX_STEP(HBX_G, d, a, b, c, m[10], 0x02441453u, 9);
+  HBX_STEP(HBX_G, c, d, a, b, m[15], 0xd8a1e681u, 14);
+  HBX_STEP(HBX_G, b, c, d, a, m[4], 0xe7d3fbc8u, 20);
+  HBX_STEP(HBX_G, a, b, c, d, m[9], 0x21e1cde6u, 5);
+  HBX_STEP(HBX_G, d, a, b, c, m[14], 0xc33707d6u, 9);
+  HBX_STEP(HBX_G, c, d, a, b, m[3], 0xf4d50d87u, 14);
+  HBX_STEP(HBX_G, b, c, d, a, m[8], 0x455a14edu, 20);
+  HBX_STEP(HBX_G, a, b, c, d, m[13], 0xa9e3e905u, 5);
+  HBX_STEP(HBX_G, d, a, b, c, m[2], 0xfcefa3f8u, 9);
+  HBX_STEP(HBX_G, c, d, a, b, m[7], 0x676f02d9u, 14);
+  HBX_STEP(HBX_G, b, c, d, a, m[12], 0x8d2a4c8au, 20);
+  HBX_STEP_H(a, b, c, d, m[5], 0xfffa3942u, 4);
+  HBX_STEP_H(d, a, b, c, m[8], 0x8771f681u, 11);
+  HBX_STEP_H(c, d, a, b, m[11], 0x6d9d6122u, 16);
+  HBX_STEP_H(b, c, d, a, m[14], 0xfde5380cu, 23);
+  HBX_STEP_H(a, b, c, d, m[1], 0xa4beea44u, 4);
+  HBX_STEP_H(d, a, b, c, m[4], 0x4bdecfa9u, 11);
+  HBX_STEP_H(c, d, a, b, m[7], 0xf6bb4b60u, 16);
+  HBX_STEP_H(b, c, d, a, m[10], 0xbebfbc70u, 23);
+  HBX_STEP_H(a, b, c, d, m[13], 0x289b7ec6u, 4);
+  HBX_STEP_H(d, a, b, c, m[0], 0xeaa127fau, 11);
+  HBX_STEP_H(c, d, a, b, m[3], 0xd4ef3085u, 16);
+  HBX_STEP_H(b, c, d, a, m[6], 0x04881d05u, 23);
+  HBX_STEP_H(a, b, c, d, m[9], 0xd9d4d039u, 4);
+  HBX_STEP_H(d, a, b, c, m[12], 0xe6db99e5u, 11);
+  HBX_STEP_H(c, d, a, b, m[15], 0x1fa27cf8u, 16);
+  HBX_STEP_H(b, c, d, a, m[2], 0xc4ac5665u, 23);
+  HBX_STEP(HBX_I, a, b, c, d, m[0], 0xf4292244u, 6);
+  HBX_STEP(HBX_I, d, a, b, c, m[7], 0x432aff97u, 10);
+  HBX_STEP(HBX_I, c, d, a, b, m[14], 0xab9423a7u, 15);
+  HBX_STEP(HBX_I, b, c, d, a, m[5], 0xfc93a039u, 21);
+  HBX_STEP(HBX_I, a, b, c, d, m[12], 0x655b59c3u, 6);
+  HBX_STEP(HBX_I, d, a, b, c, m[3], 0x8f0ccc92u, 10);
+  HBX_STEP(HBX_I, c, d, a, b, m[10], 0xffeff47du, 15);
+  HBX_STEP(HBX_I, b, c, d, a, m[1], 0x85845dd1u, 21);
+  HBX_STEP(HBX_I, a, b, c, d, m[8], 0x6fa87e4fu, 6);
+  HBX_STEP(HBX_I, d, a, b, c, m[15], 0xfe2ce6e0u, 10);
+  HBX_STEP(HBX_I, c, d, a, b, m[6], 0xa3014314u, 15);
+  HBX_STEP(HBX_I, b, c, d, a, m[13], 0x4e0811a1u, 21);
+  HBX_STEP(HBX_I, a, b, c, d, m[4], 0xf7537e82u, 6);
+  HBX_STEP(HBX_I, d, a, b, c, m[11], 0xbd3af235u, 10);
+  HBX_STEP(HBX_I, c, d, a, b, m[2], 0x2ad7d2bbu, 15);
+  HBX_STEP(HBX_I, b, c, d, a, m[9], 0xeb86d391u, 21);
   h[0] += a;
   h[1] += b;
   h[2] += c;
   h[3] += d;
-}
-__device__ __forceinline__ void md5_compress(uint32_t (&h)[4], const uint32_t (&m)[16]) {
-  md5_compress_t<false>(h, m);
 }
 
 __device__ __forceinline__ void md5_init(uint32_t (&h)[4]) {
@@ -1161,22 +978,10 @@ __device__ __forceinline__ uint32_t order_bin(uint32_t cnt, uint32_t budget) {
 // launch overhead 1.084-1.089 -> 1.040-1.050, profiles/r06h); the rest by
 // descending count in bins [abins, 1024).  Every group of the full-slice
 // region still has count == budget, so the K3 walk is unchanged.
-// Near-full chains too (round 6, `near` in 64ths of the slice, HBX_PLAN_NEAR;
-// A/B only, measured slower, hbx_engine.hip plan_near):
-// a chain in its last launch with at least budget (1 - near/64) blocks left
-// goes to its address bin beside the full slices instead of a count bin.  In
-// a count bin its wave's 64 chains lie anywhere in the resident arenas, and
-// such a wave, nearly a full slice long, ended most launches last with its
-// CU's three other waves (tools/diag_slow_cu.py: 22 of 30 launches,
-// profiles/r06w); among full slices it costs its wave one self-staged round
-// of the remaining (budget - count) blocks for the other lanes.
-__device__ __forceinline__ uint32_t plan_bin(const OrderEntry& o, uint32_t budget, uint32_t abins, uint32_t ashift,
-                                             uint32_t near = 0u) {
+__device__ __forceinline__ uint32_t plan_bin(const OrderEntry& o, uint32_t budget, uint32_t abins, uint32_t ashift) {
   const uint32_t cnt = min(o.rem - 1u, budget);
   if (!abins) return order_bin(cnt, budget);
-  const uint64_t thr = (uint64_t)budget - (uint64_t)budget * near / 64u;
-  if (cnt == budget || (uint64_t)cnt >= thr)
-    return (uint32_t)((reinterpret_cast<const Chain*>(o.chain)->src >> ashift) % abins);
+  if (cnt == budget) return (uint32_t)((reinterpret_cast<const Chain*>(o.chain)->src >> ashift) % abins);
   const uint32_t ref = min(budget, (uint32_t)(kMaxBlock >> 6) + 1u);
   const uint32_t c = min(cnt, ref);
   return abins + (ref - c) * (kPlanBins - 1u - abins) / ref;
@@ -1252,8 +1057,7 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
     uint32_t* __restrict__ gh, uint32_t phase) {
   const uint32_t abins = (phase >> 8) & 0xfffu;  // address bins for full slices (plan_bin), 0 = off
   const uint32_t ashift = phase >> 24;            // their granule: 2^ashift bytes
-  const uint32_t near = (phase >> 1) & 0x7fu;     // near-full chains to the address bins (plan_bin)
-  phase &= 1u;
+  phase &= 0xffu;
   __shared__ uint32_t hist[kPlanBins], pos[kPlanBins], wsum[kPlanThreads / 64];
   const uint32_t tid = threadIdx.x;
   const uint32_t gt = blockIdx.x * kPlanThreads + tid, gn = gridDim.x * kPlanThreads;
@@ -1288,7 +1092,7 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
   __syncthreads();
   for (uint32_t e = gt; e < n_all; e += gn) {
     const OrderEntry o = entry(e);
-    if (o.rem) atomicAdd(&hist[plan_bin(o, budget, abins, ashift, near)], 1u);
+    if (o.rem) atomicAdd(&hist[plan_bin(o, budget, abins, ashift)], 1u);
   }
   __syncthreads();
   if (phase == 0u) {
@@ -1309,15 +1113,12 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
       *n_out = before + inc;
       n_out[1] = 0u;  // K3Q's item queue head and tail for this order slot
       n_out[2] = 0u;
-      if (!abins) n_out[3] = 0xFFFFFFFFu;  // no address bins: K3 places groups densely (k3_slots)
     }
-    // entries in the address (full-slice) bins, for K3's placement (k3_slots)
-    if (blockIdx.x == 0 && abins && tid == abins) n_out[3] = before + inc - v;
   }
   __syncthreads();
   for (uint32_t e = gt; e < n_all; e += gn) {
     const OrderEntry o = entry(e);
-    if (o.rem) out[atomicAdd(&pos[plan_bin(o, budget, abins, ashift, near)], 1u)] = o;
+    if (o.rem) out[atomicAdd(&pos[plan_bin(o, budget, abins, ashift)], 1u)] = o;
   }
 }
 
@@ -1393,7 +1194,6 @@ __device__ __forceinline__ void k3p_publish(uint32_t* p, uint32_t v) {
 // A stage is freed once its last block is hashed (its reads have landed: the
 // block waited for them), except the group's last stage (freed by the caller
 // once the group is done).
-template <bool XT = false>
 __device__ __forceinline__ void k3p_consume(uint8_t* wl, uint32_t* flags, uint32_t S, uint32_t Rr, uint32_t (&h)[4],
                                             uint32_t& polls, bool spin) {
   const uint32_t row = (uint32_t)(uintptr_t)(wl + (threadIdx.x & 63u) * Coop<16>::Row);  // LDS address
@@ -1414,7 +1214,7 @@ __device__ __forceinline__ void k3p_consume(uint8_t* wl, uint32_t* flags, uint32
   auto hash = [&](const u32x4(&W)[4]) {
     const uint32_t m[16] = {W[0].x, W[0].y, W[0].z, W[0].w, W[1].x, W[1].y, W[1].z, W[1].w,
                             W[2].x, W[2].y, W[2].z, W[2].w, W[3].x, W[3].y, W[3].z, W[3].w};
-    md5_compress_t<XT>(h, m);  // XT: the producer added round 1's constants
+    md5_compress(h, m);
   };
   const uint32_t nst = (4u * Rr + 15u) / 16u;  // >= 2 (Rr >= kCoopMinBudget - 1)
   u32x4 WA[4], WB[4];
@@ -1494,105 +1294,15 @@ __device__ __forceinline__ K3Group k3_group(const OrderEntry* __restrict__ order
 // loads at any byte offset, as md5_coop).  Returns the group's stage count.
 // SETS register sets of loads in flight (3 by default: one stage more of
 // memory latency hidden than 2, HBX_K3_PSETS=2 for A/B).
-// Hand-counted producer loads (round 6, HBX_K3_HAND=1, A/B only: bit-exact,
-// measured no faster, profiles/r06j; tools/check_asm_loads.py lists the ISA
-// accesses to registers of loads still in flight): the compiler placed
-// `s_waitcnt vmcnt(0)` before the first coop_write of every three stages (its
-// count is lost across the conditional puts and the flag-wait loops), so the
-// producer waited for all three register sets in flight, not the oldest one,
-// and a stage's loads had about one stage of lead instead of three.  Here the
-// 16 loads of a set are inline asm (the compiler inserts no wait for them),
-// every put issues exactly one set (clamped re-reads past the group's last
-// stage, as coop_load), so at each put the oldest set is followed by exactly
-// 2 x 16 newer loads: `s_waitcnt vmcnt(32)` (vmcnt(16) with two sets), bound
-// to the set's registers, lands it.  Loads the compiler issues itself (the
-// order entries at a group's start) only make its own waits stricter.
-__device__ __forceinline__ void coop_load_asm(u32x4 (&Gs)[16], const uint64_t (&Q)[16], uint32_t st, uint32_t t,
-                                              uint32_t ngr) {
-  const uint32_t g = min(16u * st + t, ngr - 1u);
-  const uint64_t off = 16ull * (g - t);
-#pragma unroll
-  for (int q = 0; q < 16; q++)
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(Gs[q]) : "v"(Q[q] + off));
-}
-template <int N>
-__device__ __forceinline__ void coop_vmwait(u32x4 (&G)[16]) {
-  asm volatile("s_waitcnt vmcnt(%16)"
-               : "+v"(G[0]), "+v"(G[1]), "+v"(G[2]), "+v"(G[3]), "+v"(G[4]), "+v"(G[5]), "+v"(G[6]), "+v"(G[7]),
-                 "+v"(G[8]), "+v"(G[9]), "+v"(G[10]), "+v"(G[11]), "+v"(G[12]), "+v"(G[13]), "+v"(G[14]), "+v"(G[15])
-               : "n"(N)
-               : "memory");
-}
-
-// XT (round 6): the producer adds round 1's constants to the words of a stage
-// in its registers before writing the rows (granule t of a chain's stage holds
-// words 4 (t % 4) .. +3 of a block), 64 v_add_u32 per stage.  They share the
-// SIMD with the MD5 wave, but at a lower priority (s_setprio 2 vs 3) they
-// issue only in the MD5 wave's bubbles (~30 VALU slots per block at 1,450
-// cycles).  (The same adds as LDS atomics after the writes, 64 ds_add_u32 per
-// stage, kept the VALU free but the rows' atomics, 2-3-way bank-conflicted,
-// held the LDS path the MD5 wave reads through: 1,512-1,520 vs 1,454-1,456
-// cycles per block, profiles/r06q.)
-__device__ __forceinline__ void coop_write_k(uint8_t* wl, uint32_t wr, uint32_t half, const u32x4 (&Gs)[16],
-                                             const uint32_t (&kc)[4]) {
-#pragma unroll
-  for (int q = 0; q < 16; q++) {
-    const u32x4 v = {Gs[q].x + kc[0], Gs[q].y + kc[1], Gs[q].z + kc[2], Gs[q].w + kc[3]};
-    *reinterpret_cast<u32x4*>(wl + wr + half * Coop<16>::Half + Coop<16>::C * Coop<16>::Row * (uint32_t)q) = v;
-  }
-}
-__device__ __forceinline__ void k3_lane_r1(uint32_t (&kc)[4]) {  // this producer lane's 4 round-1 constants
-  const uint32_t j0 = 4u * ((threadIdx.x & 63u) % 4u);
-#pragma unroll
-  for (int w = 0; w < 4; w++) {
-    uint32_t v = 0u;
-#pragma unroll
-    for (int j = 0; j < 16; j += 4) v = j0 == (uint32_t)j ? kR1[j + w] : v;
-    kc[w] = v;
-  }
-}
-
-template <int SETS = 2, bool HAND = false, bool XT = false>
+template <int SETS = 2>
 __device__ __forceinline__ uint32_t k3p_produce(uint8_t* wl, uint32_t* flags, uint32_t S, uint64_t src, uint32_t Rr) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t t = lane % 16u, sub = lane / 16u;
   const uint32_t wr = sub * Coop<16>::Row + 16u * t;
-  uint32_t kc[4];
-  if constexpr (XT) k3_lane_r1(kc);
   const uint32_t ngr = 4u * Rr, nst = (ngr + 15u) / 16u;
   uint64_t Q[16];
 #pragma unroll
   for (int q = 0; q < 16; q++) Q[q] = shfl64(src, 4u * (uint32_t)q + sub) + 16ull * t;
-  if constexpr (HAND) {
-    u32x4 GA[16], GB[16], GC[16];
-    coop_load_asm(GA, Q, 0u, t, ngr);
-    coop_load_asm(GB, Q, min(1u, nst - 1u), t, ngr);
-    if (SETS == 3) coop_load_asm(GC, Q, min(2u, nst - 1u), t, ngr);
-    // stage x goes to LDS half x & 1 once stage x - 2 is freed (flags[1] >= S + x - 1)
-    auto put = [&](uint32_t x, u32x4(&G)[16]) {
-      k3p_wait_ge(&flags[1], x < 2u ? S : S + x - 1u);
-      coop_vmwait<16 * (SETS - 1)>(G);
-      if constexpr (XT)
-        coop_write_k(wl, wr, (S + x) & 1u, G, kc);
-      else
-        coop_write<16>(wl, wr, (S + x) & 1u, G);
-      k3p_publish(&flags[0], S + x + 1u);
-      coop_load_asm(G, Q, min(x + (uint32_t)SETS, nst - 1u), t, ngr);
-    };
-    if (SETS == 3) {
-      for (uint32_t s = 0; s < nst; s += 3u) {
-        put(s, GA);
-        if (s + 1u < nst) put(s + 1u, GB);
-        if (s + 2u < nst) put(s + 2u, GC);
-      }
-    } else {
-      for (uint32_t s = 0; s < nst; s += 2u) {
-        put(s, GA);
-        if (s + 1u < nst) put(s + 1u, GB);
-      }
-    }
-    return nst;
-  }
   u32x4 GA[16], GB[16];
   coop_load<16>(GA, Q, 0u, t, ngr);
   coop_load<16>(GB, Q, min(1u, nst - 1u), t, ngr);
@@ -1602,10 +1312,7 @@ __device__ __forceinline__ uint32_t k3p_produce(uint8_t* wl, uint32_t* flags, ui
     // stage x goes to LDS half x & 1 once stage x - 2 is freed (flags[1] >= S + x - 1)
     auto put = [&](uint32_t x, u32x4 (&G)[16]) {
       k3p_wait_ge(&flags[1], x < 2u ? S : S + x - 1u);
-      if constexpr (XT)
-        coop_write_k(wl, wr, (S + x) & 1u, G, kc);
-      else
-        coop_write<16>(wl, wr, (S + x) & 1u, G);
+      coop_write<16>(wl, wr, (S + x) & 1u, G);
       k3p_publish(&flags[0], S + x + 1u);
       coop_load<16>(G, Q, min(x + 3u, nst - 1u), t, ngr);
     };
@@ -1618,18 +1325,12 @@ __device__ __forceinline__ uint32_t k3p_produce(uint8_t* wl, uint32_t* flags, ui
   }
   for (uint32_t s = 0; s < nst; s += 2u) {
     k3p_wait_ge(&flags[1], s < 2u ? S : S + s - 1u);
-    if constexpr (XT)
-      coop_write_k(wl, wr, (S + s) & 1u, GA, kc);
-    else
-      coop_write<16>(wl, wr, (S + s) & 1u, GA);
+    coop_write<16>(wl, wr, (S + s) & 1u, GA);
     k3p_publish(&flags[0], S + s + 1u);
     coop_load<16>(GA, Q, min(s + 2u, nst - 1u), t, ngr);
     if (s + 1u < nst) {
       k3p_wait_ge(&flags[1], s + 1u < 2u ? S : S + s);
-      if constexpr (XT)
-        coop_write_k(wl, wr, (S + s + 1u) & 1u, GB, kc);
-      else
-        coop_write<16>(wl, wr, (S + s + 1u) & 1u, GB);
+      coop_write<16>(wl, wr, (S + s + 1u) & 1u, GB);
       k3p_publish(&flags[0], S + s + 2u);
       coop_load<16>(GB, Q, min(s + 3u, nst - 1u), t, ngr);
     }
@@ -1796,56 +1497,16 @@ __device__ __forceinline__ void k3q_push(uint32_t* __restrict__ qc, uint64_t* __
 // The producer wave of pair `flags`: the same groups as its MD5 wave; for a
 // group on the cooperative path (R >= kCoopMinBudget), the stages of blocks
 // next+1 .. next+R-1 of its 64 chains, SETS register sets in flight.
-// Placement of the groups on the waves (round 6, K3 `pair`, HBX_K3_PAIR=1;
-// A/B only, measured slower, hbx_engine.hip k3_pair; default dense).  The groups come in the planner's order: the full slices (address
-// bins) first, then the partial ones (chains in their last launch) by
-// descending count.  A partial group's 64 chains lie anywhere in the resident
-// arenas, and the longest of them ended most launches last, together with
-// their CU's other waves (tools/diag_slow_cu.py, profiles/r06w).  So the full
-// slices fill whole workgroups densely, as before, and each workgroup after
-// them pairs one long partial group with three of the shortest: those finish
-// early and leave the long one the CU's memory path.  Wave slot v of the
-// launch (blockIdx * 4 + wave, then + nwaves ...) takes group
-// k3_slot_group(v); a hole takes none.  Any slot map that is a bijection onto
-// the groups gives the same results.
-constexpr uint32_t kNoGroup = 0xFFFFFFFFu;
-struct K3Slots {
-  uint32_t F, F4, P, K, S;  // full groups, padded to a workgroup; partial groups, their workgroups; slots
-};
-__device__ __forceinline__ K3Slots k3_slots(uint32_t groups, uint32_t nfull_entries, bool pair) {
-  K3Slots s;
-  s.F = pair ? min(nfull_entries / 64u, groups) : groups;
-  s.F4 = pair ? (s.F + 3u) & ~3u : s.F;
-  s.P = groups - s.F;
-  s.K = (s.P + 3u) / 4u;
-  s.S = s.F4 + 4u * s.K;
-  return s;
-}
-__device__ __forceinline__ uint32_t k3_slot_group(const K3Slots& s, uint32_t v) {
-  if (v < s.F) return v;
-  if (v < s.F4) return kNoGroup;
-  const uint32_t k = (v - s.F4) >> 2, j = (v - s.F4) & 3u;
-  if (j == 0u) return s.F + k;          // the k-th longest partial group
-  const uint32_t d = 3u * k + (j - 1u);  // the d-th shortest
-  if (d >= s.P) return kNoGroup;
-  const uint32_t q = s.P - 1u - d;
-  return q >= s.K ? s.F + q : kNoGroup;
-}
-
-template <int SETS, bool HAND = false, bool XT = false>
+template <int SETS>
 __device__ void k3p_producer(uint8_t* wl, uint32_t* flags, const OrderEntry* __restrict__ order,
-                             const uint32_t* __restrict__ n_order, uint32_t budget, uint32_t g0, uint32_t nwaves,
-                             bool pair = false) {
+                             const uint32_t* __restrict__ n_order, uint32_t budget, uint32_t g0, uint32_t nwaves) {
   const uint32_t n_total = *n_order;
   const uint32_t groups = (n_total + 63u) / 64u;
-  const K3Slots sl = k3_slots(groups, n_order[3], pair);
   uint32_t S = 0;  // stages of this launch so far
-  for (uint32_t v = g0; v < sl.S; v += nwaves) {
-    const uint32_t g = k3_slot_group(sl, v);
-    if (g == kNoGroup) continue;
+  for (uint32_t g = g0; g < groups; g += nwaves) {
     const K3Group G = k3_group(order, n_total, g, budget);
     if (G.R < kCoopMinBudget) continue;  // wave-uniform: the MD5 wave takes the lane path
-    S += k3p_produce<SETS, HAND, XT>(wl, flags, S, G.src + 64ull * (G.next + 1u) - 8ull, G.R - 1u);  // from block next+1
+    S += k3p_produce<SETS>(wl, flags, S, G.src + 64ull * (G.next + 1u) - 8ull, G.R - 1u);  // from block next+1
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (clamped re-reads of the last stage)
 }
@@ -1881,12 +1542,11 @@ struct K3Queue {
   uint32_t tag, parts;
   uint32_t* err;
 };
-template <bool PROD, bool ITEMS = false, bool XT = false>
+template <bool PROD, bool ITEMS = false>
 __device__ __forceinline__ void k3_body(
     uint8_t* wl, const OrderEntry* __restrict__ order, const uint32_t* __restrict__ n_order, uint32_t budget,
     uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last, uint64_t* __restrict__ tslot,
-    uint64_t* __restrict__ probe, uint32_t* flags = nullptr, K3Queue Q = K3Queue{}, bool spin = false,
-    bool pair = false) {
+    uint64_t* __restrict__ probe, uint32_t* flags = nullptr, K3Queue Q = K3Queue{}, bool spin = false) {
   static_assert(PROD || !ITEMS, "items need the producer waves");
   // the MD5 chains are issue-bound: win the SIMD's issue arbitration against
   // co-resident waves of other kernels
@@ -1924,9 +1584,8 @@ __device__ __forceinline__ void k3_body(
   uint32_t seq = 0;  // ITEMS: items announced to the producer
   uint32_t polls = 0;  // PROD: polls that found the producer's stage not yet written
   bool first = true;
-  const K3Slots sl = k3_slots(groups, ITEMS ? kNoGroup : n_order[3], pair && !ITEMS);
-  for (uint32_t v = g0;; v += nwaves) {
-    uint32_t part = 0u, item = 0u, g = v;
+  for (uint32_t g = g0;; g += nwaves) {
+    uint32_t part = 0u, item = 0u;
     if constexpr (ITEMS) {
       item = g0 < groups ? k3q_pop(Q.qc, Q.q, groups, groups * Q.parts, Q.tag, Q.err) : kItemExit;
       if ((threadIdx.x & 63u) == 0u) {  // announce it to the producer (kItemExit: it stops too)
@@ -1937,9 +1596,7 @@ __device__ __forceinline__ void k3_body(
       g = item % groups;
       part = item / groups;
     } else {
-      if (v >= sl.S) break;
-      g = k3_slot_group(sl, v);
-      if (g == kNoGroup) continue;
+      if (g >= groups) break;
     }
     K3Lane L = k3_lane<ITEMS>(order, n_total, g, part, budget, per_part);
     uint32_t(&h)[4] = L.h;
@@ -1956,7 +1613,7 @@ __device__ __forceinline__ void k3_body(
         pmax = wave_max_all(cnt);
       }
       if constexpr (PROD) {  // stages from the producer wave; the group's last is freed at its end
-        k3p_consume<XT>(wl, flags, S, R - 1u, h, polls, spin);
+        k3p_consume(wl, flags, S, R - 1u, h, polls, spin);
         S += (4u * (R - 1u) + 15u) / 16u;
       } else {
         md5_coop<16>(wl, src, h, L.next + 1u, R - 1u);
@@ -2063,44 +1720,23 @@ extern "C" __global__ __launch_bounds__(kK3PThreads, 1) void hbx_k3p_block_md5(
     uint32_t* __restrict__ started, uint32_t t_first, uint32_t t_last, uint64_t* __restrict__ tslot,
     uint64_t* __restrict__ probe, uint32_t psets) {
   // psets: producer register sets (2 or 3) | 0x100 for the spinning stage wait
-  // | 0x200 for the hand-counted producer loads (k3p_produce HAND)
-  // | 0x400 for round 1's constants added by the producer (XT)
   const bool spin = (psets & 0x100u) != 0u;
-  const bool hand = (psets & 0x200u) != 0u;
-  const bool xt = (psets & 0x400u) != 0u && !hand;  // (the hand-counted producer has no XT form)
-  const bool pairing = (psets & 0x800u) != 0u;      // long/short partial groups per CU (k3_slots)
   psets &= 0xffu;
   __shared__ __attribute__((aligned(16))) uint8_t k3_lds[4][kK3WaveLds];
   __shared__ uint32_t k3_flags[4][2];
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const uint32_t wp = wave & 3u;  // the MD5 / producer pair
+  const uint32_t pair = wave & 3u;
   if (threadIdx.x < 8u) k3_flags[threadIdx.x >> 1][threadIdx.x & 1u] = 0u;
   __syncthreads();
   if (wave < 4u) {
-    if (xt)
-      k3_body<true, false, true>(k3_lds[wp], order, n_order, budget, started, t_first, t_last, tslot, probe,
-                                 k3_flags[wp], K3Queue{}, spin, pairing);
-    else
-      k3_body<true>(k3_lds[wp], order, n_order, budget, started, t_first, t_last, tslot, probe, k3_flags[wp],
-                    K3Queue{}, spin, pairing);
+    k3_body<true>(k3_lds[pair], order, n_order, budget, started, t_first, t_last, tslot, probe, k3_flags[pair],
+                  K3Queue{}, spin);
   } else {
     __builtin_amdgcn_s_setprio(2);
-    const uint32_t g0 = blockIdx.x * 4u + wp, nw = gridDim.x * 4u;
-    if (hand) {
-      if (psets == 3u)
-        k3p_producer<3, true>(k3_lds[wp], k3_flags[wp], order, n_order, budget, g0, nw, pairing);
-      else
-        k3p_producer<2, true>(k3_lds[wp], k3_flags[wp], order, n_order, budget, g0, nw, pairing);
-    } else if (xt) {
-      if (psets == 3u)
-        k3p_producer<3, false, true>(k3_lds[wp], k3_flags[wp], order, n_order, budget, g0, nw, pairing);
-      else
-        k3p_producer<2, false, true>(k3_lds[wp], k3_flags[wp], order, n_order, budget, g0, nw, pairing);
-    } else if (psets == 3u) {
-      k3p_producer<3>(k3_lds[wp], k3_flags[wp], order, n_order, budget, g0, nw, pairing);
-    } else {
-      k3p_producer<2>(k3_lds[wp], k3_flags[wp], order, n_order, budget, g0, nw, pairing);
-    }
+    if (psets == 3u)
+      k3p_producer<3>(k3_lds[pair], k3_flags[pair], order, n_order, budget, blockIdx.x * 4u + pair, gridDim.x * 4u);
+    else
+      k3p_producer<2>(k3_lds[pair], k3_flags[pair], order, n_order, budget, blockIdx.x * 4u + pair, gridDim.x * 4u);
   }
 }
 
