@@ -944,6 +944,23 @@ struct alignas(16) Chain {
 constexpr uint32_t kChainDone = 0xFFFFFFFFu;
 constexpr uint32_t kBudgetAll = 0xFFFFFFFFu;
 
+// Full message blocks a launch with `budget` hashes of a chain with `left`
+// still to hash.  kSliceRemFirst (round 6, A/B): the chain takes the part
+// that does not fill a slice in its FIRST launch ((left - 1) mod budget + 1)
+// and a full slice in every later one, instead of full slices first and the
+// remainder last.  The launches per chain are the same (ceil(left/budget)),
+// so every schedule and completion count holds; what moves is where the
+// short counts fall: on the joining batch's chains, which all lie in one
+// arena, instead of on chains in their last launch scattered over all of
+// them (the launch tail, tools/diag_slow_cu.py).
+#ifndef HBX_SLICE_REM_FIRST
+#define HBX_SLICE_REM_FIRST 1
+#endif
+__device__ __forceinline__ uint32_t slice_cnt(uint32_t left, uint32_t budget) {
+  if (left <= budget) return left;
+  return HBX_SLICE_REM_FIRST ? (left - 1u) % budget + 1u : budget;
+}
+
 // ------------------------------------------------------- chain schedule --
 // A batch's chains live in the batch's own array for their whole life (K2r
 // writes them; K3 updates `next` and the MD5 state in place).  What changes
@@ -979,7 +996,7 @@ __device__ __forceinline__ uint32_t order_bin(uint32_t cnt, uint32_t budget) {
 // descending count in bins [abins, 1024).  Every group of the full-slice
 // region still has count == budget, so the K3 walk is unchanged.
 __device__ __forceinline__ uint32_t plan_bin(const OrderEntry& o, uint32_t budget, uint32_t abins, uint32_t ashift) {
-  const uint32_t cnt = min(o.rem - 1u, budget);
+  const uint32_t cnt = slice_cnt(o.rem - 1u, budget);
   if (!abins) return order_bin(cnt, budget);
   if (cnt == budget) return (uint32_t)((reinterpret_cast<const Chain*>(o.chain)->src >> ashift) % abins);
   const uint32_t ref = min(budget, (uint32_t)(kMaxBlock >> 6) + 1u);
@@ -1074,7 +1091,7 @@ extern "C" __global__ __launch_bounds__(kPlanThreads) void hbx_k2c_plan(
     OrderEntry o;
     if (e < n_prev) {  // the launch with budget bprev finished it iff its full blocks fit
       o = prev[e];
-      o.rem = o.rem - 1u <= bprev ? 0u : o.rem - bprev;
+      o.rem = o.rem - 1u <= bprev ? 0u : o.rem - slice_cnt(o.rem - 1u, bprev);
     } else {
       const OrderEntry* f = fs.f[0];
       uint32_t base = n_prev;
@@ -1283,7 +1300,7 @@ __device__ __forceinline__ K3Group k3_group(const OrderEntry* __restrict__ order
   G.src = chp->src;
   const uint32_t left = o.rem - 1u;  // listed entries have rem >= 1
   G.next = ((chp->len + 8u) >> 6) - left;
-  G.cnt = G.active ? min(left, budget) : 0u;
+  G.cnt = G.active ? slice_cnt(left, budget) : 0u;
   // R = the wave's smallest count: all 64 chains advance R blocks together
   G.R = ~wave_max_all(G.active ? ~G.cnt : 0u);
   return G;
@@ -1386,7 +1403,7 @@ __device__ __forceinline__ K3Lane k3_lane(const OrderEntry* __restrict__ order, 
     L.next = ((ch.len + 8u) >> 6) - left;
     L.len = active ? ch.len : 0u;
     L.b0 = active ? L.next : 0u;
-    L.cnt = active ? min(left, budget) : 0u;
+    L.cnt = active ? slice_cnt(left, budget) : 0u;
     L.finish = active && left <= budget;
     L.live = active;
     L.src = reinterpret_cast<const uint8_t*>(ch.src);
@@ -1406,7 +1423,7 @@ __device__ __forceinline__ K3Lane k3_lane(const OrderEntry* __restrict__ order, 
     const uint32_t nfull = (ch.len + 8u) >> 6;
     // this launch's slice of the chain: the planner's rem (1 + blocks left
     // before the launch) and the budget; part `part` of it
-    const uint32_t total = min(o.rem - 1u, budget);
+    const uint32_t total = slice_cnt(o.rem - 1u, budget);
     const uint32_t start = nfull - (o.rem - 1u);
     const uint64_t lo64 = (uint64_t)part * per_part;
     const uint32_t lo = lo64 < total ? (uint32_t)lo64 : total;
