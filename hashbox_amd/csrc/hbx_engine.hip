@@ -1037,8 +1037,8 @@ int submit_batch_timed(hbx_ctx* c, const void* d_arena, uint64_t n, const uint64
   b->caps = tcaps;
   // launches this batch's chains need: a chunk is <= min(longest file, MAX)
   // bytes, i.e. <= nfull full message blocks, and each launch advances it by
-  // min(remaining, budget) blocks, finishing it in the launch where the
-  // remainder fits
+  // slice_cnt(remaining, budget) blocks (the part short of a slice first, then
+  // full slices): ceil(blocks / budget) launches either way
   const uint64_t nfull = (std::min<uint64_t>(longest, HBX_MAX_BLOCK_SIZE) + 8) >> 6;
   const uint64_t lb = launch_budget(c, budget);  // a K3 period multiplies the slice
   b->need = budget == kBudgetAll ? 1u : (uint32_t)std::max<uint64_t>(1, (nfull + lb - 1) / lb);

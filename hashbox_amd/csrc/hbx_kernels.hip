@@ -970,7 +970,7 @@ __device__ __forceinline__ uint32_t slice_cnt(uint32_t left, uint32_t budget) {
 // batch in flight, so the 64 chains of a K3 wave have nearly equal counts and
 // the wave advances them together by its minimum (the cooperative path) with
 // only a small per-lane remainder.  A chain's progress is deterministic (it
-// advances min(remaining, budget) blocks per launch), so the planner builds
+// advances slice_cnt(remaining, budget) blocks per launch), so the planner builds
 // the order of launch j from the order of launch j-1 without waiting for K3
 // j-1: it runs on the scan stream, beside the hash stream's K3 launches.
 struct OrderEntry {
@@ -1049,7 +1049,7 @@ extern "C" __global__ __launch_bounds__(256) void hbx_k2r_new_chains(
 // `bprev`, hashed; the ones it finished dropped) plus the fresh entries of
 // the batches joining it (`fs`: up to kMaxFresh lists, list i with count
 // *fs.n[i]; a K3 period > 1 joins several batches per launch; either part may
-// be absent), binned by this launch's count min(rem, budget).  Two launches
+// be absent), binned by this launch's count slice_cnt(rem - 1, budget).  Two launches
 // of the same grid over the same
 // partition:
 //   phase 0: per-workgroup histogram of the bins, added into gh[0, 1024)
@@ -1359,7 +1359,7 @@ __device__ __forceinline__ uint32_t k3p_produce(uint8_t* wl, uint32_t* flags, ui
 // K3Q (hbx_k3q_block_md5): the launch's work is cut into items (g, h), part h
 // of P of group g's slice (at most ceil(budget / P) blocks of each chain),
 // handed out dynamically: every wave takes the next item from a queue, and
-// finishing (g, h) queues (g, h+1).  A chain still advances exactly min(rem,
+// finishing (g, h) queues (g, h+1).  A chain still advances exactly slice_cnt(rem,
 // budget) blocks per launch (the planner's and the engine's schedule are
 // unchanged), but its slice may continue on another CU: a CU that runs slow
 // (which one varies launch by launch, tools/diag_slow_cu.py) no longer holds
