@@ -136,7 +136,8 @@ int hbx_wait(hbx_ctx *ctx);
 int hbx_pending(hbx_ctx *ctx);
 /* Time slice of the block-MD5 stage: full 64-byte MD5 blocks each chain in
  * flight advances per launch (default 16384 = 1 MiB; 0 = unlimited, one
- * launch per batch).  A submitted batch is complete after join lag (below)
+ * launch per batch); a chain takes the part short of a whole slice in its
+ * first launch and whole slices after.  A submitted batch is complete after join lag (below)
  * + ceil(min(longest file, 8 MiB)/64 / blocks) - 1 further launches; results are
  * identical for every setting. */
 int hbx_set_md5_slice(hbx_ctx *ctx, uint32_t blocks);
