@@ -122,7 +122,7 @@ def parse():
                          "1 at 32 or more files per GPU, else 4 (or 2) if it divides --steps)")
     ap.add_argument("--lead", type=int, default=-1,
                     help="steps an arena stays resident beyond the launches its batch needs: R = launches "
-                         "per batch + lead (-1 = the library's: the join lag at 32+ files per GPU, lag + 1 below "
+                         "per batch + lead (-1 = the library's: the join lag at 64+ files per GPU, lag + 1 below "
                          "and with --e2e).  Lead = join lag is the least that lets the next batch's scan overlap "
                          "the launch finishing the old one (hbx_input_after_oldest)")
     ap.add_argument("--e2e", action="store_true",

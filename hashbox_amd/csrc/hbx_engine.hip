@@ -1686,13 +1686,14 @@ int hbx_plan_pipeline(hbx_ctx* c, const hbx_plan_request* q, hbx_pipeline_plan* 
     per = (q->steps == 0 || q->steps % 4 == 0) ? 4 : (q->steps % 2 == 0) ? 2 : 1;
   }
   // lead (steps an arena stays resident beyond its batch's launches): the join
-  // lag at 32 or more files per GPU (round 6: the next batch's K1 follows the
+  // lag at 64 or more files per GPU (round 6: the next batch's K1 follows the
   // launch that finishes the old one through hbx_input_after_oldest; R = 33 at
   // 64 files then holds 31 launches instead of 30: 2,380-2,391 vs 2,303-2,350
-  // GiB/s in three alternating pairs, profiles/r06p), lag + 1 below (8 files:
-  // 2,045 vs 2,082, where R ~ 256 makes the lead's share negligible) and for
+  // GiB/s in three alternating pairs, profiles/r06p), lag + 1 below (32 files:
+  // 2,229/2,232 vs 2,279/2,273, profiles/r06zf, where the extra chains take
+  // CUs from a K1 that already sets the step; 8 files: 2,045 vs 2,082) and for
   // host input
-  const int64_t ld = q->lead >= 0 ? q->lead : lag + ((q->n_files >= 32 && !host_in) ? 0 : 1);
+  const int64_t ld = q->lead >= 0 ? q->lead : lag + ((q->n_files >= 64 && !host_in) ? 0 : 1);
   const uint64_t nfull = (std::min<uint64_t>(q->longest_file, HBX_MAX_BLOCK_SIZE) + 8u) >> 6;
   const double frac = q->hbm_frac > 0.0 ? q->hbm_frac : 0.95;
   const uint64_t share = (uint64_t)((double)free_b * frac / (double)std::max<uint32_t>(1u, q->ranks_per_device));

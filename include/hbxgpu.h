@@ -535,7 +535,7 @@ int hbx_set_k3_period(hbx_ctx *ctx, uint32_t period);
  * hbx_submit_device reaches the engine's measured rate only with the
  * schedule below: R batches resident in device memory,
  * each MD5 launch advancing every chain by the slice, a join lag of 2, a
- * lead of 2 (3 below 32 files per batch) and, below 32 files per batch, one MD5
+ * lead of 2 (3 below 64 files per batch) and, below 32 files per batch, one MD5
  * launch every 4 submits.
  * hbx_plan_pipeline computes that schedule (bench.py runs exactly this plan)
  * and hbx_apply_plan sets it on a context.  Request fields <= 0 (md5_slice:
@@ -555,7 +555,7 @@ typedef struct {
   int32_t md5_slice;         /* blocks per chain per submit (< 0: sized from R; 0: unlimited) */
   int32_t join_lag;          /* 1..4 (<= 0: 2) */
   int32_t lead;              /* steps an arena stays resident beyond its batch's launches (< 0: the join lag
-                                at 32 or more files per batch with device input, else lag + 1) */
+                                at 64 or more files per batch with device input, else lag + 1) */
   int32_t k3_period;         /* 1..8 (<= 0: 4, or 2 if 4 does not divide steps, below 32 files; else 1) */
   uint32_t flags;            /* HBX_PLAN_HOST_INPUT */
 } hbx_plan_request;

@@ -69,7 +69,7 @@ def test_bench_configs2_full_corpus_world2():
     MiB corpus a one-GPU run hashes, strong-scaled over 2 ranks (32 files
     each, LPT), both ranks on cuda:0 sharing its HBM (each plans half of the
     free memory: ranks_per_device 2), each with the library's plan
-    (hbx_plan_pipeline: lag 2, lead 2, period 1 at 32 files).  Every file of
+    (hbx_plan_pipeline: lag 2, lead 3, period 1 at 32 files).  Every file of
     the last 4 batches each rank collected in the timed window, and of its
     last drained batch, is checked against the oracle."""
     d = _torchrun(2, ["bench.py", "--gpus", "2", "--steps", "8", "--warmup", "2", "--dist-backend", "gloo",
@@ -78,7 +78,7 @@ def test_bench_configs2_full_corpus_world2():
     c = d["config"]
     assert d["n_gpus"] == 2 and d["scaling"] == "strong"
     assert c["files_per_step"] == 64 and c["files_per_gpu"] == 32 and c["file_bytes"] == 128 << 20
-    assert (c["join_lag"], c["scan_lead"], c["k3_period"]) == (2, 2, 1)
+    assert (c["join_lag"], c["scan_lead"], c["k3_period"]) == (2, 3, 1)
     assert c["pipeline_depth"] >= 16  # about half of one device's batches at 4 GiB per batch
     assert d["window_launches"]["k1_digest_scan"] == 8 and d["window_launches"]["k3_block_md5"] == 8
     assert d["check_vs_oracle"] is True and d["checked_batches_per_gpu"] == 5

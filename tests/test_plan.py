@@ -5,7 +5,7 @@ the library gets).  Pure host arithmetic: runs without a GPU.
 
 `_py_plan` below is bench.residency_plan's schedule as of round 5 (commit
 526942d, bench.py:587-654), kept as the reference, with round 6's one change:
-the default lead is the join lag at 32 or more files per GPU."""
+the default lead is the join lag at 64 or more files per GPU."""
 import pytest
 
 ARENA_SLACK = 64 << 20
@@ -19,8 +19,8 @@ def _py_plan(nf, total, fbytes, free_bytes, hbm_frac=0.95, ranks_per_device=1, a
         per = k3_period
     else:
         per = next((p for p in (4, 2) if steps <= 0 or steps % p == 0), 1) if nf < 32 and not e2e else 1
-    # round 6: lead = lag at 32+ files per GPU (device input), lag + 1 below
-    ld = lead if lead >= 0 else lag + (0 if nf >= 32 and not e2e else 1)
+    # round 6: lead = lag at 64+ files per GPU (device input), lag + 1 below
+    ld = lead if lead >= 0 else lag + (0 if nf >= 64 and not e2e else 1)
     nfull = (min(fbytes, 8 << 20) + 8) >> 6
     r_fit = max(ld + 1, int(free_bytes * hbm_frac / max(1, ranks_per_device)) // (total + ARENA_SLACK))
     if e2e:
