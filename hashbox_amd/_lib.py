@@ -22,7 +22,7 @@ ERRORS = {-1: "HBX_ERR_ARG", -2: "HBX_ERR_HIP", -3: "HBX_ERR_CAPACITY", -4: "HBX
 EXPORTS = [
     "hbx_version", "hbx_device_count", "hbx_max_chunks", "hbx_ctx_create", "hbx_ctx_destroy",
     "hbx_last_error", "hbx_chunk_hash", "hbx_chunk_hash_batch", "hbx_chunk_hash_device",
-    "hbx_submit_device", "hbx_wait", "hbx_store_paths", "hbx_block_id", "hbx_arena_alloc", "hbx_arena_free",
+    "hbx_submit_device", "hbx_wait", "hbx_store_paths", "hbx_block_id", "hbx_md5", "hbx_arena_alloc", "hbx_arena_free",
     "hbx_memcpy_h2d", "hbx_memcpy_h2d_async", "hbx_alloc_pinned", "hbx_free_pinned", "hbx_stage_times",
     "hbx_set_tile_iters", "hbx_pending", "hbx_set_md5_slice", "hbx_stage_totals", "hbx_io_times",
     "hbx_reserve", "hbx_verify_blocks", "hbx_verify_blocks_device",
@@ -133,6 +133,7 @@ def load() -> ctypes.CDLL:
     L.hbx_wait.argtypes = [P]
     L.hbx_store_paths.argtypes = [P, U64, P, P, P, P, P, P, P, ctypes.c_uint32, U64]
     L.hbx_block_id.argtypes = [P, P, ctypes.c_uint32, P, U64, P]
+    L.hbx_md5.argtypes = [P, P, U64, P]
     L.hbx_arena_alloc.argtypes = [P, U64, ctypes.POINTER(P)]
     L.hbx_arena_free.argtypes = [P, P]
     L.hbx_memcpy_h2d.argtypes = [P, P, P, U64]

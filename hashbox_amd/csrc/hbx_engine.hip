@@ -1968,6 +1968,24 @@ int hbx_block_id(hbx_ctx* c, const uint8_t* links, uint32_t n_links, const uint8
   return HBX_OK;
 }
 
+// MD5(data) on the device (K5 over the raw message): core.Hash (core.go:46-48),
+// the primitive under Hmac/DeepHmac (core.go:51-80), whose KAT rows
+// (core_test.go:23-30) tests/test_gpu_parity.py runs through this call.
+int hbx_md5(hbx_ctx* c, const uint8_t* data, uint64_t len, uint8_t out[16]) {
+  if (!c || !out || (len && !data) || len > 0xFFFFFFFEull - 16ull) return HBX_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  HBX_TRY(c, hipSetDevice(c->device));
+  HBX_TRY(c, c->d_msg.ensure(len + 16));
+  uint8_t* dm = c->d_msg.as<uint8_t>();
+  if (len) HBX_TRY(c, hipMemcpyAsync(dm + 16, data, len, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(hbx_k5_md5_raw, dim3(1), dim3(64), 0, c->stream, dm + 16, (uint32_t)len,
+                     reinterpret_cast<uint32_t*>(dm));
+  HBX_TRY(c, hipGetLastError());
+  HBX_TRY(c, hipMemcpyAsync(out, dm, 16, hipMemcpyDeviceToHost, c->stream));
+  HBX_TRY(c, hipStreamSynchronize(c->stream));
+  return HBX_OK;
+}
+
 namespace {
 // K6 over n blocks whose data is already on the device (block i at
 // arena + offs[i]); lanes are ordered longest first so each wave's 64 chains

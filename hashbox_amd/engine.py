@@ -372,6 +372,26 @@ class Engine:
                     "hbx_block_id")
         return out.tobytes()
 
+    def md5(self, data: BytesLike) -> bytes:
+        """core.Hash (pkg/core/core.go:46-48): MD5 of the raw bytes on the device."""
+        a = _u8(data)
+        out = np.zeros(16, np.uint8)
+        self._check(self._L.hbx_md5(self._ctx, _p(a), a.size, _p(out)), "hbx_md5")
+        return out.tobytes()
+
+    def hmac(self, data: bytes, key: bytes) -> bytes:
+        """core.Hmac (pkg/core/core.go:51-68) with the device MD5 as the hash."""
+        k = (bytes(key) + bytes(16))[:16] + bytes(48)  # Byte128 key, zero-padded to md5.BlockSize
+        inner = self.md5(bytes(b ^ 0x36 for b in k) + bytes(data))
+        return self.md5(bytes(b ^ 0x5C for b in k) + inner)
+
+    def deep_hmac(self, depth: int, data: bytes, key: bytes) -> bytes:
+        """core.DeepHmac (pkg/core/core.go:70-80): depth rounds of Hmac."""
+        h, d = bytes(16), bytes(data)
+        for _ in range(depth):
+            h = d = self.hmac(d, key)
+        return h
+
     @staticmethod
     def _links_arrays(links_per_block: Optional[Sequence[Sequence[bytes]]], n: int):
         if not links_per_block or not any(len(x) for x in links_per_block):

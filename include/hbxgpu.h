@@ -194,6 +194,10 @@ int hbx_io_times(hbx_ctx *ctx, double s[3], int reset);
  * DESIGN.md §8). */
 int hbx_host_call_max(hbx_ctx *ctx, double ms[2], int reset);
 
+/* MD5(data) on the device: core.Hash (pkg/core/core.go:46-48), the primitive
+ * under core.Hmac / DeepHmac (core.go:51-80). */
+int hbx_md5(hbx_ctx *ctx, const uint8_t *data, uint64_t len, uint8_t out[16]);
+
 /* MD5(BE32(n_links) || links || BE32(len) || data) on the device. */
 int hbx_block_id(hbx_ctx *ctx, const uint8_t *links, uint32_t n_links, const uint8_t *data,
                  uint64_t len, uint8_t out[16]);

@@ -166,6 +166,27 @@ def test_golden_fixtures_on_device(engine):
         assert g.content_type == c["content_type"] and g.content_id.hex() == c["content_id"]
 
 
+def test_hmac_kats_on_device_md5(engine):
+    """The reference's own HMAC-MD5 rows (pkg/core/core_test.go:23-30, kept in
+    tests/golden/kat.json) computed with the device MD5 (hbx_md5, K5) as the
+    hash under core.Hmac / DeepHmac: pins the GPU MD5 to the reference's
+    vectors directly, not only through the oracle."""
+    import json
+    with open(os.path.join(os.path.dirname(__file__), "golden", "kat.json")) as f:
+        kat = json.load(f)
+    for r in kat["hmac"]:
+        got = engine.deep_hmac(r["depth"], r["text"].encode(), r["key"].encode())
+        assert got.hex() == r["out"], r
+
+
+@pytest.mark.parametrize("n", [0, 1, 55, 56, 63, 64, 65, 119, 120, 127, 128, 1000, 65536, 1 << 20])
+def test_md5_raw_lengths(engine, n):
+    """hbx_md5 against hashlib over the padding boundaries (55/56/64 mod 64)."""
+    import hashlib
+    data = np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8).tobytes()
+    assert engine.md5(data) == hashlib.md5(data).digest()
+
+
 def test_kat_block_ids_on_device(engine):
     import json
     import os
