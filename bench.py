@@ -230,7 +230,7 @@ def oracle_check(arena, offs, lens, res, threads):
     return bool(ok)
 
 
-TRAFFIC_FILE = "profiles/r05y8_traffic.json"  # PMC FETCH_SIZE pass of the round-5 final tree (tools/profile_round.sh)
+TRAFFIC_FILE = "profiles/r06zd_traffic.json"  # PMC FETCH_SIZE pass of the round-6 final kernels (tools/profile_round.sh)
 
 
 def measured_traffic(kernel, per_launch_bytes, batch_bytes):
@@ -249,7 +249,7 @@ def measured_traffic(kernel, per_launch_bytes, batch_bytes):
         return None, None
     d = json.load(open(files[-1]))
     kk = d.get("kernels", {})
-    # K1 has two kernels (K1D, round 6, and the one-workgroup-per-tile form)
+    # K1 may be named by more than one kernel (older profiles name K1D, the pruned round-6 variant)
     k = next((kk[n] for n in ((kernel,) if isinstance(kernel, str) else kernel) if n in kk), None)
     if not k:
         return None, None
