@@ -95,3 +95,36 @@ def test_plain_c_driver_links_and_reports_no_device(tmp_path):
     r = subprocess.run([str(tmp_path / "abi_driver"), str(f), "--expect-nodev"], capture_output=True, text=True)
     assert r.returncode == 0 and r.stdout.strip().splitlines()[-1] == "nodev ok", (r.returncode, r.stdout, r.stderr)
     assert r.stdout.startswith("plan R=") and " lag=2 lead=3 period=4 " in r.stdout
+
+
+def test_md5_argument_checks_without_device():
+    """hbx_md5 rejects a null context or output before any HIP call."""
+    from hashbox_amd import _lib
+    L = _lib.load()
+    out = (ctypes.c_uint8 * 16)()
+    assert L.hbx_md5(None, None, 0, out) == -1
+    assert L.hbx_md5(None, None, 0, None) == -1
+
+
+def test_engine_hmac_construction_matches_reference_kats():
+    """Engine.hmac / deep_hmac (core.go:51-80) is host logic around the device
+    MD5; with hashlib standing in for hbx_md5 it reproduces the reference's
+    HMAC rows (core_test.go:23-30, tests/golden/kat.json).  The GPU test
+    test_hmac_kats_on_device_md5 runs the same rows through the device."""
+    import hashlib
+    import json
+    from hashbox_amd.engine import Engine
+
+    class HostMd5(Engine):
+        def __init__(self):  # no device context
+            pass
+
+        def md5(self, data):
+            return hashlib.md5(bytes(data)).digest()
+
+    e = HostMd5()
+    with open(os.path.join(ROOT, "tests", "golden", "kat.json")) as f:
+        rows = json.load(f)["hmac"]
+    for r in rows:
+        assert e.deep_hmac(r["depth"], r["text"].encode(), r["key"].encode()).hex() == r["out"], r
+    assert e.deep_hmac(0, b"x", b"k") == bytes(16)  # DeepHmac with depth 0 returns the zero hash
